@@ -1,0 +1,806 @@
+/*
+ * octvr_oracle.c — CPU restatement of the reference octVR hot path (TEST INFRASTRUCTURE ONLY).
+ * See octvr_oracle.h.  Compiled with -ffp-contract=off so every float/double expression rounds
+ * exactly as written (the reference x86-64 build has no FMA contraction).
+ */
+#include "octvr_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+/* ------------------------------------------------------------------------------------------ */
+/* Rotation: Camera::Camera (octvr/src/camera.cpp:49-70)                                       */
+/* ------------------------------------------------------------------------------------------ */
+
+/* cvRodrigues2 vector -> matrix (calib3d/src/calibration.cpp:300-345). */
+static void rodrigues(double rx, double ry, double rz, double R[9]) {
+    double theta = sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double c = cos(theta), s = sin(theta), c1 = 1. - c;
+    double itheta = theta ? 1. / theta : 0.;
+    rx *= itheta; ry *= itheta; rz *= itheta;
+    double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    double rx_[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    for (int k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * rx_[k];
+}
+
+/* 3x3 product through cv::gemm's len==3 fast path (core/src/matmul.cpp:934-1000):
+ * t = a0*b0 + a1*b1 + a2*b2 ; d = t*alpha + c*beta with alpha=1, beta=0, c=zero. */
+static void mul33(const double* a, const double* b, double* d) {
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double t = a[i * 3 + 0] * b[0 * 3 + j] + a[i * 3 + 1] * b[1 * 3 + j] + a[i * 3 + 2] * b[2 * 3 + j];
+            d[i * 3 + j] = t * 1.0 + 0.0 * 0.0;
+        }
+}
+
+void orc_rotation_rpy(double roll, double yaw, double pitch, double R[9]) {
+    double v0 = roll, v1 = -yaw, v2 = -pitch;
+    double Rx[9], Ry[9], Rz[9], T[9];
+    rodrigues(v0, 0, 0, Rx);
+    rodrigues(0, v1, 0, Ry);
+    rodrigues(0, 0, v2, Rz);
+    mul33(Rx, Rz, T);
+    mul33(T, Ry, R);
+}
+
+/* cv::invert 3x3 double closed form (core/src/lapack.cpp:709-712 det3, :970-990). */
+void orc_invert3(const double* S, double* D) {
+#define Sd(y, x) S[(y) * 3 + (x)]
+    double d = Sd(0, 0) * ((double)Sd(1, 1) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 1)) -
+               Sd(0, 1) * ((double)Sd(1, 0) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 0)) +
+               Sd(0, 2) * ((double)Sd(1, 0) * Sd(2, 1) - (double)Sd(1, 1) * Sd(2, 0));
+    if (d == 0.) {
+        for (int k = 0; k < 9; k++) D[k] = 0;
+        return;
+    }
+    d = 1. / d;
+    D[0] = (Sd(1, 1) * Sd(2, 2) - Sd(1, 2) * Sd(2, 1)) * d;
+    D[1] = (Sd(0, 2) * Sd(2, 1) - Sd(0, 1) * Sd(2, 2)) * d;
+    D[2] = (Sd(0, 1) * Sd(1, 2) - Sd(0, 2) * Sd(1, 1)) * d;
+    D[3] = (Sd(1, 2) * Sd(2, 0) - Sd(1, 0) * Sd(2, 2)) * d;
+    D[4] = (Sd(0, 0) * Sd(2, 2) - Sd(0, 2) * Sd(2, 0)) * d;
+    D[5] = (Sd(0, 2) * Sd(1, 0) - Sd(0, 0) * Sd(1, 2)) * d;
+    D[6] = (Sd(1, 0) * Sd(2, 1) - Sd(1, 1) * Sd(2, 0)) * d;
+    D[7] = (Sd(0, 1) * Sd(2, 0) - Sd(0, 0) * Sd(2, 1)) * d;
+    D[8] = (Sd(0, 0) * Sd(1, 1) - Sd(0, 1) * Sd(1, 0)) * d;
+#undef Sd
+}
+
+void orc_camera_set_rotation(orc_camera* c, const double R[9]) {
+    memcpy(c->R, R, sizeof(c->R));
+    orc_invert3(R, c->Rinv);
+}
+
+static void camera_defaults(orc_camera* c, int type) {
+    memset(c, 0, sizeof(*c));
+    c->type = type;
+    double R[9];
+    orc_rotation_rpy(0, 0, 0, R);
+    orc_camera_set_rotation(c, R);
+    c->min_lon = -M_PI;
+    c->max_lon = M_PI;
+}
+
+void orc_camera_equirect(orc_camera* c, double min_lat, double max_lat, double scale_lon) {
+    camera_defaults(c, ORC_EQUIRECT);
+    c->min_lat = min_lat;
+    c->max_lat = max_lat;
+    c->scale_lon = scale_lon;
+}
+
+/* CalcCorrectionRadius_copy and helpers (octvr/src/cameras/fullframe_fisheye_cam.cpp:20-103). */
+static double cube_root(double x) {
+    if (x == 0.0) return 0.0;
+    if (x > 0.0) return pow(x, 1.0 / 3.0);
+    return -pow(-x, 1.0 / 3.0);
+}
+static void square_zero(double* a, int* n, double* root) {
+    if (a[2] == 0.0) {
+        if (a[1] == 0.0) {
+            if (a[0] == 0.0) { *n = 1; root[0] = 0.0; }
+            else *n = 0;
+        } else { *n = 1; root[0] = -a[0] / a[1]; }
+    } else {
+        if (4.0 * a[2] * a[0] > a[1] * a[1]) *n = 0;
+        else {
+            *n = 2;
+            root[0] = (-a[1] + sqrt(a[1] * a[1] - 4.0 * a[2] * a[0])) / (2.0 * a[2]);
+            root[1] = (-a[1] - sqrt(a[1] * a[1] - 4.0 * a[2] * a[0])) / (2.0 * a[2]);
+        }
+    }
+}
+static void cube_zero(double* a, int* n, double* root) {
+    if (a[3] == 0.0) {
+        square_zero(a, n, root);
+    } else {
+        double p = ((-1.0 / 3.0) * (a[2] / a[3]) * (a[2] / a[3]) + a[1] / a[3]) / 3.0;
+        double q = ((2.0 / 27.0) * (a[2] / a[3]) * (a[2] / a[3]) * (a[2] / a[3]) - (1.0 / 3.0) * (a[2] / a[3]) * (a[1] / a[3]) +
+                    a[0] / a[3]) / 2.0;
+        if (q * q + p * p * p >= 0.0) {
+            *n = 1;
+            root[0] = cube_root(-q + sqrt(q * q + p * p * p)) + cube_root(-q - sqrt(q * q + p * p * p)) - a[2] / (3.0 * a[3]);
+        } else {
+            double phi = acos(-q / sqrt(-p * p * p));
+            *n = 3;
+            root[0] = 2.0 * sqrt(-p) * cos(phi / 3.0) - a[2] / (3.0 * a[3]);
+            root[1] = -2.0 * sqrt(-p) * cos(phi / 3.0 + M_PI / 3.0) - a[2] / (3.0 * a[3]);
+            root[2] = -2.0 * sqrt(-p) * cos(phi / 3.0 - M_PI / 3.0) - a[2] / (3.0 * a[3]);
+        }
+    }
+}
+static double correction_radius(const double* coeff) {
+    double a[4];
+    for (int k = 0; k < 4; k++) {
+        a[k] = 0.0;
+        if (coeff[k] != 0.0) a[k] = (k + 1) * coeff[k];
+    }
+    int n, i;
+    double root[3], sroot = 1000.0;
+    cube_zero(a, &n, root);
+    for (i = 0; i < n; i++)
+        if (root[i] > 0.0 && root[i] < sroot) sroot = root[i];
+    return sroot;
+}
+
+void orc_camera_fullframe_fisheye(orc_camera* c, int width, int height, int crop_l, int crop_r, int crop_t,
+                                  int crop_b, int has_crop, int crop_circular, double hfov, double center_dx,
+                                  double center_dy, const double radial[3]) {
+    camera_defaults(c, ORC_FULLFRAME_FISHEYE);
+    c->width = width;
+    c->height = height;
+    if (has_crop) {
+        c->crop_x = crop_l;
+        c->crop_y = crop_t;
+        c->crop_w = crop_r - crop_l;
+        c->crop_h = crop_b - crop_t;
+        c->crop_circular = crop_circular;
+    }
+    if (c->crop_w * c->crop_h == 0) { /* crop.area() == 0 (fullframe_fisheye_cam.cpp:122-125) */
+        c->crop_x = c->crop_y = 0;
+        c->crop_w = width;
+        c->crop_h = height;
+        c->crop_circular = 0;
+    }
+    c->hfov = hfov;
+    c->center_dx = center_dx;
+    c->center_dy = center_dy;
+    c->rad[3] = radial[0];
+    c->rad[2] = radial[1];
+    c->rad[1] = radial[2];
+    c->rad[0] = 1.0 - radial[0] - radial[1] - radial[2];
+    c->rad[4] = (c->crop_w < c->crop_h ? c->crop_w : c->crop_h) / 2.0;
+    c->rad[5] = correction_radius(c->rad);
+}
+
+void orc_camera_fisheye(orc_camera* c, int width, int height, double fx, double fy, double cx, double cy,
+                        const double k[4]) {
+    camera_defaults(c, ORC_FISHEYE);
+    c->width = width;
+    c->height = height;
+    c->fx = fx; c->fy = fy; c->cx = cx; c->cy = cy;
+    for (int i = 0; i < 4; i++) c->k[i] = k[i];
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Sphere helpers (camera.cpp:189-210)                                                         */
+/* ------------------------------------------------------------------------------------------ */
+static void lonlat_to_xyz(double lon, double lat, double* p) {
+    p[0] = cos(lon) * cos(lat);
+    p[1] = sin(lat);
+    p[2] = -sin(lon) * cos(lat);
+}
+/* rotated = m * r.t() through GEMMSingleMul's A*Bt loop (matmul.cpp:234-262): s = ((0+a0b0)+a1b1)+a2b2. */
+static void rotate(const double* r, const double* p, double* q) {
+    for (int k = 0; k < 3; k++) {
+        double s0 = 0;
+        s0 += p[0] * r[k * 3 + 0];
+        s0 += p[1] * r[k * 3 + 1];
+        s0 += p[2] * r[k * 3 + 2];
+        double s1 = 0, s2 = 0, s3 = 0;
+        q[k] = (s0 + s1 + s2 + s3) * 1.0;
+    }
+}
+static void xyz_to_lonlat(const double* xyz, double* lon, double* lat) {
+    double n = sqrt(xyz[0] * xyz[0] + xyz[1] * xyz[1] + xyz[2] * xyz[2]);
+    double inv = 1.0 / n;
+    double px = xyz[0] * inv, py = xyz[1] * inv, pz = xyz[2] * inv;
+    *lon = atan2(-pz, px);
+    *lat = asin(py);
+}
+static int valid_longitude(const orc_camera* c, double l) {
+#define BETWEEN(x) ((x) >= c->min_lon && (x) <= c->max_lon)
+    return BETWEEN(l) || BETWEEN(l + 2 * M_PI) || BETWEEN(l - 2 * M_PI) || BETWEEN(l + 4 * M_PI) ||
+           BETWEEN(l - 4 * M_PI);
+#undef BETWEEN
+}
+
+/* Equirectangular::image_to_obj_single / obj_to_image_single (cameras/equirectangular.cpp:25-35). */
+static void equirect_i2o(const orc_camera* c, double x, double y, double* lon, double* lat) {
+    *lon = (x - 0.5) * M_PI * 2.0;
+    *lat = (c->min_lat - c->max_lat) * y + c->max_lat;
+}
+static void equirect_o2i(const orc_camera* c, double lon, double lat, double* x, double* y) {
+    *x = lon / (M_PI * 2.0) + 0.5;
+    *y = (lat - c->max_lat) / (c->min_lat - c->max_lat);
+}
+
+/* FullFrameFisheyeCamera::obj_to_image_single (fullframe_fisheye_cam.cpp:146-221). */
+static void ffisheye_o2i(const orc_camera* c, double lon, double lat, double* ox, double* oy) {
+    double s = cos(lat) * cos(lon);
+    double v1 = sin(lat);
+    double v0 = -cos(lat) * sin(lon);
+    double r = sqrt(v0 * v0 + v1 * v1);
+    double theta = atan2(r, s);
+    double distance = (double)(c->crop_w) / (c->hfov);
+    double x = -(theta * v0 / r) * distance;
+    double y = -(theta * v1 / r) * distance;
+    if (fabs(lon) < 1e-5 && fabs(lat) < 1e-5) x = y = 0;
+    /* do_radial_distort */
+    double rr = (sqrt(x * x + y * y)) / c->rad[4];
+    double scale;
+    if (rr < c->rad[5])
+        scale = ((c->rad[3] * rr + c->rad[2]) * rr + c->rad[1]) * rr + c->rad[0];
+    else
+        scale = 1000.0;
+    double rx = x * scale, ry = y * scale;
+    rx += c->center_dx;
+    ry += c->center_dy;
+    rx /= (double)c->crop_w;
+    ry /= (double)c->crop_h;
+    rx += 0.5;
+    ry += 0.5;
+    if (c->crop_circular && (rx - 0.5) * (rx - 0.5) + (ry - 0.5) * (ry - 0.5) > 0.25) {
+        *ox = NAN;
+        *oy = NAN;
+        return;
+    }
+    rx = (rx * c->crop_w) + c->crop_x;
+    ry = (ry * c->crop_h) + c->crop_y;
+    rx /= (double)c->width;
+    ry /= (double)c->height;
+    *ox = rx;
+    *oy = ry;
+}
+
+/* PinholeCamera::obj_to_image + cv::fisheye::projectPoints (pinhole_cam.cpp:32-50, calib3d/src/fisheye.cpp:95-146).
+ * Input: the rotated xyz (sphere_rotate(xyzs, false) output). */
+static void fisheye_project(const orc_camera* c, const double* Y, double* ox, double* oy) {
+    if (Y[2] <= 0) { *ox = NAN; *oy = NAN; return; }
+    double x0 = Y[0] / Y[2], x1 = Y[1] / Y[2];
+    double r2 = x0 * x0 + x1 * x1;
+    double r = sqrt(r2);
+    double theta = atan(r);
+    double theta2 = theta * theta, theta3 = theta2 * theta, theta4 = theta2 * theta2, theta5 = theta4 * theta,
+           theta6 = theta3 * theta3, theta7 = theta6 * theta, theta8 = theta4 * theta4, theta9 = theta8 * theta;
+    double theta_d = theta + c->k[0] * theta3 + c->k[1] * theta5 + c->k[2] * theta7 + c->k[3] * theta9;
+    double inv_r = r > 1e-8 ? 1.0 / r : 1;
+    double cdist = r > 1e-8 ? theta_d * inv_r : 1;
+    double xd0 = x0 * cdist, xd1 = x1 * cdist;
+    double alpha = 0;
+    double xd3_0 = xd0 + alpha * xd1, xd3_1 = xd1;
+    double u = xd3_0 * c->fx + c->cx, v = xd3_1 * c->fy + c->cy;
+    *ox = u / c->width;
+    *oy = 1.0 - v / c->height;
+}
+
+/* One output pixel through out->image_to_obj then in->obj_to_image (camera.cpp:212-253, 296-315). */
+static void project_pixel(const orc_camera* out, const orc_camera* in, double u, double v, double* x, double* y) {
+    double lon, lat, p[3], q[3];
+    /* output: image_to_obj */
+    equirect_i2o(out, u, v, &lon, &lat);
+    lonlat_to_xyz(lon, lat, p);
+    rotate(out->Rinv, p, q);
+    xyz_to_lonlat(q, &lon, &lat);
+    /* input: obj_to_image */
+    lonlat_to_xyz(lon, lat, p);
+    int lon_ok = valid_longitude(in, lon);
+    rotate(in->R, p, q);
+    if (in->type == ORC_FISHEYE) { /* PinholeCamera::obj_to_image overrides the base (no lon/excl masks) */
+        fisheye_project(in, q, x, y);
+        return;
+    }
+    double ll, la;
+    xyz_to_lonlat(q, &ll, &la);
+    double px = NAN, py = NAN;
+    if (lon_ok) {
+        if (in->type == ORC_FULLFRAME_FISHEYE) ffisheye_o2i(in, ll, la, &px, &py);
+        else equirect_o2i(in, ll, la, &px, &py);
+    }
+    *x = px;
+    *y = py;
+}
+
+int orc_lut_build(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
+                  uint8_t* mask, int use_roi, int roi[4]) {
+    int min_h = H, max_h = 0, min_w = W, max_w = 0;
+    for (int h = 0; h < H; h++)
+        for (int w = 0; w < W; w++) {
+            double dx, dy;
+            project_pixel(out, in, (double)w / W, (double)h / H, &dx, &dy);
+            float x = (float)dx, y = (float)dy;
+            size_t idx = (size_t)h * W + w;
+            if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f) {
+                mask[idx] = 0;
+                map1[idx] = map2[idx] = -1.0f;
+            } else {
+                mask[idx] = 255;
+                map1[idx] = x;
+                map2[idx] = y;
+                if (h < min_h) min_h = h;
+                if (h > max_h) max_h = h;
+                if (w < min_w) min_w = w;
+                if (w > max_w) max_w = w;
+            }
+        }
+    if (!(min_h <= max_h && min_w <= max_w)) return -1; /* CV_Assert, template.cpp:124 */
+    min_w = min_w - 8 > 0 ? min_w - 8 : 0;
+    min_h = min_h - 8 > 0 ? min_h - 8 : 0;
+    max_w = max_w + 8 < W - 1 ? max_w + 8 : W - 1;
+    max_h = max_h + 8 < H - 1 ? max_h + 8 : H - 1;
+    if (use_roi) {
+        roi[0] = min_w; roi[1] = min_h; roi[2] = max_w + 1 - min_w; roi[3] = max_h + 1 - min_h;
+    } else {
+        roi[0] = 0; roi[1] = 0; roi[2] = W; roi[3] = H;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Fixed-point bilinear remap (imgproc/src/imgwarp.cpp)                                        */
+/* ------------------------------------------------------------------------------------------ */
+static short sat_s16_f(float v) {
+    int iv = (int)lrintf(v);
+    return (short)(iv < -32768 ? -32768 : iv > 32767 ? 32767 : iv);
+}
+
+void orc_bilinear_tab(int16_t out[1024 * 4]) {
+    /* initInterTab1D(INTER_LINEAR): coeffs {1-x, x}, x = i*(1/32) (imgwarp.cpp:146-150, 188-195) */
+    float tab1[32 * 2];
+    float scale = 1.f / 32;
+    for (int i = 0; i < 32; i++) { tab1[i * 2] = 1.f - i * scale; tab1[i * 2 + 1] = i * scale; }
+    /* flat table with slack: the sum fix-up of the last cell reads past the end (imgwarp.cpp:249-264) */
+    static short itab_buf[1024 * 4 + 8];
+    short* itab = itab_buf;
+    memset(itab_buf, 0, sizeof itab_buf);
+    const int ksize = 2;
+    for (int i = 0; i < 32; i++)
+        for (int j = 0; j < 32; j++, itab += ksize * ksize) {
+            int isum = 0;
+            for (int k1 = 0; k1 < ksize; k1++) {
+                float vy = tab1[i * ksize + k1];
+                for (int k2 = 0; k2 < ksize; k2++) {
+                    float v = vy * tab1[j * ksize + k2];
+                    isum += itab[k1 * ksize + k2] = sat_s16_f(v * 32768);
+                }
+            }
+            if (isum != 32768) {
+                int diff = isum - 32768;
+                int ksize2 = ksize / 2, Mk1 = ksize2, Mk2 = ksize2, mk1 = ksize2, mk2 = ksize2;
+                for (int k1 = ksize2; k1 < ksize2 + 2; k1++)
+                    for (int k2 = ksize2; k2 < ksize2 + 2; k2++) {
+                        if (itab[k1 * ksize + k2] < itab[mk1 * ksize + mk2]) mk1 = k1, mk2 = k2;
+                        else if (itab[k1 * ksize + k2] > itab[Mk1 * ksize + Mk2]) Mk1 = k1, Mk2 = k2;
+                    }
+                if (diff < 0) itab[Mk1 * ksize + Mk2] = (short)(itab[Mk1 * ksize + Mk2] - diff);
+                else itab[mk1 * ksize + mk2] = (short)(itab[mk1 * ksize + mk2] - diff);
+            }
+        }
+    memcpy(out, itab_buf, 1024 * 4 * sizeof(short));
+}
+
+static int16_t g_tab[1024 * 4];
+static pthread_once_t g_tab_once = PTHREAD_ONCE_INIT;
+static void init_tab(void) { orc_bilinear_tab(g_tab); }
+
+static inline int round_half_even_f(float v) { return (int)lrintf(v); }
+static inline short sat_s16_i(int v) { return (short)(v < -32768 ? -32768 : v > 32767 ? 32767 : v); }
+
+void orc_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, const float* map1, const float* map2,
+                  int mw, int mh, size_t mpitch, float scale_x, float scale_y, uint8_t* dst, size_t dpitch) {
+    pthread_once(&g_tab_once, init_tab);
+    for (int y = 0; y < mh; y++) {
+        const float* m1 = map1 + (size_t)y * mpitch;
+        const float* m2 = map2 + (size_t)y * mpitch;
+        uint8_t* d = dst + (size_t)y * dpitch;
+        for (int x = 0; x < mw; x++) {
+            float X = m1[x] * scale_x, Y = m2[x] * scale_y;
+            /* _mm_cvtps_epi32: out-of-range / NaN -> INT_MIN (RemapInvoker, imgwarp.cpp:4385-4420) */
+            float fx32 = X * 32.0f, fy32 = Y * 32.0f;
+            int ix = (fx32 != fx32 || fx32 >= 2147483648.f || fx32 < -2147483648.f) ? INT32_MIN : round_half_even_f(fx32);
+            int iy = (fy32 != fy32 || fy32 >= 2147483648.f || fy32 < -2147483648.f) ? INT32_MIN : round_half_even_f(fy32);
+            int sx = sat_s16_i(ix >> 5), sy = sat_s16_i(iy >> 5);
+            int a = ((iy & 31) << 5) | (ix & 31);
+            const int16_t* w = g_tab + a * 4;
+            for (int k = 0; k < cn; k++) {
+                int v[4];
+                for (int t = 0; t < 4; t++) {
+                    int tx = sx + (t & 1), ty = sy + (t >> 1);
+                    v[t] = (tx >= 0 && tx < sw && ty >= 0 && ty < sh) ? src[(size_t)ty * spitch + (size_t)tx * cn + k] : 0;
+                }
+                int acc = v[0] * w[0] + v[1] * w[1] + v[2] * w[2] + v[3] * w[3];
+                int r = (acc + (1 << 14)) >> 15;
+                d[(size_t)x * cn + k] = (uint8_t)(r < 0 ? 0 : r > 255 ? 255 : r);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* YUV420 <-> RGB (own BT.601 definition; NPP's arithmetic is closed and unpinned)             */
+/* ------------------------------------------------------------------------------------------ */
+static inline uint8_t sat_u8_rne(float v) {
+    if (!(v > 0.f)) return 0; /* also NaN */
+    if (v >= 255.f) return 255;
+    return (uint8_t)lrintf(v);
+}
+
+void orc_yuv420_to_rgba(const uint8_t* yuv, int w, int h, size_t pitch, uint8_t* rgba, size_t rgba_pitch) {
+    const uint8_t* U = yuv + (size_t)h * pitch;
+    const uint8_t* V = U + w / 2;
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            float Yf = (float)yuv[(size_t)y * pitch + x];
+            float Uf = (float)U[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
+            float Vf = (float)V[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
+            float R = Yf + 1.140f * Vf;
+            float G = Yf - 0.394f * Uf - 0.581f * Vf;
+            float B = Yf + 2.032f * Uf;
+            uint8_t* o = rgba + (size_t)y * rgba_pitch + (size_t)x * 4;
+            o[0] = sat_u8_rne(R);
+            o[1] = sat_u8_rne(G);
+            o[2] = sat_u8_rne(B);
+            o[3] = 255;
+        }
+}
+
+void orc_rgb_to_yuv420(const uint8_t* rgb, int w, int h, size_t rgb_pitch, int cn, uint8_t* yuv, size_t pitch) {
+    uint8_t* Uo = yuv + (size_t)h * pitch;
+    uint8_t* Vo = Uo + w / 2;
+    for (int y = 0; y < h; y += 2)
+        for (int x = 0; x < w; x += 2) {
+            float us = 0.f, vs = 0.f;
+            for (int dy = 0; dy < 2; dy++)
+                for (int dx = 0; dx < 2; dx++) {
+                    const uint8_t* p = rgb + (size_t)(y + dy) * rgb_pitch + (size_t)(x + dx) * cn;
+                    float R = p[0], G = p[1], B = p[2];
+                    float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
+                    yuv[(size_t)(y + dy) * pitch + x + dx] = sat_u8_rne(Yf);
+                    us = us + (0.492f * (B - Yf) + 128.f);
+                    vs = vs + (0.877f * (R - Yf) + 128.f);
+                }
+            Uo[(size_t)(y >> 1) * pitch + (x >> 1)] = sat_u8_rne(us * 0.25f);
+            Vo[(size_t)(y >> 1) * pitch + (x >> 1)] = sat_u8_rne(vs * 0.25f);
+        }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* cv::solve (core/src/lapack.cpp:1050-1275; LUImpl core/src/matrix_decomp.cpp:50-110)        */
+/* ------------------------------------------------------------------------------------------ */
+int orc_solve(const double* Ain, const double* bin, int n, double* x) {
+#define Sd(y, xx) Ain[(y) * n + (xx)]
+#define bd(y) bin[y]
+    if (n == 1) {
+        double d = Sd(0, 0);
+        if (d == 0.) return 0;
+        x[0] = bd(0) / d;
+        return 1;
+    }
+    if (n == 2) {
+        double d = (double)Sd(0, 0) * Sd(1, 1) - (double)Sd(0, 1) * Sd(1, 0);
+        if (d == 0.) return 0;
+        double t;
+        d = 1. / d;
+        t = (bd(0) * Sd(1, 1) - bd(1) * Sd(0, 1)) * d;
+        x[1] = (bd(1) * Sd(0, 0) - bd(0) * Sd(1, 0)) * d;
+        x[0] = t;
+        return 1;
+    }
+    if (n == 3) {
+        double d = Sd(0, 0) * ((double)Sd(1, 1) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 1)) -
+                   Sd(0, 1) * ((double)Sd(1, 0) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 0)) +
+                   Sd(0, 2) * ((double)Sd(1, 0) * Sd(2, 1) - (double)Sd(1, 1) * Sd(2, 0));
+        if (d == 0.) return 0;
+        d = 1. / d;
+        double t0 = ((Sd(1, 1) * Sd(2, 2) - Sd(1, 2) * Sd(2, 1)) * bd(0) + (Sd(0, 2) * Sd(2, 1) - Sd(0, 1) * Sd(2, 2)) * bd(1) +
+                     (Sd(0, 1) * Sd(1, 2) - Sd(0, 2) * Sd(1, 1)) * bd(2)) * d;
+        double t1 = ((Sd(1, 2) * Sd(2, 0) - Sd(1, 0) * Sd(2, 2)) * bd(0) + (Sd(0, 0) * Sd(2, 2) - Sd(0, 2) * Sd(2, 0)) * bd(1) +
+                     (Sd(0, 2) * Sd(1, 0) - Sd(0, 0) * Sd(1, 2)) * bd(2)) * d;
+        double t2 = ((Sd(1, 0) * Sd(2, 1) - Sd(1, 1) * Sd(2, 0)) * bd(0) + (Sd(0, 1) * Sd(2, 0) - Sd(0, 0) * Sd(2, 1)) * bd(1) +
+                     (Sd(0, 0) * Sd(1, 1) - Sd(0, 1) * Sd(1, 0)) * bd(2)) * d;
+        x[0] = t0; x[1] = t1; x[2] = t2;
+        return 1;
+    }
+#undef Sd
+#undef bd
+    double* A = (double*)malloc(sizeof(double) * n * n);
+    memcpy(A, Ain, sizeof(double) * n * n);
+    memcpy(x, bin, sizeof(double) * n);
+    double* b = x;
+    int i, j, k, m = n;
+    const double eps = DBL_EPSILON * 100;
+    for (i = 0; i < m; i++) {
+        k = i;
+        for (j = i + 1; j < m; j++)
+            if (fabs(A[j * m + i]) > fabs(A[k * m + i])) k = j;
+        if (fabs(A[k * m + i]) < eps) { free(A); return 0; }
+        if (k != i) {
+            for (j = i; j < m; j++) { double t = A[i * m + j]; A[i * m + j] = A[k * m + j]; A[k * m + j] = t; }
+            double t = b[i]; b[i] = b[k]; b[k] = t;
+        }
+        double d = -1 / A[i * m + i];
+        for (j = i + 1; j < m; j++) {
+            double alpha = A[j * m + i] * d;
+            for (k = i + 1; k < m; k++) A[j * m + k] += alpha * A[i * m + k];
+            b[j] += alpha * b[i];
+        }
+        A[i * m + i] = -d;
+    }
+    for (i = m - 1; i >= 0; i--) {
+        double s = b[i];
+        for (k = i + 1; k < m; k++) s -= A[i * m + k] * b[k];
+        b[i] = s * A[i * m + i];
+    }
+    free(A);
+    return 1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* CUDA resize kernels used on the gain path (cudawarping/src/cuda/resize.cu:57-103)            */
+/* ------------------------------------------------------------------------------------------ */
+static float resize_inv_scale(int d, int s) {
+    /* resize.cpp:82-83,105: fx = double(dsize)/src ; kernel gets (float)(1.0/fx) */
+    double f = (double)d / s;
+    return (float)(1.0 / f);
+}
+
+void orc_resize_nearest_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw, int dh,
+                           size_t dpitch) {
+    float fx = resize_inv_scale(dw, sw), fy = resize_inv_scale(dh, sh);
+    (void)sh;
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float sxf = x * fx, syf = y * fy;
+            int sx = (int)sxf, sy = (int)syf; /* __float2int_rz */
+            memcpy(dst + (size_t)y * dpitch + (size_t)x * cn, src + (size_t)sy * spitch + (size_t)sx * cn, cn);
+        }
+}
+
+/* resize_linear (resize.cu:71-103). nvcc contracts `out + src*w` into fmaf by default (-fmad=true);
+ * restated with explicit fmaf. */
+void orc_resize_linear_cuda_u8(const uint8_t* src, int sw, int sh, size_t spitch, uint8_t* dst, int dw, int dh,
+                               size_t dpitch) {
+    float fx = resize_inv_scale(dw, sw), fy = resize_inv_scale(dh, sh);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float src_x = x * fx, src_y = y * fy;
+            int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+            int x2 = x1 + 1, y2 = y1 + 1;
+            int x2r = x2 < sw - 1 ? x2 : sw - 1, y2r = y2 < sh - 1 ? y2 : sh - 1;
+            float out = 0.f;
+            out = fmaf((float)src[(size_t)y1 * spitch + x1], (x2 - src_x) * (y2 - src_y), out);
+            out = fmaf((float)src[(size_t)y1 * spitch + x2r], (src_x - x1) * (y2 - src_y), out);
+            out = fmaf((float)src[(size_t)y2r * spitch + x1], (x2 - src_x) * (src_y - y1), out);
+            out = fmaf((float)src[(size_t)y2r * spitch + x2r], (src_x - x1) * (src_y - y1), out);
+            dst[(size_t)y * dpitch + x] = sat_u8_rne(out);
+        }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Gain compensator (stitching/src/exposure_compensate.cpp:174-297; mapper.cpp:94-114)         */
+/* ------------------------------------------------------------------------------------------ */
+static void working_scale(int out_w, int out_h, double* ws) {
+    double s = sqrt(0.1 * 1e6 / ((double)out_w * out_h)); /* WORKING_MEGAPIX, mapper.cpp:43,94 */
+    *ws = s < 1.0 ? s : 1.0;
+}
+
+int orc_gain_feed(int n, const int* rois, const uint8_t* const* warped, const uint8_t* const* masks, int out_w,
+                  int out_h, double* gains) {
+    double ws;
+    working_scale(out_w, out_h, &ws);
+    int* wr = (int*)malloc(sizeof(int) * 4 * n);
+    uint8_t** smask = (uint8_t**)malloc(sizeof(void*) * n);
+    uint8_t** simg = (uint8_t**)malloc(sizeof(void*) * n);
+    float** norm = (float**)malloc(sizeof(void*) * n);
+    for (int i = 0; i < n; i++) {
+        const int* r = rois + 4 * i;
+        wr[4 * i + 0] = (int)(r[0] * ws);
+        wr[4 * i + 1] = (int)(r[1] * ws);
+        wr[4 * i + 2] = (int)(r[2] * ws);
+        wr[4 * i + 3] = (int)(r[3] * ws);
+        int w = wr[4 * i + 2], h = wr[4 * i + 3];
+        smask[i] = (uint8_t*)malloc((size_t)w * h + 1);
+        simg[i] = (uint8_t*)malloc((size_t)w * h * 4 + 1);
+        norm[i] = (float*)malloc(sizeof(float) * ((size_t)w * h + 1));
+        orc_resize_linear_cuda_u8(masks[i], r[2], r[3], r[2], smask[i], w, h, w);
+        orc_resize_nearest_u8(warped[i], r[2], r[3], (size_t)r[2] * 4, 4, simg[i], w, h, (size_t)w * 4);
+        for (size_t k = 0; k < (size_t)w * h; k++) {
+            const uint8_t* p = simg[i] + 4 * k;
+            int s = p[0] * p[0] + p[1] * p[1] + p[2] * p[2];
+            norm[i][k] = sqrtf((float)s);
+        }
+    }
+    int* N = (int*)calloc((size_t)n * n, sizeof(int));
+    double* I = (double*)calloc((size_t)n * n, sizeof(double));
+    for (int i = 0; i < n; i++) {
+        int w = wr[4 * i + 2], h = wr[4 * i + 3], nz = 0;
+        for (size_t k = 0; k < (size_t)w * h; k++) nz += smask[i][k] != 0;
+        N[i * n + i] = nz > 1 ? nz : 1;
+    }
+    for (int i = 0; i < n; i++)
+        for (int j = i + 1; j < n; j++) {
+            const int *a = wr + 4 * i, *b = wr + 4 * j;
+            int x0 = a[0] > b[0] ? a[0] : b[0], y0 = a[1] > b[1] ? a[1] : b[1];
+            int x1 = (a[0] + a[2]) < (b[0] + b[2]) ? (a[0] + a[2]) : (b[0] + b[2]);
+            int y1 = (a[1] + a[3]) < (b[1] + b[3]) ? (a[1] + a[3]) : (b[1] + b[3]);
+            int ow = x1 - x0, oh = y1 - y0;
+            if (ow <= 0 || oh <= 0) { /* cv::Rect & -> empty */
+                N[i * n + j] = N[j * n + i] = 1;
+                I[i * n + j] = I[j * n + i] = 0;
+                continue;
+            }
+            int nz = 0;
+            double s1 = 0, s2 = 0;
+            for (int yy = 0; yy < oh; yy++)
+                for (int xx = 0; xx < ow; xx++) {
+                    size_t ka = (size_t)(y0 + yy - a[1]) * a[2] + (x0 + xx - a[0]);
+                    size_t kb = (size_t)(y0 + yy - b[1]) * b[2] + (x0 + xx - b[0]);
+                    if ((smask[i][ka] & smask[j][kb]) != 0) {
+                        nz++;
+                        s1 += norm[i][ka];
+                        s2 += norm[j][kb];
+                    }
+                }
+            int nn = nz > 1 ? nz : 1;
+            N[i * n + j] = N[j * n + i] = nn;
+            I[i * n + j] = s1 / nn;
+            I[j * n + i] = s2 / nn;
+        }
+    double alpha = 0.01, beta = 100;
+    double* A = (double*)calloc((size_t)n * n, sizeof(double));
+    double* bb = (double*)calloc((size_t)n, sizeof(double));
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            bb[i] += beta * N[i * n + j];
+            A[i * n + i] += beta * N[i * n + j];
+            if (j == i) continue;
+            A[i * n + i] += 2 * alpha * I[i * n + j] * I[i * n + j] * N[i * n + j];
+            A[i * n + j] -= 2 * alpha * I[i * n + j] * I[j * n + i] * N[i * n + j];
+        }
+    int ok = orc_solve(A, bb, n, gains);
+    for (int i = 0; i < n; i++) { free(smask[i]); free(simg[i]); free(norm[i]); }
+    free(smask); free(simg); free(norm); free(wr); free(N); free(I); free(A); free(bb);
+    return ok ? 0 : -1;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* One Mapper::stitch frame, blend = 0 (mapper.cpp:193-312)                                    */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct {
+    const orc_frame* f;
+    int cam;
+    int y0, y1;
+    uint8_t* rgba;
+    uint8_t* warped;
+} remap_job;
+
+static void* remap_worker(void* arg) {
+    remap_job* j = (remap_job*)arg;
+    const orc_frame* f = j->f;
+    int i = j->cam;
+    const int* r = f->rois + 4 * i;
+    orc_remap_u8(j->rgba, f->in_w[i], f->in_h[i], (size_t)f->in_w[i] * 4, 4, f->map1[i] + (size_t)j->y0 * r[2],
+                 f->map2[i] + (size_t)j->y0 * r[2], r[2], j->y1 - j->y0, r[2], (float)f->in_w[i], (float)f->in_h[i],
+                 j->warped + (size_t)j->y0 * r[2] * 4, (size_t)r[2] * 4);
+    return NULL;
+}
+
+int orc_stitch_frame(const orc_frame* f) {
+    int n = f->n;
+    int T = f->threads > 0 ? f->threads : 1;
+    uint8_t** rgba = (uint8_t**)malloc(sizeof(void*) * n);
+    uint8_t** warped = (uint8_t**)malloc(sizeof(void*) * n);
+    int rb = f->row_begin, re = f->row_end;
+    if (re <= rb) { rb = 0; re = f->out_h; }
+    for (int i = 0; i < n; i++) {
+        const int* r = f->rois + 4 * i;
+        rgba[i] = (uint8_t*)malloc((size_t)f->in_w[i] * f->in_h[i] * 4);
+        warped[i] = (uint8_t*)malloc((size_t)r[2] * r[3] * 4);
+        orc_yuv420_to_rgba(f->in_yuv[i], f->in_w[i], f->in_h[i], f->in_pitch[i], rgba[i], (size_t)f->in_w[i] * 4);
+        /* rows of this ROI that the requested output band needs (all rows when estimating gains) */
+        int y0 = 0, y1 = r[3];
+        if (!(f->enable_gain && !f->gains_in && n > 1)) {
+            y0 = rb - r[1]; y1 = re - r[1];
+            if (y0 < 0) y0 = 0;
+            if (y1 > r[3]) y1 = r[3];
+            if (y1 < y0) y1 = y0;
+        }
+        memset(warped[i], 0, (size_t)r[2] * r[3] * 4);
+        int rows = y1 - y0;
+        pthread_t th[64];
+        remap_job jobs[64];
+        int nt = T > 64 ? 64 : T;
+        for (int t = 0; t < nt; t++) {
+            jobs[t].f = f; jobs[t].cam = i; jobs[t].rgba = rgba[i]; jobs[t].warped = warped[i];
+            jobs[t].y0 = y0 + (int)((long)rows * t / nt);
+            jobs[t].y1 = y0 + (int)((long)rows * (t + 1) / nt);
+            if (nt > 1) pthread_create(&th[t], NULL, remap_worker, &jobs[t]);
+            else remap_worker(&jobs[t]);
+        }
+        if (nt > 1) for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+    }
+    double* gains = (double*)malloc(sizeof(double) * n);
+    int use_gain = f->enable_gain && n > 1; /* mapper.cpp:78-82 */
+    if (use_gain) {
+        if (f->gains_in) memcpy(gains, f->gains_in, sizeof(double) * n);
+        else if (orc_gain_feed(n, f->rois, (const uint8_t* const*)warped, f->masks, f->out_w, f->out_h, gains) != 0)
+            for (int i = 0; i < n; i++) gains[i] = 1.0; /* cv::solve failure leaves gains_ undefined; use 1 */
+        /* GainCompensatorGPU::apply -> mul_scalar_with_mask (exposure_compensate.cu:15-30) */
+        for (int i = 0; i < n; i++) {
+            const int* r = f->rois + 4 * i;
+            float g = (float)gains[i];
+            for (size_t k = 0; k < (size_t)r[2] * r[3]; k++) {
+                if (f->masks[i][k] == 0) continue;
+                uint8_t* p = warped[i] + 4 * k;
+                for (int c = 0; c < 4; c++) p[c] = sat_u8_rne((float)p[c] * g);
+            }
+        }
+    } else {
+        for (int i = 0; i < n; i++) gains[i] = 1.0;
+    }
+    if (f->gains_out) memcpy(f->gains_out, gains, sizeof(double) * n);
+    /* result = 0 ; RGBA2RGB + copyTo(result(roi), mask) in camera order (mapper.cpp:153-156,268-277) */
+    size_t W = (size_t)f->out_w;
+    uint8_t* result = (uint8_t*)calloc(W * f->out_h * 3, 1);
+    for (int i = 0; i < n; i++) {
+        const int* r = f->rois + 4 * i;
+        for (int y = 0; y < r[3]; y++) {
+            int oy = r[1] + y;
+            if (oy < rb || oy >= re) continue;
+            for (int x = 0; x < r[2]; x++) {
+                size_t k = (size_t)y * r[2] + x;
+                if (f->masks[i][k] == 0) continue;
+                uint8_t* o = result + ((size_t)oy * W + r[0] + x) * 3;
+                const uint8_t* p = warped[i] + 4 * k;
+                o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+            }
+        }
+    }
+    /* cvtRGB24toYUV420P (mapper.cpp:296-306): only the requested rows (row band is even-aligned) */
+    int ob = rb & ~1, oe = (re + 1) & ~1;
+    if (oe > f->out_h) oe = f->out_h;
+    {
+        /* convert band [ob, oe) into the output layout */
+        uint8_t* Uo = f->out_yuv + (size_t)f->out_h * f->out_pitch;
+        uint8_t* Vo = Uo + f->out_w / 2;
+        for (int y = ob; y < oe; y += 2)
+            for (int x = 0; x < f->out_w; x += 2) {
+                float us = 0.f, vs = 0.f;
+                for (int dy = 0; dy < 2; dy++)
+                    for (int dx = 0; dx < 2; dx++) {
+                        const uint8_t* p = result + ((size_t)(y + dy) * W + x + dx) * 3;
+                        float R = p[0], G = p[1], B = p[2];
+                        float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
+                        f->out_yuv[(size_t)(y + dy) * f->out_pitch + x + dx] = sat_u8_rne(Yf);
+                        us = us + (0.492f * (B - Yf) + 128.f);
+                        vs = vs + (0.877f * (R - Yf) + 128.f);
+                    }
+                Uo[(size_t)(y >> 1) * f->out_pitch + (x >> 1)] = sat_u8_rne(us * 0.25f);
+                Vo[(size_t)(y >> 1) * f->out_pitch + (x >> 1)] = sat_u8_rne(vs * 0.25f);
+            }
+    }
+    for (int i = 0; i < n; i++) { free(rgba[i]); free(warped[i]); }
+    free(rgba); free(warped); free(gains); free(result);
+    return 0;
+}

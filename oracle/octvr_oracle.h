@@ -1,0 +1,113 @@
+/*
+ * octvr_oracle.h — CPU restatement of the reference octVR hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the checker for the HIP product path
+ * (opencv-octvr_amd/) and the timed "cpu_baseline" leg of bench.py.  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline may load it; the product never links it.
+ *
+ * Every function cites the reference file:line (paths relative to the blahgeek/OpenCV-octVR root)
+ * whose arithmetic it restates.  Parity pinning: tests/golden/ (generated from the reference by
+ * oracle/golden_gen/) — see DESIGN.md "Oracle".
+ */
+#ifndef OCTVR_ORACLE_H
+#define OCTVR_ORACLE_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { ORC_EQUIRECT = 0, ORC_FULLFRAME_FISHEYE = 1, ORC_FISHEYE = 2 };
+
+typedef struct {
+    int type;
+    double R[9];      /* rotate_matrix, camera.cpp:57-70 */
+    double Rinv[9];   /* rotate_matrix.inv(), camera.cpp:205 */
+    double min_lon, max_lon;           /* longitude_selection, camera.cpp:125-135 */
+    /* equirectangular.hpp:61-62 */
+    double min_lat, max_lat, scale_lon;
+    /* fullframe_fisheye_cam.cpp:105-140 */
+    int width, height;
+    int crop_x, crop_y, crop_w, crop_h, crop_circular;
+    double hfov, center_dx, center_dy;
+    double rad[6];
+    /* pinhole_cam.cpp:13-30 (OpenCV fisheye model) */
+    double fx, fy, cx, cy, k[4];
+} orc_camera;
+
+/* Type initialisers reset rotation to identity and longitude range to [-pi, pi]; call
+ * orc_camera_set_rotation / set min_lon,max_lon afterwards.
+ * Camera::Camera rotation part (camera.cpp:49-70): R = (Rx*Rz)*Ry from (roll, -yaw, -pitch)
+ * via Rodrigues (calib3d/src/calibration.cpp:252-345); Rinv by lapack.cpp invert 3x3 closed form. */
+void orc_rotation_rpy(double roll, double yaw, double pitch, double R[9]);
+void orc_invert3(const double* A, double* out);
+void orc_camera_set_rotation(orc_camera* c, const double R[9]);
+
+void orc_camera_equirect(orc_camera* c, double min_lat, double max_lat, double scale_lon);
+void orc_camera_fullframe_fisheye(orc_camera* c, int width, int height, int crop_l, int crop_r, int crop_t,
+                                  int crop_b, int has_crop, int crop_circular, double hfov, double center_dx,
+                                  double center_dy, const double radial[3]);
+void orc_camera_fisheye(orc_camera* c, int width, int height, double fx, double fy, double cx, double cy,
+                        const double k[4]);
+
+/* MapperTemplate::add_input LUT loop (template.cpp:46-133) for one input camera.
+ * map1/map2/mask are FULL output-size buffers (W*H); roi[4] = x,y,w,h (±8 pad, or full if !use_roi). */
+int orc_lut_build(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
+                  uint8_t* mask, int use_roi, int roi[4]);
+
+/* initInterTab2D(INTER_LINEAR, fixpt) incl. its sum fix-up quirk (imgproc/src/imgwarp.cpp:211-280). */
+void orc_bilinear_tab(int16_t tab[1024 * 4]);
+
+/* cv::remap INTER_LINEAR, BORDER_CONSTANT 0, u8 with cn channels (imgwarp.cpp:3812-4030, 4246-4497).
+ * X = fl32(map1 * scale_x), Y = fl32(map2 * scale_y) (the caller's `map*W`, template.cpp:174-176). */
+void orc_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, const float* map1, const float* map2,
+                  int mw, int mh, size_t mpitch_elems, float scale_x, float scale_y, uint8_t* dst, size_t dpitch);
+
+/* Own BT.601 definitions standing in for NPP nppiYUV420ToRGB / nppiRGBToYUV420 (parity unpinned,
+ * cudaimgproc/src/color.cpp:2269,2306).  Layout "Y over [U|V]" of mapper.hpp:432-440. */
+void orc_yuv420_to_rgba(const uint8_t* yuv, int w, int h, size_t pitch, uint8_t* rgba, size_t rgba_pitch);
+void orc_rgb_to_yuv420(const uint8_t* rgb, int w, int h, size_t rgb_pitch, int rgb_cn, uint8_t* yuv, size_t pitch);
+
+/* cv::solve DECOMP_LU for doubles (core/src/lapack.cpp:1050-1275, matrix_decomp.cpp:50-110). */
+int orc_solve(const double* A, const double* b, int n, double* x);
+
+/* Gain compensator feed (GainCompensatorGPU, stitching/src/exposure_compensate.cpp:174-297 + mapper.cpp:94-114,
+ * 234-237).  warped[i]: ROI-sized u8x4 (pitch = roi_w*4), masks[i]: ROI-sized u8 LUT masks. */
+int orc_gain_feed(int n, const int* rois, const uint8_t* const* warped, const uint8_t* const* masks, int out_w,
+                  int out_h, double* gains_out);
+
+/* One Mapper::stitch frame, blend=0 (mapper.cpp:193-312): YUV420 in -> YUV420 out, optional gain.
+ * gains_in may be NULL (estimate) ; gains_out receives the gains used (may be NULL). */
+typedef struct {
+    int n;
+    const int* in_w;
+    const int* in_h;
+    const uint8_t* const* in_yuv;
+    const size_t* in_pitch;
+    const int* rois;                 /* n*4 */
+    const float* const* map1;        /* ROI-sized, normalized */
+    const float* const* map2;
+    const uint8_t* const* masks;     /* ROI-sized LUT masks */
+    int out_w, out_h;
+    uint8_t* out_yuv;
+    size_t out_pitch;
+    int enable_gain;
+    const double* gains_in;
+    double* gains_out;
+    int threads;
+    int row_begin, row_end;          /* restrict composite+output to a row band (cpu_baseline sample); 0,0 = all */
+} orc_frame;
+int orc_stitch_frame(const orc_frame* f);
+
+/* K13/K14 CUDA resize semantics used by the gain path (cudawarping/src/cuda/resize.cu:57-103). */
+void orc_resize_nearest_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw, int dh,
+                           size_t dpitch);
+void orc_resize_linear_cuda_u8(const uint8_t* src, int sw, int sh, size_t spitch, uint8_t* dst, int dw, int dh,
+                               size_t dpitch);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,287 @@
+"""ctypes bindings to oracle/liboctvr_oracle.so (TEST INFRASTRUCTURE ONLY).
+
+The oracle is the CPU restatement of the reference arithmetic; tests use it as the checker for the
+HIP product path.  Rig JSON follows the reference schema.
+"""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+_LIB = None
+
+
+class OrcCamera(C.Structure):
+    _fields_ = [
+        ("type", C.c_int),
+        ("R", C.c_double * 9),
+        ("Rinv", C.c_double * 9),
+        ("min_lon", C.c_double), ("max_lon", C.c_double),
+        ("min_lat", C.c_double), ("max_lat", C.c_double), ("scale_lon", C.c_double),
+        ("width", C.c_int), ("height", C.c_int),
+        ("crop_x", C.c_int), ("crop_y", C.c_int), ("crop_w", C.c_int), ("crop_h", C.c_int),
+        ("crop_circular", C.c_int),
+        ("hfov", C.c_double), ("center_dx", C.c_double), ("center_dy", C.c_double),
+        ("rad", C.c_double * 6),
+        ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
+        ("k", C.c_double * 4),
+    ]
+
+
+class OrcFrame(C.Structure):
+    _fields_ = [
+        ("n", C.c_int),
+        ("in_w", C.POINTER(C.c_int)),
+        ("in_h", C.POINTER(C.c_int)),
+        ("in_yuv", C.POINTER(C.c_void_p)),
+        ("in_pitch", C.POINTER(C.c_size_t)),
+        ("rois", C.POINTER(C.c_int)),
+        ("map1", C.POINTER(C.c_void_p)),
+        ("map2", C.POINTER(C.c_void_p)),
+        ("masks", C.POINTER(C.c_void_p)),
+        ("out_w", C.c_int), ("out_h", C.c_int),
+        ("out_yuv", C.c_void_p),
+        ("out_pitch", C.c_size_t),
+        ("enable_gain", C.c_int),
+        ("gains_in", C.POINTER(C.c_double)),
+        ("gains_out", C.POINTER(C.c_double)),
+        ("threads", C.c_int),
+        ("row_begin", C.c_int), ("row_end", C.c_int),
+    ]
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        so = os.path.join(ORACLE_DIR, "liboctvr_oracle.so")
+        src = os.path.join(ORACLE_DIR, "octvr_oracle.c")
+        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = C.CDLL(so)
+        L.orc_lut_build.restype = C.c_int
+        L.orc_solve.restype = C.c_int
+        L.orc_gain_feed.restype = C.c_int
+        L.orc_stitch_frame.restype = C.c_int
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def rotation_rpy(roll, yaw, pitch):
+    R = (C.c_double * 9)()
+    lib().orc_rotation_rpy(C.c_double(roll), C.c_double(yaw), C.c_double(pitch), R)
+    return np.array(R[:]).reshape(3, 3)
+
+
+def invert3(R):
+    a = np.ascontiguousarray(R, dtype=np.float64).reshape(9)
+    out = np.zeros(9)
+    lib().orc_invert3(_p(a), _p(out))
+    return out.reshape(3, 3)
+
+
+def camera_from_json(cam):
+    """Build an orc_camera from one {type, options} entry (camera.cpp:27-136)."""
+    t, o = cam["type"], cam.get("options", {})
+    c = OrcCamera()
+    L = lib()
+    if t == "equirectangular":
+        import math
+        L.orc_camera_equirect(C.byref(c), C.c_double(o.get("min_lat", -math.pi / 2)),
+                              C.c_double(o.get("max_lat", math.pi / 2)), C.c_double(o.get("scale_lon", 1.0)))
+    elif t == "fullframe_fisheye":
+        crop = o.get("crop")
+        rect = crop["rect"] if crop else [0, 0, 0, 0]
+        rad = (C.c_double * 3)(*o["radial"])
+        L.orc_camera_fullframe_fisheye(C.byref(c), o["width"], o["height"], rect[0], rect[1], rect[2], rect[3],
+                                       1 if crop else 0, 1 if (crop and crop["is_circular"]) else 0,
+                                       C.c_double(o["hfov"]), C.c_double(o["center_dx"]), C.c_double(o["center_dy"]),
+                                       rad)
+    elif t == "fisheye":
+        k = (C.c_double * 4)(*o["dist_coeffs"][:4])
+        L.orc_camera_fisheye(C.byref(c), o["width"], o["height"], C.c_double(o["fx"]), C.c_double(o["fy"]),
+                             C.c_double(o["cx"]), C.c_double(o["cy"]), k)
+    else:
+        raise ValueError("camera type not in the oracle: " + t)
+    if "rotation" in o:
+        r = o["rotation"]
+        R = rotation_rpy(r["roll"], r["yaw"], r["pitch"])
+    else:
+        R = rotation_rpy(0, 0, 0)
+    if "rotation_matrix" in o:
+        R = np.array(o["rotation_matrix"], dtype=np.float64).reshape(3, 3)
+    Rc = (C.c_double * 9)(*R.reshape(9))
+    L.orc_camera_set_rotation(C.byref(c), Rc)
+    if "longitude_selection" in o:
+        c.min_lon, c.max_lon = o["longitude_selection"]
+    return c
+
+
+def lut_build(rig, out_w, out_h, use_roi=True):
+    """Per input: (roi, map1, map2, mask) cropped to the ROI, as MapperTemplate::add_input."""
+    out = camera_from_json(rig["output"])
+    res = []
+    for cam in rig["inputs"]:
+        c = camera_from_json(cam)
+        m1 = np.empty((out_h, out_w), np.float32)
+        m2 = np.empty((out_h, out_w), np.float32)
+        mk = np.empty((out_h, out_w), np.uint8)
+        roi = (C.c_int * 4)()
+        rc = lib().orc_lut_build(C.byref(out), C.byref(c), out_w, out_h, _p(m1), _p(m2), _p(mk), int(use_roi), roi)
+        assert rc == 0
+        x, y, w, h = roi[:]
+        res.append(((x, y, w, h), m1[y:y + h, x:x + w].copy(), m2[y:y + h, x:x + w].copy(), mk[y:y + h, x:x + w].copy()))
+    return res
+
+
+def remap_u8(src, map1, map2, scale_x, scale_y):
+    src = np.ascontiguousarray(src)
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    h, w = src.shape[:2]
+    mh, mw = map1.shape
+    m1 = np.ascontiguousarray(map1, np.float32)
+    m2 = np.ascontiguousarray(map2, np.float32)
+    dst = np.zeros((mh, mw, cn) if cn > 1 else (mh, mw), np.uint8)
+    lib().orc_remap_u8(_p(src), w, h, C.c_size_t(w * cn), cn, _p(m1), _p(m2), mw, mh, C.c_size_t(mw),
+                       C.c_float(scale_x), C.c_float(scale_y), _p(dst), C.c_size_t(mw * cn))
+    return dst
+
+
+def bilinear_tab():
+    t = np.zeros(4096, np.int16)
+    lib().orc_bilinear_tab(_p(t))
+    return t.reshape(1024, 4)
+
+
+def solve(A, b):
+    A = np.ascontiguousarray(A, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.zeros_like(b)
+    ok = lib().orc_solve(_p(A), _p(b), len(b), _p(x))
+    return x if ok else None
+
+
+def yuv420_to_rgba(yuv, w, h):
+    out = np.zeros((h, w, 4), np.uint8)
+    yuv = np.ascontiguousarray(yuv)
+    lib().orc_yuv420_to_rgba(_p(yuv), w, h, C.c_size_t(yuv.shape[1]), _p(out), C.c_size_t(w * 4))
+    return out
+
+
+def rgb_to_yuv420(rgb):
+    h, w, cn = rgb.shape
+    out = np.zeros((h * 3 // 2, w), np.uint8)
+    rgb = np.ascontiguousarray(rgb)
+    lib().orc_rgb_to_yuv420(_p(rgb), w, h, C.c_size_t(w * cn), cn, _p(out), C.c_size_t(w))
+    return out
+
+
+def gain_feed(rois, warped, masks, out_w, out_h):
+    n = len(rois)
+    r = np.ascontiguousarray(np.array(rois, np.int32).reshape(-1))
+    warped = [np.ascontiguousarray(a) for a in warped]
+    masks = [np.ascontiguousarray(a) for a in masks]
+    wp = (C.c_void_p * n)(*[a.ctypes.data for a in warped])
+    mp = (C.c_void_p * n)(*[a.ctypes.data for a in masks])
+    g = np.zeros(n)
+    rc = lib().orc_gain_feed(n, r.ctypes.data_as(C.POINTER(C.c_int)), wp, mp, out_w, out_h, _p(g))
+    assert rc == 0
+    return g
+
+
+def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enable_gain=True, gains=None,
+                 threads=1, row_band=None):
+    n = len(in_yuv)
+    keep = []
+
+    def arr(t, vals):
+        a = (t * len(vals))(*vals)
+        keep.append(a)
+        return a
+
+    in_yuv = [np.ascontiguousarray(a) for a in in_yuv]
+    map1s = [np.ascontiguousarray(a, np.float32) for a in map1s]
+    map2s = [np.ascontiguousarray(a, np.float32) for a in map2s]
+    masks = [np.ascontiguousarray(a, np.uint8) for a in masks]
+    out = np.zeros((out_h * 3 // 2, out_w), np.uint8)
+    gout = np.zeros(n)
+    f = OrcFrame()
+    f.n = n
+    f.in_w = arr(C.c_int, [s[0] for s in in_sizes])
+    f.in_h = arr(C.c_int, [s[1] for s in in_sizes])
+    f.in_yuv = arr(C.c_void_p, [a.ctypes.data for a in in_yuv])
+    f.in_pitch = arr(C.c_size_t, [a.shape[1] for a in in_yuv])
+    f.rois = arr(C.c_int, [v for r in rois for v in r])
+    f.map1 = arr(C.c_void_p, [a.ctypes.data for a in map1s])
+    f.map2 = arr(C.c_void_p, [a.ctypes.data for a in map2s])
+    f.masks = arr(C.c_void_p, [a.ctypes.data for a in masks])
+    f.out_w, f.out_h = out_w, out_h
+    f.out_yuv = out.ctypes.data
+    f.out_pitch = out_w
+    f.enable_gain = int(enable_gain)
+    gin = None
+    if gains is not None:
+        gin = np.ascontiguousarray(gains, np.float64)
+        f.gains_in = gin.ctypes.data_as(C.POINTER(C.c_double))
+    f.gains_out = gout.ctypes.data_as(C.POINTER(C.c_double))
+    f.threads = threads
+    if row_band:
+        f.row_begin, f.row_end = row_band
+    rc = lib().orc_stitch_frame(C.byref(f))
+    assert rc == 0
+    return out, gout
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic data (same generator as oracle/golden_gen/gen_golden.cpp)
+# ---------------------------------------------------------------------------------------------
+def splitmix64(seed, k):
+    """k-th output (k = 0, 1, ...) of splitmix64 seeded with `seed`, vectorised over k."""
+    k = np.asarray(k, dtype=np.uint64) + np.uint64(1)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def splitmix_bytes(seed, n):
+    k = np.arange(1, n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0xFF)).astype(np.uint8)
+
+
+def rand_img(w, h, cn, seed):
+    a = splitmix_bytes(seed, w * h * cn)
+    return a.reshape((h, w, cn) if cn > 1 else (h, w))
+
+
+def remap_kat_maps(per=256):
+    """Maps of gen_golden.cpp remap_code_kat(): 256 random integer positions per fractional code."""
+    k = np.arange(1024 * per, dtype=np.uint64)
+    h = splitmix64(2718, k)
+    sx = (h % np.uint64(63)).astype(np.float32)
+    sy = ((h >> np.uint64(16)) % np.uint64(63)).astype(np.float32)
+    code = (k // np.uint64(per)).astype(np.int64)
+    m1 = sx + (code & 31).astype(np.float32) / np.float32(32)
+    m2 = sy + (code >> 5).astype(np.float32) / np.float32(32)
+    return m1.reshape(1, -1).astype(np.float32), m2.reshape(1, -1).astype(np.float32)
+
+
+def load_rig(name):
+    gdir = os.path.join(ROOT, "tests", "golden")
+    with open(os.path.join(gdir, name + ".json")) as f:
+        rig = json.load(f)
+    z = np.load(os.path.join(gdir, name + ".npz"))
+    return rig, z
