@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""bench.py — stitched megapixels/s of the octVR remap + gain + composite path on MI355X.
+
+Workload (BASELINE.json configs[1], SURVEY.md §8d "C2"): 6 x 3840x2160 fullframe_fisheye YUV420P
+frames -> 7680x3840 equirectangular YUV420P, per-frame gain estimation (GainCompensatorGPU::feed +
+apply) and the no-blend composite (mapper.cpp:193-312).  A step = one Mapper::stitch of one frame
+set, inputs and outputs resident in HBM.  Multi-GPU: one process per GPU, each stitches its own
+independent rig (rigs shard with no collective) -> "scaling": "weak".
+
+Prints ONE JSON line on rank 0.  Extra objects: "roofline" (the composite kernel, HIP-event timed
+live over the timed region) and "cpu_baseline" (the oracle restatement of the reference CPU path,
+timed on this host).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu-baseline]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "opencv-octvr_amd"))
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads():
+    n = os.environ.get("OMP_NUM_THREADS")
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
+    return max(1, min(int(n) if n else avail, avail, 64))
+
+
+def cpu_baseline(mt, frames_np, sizes, W, H):
+    """The reference CPU path restated by the oracle (YUV->RGBA, fixed-point cv::remap of every
+    camera over its full ROI, gain feed + apply, copyTo(mask), RGB->YUV420P) on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as O  # test infrastructure: used only as the timed CPU baseline
+    rois, m1s, m2s, masks = [], [], [], []
+    for i in range(len(sizes)):
+        roi, m1, m2, mk, _ = mt.input(i)
+        rois.append(roi); m1s.append(m1); m2s.append(m2); masks.append(mk)
+    T = host_threads()
+    t0 = time.perf_counter()
+    O.stitch_frame(frames_np, sizes, rois, m1s, m2s, masks, W, H, enable_gain=True, gains=None, threads=T)
+    dt = time.perf_counter() - t0
+    return {"value": round(W * H / 1e6 / dt, 3), "unit": "MP/s", "cores": T, "kind": "port",
+            "sample": "one full %dx%d frame (%d cameras, gain estimated) through oracle/octvr_oracle.c, %.2f s, "
+                      "host CPU: %s" % (W, H, len(sizes), dt, cpu_model())}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import octvr_amd as ox
+    from octvr_amd import synthetic
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        # no data-path collective: gloo carries only the barrier and the max-over-ranks time
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+    dev = local_rank
+
+    rig, W, H, sizes = synthetic.CONFIGS[args.config]()
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=True, device=dev)
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True, device=dev)
+    # each rank stitches an independent rig instance: frames seeded by (rank, camera)
+    frames_np = [synthetic.yuv_frame(w, h, 1000 * (rank + 1) + i) for i, (w, h) in enumerate(sizes)]
+    frames = [torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]
+    out = torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}")
+    stream = torch.cuda.current_stream(dev)
+
+    if args.pmc_child:  # a few launches for rocprofv3 --pmc passes
+        for _ in range(max(args.steps, 1)):
+            m.stitch(frames, out, stream=stream)
+        torch.cuda.synchronize(dev)
+        return
+
+    for _ in range(args.warmup):
+        m.stitch(frames, out, stream=stream)
+    torch.cuda.synchronize(dev)
+    m.kernel_time()  # drop anything recorded before the timed region
+    m.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m.stitch(frames, out, stream=stream)
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    m.set_timing(False)
+    kern_ms, launches = m.kernel_time()
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+
+    gains = m.gains()
+    frame_px = W * H
+    value = world * args.steps * frame_px / 1e6 / elapsed
+    bytes_per_launch = m.traffic_bytes()
+    avg_kernel_s = kern_ms / 1e3 / max(launches, 1)
+    achieved = bytes_per_launch / avg_kernel_s / 1e9
+    n_valid = 0
+    for i in range(len(sizes)):
+        n_valid += int((mt.input(i)[3] > 0).sum())
+    survey_b_alg = 1.5 * sum(w * h for w, h in sizes) + 9.0 * n_valid + 1.5 * frame_px
+
+    result = {
+        "metric": "stitched megapixels/sec (6x4K->8K equirect)",
+        "value": round(value, 1),
+        "unit": "MP/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 YUV420P frames, SURVEY.md §8d rig)",
+        "config": {"workload": "%s: %d x %dx%d fullframe_fisheye -> %dx%d equirect, remap + gain (estimated per "
+                               "frame) + no-blend composite, YUV420P in/out" % (
+                                   args.config, len(sizes), sizes[0][0], sizes[0][1], W, H),
+                   "rigs_per_gpu": 1, "parallelism": "independent rig per GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "kernel": "stitch_kernel", "kernel_us": round(avg_kernel_s * 1e6, 2),
+                     "bytes_per_launch": bytes_per_launch,
+                     "survey_b_alg_bytes": survey_b_alg,
+                     "survey_b_alg_frac_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "gains": [round(g, 6) for g in gains],
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

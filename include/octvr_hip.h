@@ -1,0 +1,120 @@
+/*
+ * octvr_hip.h — C ABI of the MI355X-native octVR stitching path (remap + gain + seam composite).
+ *
+ * This is the drop-in boundary for the reference's octvr per-frame path.  Each entry point names
+ * the reference interface it replaces (paths relative to the blahgeek/OpenCV-octVR root):
+ *
+ *   octvr_rig_*      <- vr::MapperTemplate           modules/octvr/include/octvr.hpp:47-91,
+ *                                                     modules/octvr/src/template.cpp:23-322
+ *   octvr_mapper_*   <- vr::Mapper                   modules/octvr/src/mapper.hpp:386-452,
+ *                                                     modules/octvr/src/mapper.cpp:47-323
+ *   octvr_remap_*    <- cv::remap INTER_LINEAR u8    modules/imgproc/src/imgwarp.cpp:4689-4828
+ *
+ * Conventions: no exceptions cross the boundary; every call returns an int status
+ * (OCTVR_OK = 0, negative = error, message via octvr_last_error()).  Pointers named *_dev are HIP
+ * device pointers; `stream` is a hipStream_t (NULL = the legacy default stream).  A rig owns host
+ * memory; a mapper owns device memory on one device and is not thread-safe.  Separate mappers on
+ * separate devices are independent (the multi-GPU model: one rig per GPU).
+ */
+#ifndef OCTVR_HIP_H
+#define OCTVR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OCTVR_HIP_ABI_VERSION 1
+
+enum {
+    OCTVR_OK = 0,
+    OCTVR_E_INVALID = -1,   /* bad argument / shape (reference: CV_Assert) */
+    OCTVR_E_PARSE = -2,     /* bad JSON or .dat (reference: throw std::string) */
+    OCTVR_E_HIP = -3,       /* HIP runtime failure */
+    OCTVR_E_UNSUPPORTED = -4,
+    OCTVR_E_IO = -5
+};
+
+typedef struct octvr_rig octvr_rig;
+typedef struct octvr_mapper octvr_mapper;
+
+/* One input of a MapperTemplate (octvr.hpp:55-61): ROI in output pixels, ROI-sized maps
+ * (normalized x/W_in, y/H_in, or -1), ROI-sized LUT mask {0,255} and seam mask (may be NULL). */
+typedef struct {
+    int roi_x, roi_y, roi_w, roi_h;
+    const float* map1;
+    const float* map2;
+    const uint8_t* mask;
+    const uint8_t* seam_mask;
+    const float* vignette;     /* 512x512 f32 or NULL (vignette.cpp:39-54) */
+    int vignette_w, vignette_h;
+} octvr_input_view;
+
+int octvr_abi_version(void);
+const char* octvr_last_error(void);
+int octvr_device_count(int* count);
+
+/* ---- device memory helpers (for C/C++ callers without their own allocator) ------------------- */
+int octvr_dev_malloc(int device, size_t bytes, void** ptr);
+int octvr_dev_free(void* ptr);
+int octvr_memcpy_h2d(void* dst_dev, const void* src_host, size_t bytes);
+int octvr_memcpy_d2h(void* dst_host, const void* src_dev, size_t bytes);
+int octvr_stream_sync(void* stream);
+
+/* ---- vr::MapperTemplate -------------------------------------------------------------------- */
+/* MapperTemplate(to, to_opts, w, h) + add_input(..., use_roi) for every entry of `inputs`
+ * (template.cpp:23-153, apps/octvr/dump.cpp:76-93).  The projection LUT is built on `device`
+ * by a gfx950 FP64 kernel.  out_w/out_h <= 0 derive from the output aspect ratio (template.cpp:32-38).
+ * Seam masks are NOT built here (see octvr_rig_create_masks). */
+int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, int device, octvr_rig** rig);
+/* MapperTemplate(std::ifstream&) — VRv11 reader (template.cpp:258-314). */
+int octvr_rig_load_dat(const char* path, octvr_rig** rig);
+/* MapperTemplate::dump — VRv11 writer, byte-compatible (template.cpp:206-256).  Requires seam masks. */
+int octvr_rig_dump_dat(const octvr_rig* rig, const char* path);
+/* Build a rig from caller arrays (ROI-sized maps/masks, row-major, tightly packed). */
+int octvr_rig_create_from_arrays(int out_w, int out_h, int n_inputs, const int* rois, const float* const* map1,
+                                 const float* const* map2, const uint8_t* const* masks,
+                                 const uint8_t* const* seam_masks_or_null, octvr_rig** rig);
+int octvr_rig_num_inputs(const octvr_rig* rig, int* n);
+int octvr_rig_out_size(const octvr_rig* rig, int* w, int* h);
+int octvr_rig_get_input(const octvr_rig* rig, int i, octvr_input_view* view);
+void octvr_rig_destroy(octvr_rig* rig);
+
+/* ---- vr::Mapper ---------------------------------------------------------------------------- */
+/* Mapper(mt, in_sizes, blend, enable_gain, scale_output) (mapper.cpp:47-191).
+ * blend: 0 = no blend (composite by LUT mask, later input wins; mapper.cpp:268-277).
+ * (blend > 0 multi-band and blend < 0 feather return OCTVR_E_UNSUPPORTED in this ABI version.)
+ * scale_w/scale_h: 0 = output at template size. */
+int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
+                        int enable_gain, int scale_w, int scale_h, octvr_mapper** mapper);
+/* Mapper::stitch (mapper.cpp:193-323) on device-resident YUV420P frames in the "Y over [U|V]"
+ * layout of mapper.hpp:432-440: rows [0,H) = Y (W bytes), rows [H, 3H/2) = U in bytes [0, W/2) and
+ * V in bytes [W/2, W) of each row; `pitch` = bytes per row (>= W).  gains: NULL = estimate
+ * (GainCompensatorGPU::feed), else set_gains (n_gains == n_inputs).  Stream-ordered, no host sync. */
+int octvr_mapper_stitch_yuv420p(octvr_mapper* mapper, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream);
+/* Mapper::gains() (mapper.hpp:445-447): gains used by the last stitch (synchronizes the stream). */
+int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
+/* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 8 B LUT +
+ * 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each source frame read once). */
+int octvr_mapper_traffic(const octvr_mapper* mapper, double* bytes_per_frame);
+/* Live per-kernel timing for roofline accounting: while enabled, every stitch brackets its main
+ * (composite) kernel with HIP events on the caller's stream.  kernel_time synchronizes on the
+ * recorded events, returns the summed device time and launch count, and resets the log. */
+int octvr_mapper_set_timing(octvr_mapper* mapper, int enable);
+int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launches);
+void octvr_mapper_destroy(octvr_mapper* mapper);
+
+/* ---- standalone kernels --------------------------------------------------------------------- */
+/* cv::remap(src, dst, map1*sx, map2*sy, INTER_LINEAR, BORDER_CONSTANT) on u8 with cn in {1,3,4}
+ * channels: 5-bit coordinates, 15-bit weights (imgwarp.cpp:211-280, 3812-4030, 4246-4497). */
+int octvr_remap_u8(const uint8_t* src_dev, int sw, int sh, size_t spitch, int cn, const float* map1_dev,
+                   const float* map2_dev, int mw, int mh, size_t mpitch_elems, float scale_x, float scale_y,
+                   uint8_t* dst_dev, size_t dpitch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

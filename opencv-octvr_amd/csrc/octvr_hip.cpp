@@ -1,0 +1,980 @@
+// octvr_hip.cpp — C ABI (include/octvr_hip.h): rig (vr::MapperTemplate) and mapper (vr::Mapper).
+//
+// Host orchestration only; all per-pixel work runs in kernels.hip.  Exceptions never cross the
+// boundary: every entry point converts them into a status code + octvr_last_error().
+#include "octvr_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <memory>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "camera_math.hpp"
+#include "json_lite.hpp"
+#include "kernels.hpp"
+
+using namespace octvr;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct OctvrError : std::runtime_error {
+    int code;
+    OctvrError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_CHECK(expr)                                                                                \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess)                                                                          \
+            throw OctvrError(OCTVR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+    } while (0)
+
+#define REQUIRE(cond, msg)                                          \
+    do {                                                            \
+        if (!(cond)) throw OctvrError(OCTVR_E_INVALID, (msg));      \
+    } while (0)
+
+template <class F>
+int guarded(F&& f) {
+    try {
+        f();
+        return OCTVR_OK;
+    } catch (const OctvrError& e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc&) {
+        g_last_error = "out of host memory";
+        return OCTVR_E_INVALID;
+    } catch (const std::exception& e) {
+        g_last_error = e.what();
+        return OCTVR_E_PARSE;
+    }
+}
+
+// Scoped device selection: restores the caller's current device.
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        HIP_CHECK(hipGetDevice(&prev));
+        if (dev != prev) HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { reset(); }
+    void alloc(size_t count) {
+        reset();
+        if (count == 0) return;
+        HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
+        n = count;
+    }
+    void upload(const T* h, size_t count) {
+        alloc(count);
+        if (count) HIP_CHECK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
+    }
+    void reset() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+}  // namespace
+
+// =================================================================================================
+// Rig (vr::MapperTemplate)
+// =================================================================================================
+struct RigInput {
+    int roi[4] = {0, 0, 0, 0};
+    int in_w = 0, in_h = 0;  // input image size when known (JSON rigs)
+    std::vector<float> map1, map2;
+    std::vector<uint8_t> mask;
+    std::vector<float> vignette;
+    int vig_w = 0, vig_h = 0;
+};
+
+struct octvr_rig {
+    int out_w = 0, out_h = 0;
+    std::vector<RigInput> inputs;
+    std::vector<RigInput> overlays;
+    std::vector<std::vector<uint8_t>> seam_masks;
+};
+
+namespace {
+
+// ---- camera setup from JSON (camera.cpp:49-136 and the per-type constructors) ------------------
+void rodrigues(double rx, double ry, double rz, double R[9]) {
+    // cvRodrigues2 (calib3d/src/calibration.cpp:300-345)
+    double theta = sqrt(rx * rx + ry * ry + rz * rz);
+    if (theta < DBL_EPSILON) {
+        for (int k = 0; k < 9; k++) R[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        return;
+    }
+    static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    double c = cos(theta), s = sin(theta), c1 = 1. - c;
+    double itheta = theta ? 1. / theta : 0.;
+    rx *= itheta;
+    ry *= itheta;
+    rz *= itheta;
+    double rrt[9] = {rx * rx, rx * ry, rx * rz, rx * ry, ry * ry, ry * rz, rx * rz, ry * rz, rz * rz};
+    double rx_[9] = {0, -rz, ry, rz, 0, -rx, -ry, rx, 0};
+    for (int k = 0; k < 9; k++) R[k] = c * I[k] + c1 * rrt[k] + s * rx_[k];
+}
+
+void mul33(const double* a, const double* b, double* d) {
+    // cv::gemm len==3 path (core/src/matmul.cpp:934-1000): t*1 + 0*0
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double t = a[i * 3 + 0] * b[0 * 3 + j] + a[i * 3 + 1] * b[1 * 3 + j] + a[i * 3 + 2] * b[2 * 3 + j];
+            d[i * 3 + j] = t * 1.0 + 0.0 * 0.0;
+        }
+}
+
+void invert33(const double* S, double* D) {
+    // cv::invert 3x3 closed form (core/src/lapack.cpp:709-712, 970-990)
+#define Sd(y, x) S[(y) * 3 + (x)]
+    double d = Sd(0, 0) * ((double)Sd(1, 1) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 1)) -
+               Sd(0, 1) * ((double)Sd(1, 0) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 0)) +
+               Sd(0, 2) * ((double)Sd(1, 0) * Sd(2, 1) - (double)Sd(1, 1) * Sd(2, 0));
+    if (d == 0.) {
+        for (int k = 0; k < 9; k++) D[k] = 0;
+        return;
+    }
+    d = 1. / d;
+    D[0] = (Sd(1, 1) * Sd(2, 2) - Sd(1, 2) * Sd(2, 1)) * d;
+    D[1] = (Sd(0, 2) * Sd(2, 1) - Sd(0, 1) * Sd(2, 2)) * d;
+    D[2] = (Sd(0, 1) * Sd(1, 2) - Sd(0, 2) * Sd(1, 1)) * d;
+    D[3] = (Sd(1, 2) * Sd(2, 0) - Sd(1, 0) * Sd(2, 2)) * d;
+    D[4] = (Sd(0, 0) * Sd(2, 2) - Sd(0, 2) * Sd(2, 0)) * d;
+    D[5] = (Sd(0, 2) * Sd(1, 0) - Sd(0, 0) * Sd(1, 2)) * d;
+    D[6] = (Sd(1, 0) * Sd(2, 1) - Sd(1, 1) * Sd(2, 0)) * d;
+    D[7] = (Sd(0, 1) * Sd(2, 0) - Sd(0, 0) * Sd(2, 1)) * d;
+    D[8] = (Sd(0, 0) * Sd(1, 1) - Sd(0, 1) * Sd(1, 0)) * d;
+#undef Sd
+}
+
+// CalcCorrectionRadius_copy (fullframe_fisheye_cam.cpp:20-103)
+double cube_root(double x) { return x == 0.0 ? 0.0 : x > 0.0 ? pow(x, 1.0 / 3.0) : -pow(-x, 1.0 / 3.0); }
+void square_zero(const double* a, int* n, double* root) {
+    if (a[2] == 0.0) {
+        if (a[1] == 0.0) {
+            if (a[0] == 0.0) {
+                *n = 1;
+                root[0] = 0.0;
+            } else {
+                *n = 0;
+            }
+        } else {
+            *n = 1;
+            root[0] = -a[0] / a[1];
+        }
+    } else if (4.0 * a[2] * a[0] > a[1] * a[1]) {
+        *n = 0;
+    } else {
+        *n = 2;
+        root[0] = (-a[1] + sqrt(a[1] * a[1] - 4.0 * a[2] * a[0])) / (2.0 * a[2]);
+        root[1] = (-a[1] - sqrt(a[1] * a[1] - 4.0 * a[2] * a[0])) / (2.0 * a[2]);
+    }
+}
+void cube_zero(const double* a, int* n, double* root) {
+    if (a[3] == 0.0) {
+        square_zero(a, n, root);
+        return;
+    }
+    double p = ((-1.0 / 3.0) * (a[2] / a[3]) * (a[2] / a[3]) + a[1] / a[3]) / 3.0;
+    double q = ((2.0 / 27.0) * (a[2] / a[3]) * (a[2] / a[3]) * (a[2] / a[3]) - (1.0 / 3.0) * (a[2] / a[3]) * (a[1] / a[3]) +
+                a[0] / a[3]) / 2.0;
+    if (q * q + p * p * p >= 0.0) {
+        *n = 1;
+        root[0] = cube_root(-q + sqrt(q * q + p * p * p)) + cube_root(-q - sqrt(q * q + p * p * p)) - a[2] / (3.0 * a[3]);
+    } else {
+        double phi = acos(-q / sqrt(-p * p * p));
+        *n = 3;
+        root[0] = 2.0 * sqrt(-p) * cos(phi / 3.0) - a[2] / (3.0 * a[3]);
+        root[1] = -2.0 * sqrt(-p) * cos(phi / 3.0 + kPi / 3.0) - a[2] / (3.0 * a[3]);
+        root[2] = -2.0 * sqrt(-p) * cos(phi / 3.0 - kPi / 3.0) - a[2] / (3.0 * a[3]);
+    }
+}
+double correction_radius(const double* coeff) {
+    double a[4];
+    for (int k = 0; k < 4; k++) a[k] = coeff[k] != 0.0 ? (k + 1) * coeff[k] : 0.0;
+    int n = 0;
+    double root[3], sroot = 1000.0;
+    cube_zero(a, &n, root);
+    for (int i = 0; i < n; i++)
+        if (root[i] > 0.0 && root[i] < sroot) sroot = root[i];
+    return sroot;
+}
+
+void reject_unsupported_options(const JsonValue& o, const std::string& type) {
+    for (const char* k : {"selection", "exclude_masks", "include_masks"})
+        if (o.has(k))
+            throw OctvrError(OCTVR_E_UNSUPPORTED, std::string("camera option '") + k + "' (" + type +
+                                                      ") is not implemented in this ABI version");
+}
+
+CameraParams camera_from_json(const JsonValue& cam) {
+    CameraParams c;
+    memset(&c, 0, sizeof c);
+    const std::string& type = cam["type"].as_string();
+    static const JsonValue empty_obj = [] {
+        JsonValue v;
+        v.kind = JsonValue::Object;
+        return v;
+    }();
+    const JsonValue& o = cam.has("options") ? cam["options"] : empty_obj;
+    reject_unsupported_options(o, type);
+    // rotation (camera.cpp:50-70)
+    double rv[3] = {0, 0, 0};
+    if (o.has("rotation")) {
+        rv[0] = o["rotation"]["roll"].as_double();
+        rv[1] = -o["rotation"]["yaw"].as_double();
+        rv[2] = -o["rotation"]["pitch"].as_double();
+    }
+    double Rx[9], Ry[9], Rz[9], T[9];
+    rodrigues(rv[0], 0, 0, Rx);
+    rodrigues(0, rv[1], 0, Ry);
+    rodrigues(0, 0, rv[2], Rz);
+    mul33(Rx, Rz, T);
+    mul33(T, Ry, c.R);
+    if (o.has("rotation_matrix"))
+        for (int k = 0; k < 9; k++) c.R[k] = o["rotation_matrix"][k].as_double();
+    invert33(c.R, c.Rinv);
+    if (o.has("longitude_selection")) {
+        c.min_lon = o["longitude_selection"][0].as_double();
+        c.max_lon = o["longitude_selection"][1].as_double();
+        REQUIRE(c.max_lon > c.min_lon, "longitude_selection: max must exceed min");
+    } else {
+        c.min_lon = -kPi;
+        c.max_lon = kPi;
+    }
+    if (type == "equirectangular") {
+        c.type = CAM_EQUIRECT;
+        c.min_lat = o.get("min_lat", -kPi / 2);
+        c.max_lat = o.get("max_lat", kPi / 2);
+        c.scale_lon = o.get("scale_lon", 1.0);
+    } else if (type == "fullframe_fisheye") {
+        c.type = CAM_FULLFRAME_FISHEYE;
+        c.width = o["width"].as_int();
+        c.height = o["height"].as_int();
+        if (o.has("crop")) {
+            const JsonValue& r = o["crop"]["rect"];
+            c.crop_x = r[0].as_int();
+            c.crop_y = r[2].as_int();
+            c.crop_w = r[1].as_int() - r[0].as_int();
+            c.crop_h = r[3].as_int() - r[2].as_int();
+            c.crop_circular = o["crop"]["is_circular"].as_bool() ? 1 : 0;
+        }
+        if (c.crop_w * c.crop_h == 0) {
+            c.crop_x = c.crop_y = 0;
+            c.crop_w = c.width;
+            c.crop_h = c.height;
+            c.crop_circular = 0;
+        }
+        c.hfov = o["hfov"].as_double();
+        c.center_dx = o["center_dx"].as_double();
+        c.center_dy = o["center_dy"].as_double();
+        const JsonValue& r = o["radial"];
+        c.rad[3] = r[0].as_double();
+        c.rad[2] = r[1].as_double();
+        c.rad[1] = r[2].as_double();
+        c.rad[0] = 1.0 - r[0].as_double() - r[1].as_double() - r[2].as_double();
+        c.rad[4] = (c.crop_w < c.crop_h ? c.crop_w : c.crop_h) / 2.0;
+        c.rad[5] = correction_radius(c.rad);
+    } else if (type == "fisheye") {
+        c.type = CAM_FISHEYE;
+        c.fx = o["fx"].as_double();
+        c.fy = o["fy"].as_double();
+        c.cx = o["cx"].as_double();
+        c.cy = o["cy"].as_double();
+        REQUIRE(o["dist_coeffs"].size() == 4, "fisheye: dist_coeffs must have 4 entries (calib3d/src/fisheye.cpp:90)");
+        for (int k = 0; k < 4; k++) c.k[k] = o["dist_coeffs"][k].as_double();
+        c.width = o["width"].as_int();
+        c.height = o["height"].as_int();
+    } else {
+        throw OctvrError(OCTVR_E_UNSUPPORTED, "camera type '" + type + "' is not implemented in this ABI version");
+    }
+    return c;
+}
+
+double aspect_ratio(const JsonValue& cam) {
+    // Camera::get_aspect_ratio overrides (equirectangular.hpp:67-69, fullframe_fisheye_cam.cpp:142-144,
+    // pinhole_cam.hpp get_aspect_ratio)
+    const std::string& t = cam["type"].as_string();
+    const JsonValue& o = cam["options"];
+    if (t == "equirectangular") {
+        double mn = o.get("min_lat", -kPi / 2), mx = o.get("max_lat", kPi / 2), sl = o.get("scale_lon", 1.0);
+        return (2.0f * sl) / ((mx - mn) / kPi);
+    }
+    if (t == "fullframe_fisheye" || t == "fisheye") return double(o["width"].as_int()) / o["height"].as_int();
+    return 1.0;
+}
+
+// Vignette::getMap (vignette.cpp:18-54) at 512x512.
+std::vector<float> vignette_map(const JsonValue& o, int width, int height) {
+    if (!o.has("vignette")) return {};
+    double a = o["vignette"][0].as_double(), b = o["vignette"][1].as_double(), c = o["vignette"][2].as_double(),
+           d = o["vignette"][3].as_double();
+    if (o.has("exposure")) {
+        float ev = (float)std::pow(2.0, o["exposure"].as_double());
+        a /= ev;
+        b /= ev;
+        c /= ev;
+        d /= ev;
+    }
+    std::vector<float> m((size_t)width * height);
+    for (int j = 0; j < height; j++)
+        for (int i = 0; i < width; i++) {
+#define P(X) (float(X) * float(X))
+            float r = std::sqrt(P(i - width / 2) + P(j - height / 2)) / std::sqrt(P(width / 2) + P(height / 2));
+#undef P
+            m[(size_t)j * width + i] = (float)(1.0 / (a + r * r * (b + r * r * (c + d * r * r))));
+        }
+    return m;
+}
+
+void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H, bool use_roi, int device,
+                 RigInput& in) {
+    CameraParams c = camera_from_json(cam);
+    DeviceGuard dg(device);
+    const size_t total = (size_t)W * H;
+    DevBuf<float> m1, m2;
+    DevBuf<uint8_t> mk;
+    DevBuf<int32_t> bb;
+    m1.alloc(total);
+    m2.alloc(total);
+    mk.alloc(total);
+    bb.alloc(4);
+    int32_t init[4] = {INT32_MAX, INT32_MAX, -1, -1};
+    HIP_CHECK(hipMemcpy(bb.p, init, sizeof init, hipMemcpyHostToDevice));
+    HIP_CHECK(launch_lut_build(out_cam, c, W, H, m1.p, m2.p, mk.p, bb.p, nullptr));
+    HIP_CHECK(hipDeviceSynchronize());
+    int32_t b[4];
+    HIP_CHECK(hipMemcpy(b, bb.p, sizeof b, hipMemcpyDeviceToHost));
+    // CV_Assert(min_h <= max_h && min_w <= max_w) (template.cpp:124)
+    if (!(b[1] <= b[3] && b[0] <= b[2])) throw OctvrError(OCTVR_E_INVALID, "input camera covers no output pixel");
+    int min_w = std::max(0, b[0] - 8), min_h = std::max(0, b[1] - 8);
+    int max_w = std::min(W - 1, b[2] + 8), max_h = std::min(H - 1, b[3] + 8);
+    int roi[4] = {min_w, min_h, max_w + 1 - min_w, max_h + 1 - min_h};
+    if (!use_roi) {
+        roi[0] = roi[1] = 0;
+        roi[2] = W;
+        roi[3] = H;
+    }
+    memcpy(in.roi, roi, sizeof roi);
+    const size_t rn = (size_t)roi[2] * roi[3];
+    in.map1.resize(rn);
+    in.map2.resize(rn);
+    in.mask.resize(rn);
+    const size_t off = (size_t)roi[1] * W + roi[0];
+    HIP_CHECK(hipMemcpy2D(in.map1.data(), roi[2] * sizeof(float), m1.p + off, W * sizeof(float), roi[2] * sizeof(float),
+                          roi[3], hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy2D(in.map2.data(), roi[2] * sizeof(float), m2.p + off, W * sizeof(float), roi[2] * sizeof(float),
+                          roi[3], hipMemcpyDeviceToHost));
+    HIP_CHECK(hipMemcpy2D(in.mask.data(), roi[2], mk.p + off, W, roi[2], roi[3], hipMemcpyDeviceToHost));
+    const JsonValue& o = cam["options"];
+    in.in_w = o.has("width") ? o["width"].as_int() : 0;
+    in.in_h = o.has("height") ? o["height"].as_int() : 0;
+    in.vignette = vignette_map(o, 512, 512);
+    if (!in.vignette.empty()) in.vig_w = in.vig_h = 512;
+}
+
+// ---- VRv11 .dat (template.cpp:206-314) -----------------------------------------------------------
+constexpr const char* kDatMagic = "VRv11";
+constexpr int CV_8UC1 = 0, CV_32FC1 = 5;
+
+struct DatWriter {
+    std::ofstream f;
+    void i64(int64_t v) { f.write(reinterpret_cast<const char*>(&v), 8); }
+    void mat(int type, int rows, int cols, const void* data, size_t elem) {
+        i64(type);
+        i64(rows);
+        i64(cols);
+        if (rows * cols == 0 || !data) return;
+        f.write(reinterpret_cast<const char*>(data), (std::streamsize)((size_t)rows * cols * elem));
+    }
+    void input(const RigInput& in) {
+        for (int k = 0; k < 4; k++) i64(in.roi[k]);
+        mat(CV_32FC1, in.roi[3], in.roi[2], in.map1.data(), 4);
+        mat(CV_32FC1, in.roi[3], in.roi[2], in.map2.data(), 4);
+        mat(CV_8UC1, in.roi[3], in.roi[2], in.mask.data(), 1);
+        if (in.vignette.empty())
+            mat(0, 0, 0, nullptr, 1);  // empty cv::Mat: type 0, 0x0 (Mat() header)
+        else
+            mat(CV_32FC1, in.vig_h, in.vig_w, in.vignette.data(), 4);
+    }
+};
+
+struct DatReader {
+    std::ifstream f;
+    int64_t i64() {
+        int64_t v = 0;
+        f.read(reinterpret_cast<char*>(&v), 8);
+        if (!f) throw OctvrError(OCTVR_E_PARSE, "truncated .dat file");
+        return v;
+    }
+    // Rmat: returns rows, cols, type; data appended to `out` (bytes)
+    void mat(int want_type, int& rows, int& cols, std::vector<uint8_t>& out) {
+        int type = (int)i64();
+        rows = (int)i64();
+        cols = (int)i64();
+        out.clear();
+        if ((int64_t)rows * cols == 0) {
+            rows = cols = 0;
+            return;
+        }
+        if (want_type >= 0 && type != want_type) throw OctvrError(OCTVR_E_PARSE, "unexpected Mat type in .dat");
+        size_t elem = type == CV_32FC1 ? 4 : type == CV_8UC1 ? 1 : 0;
+        if (!elem) throw OctvrError(OCTVR_E_PARSE, "unsupported Mat type in .dat");
+        out.resize((size_t)rows * cols * elem);
+        f.read(reinterpret_cast<char*>(out.data()), (std::streamsize)out.size());
+        if (!f) throw OctvrError(OCTVR_E_PARSE, "truncated .dat file");
+    }
+    void input(RigInput& in) {
+        for (int k = 0; k < 4; k++) in.roi[k] = (int)i64();
+        std::vector<uint8_t> b;
+        int r, c;
+        mat(CV_32FC1, r, c, b);
+        in.map1.resize((size_t)r * c);
+        memcpy(in.map1.data(), b.data(), b.size());
+        mat(CV_32FC1, r, c, b);
+        in.map2.resize((size_t)r * c);
+        memcpy(in.map2.data(), b.data(), b.size());
+        mat(CV_8UC1, r, c, b);
+        in.mask = b;
+        if ((int)in.map1.size() != in.roi[2] * in.roi[3] || (int)in.mask.size() != in.roi[2] * in.roi[3])
+            throw OctvrError(OCTVR_E_PARSE, ".dat: map size does not match ROI");
+        mat(-1, r, c, b);
+        in.vignette.resize(b.size() / 4);
+        if (!b.empty()) memcpy(in.vignette.data(), b.data(), b.size());
+        in.vig_w = c;
+        in.vig_h = r;
+    }
+};
+
+}  // namespace
+
+// =================================================================================================
+// Mapper (vr::Mapper)
+// =================================================================================================
+struct octvr_mapper {
+    int device = 0;
+    int n = 0;
+    int W = 0, H = 0;
+    int use_gain = 0;
+    std::vector<int> in_w, in_h;
+    DevBuf<int16_t> tab;
+    DevBuf<CompositeEntry> lut;
+    DevBuf<double> gains;
+    // gain feed
+    DevBuf<CompositeEntry> sa, sb;
+    DevBuf<GainChunk> chunks;
+    DevBuf<double> partials;
+    DevBuf<int32_t> pair_ij, N;
+    int n_chunks = 0;
+    size_t n_entries = 0;
+    std::vector<double> last_gains;
+    hipStream_t last_stream = nullptr;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    ~octvr_mapper() {
+        for (auto& e : events) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+    }
+};
+
+namespace {
+
+float resize_inv_scale(int d, int s) {
+    // cudawarping/src/resize.cpp:82-83,105
+    double f = (double)d / s;
+    return (float)(1.0 / f);
+}
+
+// cuda::resize INTER_LINEAR on u8 (glob path, resize.cu:71-103); nvcc's default FMA contraction of
+// `out + src * w` is reproduced with explicit fmaf.
+std::vector<uint8_t> resize_linear_u8(const uint8_t* src, int sw, int sh, int dw, int dh) {
+    std::vector<uint8_t> dst((size_t)dw * dh);
+    float fx = resize_inv_scale(dw, sw), fy = resize_inv_scale(dh, sh);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float src_x = x * fx, src_y = y * fy;
+            int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+            int x2 = x1 + 1, y2 = y1 + 1;
+            int x2r = std::min(x2, sw - 1), y2r = std::min(y2, sh - 1);
+            float out = 0.f;
+            out = fmaf((float)src[(size_t)y1 * sw + x1], (x2 - src_x) * (y2 - src_y), out);
+            out = fmaf((float)src[(size_t)y1 * sw + x2r], (src_x - x1) * (y2 - src_y), out);
+            out = fmaf((float)src[(size_t)y2r * sw + x1], (x2 - src_x) * (src_y - y1), out);
+            out = fmaf((float)src[(size_t)y2r * sw + x2r], (src_x - x1) * (src_y - y1), out);
+            int v = !(out > 0.f) ? 0 : out >= 255.f ? 255 : (int)rintf(out);
+            dst[(size_t)y * dw + x] = (uint8_t)v;
+        }
+    return dst;
+}
+
+// Working-scale gain setup: Mapper ctor (mapper.cpp:94-114,140-142) + GainCompensatorGPU ctor
+// (exposure_compensate.cpp:174-221).  Produces per-pair sample entries of both cameras for every
+// pixel of the bitwise-AND intersection of the resized masks, N(i,j), and chunking.
+void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
+    const int n = m.n;
+    double ws = std::min(1.0, std::sqrt(0.1 * 1e6 / ((double)rig.out_w * rig.out_h)));
+    std::vector<std::array<int, 4>> wr(n);
+    std::vector<std::vector<uint8_t>> smask(n);
+    std::vector<std::vector<CompositeEntry>> samp(n);
+    std::vector<int32_t> N((size_t)n * n, 0);
+    for (int i = 0; i < n; i++) {
+        const RigInput& in = rig.inputs[i];
+        wr[i] = {(int)(in.roi[0] * ws), (int)(in.roi[1] * ws), (int)(in.roi[2] * ws), (int)(in.roi[3] * ws)};
+        const int ww = wr[i][2], wh = wr[i][3];
+        REQUIRE(ww > 0 && wh > 0, "working-scale ROI is empty");
+        smask[i] = resize_linear_u8(in.mask.data(), in.roi[2], in.roi[3], ww, wh);
+        // warped -> working scale: resize_nearest (resize.cu:57-69), src index = trunc(dst * (float)(1/f))
+        float fx = resize_inv_scale(ww, in.roi[2]), fy = resize_inv_scale(wh, in.roi[3]);
+        samp[i].resize((size_t)ww * wh);
+        for (int y = 0; y < wh; y++)
+            for (int x = 0; x < ww; x++) {
+                int sx = (int)(x * fx), sy = (int)(y * fy);
+                size_t k = (size_t)sy * in.roi[2] + sx;
+                CompositeEntry e{0, 0};
+                if (in.mask[k]) e = make_entry(in.map1[k], in.map2[k], (float)m.in_w[i], (float)m.in_h[i], i);
+                samp[i][(size_t)y * ww + x] = e;
+            }
+        int nz = 0;
+        for (uint8_t v : smask[i]) nz += v != 0;
+        N[(size_t)i * n + i] = std::max(1, nz);
+    }
+    std::vector<CompositeEntry> A, B;
+    std::vector<GainChunk> chunks;
+    std::vector<int32_t> pij;
+    const int kChunk = 256 * 16;
+    int p = 0;
+    for (int i = 0; i < n; i++)
+        for (int j = i + 1; j < n; j++, p++) {
+            pij.push_back(i);
+            pij.push_back(j);
+            const auto &a = wr[i], &b = wr[j];
+            int x0 = std::max(a[0], b[0]), y0 = std::max(a[1], b[1]);
+            int x1 = std::min(a[0] + a[2], b[0] + b[2]), y1 = std::min(a[1] + a[3], b[1] + b[3]);
+            if (x1 <= x0 || y1 <= y0) {  // overlap_roi.area() == 0
+                N[(size_t)i * n + j] = N[(size_t)j * n + i] = 1;
+                continue;
+            }
+            int begin = (int)A.size(), nz = 0;
+            for (int y = y0; y < y1; y++)
+                for (int x = x0; x < x1; x++) {
+                    size_t ka = (size_t)(y - a[1]) * a[2] + (x - a[0]);
+                    size_t kb = (size_t)(y - b[1]) * b[2] + (x - b[0]);
+                    if ((smask[i][ka] & smask[j][kb]) == 0) continue;
+                    nz++;
+                    A.push_back(samp[i][ka]);
+                    B.push_back(samp[j][kb]);
+                }
+            N[(size_t)i * n + j] = N[(size_t)j * n + i] = std::max(1, nz);
+            for (int s = begin; s < (int)A.size(); s += kChunk)
+                chunks.push_back(GainChunk{p, s, std::min<int>((int)A.size(), s + kChunk), 0});
+        }
+    m.sa.upload(A.data(), A.size());
+    m.sb.upload(B.data(), B.size());
+    m.chunks.upload(chunks.data(), chunks.size());
+    m.partials.alloc(std::max<size_t>(2 * chunks.size(), 2));
+    m.pair_ij.upload(pij.data(), pij.size());
+    m.N.upload(N.data(), N.size());
+    m.n_chunks = (int)chunks.size();
+    m.n_entries = A.size();
+}
+
+}  // namespace
+
+// =================================================================================================
+// extern "C" entry points
+// =================================================================================================
+extern "C" {
+
+int octvr_abi_version(void) { return OCTVR_HIP_ABI_VERSION; }
+
+const char* octvr_last_error(void) { return g_last_error.c_str(); }
+
+int octvr_device_count(int* count) {
+    return guarded([&] {
+        REQUIRE(count, "count is NULL");
+        HIP_CHECK(hipGetDeviceCount(count));
+    });
+}
+
+int octvr_dev_malloc(int device, size_t bytes, void** ptr) {
+    return guarded([&] {
+        REQUIRE(ptr, "ptr is NULL");
+        DeviceGuard dg(device);
+        HIP_CHECK(hipMalloc(ptr, bytes));
+    });
+}
+
+int octvr_dev_free(void* ptr) {
+    return guarded([&] { HIP_CHECK(hipFree(ptr)); });
+}
+
+int octvr_memcpy_h2d(void* dst, const void* src, size_t bytes) {
+    return guarded([&] { HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)); });
+}
+
+int octvr_memcpy_d2h(void* dst, const void* src, size_t bytes) {
+    return guarded([&] { HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost)); });
+}
+
+int octvr_stream_sync(void* stream) {
+    return guarded([&] { HIP_CHECK(hipStreamSynchronize((hipStream_t)stream)); });
+}
+
+int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, int device, octvr_rig** out) {
+    return guarded([&] {
+        REQUIRE(json && out, "json/out is NULL");
+        JsonValue doc = json_parse(json);
+        const JsonValue& oc = doc["output"];
+        CameraParams out_cam = camera_from_json(oc);
+        REQUIRE(!(out_h <= 0 && out_w <= 0), "Output width/height invalid");  // template.cpp:32-33
+        double ar = aspect_ratio(oc);
+        if (out_h <= 0) out_h = int(double(out_w) / ar);
+        if (out_w <= 0) out_w = int(double(out_h) * ar);
+        REQUIRE(out_cam.type == CAM_EQUIRECT, "only equirectangular output is implemented in this ABI version");
+        auto rig = std::make_unique<octvr_rig>();
+        rig->out_w = out_w;
+        rig->out_h = out_h;
+        const JsonValue& ins = doc["inputs"];
+        rig->inputs.resize(ins.size());
+        for (size_t i = 0; i < ins.size(); i++)
+            build_input(out_cam, ins[i], out_w, out_h, use_roi != 0, device, rig->inputs[i]);
+        if (doc.has("overlays")) {
+            const JsonValue& ov = doc["overlays"];
+            rig->overlays.resize(ov.size());
+            for (size_t i = 0; i < ov.size(); i++)
+                build_input(out_cam, ov[i], out_w, out_h, use_roi != 0, device, rig->overlays[i]);
+        }
+        *out = rig.release();
+    });
+}
+
+int octvr_rig_create_from_arrays(int out_w, int out_h, int n, const int* rois, const float* const* map1,
+                                 const float* const* map2, const uint8_t* const* masks,
+                                 const uint8_t* const* seams, octvr_rig** out) {
+    return guarded([&] {
+        REQUIRE(out && rois && map1 && map2 && masks && n > 0 && out_w > 0 && out_h > 0, "bad arguments");
+        auto rig = std::make_unique<octvr_rig>();
+        rig->out_w = out_w;
+        rig->out_h = out_h;
+        rig->inputs.resize(n);
+        for (int i = 0; i < n; i++) {
+            RigInput& in = rig->inputs[i];
+            memcpy(in.roi, rois + 4 * i, 4 * sizeof(int));
+            REQUIRE(in.roi[0] >= 0 && in.roi[1] >= 0 && in.roi[2] > 0 && in.roi[3] > 0 &&
+                        in.roi[0] + in.roi[2] <= out_w && in.roi[1] + in.roi[3] <= out_h,
+                    "ROI outside the output frame");
+            size_t k = (size_t)in.roi[2] * in.roi[3];
+            in.map1.assign(map1[i], map1[i] + k);
+            in.map2.assign(map2[i], map2[i] + k);
+            in.mask.assign(masks[i], masks[i] + k);
+        }
+        if (seams) {
+            rig->seam_masks.resize(n);
+            for (int i = 0; i < n; i++) {
+                size_t k = (size_t)rig->inputs[i].roi[2] * rig->inputs[i].roi[3];
+                rig->seam_masks[i].assign(seams[i], seams[i] + k);
+            }
+        }
+        *out = rig.release();
+    });
+}
+
+int octvr_rig_load_dat(const char* path, octvr_rig** out) {
+    return guarded([&] {
+        REQUIRE(path && out, "path/out is NULL");
+        DatReader r;
+        r.f.open(path, std::ios::binary);
+        if (!r.f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);
+        char magic[5];
+        r.f.read(magic, 5);
+        if (!r.f || strncmp(magic, kDatMagic, 5) != 0)
+            throw OctvrError(OCTVR_E_PARSE, "Invalid data file (version does not match)");
+        auto rig = std::make_unique<octvr_rig>();
+        rig->out_w = (int)r.i64();
+        rig->out_h = (int)r.i64();
+        int64_t n = r.i64();
+        REQUIRE(n >= 0 && n <= kMaxCams, ".dat: bad input count");
+        rig->inputs.resize(n);
+        for (auto& in : rig->inputs) r.input(in);
+        rig->seam_masks.resize(n);
+        for (int64_t i = 0; i < n; i++) {
+            int rr, cc;
+            r.mat(CV_8UC1, rr, cc, rig->seam_masks[i]);
+        }
+        int64_t no = r.i64();
+        REQUIRE(no >= 0 && no <= kMaxCams, ".dat: bad overlay count");
+        rig->overlays.resize(no);
+        for (auto& in : rig->overlays) r.input(in);
+        *out = rig.release();
+    });
+}
+
+int octvr_rig_dump_dat(const octvr_rig* rig, const char* path) {
+    return guarded([&] {
+        REQUIRE(rig && path, "rig/path is NULL");
+        REQUIRE(rig->seam_masks.size() == rig->inputs.size(),
+                "rig has no seam masks (create them before dumping; template.cpp:209-210)");
+        DatWriter w;
+        w.f.open(path, std::ios::binary);
+        if (!w.f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);
+        w.f.write(kDatMagic, 5);
+        w.i64(rig->out_w);
+        w.i64(rig->out_h);
+        w.i64((int64_t)rig->inputs.size());
+        for (auto& in : rig->inputs) w.input(in);
+        for (size_t i = 0; i < rig->seam_masks.size(); i++) {
+            const RigInput& in = rig->inputs[i];
+            w.mat(CV_8UC1, in.roi[3], in.roi[2], rig->seam_masks[i].data(), 1);
+        }
+        w.i64((int64_t)rig->overlays.size());
+        for (auto& in : rig->overlays) w.input(in);
+        if (!w.f) throw OctvrError(OCTVR_E_IO, "write failed");
+    });
+}
+
+int octvr_rig_num_inputs(const octvr_rig* rig, int* n) {
+    return guarded([&] {
+        REQUIRE(rig && n, "NULL argument");
+        *n = (int)rig->inputs.size();
+    });
+}
+
+int octvr_rig_out_size(const octvr_rig* rig, int* w, int* h) {
+    return guarded([&] {
+        REQUIRE(rig && w && h, "NULL argument");
+        *w = rig->out_w;
+        *h = rig->out_h;
+    });
+}
+
+int octvr_rig_get_input(const octvr_rig* rig, int i, octvr_input_view* v) {
+    return guarded([&] {
+        REQUIRE(rig && v && i >= 0 && i < (int)rig->inputs.size(), "bad input index");
+        const RigInput& in = rig->inputs[i];
+        v->roi_x = in.roi[0];
+        v->roi_y = in.roi[1];
+        v->roi_w = in.roi[2];
+        v->roi_h = in.roi[3];
+        v->map1 = in.map1.data();
+        v->map2 = in.map2.data();
+        v->mask = in.mask.data();
+        v->seam_mask = i < (int)rig->seam_masks.size() ? rig->seam_masks[i].data() : nullptr;
+        v->vignette = in.vignette.empty() ? nullptr : in.vignette.data();
+        v->vignette_w = in.vig_w;
+        v->vignette_h = in.vig_h;
+    });
+}
+
+void octvr_rig_destroy(octvr_rig* rig) { delete rig; }
+
+int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
+                        int enable_gain, int scale_w, int scale_h, octvr_mapper** out) {
+    return guarded([&] {
+        REQUIRE(rig && out && in_w && in_h, "NULL argument");
+        REQUIRE(n_inputs == (int)(rig->inputs.size() + rig->overlays.size()), "in_sizes must cover inputs + overlays");
+        REQUIRE(rig->overlays.empty(), "overlay inputs are not implemented in this ABI version");
+        REQUIRE((int)rig->inputs.size() <= kMaxCams, "too many inputs");
+        if (blend != 0) throw OctvrError(OCTVR_E_UNSUPPORTED, "multi-band / feather blend is not implemented in this ABI version");
+        REQUIRE((scale_w == 0 && scale_h == 0) || (scale_w == rig->out_w && scale_h == rig->out_h),
+                "scaled output is not implemented in this ABI version");
+        REQUIRE(rig->out_w % 2 == 0 && rig->out_h % 2 == 0, "YUV420 output needs even width/height");
+        for (auto& in : rig->inputs)
+            REQUIRE(in.vignette.empty(), "vignette correction is not implemented in this ABI version");
+        auto m = std::make_unique<octvr_mapper>();
+        m->device = device;
+        m->n = (int)rig->inputs.size();
+        m->W = rig->out_w;
+        m->H = rig->out_h;
+        m->in_w.assign(in_w, in_w + n_inputs);
+        m->in_h.assign(in_h, in_h + n_inputs);
+        for (int i = 0; i < m->n; i++)
+            REQUIRE(m->in_w[i] > 0 && m->in_h[i] > 0 && m->in_w[i] % 2 == 0 && m->in_h[i] % 2 == 0 &&
+                        m->in_w[i] <= 65535 && m->in_h[i] <= 65535,
+                    "input sizes must be even and < 65536");
+        // mapper.cpp:78-82: a single input disables gain (and blend)
+        m->use_gain = (enable_gain && m->n > 1) ? 1 : 0;
+        DeviceGuard dg(device);
+        int16_t tab[4096];
+        bilinear_table(tab);
+        m->tab.upload(tab, 4096);
+        // per-camera templates -> device, composite LUT, then drop the per-camera maps
+        {
+            std::vector<DevBuf<float>> m1(m->n), m2(m->n);
+            std::vector<DevBuf<uint8_t>> mk(m->n);
+            std::vector<CamTemplate> ct(m->n);
+            for (int i = 0; i < m->n; i++) {
+                const RigInput& in = rig->inputs[i];
+                m1[i].upload(in.map1.data(), in.map1.size());
+                m2[i].upload(in.map2.data(), in.map2.size());
+                mk[i].upload(in.mask.data(), in.mask.size());
+                ct[i] = CamTemplate{m1[i].p, m2[i].p, mk[i].p, in.roi[0], in.roi[1], in.roi[2], in.roi[3],
+                                    m->in_w[i], m->in_h[i]};
+            }
+            DevBuf<CamTemplate> ctd;
+            ctd.upload(ct.data(), ct.size());
+            m->lut.alloc((size_t)m->W * m->H);
+            HIP_CHECK(launch_composite_lut(ctd.p, m->n, m->W, m->H, m->lut.p, nullptr));
+            HIP_CHECK(hipDeviceSynchronize());
+        }
+        m->gains.alloc(kMaxCams);
+        std::vector<double> ones(kMaxCams, 1.0);
+        HIP_CHECK(hipMemcpy(m->gains.p, ones.data(), kMaxCams * sizeof(double), hipMemcpyHostToDevice));
+        m->last_gains.assign(m->n, 1.0);
+        if (m->use_gain) setup_gain(*m, *rig);
+        *out = m.release();
+    });
+}
+
+int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream) {
+    return guarded([&] {
+        REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
+        REQUIRE(out_pitch >= (size_t)m->W, "output pitch smaller than width");
+        hipStream_t s = (hipStream_t)stream;
+        DeviceGuard dg(m->device);
+        FrameSet fs;
+        memset(&fs, 0, sizeof fs);
+        for (int i = 0; i < m->n; i++) {
+            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
+            fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i]};
+        }
+        if (m->use_gain) {
+            if (gains) {
+                REQUIRE(n_gains == m->n, "gains must have one entry per input");
+                HIP_CHECK(launch_set_gains(gains, m->n, m->gains.p, s));
+            } else {
+                HIP_CHECK(launch_gain_feed(fs, m->tab.p, m->sa.p, m->sb.p, m->chunks.p, m->n_chunks, m->partials.p, s));
+                HIP_CHECK(launch_gain_solve(m->partials.p, m->chunks.p, m->n_chunks, m->pair_ij.p, m->N.p, m->n,
+                                            m->gains.p, s));
+            }
+        }
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (m->timing) {
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            HIP_CHECK(hipEventRecord(e0, s));
+        }
+        HIP_CHECK(launch_stitch(fs, m->tab.p, m->lut.p, m->W, m->H, m->gains.p, m->use_gain, out_dev,
+                                (int64_t)out_pitch, s));
+        if (m->timing) {
+            HIP_CHECK(hipEventRecord(e1, s));
+            m->events.emplace_back(e0, e1);
+        }
+        m->last_stream = s;
+    });
+}
+
+int octvr_mapper_gains(octvr_mapper* m, double* g, int n) {
+    return guarded([&] {
+        REQUIRE(m && g && n >= m->n, "bad arguments");
+        DeviceGuard dg(m->device);
+        if (!m->use_gain) {
+            for (int i = 0; i < n; i++) g[i] = 1.0;
+            return;
+        }
+        HIP_CHECK(hipStreamSynchronize(m->last_stream));
+        HIP_CHECK(hipMemcpy(g, m->gains.p, m->n * sizeof(double), hipMemcpyDeviceToHost));
+    });
+}
+
+int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
+    return guarded([&] {
+        REQUIRE(m && bytes, "NULL argument");
+        // composite kernel: 8 B LUT entry + 1.5 B YUV420 output per output pixel, every source
+        // frame read once (1.5 B per input pixel)
+        double b = 8.0 * m->W * m->H + 1.5 * m->W * m->H;
+        for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
+        *bytes = b;
+    });
+}
+
+int octvr_mapper_set_timing(octvr_mapper* m, int enable) {
+    return guarded([&] {
+        REQUIRE(m, "NULL mapper");
+        m->timing = enable != 0;
+    });
+}
+
+int octvr_mapper_kernel_time(octvr_mapper* m, double* total_ms, int* launches) {
+    return guarded([&] {
+        REQUIRE(m && total_ms && launches, "NULL argument");
+        DeviceGuard dg(m->device);
+        double t = 0;
+        for (auto& e : m->events) {
+            HIP_CHECK(hipEventSynchronize(e.second));
+            float ms = 0;
+            HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
+            t += ms;
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+        *launches = (int)m->events.size();
+        *total_ms = t;
+        m->events.clear();
+    });
+}
+
+void octvr_mapper_destroy(octvr_mapper* m) {
+    if (!m) return;
+    int prev = -1;
+    if (hipGetDevice(&prev) == hipSuccess && prev != m->device) (void)hipSetDevice(m->device);
+    delete m;
+    if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, const float* map1, const float* map2,
+                   int mw, int mh, size_t mpitch, float scale_x, float scale_y, uint8_t* dst, size_t dpitch,
+                   void* stream) {
+    return guarded([&] {
+        REQUIRE(src && map1 && map2 && dst && sw > 0 && sh > 0 && mw >= 0 && mh >= 0, "bad arguments");
+        REQUIRE(cn == 1 || cn == 3 || cn == 4, "cn must be 1, 3 or 4");
+        if (mw == 0 || mh == 0) return;
+        // one shared table per device (allocated on first use, never freed: 8 KiB)
+        static thread_local std::vector<std::pair<int, int16_t*>> tabs;
+        int dev = 0;
+        HIP_CHECK(hipGetDevice(&dev));
+        int16_t* t = nullptr;
+        for (auto& kv : tabs)
+            if (kv.first == dev) t = kv.second;
+        if (!t) {
+            int16_t host[4096];
+            bilinear_table(host);
+            HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&t), sizeof host));
+            HIP_CHECK(hipMemcpy(t, host, sizeof host, hipMemcpyHostToDevice));
+            tabs.emplace_back(dev, t);
+        }
+        HIP_CHECK(launch_remap_u8(t, src, sw, sh, (int64_t)spitch, cn, map1, map2, mw, mh, (int64_t)mpitch, scale_x,
+                                  scale_y, dst, (int64_t)dpitch, (hipStream_t)stream));
+    });
+}
+
+}  // extern "C"

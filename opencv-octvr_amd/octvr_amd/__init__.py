@@ -1,0 +1,234 @@
+"""Python binding of the MI355X octVR stitching library (include/octvr_hip.h) over ctypes.
+
+Host-side mirror of the reference's octvr API for the stitching path:
+
+* :class:`MapperTemplate`  <- ``vr::MapperTemplate`` (modules/octvr/include/octvr.hpp:47-91)
+* :class:`Mapper`          <- ``vr::Mapper``         (modules/octvr/src/mapper.hpp:386-452)
+
+Device buffers are torch tensors on ``cuda:N`` (PyTorch is plumbing here: allocation, streams,
+torch.distributed); all arithmetic runs in the hand-written HIP kernels of ``liboctvr_hip.so``.
+There is no CPU fallback: importing this module fails loudly when the library is missing.
+"""
+import ctypes as C
+import json as _json
+import os
+
+import numpy as np
+import torch  # must be imported first: the library then binds to torch's HIP runtime (one per process)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "liboctvr_hip.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        "liboctvr_hip.so not found at %s — build it with `make -C opencv-octvr_amd` or "
+        "`python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+
+_lib = C.CDLL(LIB_PATH)
+
+
+class OctvrError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("octvr error %d: %s" % (code, msg))
+        self.code = code
+
+
+class InputView(C.Structure):
+    _fields_ = [("roi_x", C.c_int), ("roi_y", C.c_int), ("roi_w", C.c_int), ("roi_h", C.c_int),
+                ("map1", C.c_void_p), ("map2", C.c_void_p), ("mask", C.c_void_p), ("seam_mask", C.c_void_p),
+                ("vignette", C.c_void_p), ("vignette_w", C.c_int), ("vignette_h", C.c_int)]
+
+
+def _check(rc):
+    if rc != 0:
+        raise OctvrError(rc, _lib.octvr_last_error().decode())
+
+
+_lib.octvr_last_error.restype = C.c_char_p
+_VP = C.c_void_p
+_lib.octvr_rig_create_json.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]
+_lib.octvr_rig_load_dat.argtypes = [C.c_char_p, C.POINTER(_VP)]
+_lib.octvr_rig_dump_dat.argtypes = [_VP, C.c_char_p]
+_lib.octvr_rig_create_from_arrays.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(_VP),
+                                              C.POINTER(_VP), C.POINTER(_VP), C.POINTER(_VP), C.POINTER(_VP)]
+_lib.octvr_rig_num_inputs.argtypes = [_VP, C.POINTER(C.c_int)]
+_lib.octvr_rig_out_size.argtypes = [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]
+_lib.octvr_rig_get_input.argtypes = [_VP, C.c_int, C.POINTER(InputView)]
+_lib.octvr_rig_destroy.argtypes = [_VP]
+_lib.octvr_rig_destroy.restype = None
+_lib.octvr_mapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
+                                     C.c_int, C.c_int, C.POINTER(_VP)]
+_lib.octvr_mapper_stitch_yuv420p.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t,
+                                             C.POINTER(C.c_double), C.c_int, _VP]
+_lib.octvr_mapper_gains.argtypes = [_VP, C.POINTER(C.c_double), C.c_int]
+_lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
+_lib.octvr_mapper_set_timing.argtypes = [_VP, C.c_int]
+_lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+_lib.octvr_mapper_destroy.argtypes = [_VP]
+_lib.octvr_mapper_destroy.restype = None
+_lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
+                                C.c_float, C.c_float, _VP, C.c_size_t, _VP]
+
+
+def lib():
+    return _lib
+
+
+def abi_version():
+    return _lib.octvr_abi_version()
+
+
+def _stream_ptr(stream):
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return C.c_void_p(stream.cuda_stream)
+
+
+class MapperTemplate:
+    """vr::MapperTemplate: JSON rig (LUT built on the GPU) or a VRv11 .dat file."""
+
+    def __init__(self, handle):
+        self._h = C.c_void_p(handle)
+
+    @classmethod
+    def from_json(cls, rig, out_w, out_h, use_roi=True, device=0):
+        text = rig if isinstance(rig, str) else _json.dumps(rig)
+        h = _VP()
+        _check(_lib.octvr_rig_create_json(text.encode(), out_w, out_h, int(use_roi), device, C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def load(cls, path):
+        h = _VP()
+        _check(_lib.octvr_rig_load_dat(os.fsencode(path), C.byref(h)))
+        return cls(h.value)
+
+    @classmethod
+    def from_arrays(cls, out_w, out_h, rois, map1s, map2s, masks, seams=None):
+        n = len(rois)
+        map1s = [np.ascontiguousarray(a, np.float32) for a in map1s]
+        map2s = [np.ascontiguousarray(a, np.float32) for a in map2s]
+        masks = [np.ascontiguousarray(a, np.uint8) for a in masks]
+        r = (C.c_int * (4 * n))(*[int(v) for roi in rois for v in roi])
+        p1 = (_VP * n)(*[a.ctypes.data for a in map1s])
+        p2 = (_VP * n)(*[a.ctypes.data for a in map2s])
+        pm = (_VP * n)(*[a.ctypes.data for a in masks])
+        ps = None
+        if seams is not None:
+            seams = [np.ascontiguousarray(a, np.uint8) for a in seams]
+            ps = (_VP * n)(*[a.ctypes.data for a in seams])
+        h = _VP()
+        _check(_lib.octvr_rig_create_from_arrays(out_w, out_h, n, r, p1, p2, pm, ps, C.byref(h)))
+        return cls(h.value)
+
+    def dump(self, path):
+        _check(_lib.octvr_rig_dump_dat(self._h, os.fsencode(path)))
+
+    @property
+    def out_size(self):
+        w, h = C.c_int(), C.c_int()
+        _check(_lib.octvr_rig_out_size(self._h, C.byref(w), C.byref(h)))
+        return w.value, h.value
+
+    def __len__(self):
+        n = C.c_int()
+        _check(_lib.octvr_rig_num_inputs(self._h, C.byref(n)))
+        return n.value
+
+    def input(self, i):
+        """(roi, map1, map2, mask, seam_mask) as numpy copies."""
+        v = InputView()
+        _check(_lib.octvr_rig_get_input(self._h, i, C.byref(v)))
+        k = v.roi_w * v.roi_h
+        shape = (v.roi_h, v.roi_w)
+
+        def arr(ptr, ctype, dtype):
+            if not ptr:
+                return None
+            return np.ctypeslib.as_array(C.cast(ptr, C.POINTER(ctype)), shape=(k,)).astype(dtype).reshape(shape)
+
+        return ((v.roi_x, v.roi_y, v.roi_w, v.roi_h), arr(v.map1, C.c_float, np.float32),
+                arr(v.map2, C.c_float, np.float32), arr(v.mask, C.c_uint8, np.uint8),
+                arr(v.seam_mask, C.c_uint8, np.uint8))
+
+    def close(self):
+        if self._h and self._h.value:
+            _lib.octvr_rig_destroy(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Mapper:
+    """vr::Mapper on one device: stitch(inputs YUV420P, output YUV420P) with optional gain."""
+
+    def __init__(self, mt, in_sizes, blend=0, enable_gain=True, device=0, scale_output=(0, 0)):
+        n = len(in_sizes)
+        w = (C.c_int * n)(*[s[0] for s in in_sizes])
+        h = (C.c_int * n)(*[s[1] for s in in_sizes])
+        hd = _VP()
+        _check(_lib.octvr_mapper_create(mt._h, device, n, w, h, blend, int(enable_gain), scale_output[0],
+                                        scale_output[1], C.byref(hd)))
+        self._h = hd
+        self.n = n
+        self.device = device
+        self.out_size = mt.out_size
+
+    def stitch(self, inputs, output, gains=None, stream=None):
+        """inputs: list of uint8 cuda tensors (1.5H x W "Y over [U|V]"); output likewise."""
+        n = len(inputs)
+        ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
+        pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
+        g = None
+        ng = 0
+        if gains is not None:
+            g = (C.c_double * len(gains))(*gains)
+            ng = len(gains)
+        _check(_lib.octvr_mapper_stitch_yuv420p(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()),
+                                                output.stride(0), g, ng, _stream_ptr(stream)))
+
+    def gains(self):
+        g = (C.c_double * self.n)()
+        _check(_lib.octvr_mapper_gains(self._h, g, self.n))
+        return list(g)
+
+    def traffic_bytes(self):
+        b = C.c_double()
+        _check(_lib.octvr_mapper_traffic(self._h, C.byref(b)))
+        return b.value
+
+    def set_timing(self, enable=True):
+        _check(_lib.octvr_mapper_set_timing(self._h, int(enable)))
+
+    def kernel_time(self):
+        """(total device ms, launches) of the composite kernel since the last call (synchronizes)."""
+        t, k = C.c_double(), C.c_int()
+        _check(_lib.octvr_mapper_kernel_time(self._h, C.byref(t), C.byref(k)))
+        return t.value, k.value
+
+    def close(self):
+        if self._h and self._h.value:
+            _lib.octvr_mapper_destroy(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def remap_u8(src, map1, map2, scale_x, scale_y, out=None, stream=None):
+    """cv::remap INTER_LINEAR on cuda uint8 tensors (H x W [x cn]); maps are cuda float32 (mh x mw)."""
+    cn = 1 if src.dim() == 2 else src.shape[2]
+    mh, mw = map1.shape
+    if out is None:
+        out = torch.empty((mh, mw) if cn == 1 else (mh, mw, cn), dtype=torch.uint8, device=src.device)
+    _check(_lib.octvr_remap_u8(C.c_void_p(src.data_ptr()), src.shape[1], src.shape[0], src.stride(0), cn,
+                               C.c_void_p(map1.data_ptr()), C.c_void_p(map2.data_ptr()), mw, mh, map1.stride(0),
+                               scale_x, scale_y, C.c_void_p(out.data_ptr()), out.stride(0), _stream_ptr(stream)))
+    return out

@@ -1,0 +1,65 @@
+"""Synthetic rigs and frames of the benchmark configurations (BASELINE.json configs).
+
+Rig JSON follows the reference schema (producer modules/octvr/tools/ptx2json.py):
+`fullframe_fisheye` inputs with a centred circular crop, 200 deg hfov, no radial distortion.
+Frames are uniform-random bytes from splitmix64 (seed = 1000*rig + cam) in the "Y over [U|V]"
+YUV420P layout of mapper.hpp:432-440.
+"""
+import math
+
+import numpy as np
+
+HFOV_200 = 3.490658503988659
+
+
+def fisheye_rig(in_w, in_h, yaws, pitches=None, hfov=HFOV_200, circular=True):
+    pitches = pitches or [0.0] * len(yaws)
+    crop = [(in_w - in_h) // 2, (in_w + in_h) // 2, 0, in_h] if in_w >= in_h else [0, in_w, (in_h - in_w) // 2, (in_h + in_w) // 2]
+    inputs = []
+    for yaw, pitch in zip(yaws, pitches):
+        inputs.append({"type": "fullframe_fisheye", "options": {
+            "width": in_w, "height": in_h, "crop": {"rect": crop, "is_circular": circular},
+            "hfov": hfov, "center_dx": 0.0, "center_dy": 0.0, "radial": [0.0, 0.0, 0.0],
+            "rotation": {"roll": 0.0, "yaw": yaw, "pitch": pitch}}})
+    return {"output": {"type": "equirectangular", "options": {}}, "inputs": inputs}
+
+
+CONFIGS = {
+    # name: (rig json, out_w, out_h, in sizes)
+    "C1": lambda: (fisheye_rig(1920, 1080, [0.0, math.pi]), 4096, 2048, [(1920, 1080)] * 2),
+    "C2": lambda: (fisheye_rig(3840, 2160, [k * math.pi / 3 for k in range(6)]), 7680, 3840, [(3840, 2160)] * 6),
+    "C4": lambda: (fisheye_rig(3840, 2160, [k * math.pi / 3 for k in range(6)] + [k * math.pi / 3 + math.pi / 6 for k in range(6)],
+                               [0.6108652381980153] * 6 + [-0.6108652381980153] * 6, hfov=2.6179938779914944),
+                   15360, 7680, [(3840, 2160)] * 12),
+}
+
+
+def splitmix_bytes(seed, n):
+    k = np.arange(1, n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + k * np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return (z & np.uint64(0xFF)).astype(np.uint8)
+
+
+def yuv_frame(w, h, seed):
+    """(3h/2) x w uint8 YUV420P frame, Y over [U|V]."""
+    return splitmix_bytes(seed, w * h * 3 // 2).reshape(h * 3 // 2, w)
+
+
+def smooth_yuv_frame(w, h, seed):
+    """A frame with image-like structure (gradients + texture) — exercises gain estimation with
+    realistic overlaps rather than white noise."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    base = 128 + 60 * np.sin(xx / (17 + seed % 7)) * np.cos(yy / 23.0) + 0.02 * (xx - yy)
+    y = np.clip(base + rng.normal(0, 8, (h, w)), 0, 255).astype(np.uint8)
+    u = np.clip(128 + 30 * np.sin(xx[::2, ::2] / 41.0) + rng.normal(0, 4, (h // 2, w // 2)), 0, 255).astype(np.uint8)
+    v = np.clip(128 + 30 * np.cos(yy[::2, ::2] / 37.0) + rng.normal(0, 4, (h // 2, w // 2)), 0, 255).astype(np.uint8)
+    out = np.empty((h * 3 // 2, w), np.uint8)
+    out[:h] = y
+    out[h:, : w // 2] = u
+    out[h:, w // 2:] = v
+    return out

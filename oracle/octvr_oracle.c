@@ -322,6 +322,25 @@ static void project_pixel(const orc_camera* out, const orc_camera* in, double u,
     *y = py;
 }
 
+void orc_lut_rows(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, float* map1,
+                  float* map2, uint8_t* mask) {
+    for (int h = y0; h < y1; h++)
+        for (int w = 0; w < W; w++) {
+            double dx, dy;
+            project_pixel(out, in, (double)w / W, (double)h / H, &dx, &dy);
+            float x = (float)dx, y = (float)dy;
+            size_t idx = (size_t)(h - y0) * W + w;
+            if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f) {
+                mask[idx] = 0;
+                map1[idx] = map2[idx] = -1.0f;
+            } else {
+                mask[idx] = 255;
+                map1[idx] = x;
+                map2[idx] = y;
+            }
+        }
+}
+
 int orc_lut_build(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
                   uint8_t* mask, int use_roi, int roi[4]) {
     int min_h = H, max_h = 0, min_w = W, max_w = 0;
@@ -687,58 +706,151 @@ int orc_gain_feed(int n, const int* rois, const uint8_t* const* warped, const ui
 /* ------------------------------------------------------------------------------------------ */
 /* One Mapper::stitch frame, blend = 0 (mapper.cpp:193-312)                                    */
 /* ------------------------------------------------------------------------------------------ */
+/* Minimal row-parallel helper: fn(ctx, y0, y1) over [0, rows) split into T contiguous bands. */
+typedef void (*row_fn)(void* ctx, int y0, int y1);
+typedef struct { row_fn fn; void* ctx; int y0, y1; } row_job;
+static void* row_worker(void* a) { row_job* j = (row_job*)a; j->fn(j->ctx, j->y0, j->y1); return NULL; }
+static void parallel_rows(int T, int y0, int y1, row_fn fn, void* ctx) {
+    int rows = y1 - y0;
+    if (rows <= 0) return;
+    if (T > 64) T = 64;
+    if (T > rows) T = rows;
+    if (T <= 1) { fn(ctx, y0, y1); return; }
+    pthread_t th[64];
+    row_job jobs[64];
+    for (int t = 0; t < T; t++) {
+        jobs[t].fn = fn; jobs[t].ctx = ctx;
+        jobs[t].y0 = y0 + (int)((long)rows * t / T);
+        jobs[t].y1 = y0 + (int)((long)rows * (t + 1) / T);
+        pthread_create(&th[t], NULL, row_worker, &jobs[t]);
+    }
+    for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+}
+
 typedef struct {
     const orc_frame* f;
     int cam;
-    int y0, y1;
     uint8_t* rgba;
     uint8_t* warped;
-} remap_job;
+    float gain;
+    uint8_t* result;
+    int rb, re;
+} stage_ctx;
 
-static void* remap_worker(void* arg) {
-    remap_job* j = (remap_job*)arg;
-    const orc_frame* f = j->f;
-    int i = j->cam;
+static void yuv_rows(void* c, int y0, int y1) {
+    stage_ctx* s = (stage_ctx*)c;
+    const orc_frame* f = s->f;
+    int i = s->cam, w = f->in_w[i], h = f->in_h[i];
+    size_t pitch = f->in_pitch[i];
+    const uint8_t* yuv = f->in_yuv[i];
+    const uint8_t* U = yuv + (size_t)h * pitch;
+    const uint8_t* V = U + w / 2;
+    for (int y = y0; y < y1; y++)
+        for (int x = 0; x < w; x++) {
+            float Yf = (float)yuv[(size_t)y * pitch + x];
+            float Uf = (float)U[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
+            float Vf = (float)V[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
+            uint8_t* o = s->rgba + ((size_t)y * w + x) * 4;
+            o[0] = sat_u8_rne(Yf + 1.140f * Vf);
+            o[1] = sat_u8_rne(Yf - 0.394f * Uf - 0.581f * Vf);
+            o[2] = sat_u8_rne(Yf + 2.032f * Uf);
+            o[3] = 255;
+        }
+}
+
+static void remap_rows(void* c, int y0, int y1) {
+    stage_ctx* s = (stage_ctx*)c;
+    const orc_frame* f = s->f;
+    int i = s->cam;
     const int* r = f->rois + 4 * i;
-    orc_remap_u8(j->rgba, f->in_w[i], f->in_h[i], (size_t)f->in_w[i] * 4, 4, f->map1[i] + (size_t)j->y0 * r[2],
-                 f->map2[i] + (size_t)j->y0 * r[2], r[2], j->y1 - j->y0, r[2], (float)f->in_w[i], (float)f->in_h[i],
-                 j->warped + (size_t)j->y0 * r[2] * 4, (size_t)r[2] * 4);
-    return NULL;
+    orc_remap_u8(s->rgba, f->in_w[i], f->in_h[i], (size_t)f->in_w[i] * 4, 4, f->map1[i] + (size_t)y0 * r[2],
+                 f->map2[i] + (size_t)y0 * r[2], r[2], y1 - y0, r[2], (float)f->in_w[i], (float)f->in_h[i],
+                 s->warped + (size_t)y0 * r[2] * 4, (size_t)r[2] * 4);
+}
+
+/* mul_scalar_with_mask (stitching/src/cuda/exposure_compensate.cu:15-30) */
+static void gain_rows(void* c, int y0, int y1) {
+    stage_ctx* s = (stage_ctx*)c;
+    const orc_frame* f = s->f;
+    const int* r = f->rois + 4 * s->cam;
+    for (size_t k = (size_t)y0 * r[2]; k < (size_t)y1 * r[2]; k++) {
+        if (f->masks[s->cam][k] == 0) continue;
+        uint8_t* p = s->warped + 4 * k;
+        for (int ch = 0; ch < 4; ch++) p[ch] = sat_u8_rne((float)p[ch] * s->gain);
+    }
+}
+
+/* RGBA2RGB + copyTo(result(roi), mask) (mapper.cpp:268-277) */
+static void copy_rows(void* c, int y0, int y1) {
+    stage_ctx* s = (stage_ctx*)c;
+    const orc_frame* f = s->f;
+    const int* r = f->rois + 4 * s->cam;
+    size_t W = (size_t)f->out_w;
+    for (int y = y0; y < y1; y++) {
+        int oy = r[1] + y;
+        if (oy < s->rb || oy >= s->re) continue;
+        for (int x = 0; x < r[2]; x++) {
+            size_t k = (size_t)y * r[2] + x;
+            if (f->masks[s->cam][k] == 0) continue;
+            uint8_t* o = s->result + ((size_t)oy * W + r[0] + x) * 3;
+            const uint8_t* p = s->warped + 4 * k;
+            o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
+        }
+    }
+}
+
+/* own RGB -> YUV420P definition; rows [y0, y1) are quad rows (2 output rows each) */
+static void out_rows(void* c, int q0, int q1) {
+    stage_ctx* s = (stage_ctx*)c;
+    const orc_frame* f = s->f;
+    size_t W = (size_t)f->out_w;
+    uint8_t* Uo = f->out_yuv + (size_t)f->out_h * f->out_pitch;
+    uint8_t* Vo = Uo + f->out_w / 2;
+    for (int q = q0; q < q1; q++) {
+        int y = 2 * q;
+        for (int x = 0; x < f->out_w; x += 2) {
+            float us = 0.f, vs = 0.f;
+            for (int dy = 0; dy < 2; dy++)
+                for (int dx = 0; dx < 2; dx++) {
+                    const uint8_t* p = s->result + ((size_t)(y + dy) * W + x + dx) * 3;
+                    float R = p[0], G = p[1], B = p[2];
+                    float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
+                    f->out_yuv[(size_t)(y + dy) * f->out_pitch + x + dx] = sat_u8_rne(Yf);
+                    us = us + (0.492f * (B - Yf) + 128.f);
+                    vs = vs + (0.877f * (R - Yf) + 128.f);
+                }
+            Uo[(size_t)q * f->out_pitch + (x >> 1)] = sat_u8_rne(us * 0.25f);
+            Vo[(size_t)q * f->out_pitch + (x >> 1)] = sat_u8_rne(vs * 0.25f);
+        }
+    }
 }
 
 int orc_stitch_frame(const orc_frame* f) {
     int n = f->n;
     int T = f->threads > 0 ? f->threads : 1;
-    uint8_t** rgba = (uint8_t**)malloc(sizeof(void*) * n);
-    uint8_t** warped = (uint8_t**)malloc(sizeof(void*) * n);
     int rb = f->row_begin, re = f->row_end;
     if (re <= rb) { rb = 0; re = f->out_h; }
+    rb &= ~1;
+    re = (re + 1) & ~1;
+    if (re > f->out_h) re = f->out_h;
+    uint8_t** warped = (uint8_t**)calloc(n, sizeof(void*));
+    int estimate = f->enable_gain && !f->gains_in && n > 1;
     for (int i = 0; i < n; i++) {
         const int* r = f->rois + 4 * i;
-        rgba[i] = (uint8_t*)malloc((size_t)f->in_w[i] * f->in_h[i] * 4);
-        warped[i] = (uint8_t*)malloc((size_t)r[2] * r[3] * 4);
-        orc_yuv420_to_rgba(f->in_yuv[i], f->in_w[i], f->in_h[i], f->in_pitch[i], rgba[i], (size_t)f->in_w[i] * 4);
-        /* rows of this ROI that the requested output band needs (all rows when estimating gains) */
+        stage_ctx c = {f, i, NULL, NULL, 1.f, NULL, rb, re};
+        c.rgba = (uint8_t*)malloc((size_t)f->in_w[i] * f->in_h[i] * 4);
+        warped[i] = c.warped = (uint8_t*)calloc((size_t)r[2] * r[3] * 4, 1);
+        parallel_rows(T, 0, f->in_h[i], yuv_rows, &c);
+        /* ROI rows the output band needs (all rows when the feed needs whole warped images) */
         int y0 = 0, y1 = r[3];
-        if (!(f->enable_gain && !f->gains_in && n > 1)) {
+        if (!estimate) {
             y0 = rb - r[1]; y1 = re - r[1];
             if (y0 < 0) y0 = 0;
             if (y1 > r[3]) y1 = r[3];
             if (y1 < y0) y1 = y0;
         }
-        memset(warped[i], 0, (size_t)r[2] * r[3] * 4);
-        int rows = y1 - y0;
-        pthread_t th[64];
-        remap_job jobs[64];
-        int nt = T > 64 ? 64 : T;
-        for (int t = 0; t < nt; t++) {
-            jobs[t].f = f; jobs[t].cam = i; jobs[t].rgba = rgba[i]; jobs[t].warped = warped[i];
-            jobs[t].y0 = y0 + (int)((long)rows * t / nt);
-            jobs[t].y1 = y0 + (int)((long)rows * (t + 1) / nt);
-            if (nt > 1) pthread_create(&th[t], NULL, remap_worker, &jobs[t]);
-            else remap_worker(&jobs[t]);
-        }
-        if (nt > 1) for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+        parallel_rows(T, y0, y1, remap_rows, &c);
+        free(c.rgba);
     }
     double* gains = (double*)malloc(sizeof(double) * n);
     int use_gain = f->enable_gain && n > 1; /* mapper.cpp:78-82 */
@@ -746,61 +858,27 @@ int orc_stitch_frame(const orc_frame* f) {
         if (f->gains_in) memcpy(gains, f->gains_in, sizeof(double) * n);
         else if (orc_gain_feed(n, f->rois, (const uint8_t* const*)warped, f->masks, f->out_w, f->out_h, gains) != 0)
             for (int i = 0; i < n; i++) gains[i] = 1.0; /* cv::solve failure leaves gains_ undefined; use 1 */
-        /* GainCompensatorGPU::apply -> mul_scalar_with_mask (exposure_compensate.cu:15-30) */
         for (int i = 0; i < n; i++) {
             const int* r = f->rois + 4 * i;
-            float g = (float)gains[i];
-            for (size_t k = 0; k < (size_t)r[2] * r[3]; k++) {
-                if (f->masks[i][k] == 0) continue;
-                uint8_t* p = warped[i] + 4 * k;
-                for (int c = 0; c < 4; c++) p[c] = sat_u8_rne((float)p[c] * g);
-            }
+            stage_ctx c = {f, i, NULL, warped[i], (float)gains[i], NULL, rb, re};
+            parallel_rows(T, 0, r[3], gain_rows, &c);
         }
     } else {
         for (int i = 0; i < n; i++) gains[i] = 1.0;
     }
     if (f->gains_out) memcpy(f->gains_out, gains, sizeof(double) * n);
-    /* result = 0 ; RGBA2RGB + copyTo(result(roi), mask) in camera order (mapper.cpp:153-156,268-277) */
-    size_t W = (size_t)f->out_w;
-    uint8_t* result = (uint8_t*)calloc(W * f->out_h * 3, 1);
+    /* result = 0 (mapper.cpp:153-156), copies in camera order */
+    uint8_t* result = (uint8_t*)calloc((size_t)f->out_w * f->out_h * 3, 1);
     for (int i = 0; i < n; i++) {
         const int* r = f->rois + 4 * i;
-        for (int y = 0; y < r[3]; y++) {
-            int oy = r[1] + y;
-            if (oy < rb || oy >= re) continue;
-            for (int x = 0; x < r[2]; x++) {
-                size_t k = (size_t)y * r[2] + x;
-                if (f->masks[i][k] == 0) continue;
-                uint8_t* o = result + ((size_t)oy * W + r[0] + x) * 3;
-                const uint8_t* p = warped[i] + 4 * k;
-                o[0] = p[0]; o[1] = p[1]; o[2] = p[2];
-            }
-        }
+        stage_ctx c = {f, i, NULL, warped[i], 1.f, result, rb, re};
+        parallel_rows(T, 0, r[3], copy_rows, &c);
     }
-    /* cvtRGB24toYUV420P (mapper.cpp:296-306): only the requested rows (row band is even-aligned) */
-    int ob = rb & ~1, oe = (re + 1) & ~1;
-    if (oe > f->out_h) oe = f->out_h;
     {
-        /* convert band [ob, oe) into the output layout */
-        uint8_t* Uo = f->out_yuv + (size_t)f->out_h * f->out_pitch;
-        uint8_t* Vo = Uo + f->out_w / 2;
-        for (int y = ob; y < oe; y += 2)
-            for (int x = 0; x < f->out_w; x += 2) {
-                float us = 0.f, vs = 0.f;
-                for (int dy = 0; dy < 2; dy++)
-                    for (int dx = 0; dx < 2; dx++) {
-                        const uint8_t* p = result + ((size_t)(y + dy) * W + x + dx) * 3;
-                        float R = p[0], G = p[1], B = p[2];
-                        float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
-                        f->out_yuv[(size_t)(y + dy) * f->out_pitch + x + dx] = sat_u8_rne(Yf);
-                        us = us + (0.492f * (B - Yf) + 128.f);
-                        vs = vs + (0.877f * (R - Yf) + 128.f);
-                    }
-                Uo[(size_t)(y >> 1) * f->out_pitch + (x >> 1)] = sat_u8_rne(us * 0.25f);
-                Vo[(size_t)(y >> 1) * f->out_pitch + (x >> 1)] = sat_u8_rne(vs * 0.25f);
-            }
+        stage_ctx c = {f, 0, NULL, NULL, 1.f, result, rb, re};
+        parallel_rows(T, rb / 2, re / 2, out_rows, &c);
     }
-    for (int i = 0; i < n; i++) { free(rgba[i]); free(warped[i]); }
-    free(rgba); free(warped); free(gains); free(result);
+    for (int i = 0; i < n; i++) free(warped[i]);
+    free(warped); free(gains); free(result);
     return 0;
 }

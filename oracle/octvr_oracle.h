@@ -57,6 +57,10 @@ void orc_camera_fisheye(orc_camera* c, int width, int height, double fx, double 
 int orc_lut_build(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
                   uint8_t* mask, int use_roi, int roi[4]);
 
+/* The same per-pixel LUT rule for output rows [y0, y1) only (no ROI); buffers are (y1-y0) x W. */
+void orc_lut_rows(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, float* map1,
+                  float* map2, uint8_t* mask);
+
 /* initInterTab2D(INTER_LINEAR, fixpt) incl. its sum fix-up quirk (imgproc/src/imgwarp.cpp:211-280). */
 void orc_bilinear_tab(int16_t tab[1024 * 4]);
 

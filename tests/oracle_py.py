@@ -141,6 +141,17 @@ def lut_build(rig, out_w, out_h, use_roi=True):
     return res
 
 
+def lut_rows(rig_cam_out, rig_cam_in, W, H, y0, y1):
+    """Oracle LUT for output rows [y0, y1) of one input camera (full width, no ROI crop)."""
+    out = camera_from_json(rig_cam_out)
+    c = camera_from_json(rig_cam_in)
+    m1 = np.empty((y1 - y0, W), np.float32)
+    m2 = np.empty((y1 - y0, W), np.float32)
+    mk = np.empty((y1 - y0, W), np.uint8)
+    lib().orc_lut_rows(C.byref(out), C.byref(c), W, H, y0, y1, _p(m1), _p(m2), _p(mk))
+    return m1, m2, mk
+
+
 def remap_u8(src, map1, map2, scale_x, scale_y):
     src = np.ascontiguousarray(src)
     cn = 1 if src.ndim == 2 else src.shape[2]
@@ -279,9 +290,95 @@ def remap_kat_maps(per=256):
     return m1.reshape(1, -1).astype(np.float32), m2.reshape(1, -1).astype(np.float32)
 
 
+def rj_number(txt):
+    """rapidjson 1.0.2 default-flag number parsing (reader.h:1090-1276, strtod.h:26-44), so the oracle
+    sees the same doubles the reference sees."""
+    s, i, n = txt, 0, len(txt)
+    minus = s[0] == "-"
+    if minus:
+        i += 1
+    M64 = (1 << 64) - 1
+    iv, i64, use64, sig = 0, 0, False, 0
+    if s[i] == "0":
+        i += 1
+    else:
+        iv = ord(s[i]) - 48
+        i += 1
+        lim, lastd = (214748364, "8") if minus else (429496729, "5")
+        while i < n and s[i].isdigit():
+            if iv >= lim and (iv != lim or s[i] > lastd):
+                i64, use64 = iv, True
+                break
+            iv = iv * 10 + ord(s[i]) - 48
+            i += 1
+            sig += 1
+    use_d, d = False, 0.0
+    if use64:
+        lim, lastd = (0x0CCCCCCCCCCCCCCC, "8") if minus else (0x1999999999999999, "5")
+        while i < n and s[i].isdigit():
+            if i64 >= lim and (i64 != lim or s[i] > lastd):
+                d, use_d = float(i64), True
+                break
+            i64 = (i64 * 10 + ord(s[i]) - 48) & M64
+            i += 1
+            sig += 1
+    if use_d:
+        while i < n and s[i].isdigit():
+            d = d * 10 + (ord(s[i]) - 48)
+            i += 1
+    exp_frac = 0
+    if i < n and s[i] == ".":
+        i += 1
+        if not use_d:
+            if not use64:
+                i64 = iv
+            while i < n and s[i].isdigit():
+                if i64 > 0x1FFFFFFFFFFFFF:
+                    break
+                i64 = i64 * 10 + ord(s[i]) - 48
+                i += 1
+                exp_frac -= 1
+                if i64 != 0:
+                    sig += 1
+            d, use_d = float(i64), True
+        while i < n and s[i].isdigit():
+            if sig < 17:
+                d = d * 10.0 + (ord(s[i]) - 48)
+                exp_frac -= 1
+                if d > 0.0:
+                    sig += 1
+            i += 1
+    exp = 0
+    if i < n and s[i] in "eE":
+        i += 1
+        if not use_d:
+            d, use_d = float(i64 if use64 else iv), True
+        em = False
+        if s[i] == "+":
+            i += 1
+        elif s[i] == "-":
+            em, i = True, i + 1
+        exp = int(s[i:])
+        if em:
+            exp = -exp
+    if use_d:
+        p = exp + exp_frac
+        def fast(v, e):
+            return 0.0 if e < -308 else (v * float("1e%d" % e) if e >= 0 else v / float("1e%d" % -e))
+        d = fast(fast(d, -308), p + 308) if p < -308 else fast(d, p)
+        return -d if minus else d
+    v = i64 if use64 else iv
+    return float(-v if minus else v)
+
+
+def json_loads_rj(text):
+    """json.loads with rapidjson's (not always correctly rounded) number conversion."""
+    return json.loads(text, parse_float=rj_number)
+
+
 def load_rig(name):
     gdir = os.path.join(ROOT, "tests", "golden")
     with open(os.path.join(gdir, name + ".json")) as f:
-        rig = json.load(f)
+        rig = json_loads_rj(f.read())
     z = np.load(os.path.join(gdir, name + ".npz"))
     return rig, z

@@ -1,0 +1,234 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the reference goldens.
+
+Bars: integer / byte outputs bit-exact; the FP64 LUT bit-exact against the reference
+except where device libm (OCML) and glibc differ in the last ulp — counted and bounded below.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+RIGS = ["rigA", "rigB", "rigC", "rigD"]
+
+
+@pytest.fixture(scope="module")
+def ox(product_lib):
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    return product_lib
+
+
+def _cuda(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _rig_text(name):
+    with open(os.path.join(O.ROOT, "tests", "golden", name + ".json")) as f:
+        return f.read()
+
+
+@pytest.mark.parametrize("name", RIGS)
+def test_gpu_lut_build_vs_reference(ox, name):
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    mt = ox.MapperTemplate.from_json(_rig_text(name), W, H, use_roi=(name != "rigD"))
+    assert mt.out_size == (W, H) and len(mt) == len(z["rois"])
+    for i in range(len(mt)):
+        roi, m1, m2, mk, _ = mt.input(i)
+        assert roi == tuple(z["rois"][i])
+        g1, g2, gm = z[f"map1_{i}"], z[f"map2_{i}"], z[f"mask_{i}"]
+        d1 = m1.view(np.int32) != g1.view(np.int32)
+        d2 = m2.view(np.int32) != g2.view(np.int32)
+        dm = mk != gm
+        # OCML vs glibc: at most a handful of last-ulp f64 differences survive the f32 rounding
+        assert dm.sum() <= 2, (i, int(dm.sum()))
+        assert d1.sum() + d2.sum() <= max(4, m1.size // 20000), (i, int(d1.sum()), int(d2.sum()))
+        both = (~dm) & (gm > 0)
+        ulp1 = np.abs(m1.view(np.int32)[both].astype(np.int64) - g1.view(np.int32)[both])
+        ulp2 = np.abs(m2.view(np.int32)[both].astype(np.int64) - g2.view(np.int32)[both])
+        assert ulp1.max(initial=0) <= 1 and ulp2.max(initial=0) <= 1
+
+
+@pytest.mark.parametrize("name", RIGS)
+def test_gpu_remap_vs_reference(ox, name):
+    rig, z = O.load_rig(name)
+    tag = ord(name[3])
+    for i in range(len(z["rois"])):
+        o = rig["inputs"][i]["options"]
+        W, H = o["width"], o["height"]
+        m1, m2 = _cuda(z[f"map1_{i}"]), _cuda(z[f"map2_{i}"])
+        for cn, seed, key in ((1, 1000 * tag + i, "remap_c1"), (3, 5000 + 31 * tag + i, "remap_c3"),
+                              (4, 9000 + 17 * tag, "remap_c4")):
+            if f"{key}_{i}" not in z:
+                continue
+            img = _cuda(O.rand_img(W, H, cn, seed))
+            out = ox.remap_u8(img, m1, m2, float(W), float(H)).cpu().numpy()
+            assert np.array_equal(out.reshape(z[f"{key}_{i}"].shape), z[f"{key}_{i}"]), (i, key)
+
+
+def test_gpu_remap_all_fractional_codes(ox):
+    k = np.load(os.path.join(O.ROOT, "tests", "golden", "kats.npz"))
+    m1, m2 = O.remap_kat_maps()
+    out = ox.remap_u8(_cuda(k["remap_kat_src"]), _cuda(m1), _cuda(m2), 1.0, 1.0).cpu().numpy()
+    assert np.array_equal(out, k["remap_kat_out"])
+
+
+def test_gpu_remap_edges(ox):
+    # NaN / huge / negative coordinates and partially-outside taps (BORDER_CONSTANT, imgwarp.cpp:3931-3970)
+    src = O.rand_img(37, 23, 3, 99)
+    m1 = np.array([[np.nan, 1e30, -1e30, -0.5, 36.5, 36.99, -1.0, 0.0, 17.03125]], np.float32)
+    m2 = np.array([[3.0, 3.0, 3.0, 22.5, 22.5, -0.99, 5.0, 0.0, 11.96875]], np.float32)
+    want = O.remap_u8(src, m1, m2, 1.0, 1.0)
+    got = ox.remap_u8(_cuda(src), _cuda(m1), _cuda(m2), 1.0, 1.0).cpu().numpy()
+    assert np.array_equal(got, want)
+
+
+def _stitch_case(ox, name, frames_fn, gains):
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    sizes = [(rig["inputs"][i]["options"]["width"], rig["inputs"][i]["options"]["height"]) for i in range(n)]
+    frames = [frames_fn(w, h, 1000 * ord(name[3]) + i) for i, (w, h) in enumerate(sizes)]
+    maps1 = [z[f"map1_{i}"] for i in range(n)]
+    maps2 = [z[f"map2_{i}"] for i in range(n)]
+    masks = [z[f"mask_{i}"] for i in range(n)]
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks)
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True)
+    import torch
+    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    m.stitch([_cuda(f) for f in frames], out, gains=gains)
+    torch.cuda.synchronize()
+    g_gpu = m.gains()
+    want, g_orc = O.stitch_frame(frames, sizes, z["rois"].tolist(), maps1, maps2, masks, W, H, enable_gain=True,
+                                 gains=gains)
+    return out.cpu().numpy(), want, np.array(g_gpu), g_orc
+
+
+@pytest.mark.parametrize("name", RIGS)
+def test_gpu_stitch_fixed_gains_bit_exact(ox, name):
+    n = len(O.load_rig(name)[1]["rois"])
+    gains = [1.0 + 0.013 * k * (-1) ** k for k in range(n)]
+    got, want, g_gpu, _ = _stitch_case(ox, name, lambda w, h, s: O.rand_img(w, h * 3 // 2, 1, s), gains)
+    if n > 1:
+        np.testing.assert_array_equal(g_gpu, np.array(gains))
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("name", RIGS)
+def test_gpu_stitch_estimated_gains(ox, name):
+    from octvr_amd import synthetic
+    got, want, g_gpu, g_orc = _stitch_case(ox, name, synthetic.smooth_yuv_frame, None)
+    # deterministic block-ordered f64 sums vs the oracle's serial sums: last-bit differences only
+    np.testing.assert_allclose(g_gpu, g_orc, rtol=1e-12, atol=0)
+    if np.array_equal(g_gpu.astype(np.float32), g_orc.astype(np.float32)):
+        assert np.array_equal(got, want)
+
+
+def test_gpu_stitch_is_deterministic_and_stream_ordered(ox):
+    import torch
+    name = "rigB"
+    rig, z = O.load_rig(name)
+    n = len(z["rois"])
+    W, H = (int(v) for v in z["out_size"])
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), [z[f"map1_{i}"] for i in range(n)],
+                                       [z[f"map2_{i}"] for i in range(n)], [z[f"mask_{i}"] for i in range(n)])
+    m = ox.Mapper(mt, [(192, 108)] * n)
+    frames = [_cuda(O.rand_img(192, 162, 1, 7 + i)) for i in range(n)]
+    s = torch.cuda.Stream()
+    outs = []
+    for _ in range(3):
+        o = torch.empty((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+        with torch.cuda.stream(s):
+            m.stitch(frames, o, stream=s)
+        outs.append(o)
+    s.synchronize()
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+def test_gpu_mapper_argument_errors(ox):
+    rig, z = O.load_rig("rigA")
+    mt = ox.MapperTemplate.from_arrays(512, 256, z["rois"].tolist(), [z["map1_0"], z["map1_1"]],
+                                       [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]])
+    with pytest.raises(ox.OctvrError):
+        ox.Mapper(mt, [(256, 144)])  # wrong input count
+    with pytest.raises(ox.OctvrError) as e:
+        ox.Mapper(mt, [(256, 144)] * 2, blend=16)
+    assert e.value.code == -4
+    with pytest.raises(ox.OctvrError):
+        ox.Mapper(mt, [(255, 144)] * 2)  # odd size: not YUV420
+
+
+def test_gpu_single_input_disables_gain(ox):
+    # mapper.cpp:78-82
+    import torch
+    rig, z = O.load_rig("rigD")
+    mt = ox.MapperTemplate.from_arrays(256, 128, [z["rois"][0].tolist()], [z["map1_0"]], [z["map2_0"]], [z["mask_0"]])
+    m = ox.Mapper(mt, [(320, 240)], enable_gain=True)
+    f = O.rand_img(320, 360, 1, 5)
+    out = torch.zeros((192, 256), dtype=torch.uint8, device="cuda")
+    m.stitch([_cuda(f)], out)
+    want, _ = O.stitch_frame([f], [(320, 240)], [z["rois"][0].tolist()], [z["map1_0"]], [z["map2_0"]], [z["mask_0"]],
+                             256, 128, enable_gain=True)
+    assert m.gains() == [1.0]
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+# ------------------------------------------------------------------------------------------------
+# Full benchmark size (config C2: 6 x 3840x2160 -> 7680x3840): LUT rows vs the oracle, and the
+# stitched output on row bands (poles, equator, seams) vs the oracle fed the GPU's gains.
+# ------------------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c2(ox):
+    from octvr_amd import synthetic
+    rig, W, H, sizes = synthetic.CONFIGS["C2"]()
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
+    return rig, W, H, sizes, mt
+
+
+def test_gpu_c2_lut_rows_vs_oracle(ox, c2):
+    rig, W, H, sizes, mt = c2
+    bad = 0
+    total = 0
+    for i in (0, 3):
+        roi, m1, m2, mk, _ = mt.input(i)
+        for y0 in (0, 1237, 1919, 3830):
+            r1, r2, rk = O.lut_rows(rig["output"], rig["inputs"][i], W, H, y0, y0 + 8)
+            sl = slice(y0 - roi[1], y0 - roi[1] + 8)
+            g1 = np.zeros_like(r1) - 1
+            g1[:, roi[0]:roi[0] + roi[2]] = m1[sl]
+            g2 = np.zeros_like(r2) - 1
+            g2[:, roi[0]:roi[0] + roi[2]] = m2[sl]
+            bad += int((g1.view(np.int32) != r1.view(np.int32)).sum() + (g2.view(np.int32) != r2.view(np.int32)).sum())
+            total += r1.size * 2
+    assert bad <= max(4, total // 20000), (bad, total)
+
+
+def test_gpu_c2_stitch_row_bands_vs_oracle(ox, c2):
+    import torch
+    from octvr_amd import synthetic
+    rig, W, H, sizes, mt = c2
+    n = len(sizes)
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True)
+    frames = [synthetic.smooth_yuv_frame(w, h, 2000 + i) for i, (w, h) in enumerate(sizes)]
+    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    m.stitch([_cuda(f) for f in frames], out)
+    torch.cuda.synchronize()
+    g = m.gains()
+    assert all(0.5 < x < 2.0 for x in g)
+    got = out.cpu().numpy()
+    rois, maps1, maps2, masks = [], [], [], []
+    for i in range(n):
+        roi, m1, m2, mk, _ = mt.input(i)
+        rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk)
+    for band in ((0, 16), (1904, 1936), (3824, 3840)):
+        want, _ = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=g,
+                                 threads=8, row_band=band)
+        y0, y1 = band
+        assert np.array_equal(got[y0:y1], want[y0:y1]), band
+        assert np.array_equal(got[H + y0 // 2:H + y1 // 2], want[H + y0 // 2:H + y1 // 2]), band
