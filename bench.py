@@ -165,6 +165,7 @@ def main():
                      "survey_b_alg_bytes": survey_b_alg,
                      "survey_b_alg_frac_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
         "gains": [round(g, 6) for g in gains],
+        "mapper": m.info(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H)

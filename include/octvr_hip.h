@@ -105,6 +105,8 @@ int octvr_mapper_traffic(const octvr_mapper* mapper, double* bytes_per_frame);
  * recorded events, returns the summed device time and launch count, and resets the log. */
 int octvr_mapper_set_timing(octvr_mapper* mapper, int enable);
 int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launches);
+/* Build-time statistics of a mapper as a JSON object (tiles, wide tiles, staged bytes, gain samples). */
+int octvr_mapper_info(const octvr_mapper* mapper, char* buf, size_t len);
 void octvr_mapper_destroy(octvr_mapper* mapper);
 
 /* ---- standalone kernels --------------------------------------------------------------------- */

@@ -80,30 +80,56 @@ __device__ __forceinline__ void yuv_to_rgb(int y, int u, int v, int& r, int& g, 
 // Bilinear fixed-point sample of one camera at a composite entry: the cv::remap INTER_LINEAR /
 // BORDER_CONSTANT rule (imgwarp.cpp:3812-4030) on the RGBA image NPP would have produced.
 // Out-of-image taps contribute 0 (cval); result per channel = sat_u8((sum + 2^14) >> 15).
-__device__ __forceinline__ void sample_rgb(const SourceFrame& f, uint32_t xy, uint32_t code, const short* tab,
-                                           int& r, int& g, int& b) {
+// Branch-free: out-of-image taps read a clamped (in-bounds) address with weight 0, and an invalid
+// entry (no camera) gets all-zero weights, so every load of every pixel can be issued up front.
+struct Taps {
+    uint8_t y[4], u[4], v[4];
+    int w[4];
+};
+
+__device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, const short* tab,
+                                            Taps& t) {
+    const bool valid = (code & 0x8000u) != 0;
+    const SourceFrame& f = fs.f[(code >> 10) & 31u];
     const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
-    const int a = (int)(code & 1023u);
-    const short* w = tab + a * 4;
-    const int64_t pitch = f.pitch;
+    const short* w = tab + (code & 1023u) * 4;
+    const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
+    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);  // sx <= W_in (X may round up to W)
+    const int x1 = inx ? sx + 1 : x0, y1 = iny ? sy + 1 : y0;
+    const bool in0 = valid && sx < f.w && sy < f.h;
+    t.w[0] = in0 ? w[0] : 0;
+    t.w[1] = (valid && inx && sy < f.h) ? w[1] : 0;
+    t.w[2] = (valid && iny && sx < f.w) ? w[2] : 0;
+    t.w[3] = (valid && inx && iny) ? w[3] : 0;
+    const int64_t p = f.pitch;
     const uint8_t* Y = f.yuv;
-    const uint8_t* U = f.yuv + (int64_t)f.h * pitch;
+    const uint8_t* U = Y + (int64_t)f.h * p;
     const uint8_t* V = U + (f.w >> 1);
+    const int64_t r0 = (int64_t)y0 * p, r1 = (int64_t)y1 * p;
+    const int64_t c0 = (int64_t)(y0 >> 1) * p, c1 = (int64_t)(y1 >> 1) * p;
+    t.y[0] = Y[r0 + x0];
+    t.y[1] = Y[r0 + x1];
+    t.y[2] = Y[r1 + x0];
+    t.y[3] = Y[r1 + x1];
+    t.u[0] = U[c0 + (x0 >> 1)];
+    t.u[1] = U[c0 + (x1 >> 1)];
+    t.u[2] = U[c1 + (x0 >> 1)];
+    t.u[3] = U[c1 + (x1 >> 1)];
+    t.v[0] = V[c0 + (x0 >> 1)];
+    t.v[1] = V[c0 + (x1 >> 1)];
+    t.v[2] = V[c1 + (x0 >> 1)];
+    t.v[3] = V[c1 + (x1 >> 1)];
+}
+
+__device__ __forceinline__ void blend_taps(const Taps& t, int& r, int& g, int& b) {
     int ar = 0, ag = 0, ab = 0;
 #pragma unroll
-    for (int t = 0; t < 4; t++) {
-        const int tx = sx + (t & 1), ty = sy + (t >> 1);
-        if (tx < f.w && ty < f.h) {  // sx, sy >= 0 for every valid entry
-            int yy = Y[(int64_t)ty * pitch + tx];
-            int uu = U[(int64_t)(ty >> 1) * pitch + (tx >> 1)];
-            int vv = V[(int64_t)(ty >> 1) * pitch + (tx >> 1)];
-            int cr, cg, cb;
-            yuv_to_rgb(yy, uu, vv, cr, cg, cb);
-            const int wt = w[t];
-            ar += cr * wt;
-            ag += cg * wt;
-            ab += cb * wt;
-        }
+    for (int k = 0; k < 4; k++) {
+        int cr, cg, cb;
+        yuv_to_rgb(t.y[k], t.u[k], t.v[k], cr, cg, cb);
+        ar += cr * t.w[k];
+        ag += cg * t.w[k];
+        ab += cb * t.w[k];
     }
     r = min(max((ar + (1 << 14)) >> 15, 0), 255);
     g = min(max((ag + (1 << 14)) >> 15, 0), 255);
@@ -209,34 +235,44 @@ hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H
 }
 
 // ---------------------------------------------------------------------------------------------
-// Gain feed (GainCompensatorGPU::feed, exposure_compensate.cpp:223-263): for every overlap pixel of
-// every camera pair (i<j), the warped working-scale pixel of both cameras (nearest resize of the
-// warped ROI, mapper.cpp:234-237, pre-resolved on the host into sample entries), its f32 RGB norm
-// (elementNorm, core/src/cuda/gpu_mat.cu:443-449) and the masked f64 sums (calcSum).  One chunk per
-// block; partial sums go to `partials` in chunk order (deterministic, no atomics).
+// Gain feed (GainCompensatorGPU::feed, exposure_compensate.cpp:223-263).  The working-scale images
+// are nearest resizes of the warped ROIs (mapper.cpp:234-237); the host pre-resolves every working
+// pixel that lies in some pair intersection into a sample entry of its camera, so one thread per
+// sample computes the warped pixel's f32 norm (elementNorm, core/src/cuda/gpu_mat.cu:443-449).
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const int16_t* tab,
-                                                        const CompositeEntry* sa, const CompositeEntry* sb,
-                                                        const GainChunk* chunks, double* partials) {
+__global__ void __launch_bounds__(256) gain_norm_kernel(FrameSet frames, const int16_t* tab,
+                                                        const CompositeEntry* samples, int n, float* norms) {
     __shared__ short s_tab[1024 * 4];
-    __shared__ double s_red[2][256];
     load_table_lds(tab, s_tab);
+    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+        const CompositeEntry e = samples[k];
+        Taps t;
+        gather_taps(frames, e.xy, e.code, s_tab, t);
+        int r, g, b;
+        blend_taps(t, r, g, b);
+        norms[k] = sqrtf((float)(r * r + g * g + b * b));
+    }
+}
+
+hipError_t launch_gain_norm(const FrameSet& frames, const int16_t* tab, const CompositeEntry* samples, int n_samples,
+                            float* norms, hipStream_t s) {
+    if (n_samples <= 0) return hipSuccess;
+    const int blocks = std::min((n_samples + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(gain_norm_kernel, dim3(blocks), dim3(256), 0, s, frames, tab, samples, n_samples, norms);
+    return hipGetLastError();
+}
+
+// calcSum over the intersection mask (cudaarithm calcSum, f32 -> f64): one chunk per block, fixed
+// reduction order, partial sums stored in chunk order (deterministic, no atomics).
+__global__ void __launch_bounds__(256) gain_pairs_kernel(const float* norms, const uint2* idx, const GainChunk* chunks,
+                                                         double* partials) {
+    __shared__ double s_red[2][256];
     const GainChunk ch = chunks[blockIdx.x];
     double s1 = 0.0, s2 = 0.0;
     for (int e = ch.begin + (int)threadIdx.x; e < ch.end; e += blockDim.x) {
-        const CompositeEntry a = sa[e], b = sb[e];
-        int r, g, bl;
-        float na = 0.f, nb = 0.f;
-        if (a.code & 0x8000u) {
-            sample_rgb(frames.f[(a.code >> 10) & 31u], a.xy, a.code, s_tab, r, g, bl);
-            na = sqrtf((float)(r * r + g * g + bl * bl));
-        }
-        if (b.code & 0x8000u) {
-            sample_rgb(frames.f[(b.code >> 10) & 31u], b.xy, b.code, s_tab, r, g, bl);
-            nb = sqrtf((float)(r * r + g * g + bl * bl));
-        }
-        s1 += (double)na;
-        s2 += (double)nb;
+        const uint2 p = idx[e];
+        s1 += (double)norms[p.x];
+        s2 += (double)norms[p.y];
     }
     s_red[0][threadIdx.x] = s1;
     s_red[1][threadIdx.x] = s2;
@@ -254,51 +290,109 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const i
     }
 }
 
-hipError_t launch_gain_feed(const FrameSet& frames_dev, const int16_t* tab, const CompositeEntry* samples_a,
-                            const CompositeEntry* samples_b, const GainChunk* chunks, int n_chunks,
-                            double* partials, hipStream_t s) {
+hipError_t launch_gain_pairs(const float* norms, const uint2* pair_idx, const GainChunk* chunks, int n_chunks,
+                             double* partials, hipStream_t s) {
     if (n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames_dev, tab, samples_a, samples_b,
-                       chunks, partials);
+    hipLaunchKernelGGL(gain_pairs_kernel, dim3(n_chunks), dim3(256), 0, s, norms, pair_idx, chunks, partials);
     return hipGetLastError();
 }
 
-// cv::solve (lapack.cpp:1050-1275): closed forms for n <= 3, LUImpl (matrix_decomp.cpp:50-110) above.
-__device__ bool solve_small(double* A, double* b, int n, double* x) {
-#define Sd(y, xx) A[(y) * n + (xx)]
-    if (n == 1) {
-        double d = Sd(0, 0);
+// cv::solve (lapack.cpp:1050-1275) with the matrix in registers: closed forms for n <= 3, LUImpl
+// (matrix_decomp.cpp:50-110) above, instantiated per n so every index is static.
+template <int N>
+__device__ bool lu_solve(double (&A)[N * N], double (&b)[N]) {
+    const double eps = DBL_EPSILON * 100;
+#pragma unroll
+    for (int i = 0; i < N; i++) {
+        int k = i;
+        double best = fabs(A[i * N + i]);
+#pragma unroll
+        for (int j = i + 1; j < N; j++) {
+            const double v = fabs(A[j * N + i]);
+            if (v > best) {
+                best = v;
+                k = j;
+            }
+        }
+        if (best < eps) return false;
+#pragma unroll
+        for (int j = i + 1; j < N; j++) {  // row swap i <-> k as selects (static indices only)
+            const bool sw = (j == k);
+#pragma unroll
+            for (int c = i; c < N; c++) {
+                const double ai = A[i * N + c], aj = A[j * N + c];
+                A[i * N + c] = sw ? aj : ai;
+                A[j * N + c] = sw ? ai : aj;
+            }
+            const double bi = b[i], bj = b[j];
+            b[i] = sw ? bj : bi;
+            b[j] = sw ? bi : bj;
+        }
+        const double d = -1 / A[i * N + i];
+#pragma unroll
+        for (int j = i + 1; j < N; j++) {
+            const double alpha = A[j * N + i] * d;
+#pragma unroll
+            for (int c = i + 1; c < N; c++) A[j * N + c] += alpha * A[i * N + c];
+            b[j] += alpha * b[i];
+        }
+        A[i * N + i] = -d;
+    }
+#pragma unroll
+    for (int i = N - 1; i >= 0; i--) {
+        double s = b[i];
+#pragma unroll
+        for (int c = i + 1; c < N; c++) s -= A[i * N + c] * b[c];
+        b[i] = s * A[i * N + i];
+    }
+    return true;
+}
+
+template <int N>
+__device__ bool solve_fixed(const double* Ain, const double* bin, double* x) {
+    double A[N * N], b[N];
+#pragma unroll
+    for (int k = 0; k < N * N; k++) A[k] = Ain[k];
+#pragma unroll
+    for (int k = 0; k < N; k++) b[k] = bin[k];
+#define Sd(y, xx) A[(y) * N + (xx)]
+    if constexpr (N == 1) {
+        const double d = Sd(0, 0);
         if (d == 0.) return false;
         x[0] = b[0] / d;
         return true;
-    }
-    if (n == 2) {
+    } else if constexpr (N == 2) {
         double d = (double)Sd(0, 0) * Sd(1, 1) - (double)Sd(0, 1) * Sd(1, 0);
         if (d == 0.) return false;
         d = 1. / d;
-        double t = (b[0] * Sd(1, 1) - b[1] * Sd(0, 1)) * d;
+        const double t = (b[0] * Sd(1, 1) - b[1] * Sd(0, 1)) * d;
         x[1] = (b[1] * Sd(0, 0) - b[0] * Sd(1, 0)) * d;
         x[0] = t;
         return true;
-    }
-    if (n == 3) {
+    } else if constexpr (N == 3) {
         double d = Sd(0, 0) * ((double)Sd(1, 1) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 1)) -
                    Sd(0, 1) * ((double)Sd(1, 0) * Sd(2, 2) - (double)Sd(1, 2) * Sd(2, 0)) +
                    Sd(0, 2) * ((double)Sd(1, 0) * Sd(2, 1) - (double)Sd(1, 1) * Sd(2, 0));
         if (d == 0.) return false;
         d = 1. / d;
-        double t0 = ((Sd(1, 1) * Sd(2, 2) - Sd(1, 2) * Sd(2, 1)) * b[0] + (Sd(0, 2) * Sd(2, 1) - Sd(0, 1) * Sd(2, 2)) * b[1] +
-                     (Sd(0, 1) * Sd(1, 2) - Sd(0, 2) * Sd(1, 1)) * b[2]) * d;
-        double t1 = ((Sd(1, 2) * Sd(2, 0) - Sd(1, 0) * Sd(2, 2)) * b[0] + (Sd(0, 0) * Sd(2, 2) - Sd(0, 2) * Sd(2, 0)) * b[1] +
-                     (Sd(0, 2) * Sd(1, 0) - Sd(0, 0) * Sd(1, 2)) * b[2]) * d;
-        double t2 = ((Sd(1, 0) * Sd(2, 1) - Sd(1, 1) * Sd(2, 0)) * b[0] + (Sd(0, 1) * Sd(2, 0) - Sd(0, 0) * Sd(2, 1)) * b[1] +
-                     (Sd(0, 0) * Sd(1, 1) - Sd(0, 1) * Sd(1, 0)) * b[2]) * d;
-        x[0] = t0;
-        x[1] = t1;
-        x[2] = t2;
+        x[0] = ((Sd(1, 1) * Sd(2, 2) - Sd(1, 2) * Sd(2, 1)) * b[0] + (Sd(0, 2) * Sd(2, 1) - Sd(0, 1) * Sd(2, 2)) * b[1] +
+                (Sd(0, 1) * Sd(1, 2) - Sd(0, 2) * Sd(1, 1)) * b[2]) * d;
+        x[1] = ((Sd(1, 2) * Sd(2, 0) - Sd(1, 0) * Sd(2, 2)) * b[0] + (Sd(0, 0) * Sd(2, 2) - Sd(0, 2) * Sd(2, 0)) * b[1] +
+                (Sd(0, 2) * Sd(1, 0) - Sd(0, 0) * Sd(1, 2)) * b[2]) * d;
+        x[2] = ((Sd(1, 0) * Sd(2, 1) - Sd(1, 1) * Sd(2, 0)) * b[0] + (Sd(0, 1) * Sd(2, 0) - Sd(0, 0) * Sd(2, 1)) * b[1] +
+                (Sd(0, 0) * Sd(1, 1) - Sd(0, 1) * Sd(1, 0)) * b[2]) * d;
+        return true;
+    } else {
+        if (!lu_solve<N>(A, b)) return false;
+#pragma unroll
+        for (int k = 0; k < N; k++) x[k] = b[k];
         return true;
     }
 #undef Sd
+}
+
+// Same LUImpl on a matrix held in LDS (n = 9..16: too large to keep in registers).
+__device__ bool lu_solve_lds(double* A, double* b, int n, double* x) {
     const double eps = DBL_EPSILON * 100;
     for (int i = 0; i < n; i++) {
         int k = i;
@@ -307,78 +401,119 @@ __device__ bool solve_small(double* A, double* b, int n, double* x) {
         if (fabs(A[k * n + i]) < eps) return false;
         if (k != i) {
             for (int j = i; j < n; j++) {
-                double t = A[i * n + j];
+                const double t = A[i * n + j];
                 A[i * n + j] = A[k * n + j];
                 A[k * n + j] = t;
             }
-            double t = b[i];
+            const double t = b[i];
             b[i] = b[k];
             b[k] = t;
         }
-        double d = -1 / A[i * n + i];
+        const double d = -1 / A[i * n + i];
         for (int j = i + 1; j < n; j++) {
-            double alpha = A[j * n + i] * d;
-            for (int kk = i + 1; kk < n; kk++) A[j * n + kk] += alpha * A[i * n + kk];
+            const double alpha = A[j * n + i] * d;
+            for (int c = i + 1; c < n; c++) A[j * n + c] += alpha * A[i * n + c];
             b[j] += alpha * b[i];
         }
         A[i * n + i] = -d;
     }
     for (int i = n - 1; i >= 0; i--) {
         double s = b[i];
-        for (int kk = i + 1; kk < n; kk++) s -= A[i * n + kk] * b[kk];
+        for (int c = i + 1; c < n; c++) s -= A[i * n + c] * b[c];
         b[i] = s * A[i * n + i];
     }
     for (int i = 0; i < n; i++) x[i] = b[i];
     return true;
 }
 
-// I(i,j), A, b assembly (exposure_compensate.cpp:265-296) and the solve, on one lane.
-__global__ void gain_solve_kernel(const double* partials, const GainChunk* chunks, int n_chunks,
-                                  const int32_t* pair_ij, const int32_t* N, int n, double* gains) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    double I[kMaxCams * kMaxCams];
-    double A[kMaxCams * kMaxCams];
-    double b[kMaxCams], x[kMaxCams];
-    for (int k = 0; k < n * n; k++) I[k] = 0.0;
-    // chunks of one pair are contiguous and in order
-    int c = 0;
-    const int n_pairs = n * (n - 1) / 2;
-    for (int p = 0; p < n_pairs; p++) {
-        const int i = pair_ij[2 * p], j = pair_ij[2 * p + 1];
-        double s1 = 0.0, s2 = 0.0;
-        bool any = false;
-        while (c < n_chunks && chunks[c].pair == p) {
-            s1 += partials[2 * c];
-            s2 += partials[2 * c + 1];
-            any = true;
-            c++;
-        }
-        const int nij = N[i * n + j];
-        if (nij > 0 && any) {
-            I[i * n + j] = s1 / nij;
-            I[j * n + i] = s2 / nij;
-        }
+__device__ bool solve_dispatch(double* A, double* b, int n, double* x) {
+    switch (n) {
+#define CASE(K) \
+    case K:     \
+        return solve_fixed<K>(A, b, x);
+        CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+        default:
+            return n <= 16 ? lu_solve_lds(A, b, n, x) : false;
     }
-    const double alpha = 0.01, beta = 100;
-    for (int k = 0; k < n * n; k++) A[k] = 0.0;
-    for (int i = 0; i < n; i++) b[i] = 0.0;
-    for (int i = 0; i < n; i++)
-        for (int j = 0; j < n; j++) {
-            const int Nij = N[i * n + j];
-            b[i] += beta * Nij;
-            A[i * n + i] += beta * Nij;
-            if (j == i) continue;
-            A[i * n + i] += 2 * alpha * I[i * n + j] * I[i * n + j] * Nij;
-            A[i * n + j] -= 2 * alpha * I[i * n + j] * I[j * n + i] * Nij;
-        }
-    if (!solve_small(A, b, n, x))
-        for (int i = 0; i < n; i++) x[i] = 1.0;
-    for (int i = 0; i < n; i++) gains[i] = x[i];
 }
 
-hipError_t launch_gain_solve(const double* partials, const GainChunk* chunks, int n_chunks, const int32_t* pair_ij,
-                             const int32_t* N, int n, double* gains, hipStream_t s) {
-    hipLaunchKernelGGL(gain_solve_kernel, dim3(1), dim3(64), 0, s, partials, chunks, n_chunks, pair_ij, N, n, gains);
+// One workgroup: the chunk partials, their pair ids and N are first staged into LDS by all lanes
+// (parallel loads instead of a dependent chain on one lane), lane p then sums pair p's partials in
+// chunk order, and lane 0 assembles I, A, b (exposure_compensate.cpp:265-296) and solves.
+constexpr int kSolveMaxChunks = 4096;
+__global__ void __launch_bounds__(256) gain_solve_kernel(const double* partials, const GainChunk* chunks, int n_chunks,
+                                                         const int32_t* N, int n, double* gains) {
+    __shared__ double s_part[2 * kSolveMaxChunks];
+    __shared__ int s_pair[kSolveMaxChunks];
+    __shared__ int s_N[16 * 16];
+    __shared__ double s_I[16 * 16];
+    __shared__ double s_A[16 * 16];
+    __shared__ double s_b[16];
+    __shared__ double s_x[16];
+    const int tid = threadIdx.x;
+    const int n_pairs = n * (n - 1) / 2;
+    const int nc = min(n_chunks, kSolveMaxChunks);
+    for (int c = tid; c < nc; c += blockDim.x) {
+        s_part[2 * c] = partials[2 * c];
+        s_part[2 * c + 1] = partials[2 * c + 1];
+        s_pair[c] = chunks[c].pair;
+    }
+    for (int k = tid; k < n * n; k += blockDim.x) {
+        s_N[k] = N[k];
+        s_I[k] = 0.0;
+    }
+    __syncthreads();
+    for (int p = tid; p < n_pairs; p += blockDim.x) {
+        int i = 0, rem = p;  // pair p = (i, j), i < j, in the constructor's loop order
+        while (rem >= n - 1 - i) {
+            rem -= n - 1 - i;
+            i++;
+        }
+        const int j = i + 1 + rem;
+        // chunks are grouped by pair in pair order: binary search for the first chunk of p
+        int lo = 0, hi = nc;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_pair[mid] < p) lo = mid + 1;
+            else hi = mid;
+        }
+        double s1 = 0.0, s2 = 0.0;
+        bool any = false;
+        for (int c = lo; c < nc && s_pair[c] == p; c++) {
+            s1 += s_part[2 * c];
+            s2 += s_part[2 * c + 1];
+            any = true;
+        }
+        if (any) {
+            const int nij = s_N[i * n + j];
+            s_I[i * n + j] = s1 / nij;
+            s_I[j * n + i] = s2 / nij;
+        }
+    }
+    __syncthreads();
+    if (tid != 0) return;
+    const double alpha = 0.01, beta = 100;
+    for (int k = 0; k < n * n; k++) s_A[k] = 0.0;
+    for (int i = 0; i < n; i++) s_b[i] = 0.0;
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            const int Nij = s_N[i * n + j];
+            s_b[i] += beta * Nij;
+            s_A[i * n + i] += beta * Nij;
+            if (j == i) continue;
+            s_A[i * n + i] += 2 * alpha * s_I[i * n + j] * s_I[i * n + j] * Nij;
+            s_A[i * n + j] -= 2 * alpha * s_I[i * n + j] * s_I[j * n + i] * Nij;
+        }
+    if (!solve_dispatch(s_A, s_b, n, s_x))
+        for (int i = 0; i < n; i++) s_x[i] = 1.0;
+    for (int i = 0; i < n; i++) gains[i] = s_x[i];
+}
+
+hipError_t launch_gain_solve(const double* partials, const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
+                             double* gains, hipStream_t s) {
+    if (n_chunks > kSolveMaxChunks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gain_solve_kernel, dim3(1), dim3(256), 0, s, partials, chunks, n_chunks, N, n, gains);
     return hipGetLastError();
 }
 
@@ -397,82 +532,193 @@ hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Per-frame stitch, blend = 0: for every 2x2 output quad, the winning camera of each pixel is
-// sampled from its YUV420P source (YUV->RGB per tap, 15-bit bilinear), gain-scaled
-// (mul_scalar_with_mask, exposure_compensate.cu:15-30: sat_u8(px * (float)g)), and the quad is
-// written as YUV420P (own BT.601, stands in for NPP nppiRGBToYUV420_8u_C3P3R).
-// Grid-stride over quads; each XCD (blockIdx % 8) takes a contiguous band of output rows so the
-// source footprint of its tiles stays in that XCD's L2.
+// Per-frame stitch, blend = 0 (mapper.cpp:219-306 with the copy chain resolved into the tiled LUT):
+// for every 2x2 output quad the winning camera of each pixel is sampled from its YUV420P source
+// (YUV->RGB per tap, 15-bit bilinear), gain-scaled (mul_scalar_with_mask, exposure_compensate.cu:
+// 15-30: sat_u8(px * (float)g)) and written as YUV420P (own BT.601 in place of NPP RGBToYUV420).
+// One workgroup per 128x8 tile; staged tiles read every tap from LDS (see kernels.hpp).  Tiles are
+// walked grid-stride; blocks b, b+8, ... (one XCD under round-robin dispatch) take a contiguous
+// band of tiles so their source boxes share that XCD's L2.
 // ---------------------------------------------------------------------------------------------
-constexpr int kQuadsX = 64;   // quads per tile row (128 output pixels)
-constexpr int kQuadsY = 4;    // quad rows per tile (8 output rows)
+__device__ __forceinline__ void finish_quad(const int (&rgb)[4][3], const uint32_t (&cam)[4], const float* s_gain,
+                                            uint8_t* out, uint8_t* outU, uint8_t* outV, int64_t out_pitch, int x,
+                                            int y, int qxg, int qyg) {
+    int Yo[4];
+    float us = 0.f, vs = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const float gf = s_gain[cam[p]];  // a black pixel stays black under any gain
+        const int r = sat_u8_rne((float)rgb[p][0] * gf);
+        const int g = sat_u8_rne((float)rgb[p][1] * gf);
+        const int b = sat_u8_rne((float)rgb[p][2] * gf);
+        const float R = (float)r, G = (float)g, B = (float)b;
+        const float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
+        Yo[p] = sat_u8_rne(Yf);
+        us = us + (0.492f * (B - Yf) + 128.f);
+        vs = vs + (0.877f * (R - Yf) + 128.f);
+    }
+    *reinterpret_cast<uint16_t*>(out + (int64_t)y * out_pitch + x) = (uint16_t)(Yo[0] | (Yo[1] << 8));
+    *reinterpret_cast<uint16_t*>(out + (int64_t)(y + 1) * out_pitch + x) = (uint16_t)(Yo[2] | (Yo[3] << 8));
+    outU[(int64_t)qyg * out_pitch + qxg] = (uint8_t)sat_u8_rne(us * 0.25f);
+    outV[(int64_t)qyg * out_pitch + qxg] = (uint8_t)sat_u8_rne(vs * 0.25f);
+}
 
-__global__ void __launch_bounds__(256) stitch_kernel(FrameSet frames, const int16_t* tab,
-                                                     const CompositeEntry* lut, int W, int H, const double* gains,
-                                                     int use_gain, uint8_t* out, int64_t out_pitch) {
+template <bool DWORD_STAGE>
+__global__ void __launch_bounds__(256) stitch_tiled_kernel(FrameSet frames, const int16_t* tab, TiledLut lut, int W,
+                                                           int H, const double* gains, int use_gain, uint8_t* out,
+                                                           int64_t out_pitch) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_src[kTileLdsBytes];
     __shared__ short s_tab[1024 * 4];
     __shared__ float s_gain[kMaxCams];
+    __shared__ TileSlot s_slot[kTileSlots];
     load_table_lds(tab, s_tab);
     if (threadIdx.x < kMaxCams) s_gain[threadIdx.x] = use_gain ? (float)gains[threadIdx.x] : 1.0f;
     __syncthreads();
 
-    const int tiles_x = (W / 2 + kQuadsX - 1) / kQuadsX;
-    const int tiles_y = (H / 2 + kQuadsY - 1) / kQuadsY;
-    const int n_tiles = tiles_x * tiles_y;
-    // XCD-aware split: blocks b, b+8, ... share an XCD; give that group a contiguous tile range.
+    const int n_tiles = lut.tiles_x * lut.tiles_y;
     const int groups = 8;
     const int g = blockIdx.x % groups;
     const int blocks_in_g = (gridDim.x - g + groups - 1) / groups;
-    const int local = blockIdx.x / groups;
     const int t_begin = (int)((int64_t)n_tiles * g / groups);
     const int t_end = (int)((int64_t)n_tiles * (g + 1) / groups);
-
     uint8_t* outU = out + (int64_t)H * out_pitch;
     uint8_t* outV = outU + (W >> 1);
-    const int lx = threadIdx.x % kQuadsX, ly = threadIdx.x / kQuadsX;
+    const int tid = threadIdx.x;
+    const int qx = tid & 63, qy = tid >> 6;
 
-    for (int t = t_begin + local; t < t_end; t += blocks_in_g) {
-        const int tyi = t / tiles_x, txi = t - tyi * tiles_x;
-        const int qx = txi * kQuadsX + lx, qy = tyi * kQuadsY + ly;
-        if (qx >= (W >> 1) || qy >= (H >> 1)) continue;
-        const int x = qx * 2, y = qy * 2;
-        const uint4 e0 = *reinterpret_cast<const uint4*>(lut + (int64_t)y * W + x);
-        const uint4 e1 = *reinterpret_cast<const uint4*>(lut + (int64_t)(y + 1) * W + x);
-        const uint32_t xy[4] = {e0.x, e0.z, e1.x, e1.z};
-        const uint32_t cd[4] = {e0.y, e0.w, e1.y, e1.w};
-        int Yo[4];
-        float us = 0.f, vs = 0.f;
+    for (int t = t_begin + (int)(blockIdx.x / groups); t < t_end; t += blocks_in_g) {
+        const TileHdr hd = lut.hdr[t];
+        const int tyi = t / lut.tiles_x, txi = t - tyi * lut.tiles_x;
+        const int x = txi * kTileW + qx * 2, y = tyi * kTileH + qy * 2;
+        const bool wide = (hd.nslots_flags & 0x100u) != 0;
+        const int nslots = (int)(hd.nslots_flags & 7u);
+        int rgb[4][3];
+        uint32_t cam[4];
+        if (wide) {
+            const uint4* wp = reinterpret_cast<const uint4*>(lut.wide + hd.wide_off) + tid * 2;
+            const uint4 e0 = wp[0], e1 = wp[1];
+            const uint32_t xy[4] = {e0.x, e0.z, e1.x, e1.z};
+            const uint32_t cd[4] = {e0.y, e0.w, e1.y, e1.w};
+            Taps tp[4];
+#pragma unroll
+            for (int p = 0; p < 4; p++) gather_taps(frames, xy[p], cd[p], s_tab, tp[p]);
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                blend_taps(tp[p], rgb[p][0], rgb[p][1], rgb[p][2]);
+                cam[p] = (cd[p] >> 10) & 31u;
+            }
+            if (x < W && y < H) finish_quad(rgb, cam, s_gain, out, outU, outV, out_pitch, x, y, x >> 1, y >> 1);
+            continue;  // no LDS touched: no barrier needed
+        }
+        const uint4 e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)t * kTilePx)[tid];
+        __syncthreads();  // previous staged tile's LDS readers are done
+        if (tid < kTileSlots) s_slot[tid] = lut.slots[(int64_t)t * kTileSlots + tid];
+        // ---- stage every slot's Y/U/V box into LDS --------------------------------------------
+        {
+            const uint32_t total = hd.stage_dwords;
+            for (uint32_t k = tid; k < total; k += 256) {
+                uint32_t kk = k;
+                int s = 0;
+                TileSlot sl = lut.slots[(int64_t)t * kTileSlots];
+#pragma unroll
+                for (int q = 0; q < kTileSlots; q++) {
+                    if (q >= nslots) break;
+                    const TileSlot c = lut.slots[(int64_t)t * kTileSlots + q];
+                    const uint32_t n = 3u * c.bw * c.bh / 8u;
+                    if (kk < n) {
+                        sl = c;
+                        s = q;
+                        break;
+                    }
+                    kk -= n;
+                }
+                (void)s;
+                const SourceFrame& f = frames.f[sl.cam];
+                const uint32_t ydw = (uint32_t)sl.bw * sl.bh / 4u;
+                const uint8_t* src;
+                uint32_t dst;
+                if (kk < ydw) {
+                    const uint32_t rowdw = sl.bw / 4u;
+                    const uint32_t row = kk / rowdw, col = kk - row * rowdw;
+                    src = f.yuv + (int64_t)(sl.by0 + row) * f.pitch + sl.bx0 + col * 4u;
+                    dst = sl.lds_y + row * sl.bw + col * 4u;
+                } else {
+                    kk -= ydw;
+                    const uint32_t cdw = ydw / 4u;  // each chroma plane: (bw/2) x (bh/2)
+                    const bool isv = kk >= cdw;
+                    if (isv) kk -= cdw;
+                    const uint32_t rowdw = sl.bw / 8u;
+                    const uint32_t row = kk / rowdw, col = kk - row * rowdw;
+                    const uint8_t* plane = f.yuv + (int64_t)f.h * f.pitch + (isv ? (f.w >> 1) : 0);
+                    src = plane + (int64_t)((sl.by0 >> 1) + row) * f.pitch + (sl.bx0 >> 1) + col * 4u;
+                    dst = (isv ? sl.lds_v : sl.lds_u) + row * (sl.bw >> 1) + col * 4u;
+                }
+                uint32_t v;
+                if (DWORD_STAGE) {
+                    v = *reinterpret_cast<const uint32_t*>(src);
+                } else {
+                    v = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
+                }
+                *reinterpret_cast<uint32_t*>(s_src + dst) = v;
+            }
+        }
+        __syncthreads();
+        const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            int r = 0, gg = 0, b = 0;
-            if (cd[p] & 0x8000u) {
-                const int cam = (int)((cd[p] >> 10) & 31u);
-                sample_rgb(frames.f[cam], xy[p], cd[p], s_tab, r, gg, b);
-                const float gf = s_gain[cam];
-                r = sat_u8_rne((float)r * gf);
-                gg = sat_u8_rne((float)gg * gf);
-                b = sat_u8_rne((float)b * gf);
-            }
-            const float R = (float)r, G = (float)gg, B = (float)b;
-            const float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
-            Yo[p] = sat_u8_rne(Yf);
-            us = us + (0.492f * (B - Yf) + 128.f);
-            vs = vs + (0.877f * (R - Yf) + 128.f);
+            const uint32_t e = ent[p];
+            const uint32_t m = e >> 28;
+            const TileSlot sl = s_slot[(e >> 26) & 3u];
+            const int rx = (int)(e & 255u), ry = (int)((e >> 8) & 255u);
+            const int dx = (int)(((m >> 1) | (m >> 3)) & 1u), dy = (int)(((m >> 2) | (m >> 3)) & 1u);
+            const short* w = s_tab + ((e >> 16) & 1023u) * 4;
+            const int bw = sl.bw, cbw = sl.bw >> 1;
+            const uint8_t* Yl = s_src + sl.lds_y;
+            const uint8_t* Ul = s_src + sl.lds_u;
+            const uint8_t* Vl = s_src + sl.lds_v;
+            const int r0 = ry * bw, r1 = (ry + dy) * bw;
+            const int c0 = (ry >> 1) * cbw, c1 = ((ry + dy) >> 1) * cbw;
+            const int xa = rx, xb = rx + dx, ca = rx >> 1, cb = (rx + dx) >> 1;
+            Taps tp;
+            tp.y[0] = Yl[r0 + xa];
+            tp.y[1] = Yl[r0 + xb];
+            tp.y[2] = Yl[r1 + xa];
+            tp.y[3] = Yl[r1 + xb];
+            tp.u[0] = Ul[c0 + ca];
+            tp.u[1] = Ul[c0 + cb];
+            tp.u[2] = Ul[c1 + ca];
+            tp.u[3] = Ul[c1 + cb];
+            tp.v[0] = Vl[c0 + ca];
+            tp.v[1] = Vl[c0 + cb];
+            tp.v[2] = Vl[c1 + ca];
+            tp.v[3] = Vl[c1 + cb];
+#pragma unroll
+            for (int q = 0; q < 4; q++) tp.w[q] = ((m >> q) & 1u) ? (int)w[q] : 0;
+            blend_taps(tp, rgb[p][0], rgb[p][1], rgb[p][2]);
+            cam[p] = sl.cam;
         }
-        *reinterpret_cast<uint16_t*>(out + (int64_t)y * out_pitch + x) = (uint16_t)(Yo[0] | (Yo[1] << 8));
-        *reinterpret_cast<uint16_t*>(out + (int64_t)(y + 1) * out_pitch + x) = (uint16_t)(Yo[2] | (Yo[3] << 8));
-        outU[(int64_t)qy * out_pitch + qx] = (uint8_t)sat_u8_rne(us * 0.25f);
-        outV[(int64_t)qy * out_pitch + qx] = (uint8_t)sat_u8_rne(vs * 0.25f);
+        if (x < W && y < H) finish_quad(rgb, cam, s_gain, out, outU, outV, out_pitch, x, y, x >> 1, y >> 1);
     }
 }
 
-hipError_t launch_stitch(const FrameSet& frames_dev, const int16_t* tab, const CompositeEntry* lut, int W, int H,
+hipError_t launch_stitch(const FrameSet& frames, const int16_t* tab, const TiledLut& lut, int W, int H,
                          const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
-    const int tiles = ((W / 2 + kQuadsX - 1) / kQuadsX) * ((H / 2 + kQuadsY - 1) / kQuadsY);
+    const int tiles = lut.tiles_x * lut.tiles_y;
     int blocks = std::min(tiles, 256 * 8);
     blocks = std::max(8, (blocks + 7) / 8 * 8);
-    hipLaunchKernelGGL(stitch_kernel, dim3(blocks), dim3(256), 0, s, frames_dev, tab, lut, W, H, gains, use_gain, out,
-                       out_pitch);
+    // dword staging needs every source row and chroma plane start 4-byte aligned
+    bool dw = true;
+    for (int i = 0; i < kMaxCams; i++) {
+        const SourceFrame& f = frames.f[i];
+        if (!f.yuv) continue;
+        if ((reinterpret_cast<uintptr_t>(f.yuv) & 3u) || (f.pitch & 3) || (f.w & 7)) dw = false;
+    }
+    if (dw)
+        hipLaunchKernelGGL(stitch_tiled_kernel<true>, dim3(blocks), dim3(256), 0, s, frames, tab, lut, W, H, gains,
+                           use_gain, out, out_pitch);
+    else
+        hipLaunchKernelGGL(stitch_tiled_kernel<false>, dim3(blocks), dim3(256), 0, s, frames, tab, lut, W, H, gains,
+                           use_gain, out, out_pitch);
     return hipGetLastError();
 }
 

@@ -36,6 +36,35 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
     return e;
 }
 
+// ---- tiled composite (the per-frame hot path) -------------------------------------------------
+// The output is cut into 128 x 8 pixel tiles (one 256-lane workgroup per tile, one 2x2 quad per
+// lane).  Per tile the host pre-computes, once per rig, which cameras win inside it (<= 4 "slots")
+// and the luma bounding box of every bilinear tap of each slot.  A staged tile first copies those
+// boxes (Y plus the matching U and V boxes) into LDS with coalesced dword loads; every tap is then
+// an LDS read.  The LUT is tile-major, 4 bytes per pixel, relative to the slot's box origin:
+//   bits 0-7 relx, 8-15 rely, 16-20 fx, 21-25 fy, 26-27 slot, 28-31 tap-valid mask (tap t = bit t;
+//   taps: 0 (x,y), 1 (x+1,y), 2 (x,y+1), 3 (x+1,y+1); all clear = black pixel).
+// Tiles that do not fit (> 4 cameras, a box > 256 px, or LDS need above kTileLdsBytes) are "wide":
+// their pixels use 8-byte absolute CompositeEntry records and direct global gathers.
+constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
+constexpr int kTileSlots = 4;
+constexpr int kTileLdsBytes = 24 * 1024;
+
+struct TileSlot {
+    uint16_t cam;
+    uint16_t bw, bh;   // luma box size (even; bw a multiple of 8)
+    uint16_t lds_y;    // byte offsets in the tile's LDS area
+    uint16_t bx0, by0; // luma box origin (bx0 multiple of 8, by0 even)
+    uint16_t lds_u, lds_v;
+};
+
+struct TileHdr {
+    uint32_t nslots_flags;  // bits 0-2: slots used; bit 8: wide
+    uint32_t wide_off;      // wide tiles: first CompositeEntry of this tile in the wide array
+    uint32_t stage_dwords;  // staged tiles: dwords to copy into LDS
+    uint32_t pad_;
+};
+
 // One input camera as the per-frame kernels see it: a YUV420P frame in "Y over [U|V]" layout.
 struct SourceFrame {
     const uint8_t* yuv;
@@ -75,18 +104,29 @@ hipError_t launch_lut_build(const CameraParams& out, const CameraParams& in, int
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
                                 hipStream_t s);
 
-hipError_t launch_gain_feed(const FrameSet& frames_dev, const int16_t* tab, const CompositeEntry* samples_a,
-                            const CompositeEntry* samples_b, const GainChunk* chunks, int n_chunks,
-                            double* partials, hipStream_t s);
-
-hipError_t launch_gain_solve(const double* partials, const GainChunk* chunks, int n_chunks, const int32_t* pair_ij,
-                             const int32_t* N, int n, double* gains, hipStream_t s);
+// Gain feed, three stream-ordered launches (no host sync):
+//  1. gain_norm:  every working-scale sample that lies in some pair intersection -> f32 RGB norm
+//  2. gain_pairs: per chunk of a pair's intersection, f64 sums of both cameras' norms -> partials
+//  3. gain_solve: I(i,j), A, b assembly and the cv::solve replica -> gains (device f64)
+hipError_t launch_gain_norm(const FrameSet& frames, const int16_t* tab, const CompositeEntry* samples, int n_samples,
+                            float* norms, hipStream_t s);
+hipError_t launch_gain_pairs(const float* norms, const uint2* pair_idx, const GainChunk* chunks, int n_chunks,
+                             double* partials, hipStream_t s);
+hipError_t launch_gain_solve(const double* partials, const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
+                             double* gains, hipStream_t s);
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 
-hipError_t launch_stitch(const FrameSet& frames_dev, const int16_t* tab, const CompositeEntry* lut, int W, int H,
-                         const double* gains,
-                         int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s);
+struct TiledLut {
+    const TileHdr* hdr;
+    const TileSlot* slots;        // kTileSlots per tile
+    const uint32_t* entries;      // kTilePx per tile, tile-major, quad-major inside the tile
+    const CompositeEntry* wide;   // kTilePx per wide tile
+    int tiles_x, tiles_y;
+};
+
+hipError_t launch_stitch(const FrameSet& frames_dev, const int16_t* tab, const TiledLut& lut, int W, int H,
+                         const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s);
 
 hipError_t launch_remap_u8(const int16_t* tab, const uint8_t* src, int sw, int sh, int64_t spitch, int cn, const float* map1,
                            const float* map2, int mw, int mh, int64_t mpitch, float scale_x, float scale_y,

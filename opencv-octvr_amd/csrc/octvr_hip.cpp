@@ -17,6 +17,7 @@
 #include <sstream>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "camera_math.hpp"
@@ -485,14 +486,23 @@ struct octvr_mapper {
     int use_gain = 0;
     std::vector<int> in_w, in_h;
     DevBuf<int16_t> tab;
-    DevBuf<CompositeEntry> lut;
+    // tiled composite LUT (kernels.hpp)
+    DevBuf<TileHdr> tile_hdr;
+    DevBuf<TileSlot> tile_slots;
+    DevBuf<uint32_t> tile_entries;
+    DevBuf<CompositeEntry> tile_wide;
+    TiledLut tiled{};
+    int n_wide_tiles = 0;
+    double staged_bytes = 0;
     DevBuf<double> gains;
     // gain feed
-    DevBuf<CompositeEntry> sa, sb;
+    DevBuf<CompositeEntry> samples;  // unique working-scale samples used by some intersection
+    DevBuf<float> norms;
+    DevBuf<uint2> pair_idx;           // (sample of camera i, sample of camera j) per intersection pixel
     DevBuf<GainChunk> chunks;
     DevBuf<double> partials;
-    DevBuf<int32_t> pair_ij, N;
-    int n_chunks = 0;
+    DevBuf<int32_t> N;
+    int n_chunks = 0, n_samples = 0;
     size_t n_entries = 0;
     std::vector<double> last_gains;
     hipStream_t last_stream = nullptr;
@@ -567,15 +577,24 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
         for (uint8_t v : smask[i]) nz += v != 0;
         N[(size_t)i * n + i] = std::max(1, nz);
     }
-    std::vector<CompositeEntry> A, B;
+    // unique samples (camera-major) and per-pair index lists
+    std::vector<std::vector<int32_t>> sample_id(n);
+    for (int i = 0; i < n; i++) sample_id[i].assign(samp[i].size(), -1);
+    std::vector<CompositeEntry> uniq;
+    auto sid = [&](int cam, size_t k) {
+        int32_t& id = sample_id[cam][k];
+        if (id < 0) {
+            id = (int32_t)uniq.size();
+            uniq.push_back(samp[cam][k]);
+        }
+        return (uint32_t)id;
+    };
+    std::vector<uint2> idx;
     std::vector<GainChunk> chunks;
-    std::vector<int32_t> pij;
-    const int kChunk = 256 * 16;
+    std::vector<std::array<int, 3>> ranges;  // (pair, begin, end) of every non-empty intersection
     int p = 0;
     for (int i = 0; i < n; i++)
         for (int j = i + 1; j < n; j++, p++) {
-            pij.push_back(i);
-            pij.push_back(j);
             const auto &a = wr[i], &b = wr[j];
             int x0 = std::max(a[0], b[0]), y0 = std::max(a[1], b[1]);
             int x1 = std::min(a[0] + a[2], b[0] + b[2]), y1 = std::min(a[1] + a[3], b[1] + b[3]);
@@ -583,28 +602,168 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
                 N[(size_t)i * n + j] = N[(size_t)j * n + i] = 1;
                 continue;
             }
-            int begin = (int)A.size(), nz = 0;
+            int begin = (int)idx.size(), nz = 0;
             for (int y = y0; y < y1; y++)
                 for (int x = x0; x < x1; x++) {
                     size_t ka = (size_t)(y - a[1]) * a[2] + (x - a[0]);
                     size_t kb = (size_t)(y - b[1]) * b[2] + (x - b[0]);
                     if ((smask[i][ka] & smask[j][kb]) == 0) continue;
                     nz++;
-                    A.push_back(samp[i][ka]);
-                    B.push_back(samp[j][kb]);
+                    idx.push_back(make_uint2(sid(i, ka), sid(j, kb)));
                 }
             N[(size_t)i * n + j] = N[(size_t)j * n + i] = std::max(1, nz);
-            for (int s = begin; s < (int)A.size(); s += kChunk)
-                chunks.push_back(GainChunk{p, s, std::min<int>((int)A.size(), s + kChunk), 0});
+            if (nz) ranges.push_back({p, begin, (int)idx.size()});
         }
-    m.sa.upload(A.data(), A.size());
-    m.sb.upload(B.data(), B.size());
+    // chunk size: ~1K entries per block, grown so the solve's partial table (<= 4096 chunks) holds all
+    int kChunk = 1024;
+    while (true) {
+        size_t cnt = 0;
+        for (auto& r : ranges) cnt += (size_t)(r[2] - r[1] + kChunk - 1) / kChunk;
+        if (cnt <= 4000) break;
+        kChunk *= 2;
+    }
+    for (auto& r : ranges)
+        for (int s0 = r[1]; s0 < r[2]; s0 += kChunk) chunks.push_back(GainChunk{r[0], s0, std::min(r[2], s0 + kChunk), 0});
+    m.samples.upload(uniq.data(), uniq.size());
+    m.norms.alloc(std::max<size_t>(uniq.size(), 1));
+    m.pair_idx.upload(idx.data(), idx.size());
     m.chunks.upload(chunks.data(), chunks.size());
     m.partials.alloc(std::max<size_t>(2 * chunks.size(), 2));
-    m.pair_ij.upload(pij.data(), pij.size());
     m.N.upload(N.data(), N.size());
     m.n_chunks = (int)chunks.size();
-    m.n_entries = A.size();
+    m.n_samples = (int)uniq.size();
+    m.n_entries = idx.size();
+}
+
+// Tiled composite LUT (kernels.hpp "tiled composite") from the per-pixel winner LUT.  Once per rig.
+void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
+    const int W = m.W, H = m.H;
+    const int tx_n = (W + kTileW - 1) / kTileW, ty_n = (H + kTileH - 1) / kTileH;
+    const int n_tiles = tx_n * ty_n;
+    std::vector<TileHdr> hdr(n_tiles);
+    std::vector<TileSlot> slots((size_t)n_tiles * kTileSlots);
+    std::vector<uint32_t> entries((size_t)n_tiles * kTilePx, 0u);
+    std::vector<std::vector<CompositeEntry>> wide_parts;
+    std::vector<uint8_t> is_wide(n_tiles, 0);
+    const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::vector<std::pair<int, std::vector<CompositeEntry>>>> wide_local(T);
+    auto work = [&](int tid) {
+        for (int t = tid; t < n_tiles; t += T) {
+            const int ty = t / tx_n, tx = t % tx_n;
+            struct Px {
+                int slot, x0, y0, fxy, mask;
+            };
+            Px px[kTilePx];
+            CompositeEntry raw[kTilePx];
+            int cams[8], ns = 0;
+            int minx[8], maxx[8], miny[8], maxy[8];
+            bool wide = false;
+            for (int k = 0; k < kTilePx; k++) {
+                const int q = k >> 2, p = k & 3;
+                const int x = tx * kTileW + (q & 63) * 2 + (p & 1), y = ty * kTileH + (q >> 6) * 2 + (p >> 1);
+                CompositeEntry e{0, 0};
+                if (x < W && y < H) e = lut8[(size_t)y * W + x];
+                raw[k] = e;
+                px[k].mask = 0;
+                if (!(e.code & 0x8000u)) continue;
+                const int cam = (int)((e.code >> 10) & 31u);
+                const int sx = (int)(e.xy & 0xFFFFu), sy = (int)(e.xy >> 16);
+                const int iw = m.in_w[cam], ih = m.in_h[cam];
+                const bool inx = sx + 1 < iw, iny = sy + 1 < ih;
+                const int mask = ((sx < iw && sy < ih) ? 1 : 0) | ((inx && sy < ih) ? 2 : 0) |
+                                 ((iny && sx < iw) ? 4 : 0) | ((inx && iny) ? 8 : 0);
+                if (!mask) continue;
+                const int x0 = std::min(sx, iw - 1), y0 = std::min(sy, ih - 1);
+                const int x1 = x0 + (((mask >> 1) | (mask >> 3)) & 1), y1 = y0 + (((mask >> 2) | (mask >> 3)) & 1);
+                int sl = -1;
+                for (int j = 0; j < ns; j++)
+                    if (cams[j] == cam) sl = j;
+                if (sl < 0) {
+                    if (ns == 8) {
+                        wide = true;
+                        continue;
+                    }
+                    sl = ns++;
+                    cams[sl] = cam;
+                    minx[sl] = miny[sl] = INT32_MAX;
+                    maxx[sl] = maxy[sl] = -1;
+                }
+                minx[sl] = std::min(minx[sl], x0);
+                maxx[sl] = std::max(maxx[sl], x1);
+                miny[sl] = std::min(miny[sl], y0);
+                maxy[sl] = std::max(maxy[sl], y1);
+                px[k] = Px{sl, x0, y0, (int)(e.code & 1023u), mask};
+            }
+            if (ns > kTileSlots) wide = true;
+            TileSlot ts[kTileSlots] = {};
+            uint32_t lds = 0, dwords = 0;
+            for (int j = 0; j < ns && !wide; j++) {
+                const int iw = m.in_w[cams[j]];
+                if (iw % 8) {
+                    wide = true;
+                    break;
+                }
+                const int bx0 = minx[j] & ~7, by0 = miny[j] & ~1;
+                const int bx1 = (maxx[j] + 1 + 7) & ~7, by1 = (maxy[j] + 1 + 1) & ~1;
+                const int bw = bx1 - bx0, bh = by1 - by0;
+                if (bw > 256 || bh > 256) {
+                    wide = true;
+                    break;
+                }
+                ts[j].cam = (uint16_t)cams[j];
+                ts[j].bw = (uint16_t)bw;
+                ts[j].bh = (uint16_t)bh;
+                ts[j].bx0 = (uint16_t)bx0;
+                ts[j].by0 = (uint16_t)by0;
+                ts[j].lds_y = (uint16_t)lds;
+                ts[j].lds_u = (uint16_t)(lds + bw * bh);
+                ts[j].lds_v = (uint16_t)(lds + bw * bh + bw * bh / 4);
+                lds += (uint32_t)(bw * bh + bw * bh / 2);
+                dwords += (uint32_t)(3 * bw * bh / 8);
+            }
+            if (lds > (uint32_t)kTileLdsBytes) wide = true;
+            if (wide) {
+                is_wide[t] = 1;
+                hdr[t] = TileHdr{0x100u, 0u, 0u, 0u};
+                wide_local[tid].emplace_back(t, std::vector<CompositeEntry>(raw, raw + kTilePx));
+                continue;
+            }
+            hdr[t] = TileHdr{(uint32_t)ns, 0u, dwords, 0u};
+            for (int j = 0; j < kTileSlots; j++) slots[(size_t)t * kTileSlots + j] = ts[j];
+            uint32_t* out = entries.data() + (size_t)t * kTilePx;
+            for (int k = 0; k < kTilePx; k++) {
+                if (!px[k].mask) continue;
+                const TileSlot& sl = ts[px[k].slot];
+                const uint32_t rx = (uint32_t)(px[k].x0 - sl.bx0), ry = (uint32_t)(px[k].y0 - sl.by0);
+                out[k] = rx | (ry << 8) | ((uint32_t)px[k].fxy << 16) | ((uint32_t)px[k].slot << 26) |
+                         ((uint32_t)px[k].mask << 28);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 0; i < T; i++) th.emplace_back(work, i);
+    for (auto& x : th) x.join();
+    // wide tiles: 8-byte absolute entries in tile order
+    std::vector<std::pair<int, std::vector<CompositeEntry>>> all;
+    for (auto& v : wide_local)
+        for (auto& p : v) all.push_back(std::move(p));
+    std::sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    std::vector<CompositeEntry> wide;
+    wide.reserve(all.size() * kTilePx);
+    for (auto& p : all) {
+        hdr[p.first].wide_off = (uint32_t)wide.size();
+        wide.insert(wide.end(), p.second.begin(), p.second.end());
+    }
+    m.tile_hdr.upload(hdr.data(), hdr.size());
+    m.tile_slots.upload(slots.data(), slots.size());
+    m.tile_entries.upload(entries.data(), entries.size());
+    if (wide.empty()) wide.push_back(CompositeEntry{0, 0});
+    m.tile_wide.upload(wide.data(), wide.size());
+    m.n_wide_tiles = (int)all.size();
+    double sb = 0;
+    for (auto& h : hdr) sb += 4.0 * h.stage_dwords;
+    m.staged_bytes = sb;
+    m.tiled = TiledLut{m.tile_hdr.p, m.tile_slots.p, m.tile_entries.p, m.tile_wide.p, tx_n, ty_n};
 }
 
 }  // namespace
@@ -822,6 +981,7 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
                     "input sizes must be even and < 65536");
         // mapper.cpp:78-82: a single input disables gain (and blend)
         m->use_gain = (enable_gain && m->n > 1) ? 1 : 0;
+        REQUIRE(!m->use_gain || m->n <= 16, "gain estimation supports at most 16 inputs");
         DeviceGuard dg(device);
         int16_t tab[4096];
         bilinear_table(tab);
@@ -841,9 +1001,19 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             }
             DevBuf<CamTemplate> ctd;
             ctd.upload(ct.data(), ct.size());
-            m->lut.alloc((size_t)m->W * m->H);
-            HIP_CHECK(launch_composite_lut(ctd.p, m->n, m->W, m->H, m->lut.p, nullptr));
+            DevBuf<CompositeEntry> lut;
+            lut.alloc((size_t)m->W * m->H);
+            HIP_CHECK(launch_composite_lut(ctd.p, m->n, m->W, m->H, lut.p, nullptr));
             HIP_CHECK(hipDeviceSynchronize());
+            std::vector<CompositeEntry> lut8((size_t)m->W * m->H);
+            HIP_CHECK(hipMemcpy(lut8.data(), lut.p, lut8.size() * sizeof(CompositeEntry), hipMemcpyDeviceToHost));
+            lut.reset();
+            for (int i = 0; i < m->n; i++) {
+                m1[i].reset();
+                m2[i].reset();
+                mk[i].reset();
+            }
+            build_tiles(*m, lut8);
         }
         m->gains.alloc(kMaxCams);
         std::vector<double> ones(kMaxCams, 1.0);
@@ -872,9 +1042,9 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
                 REQUIRE(n_gains == m->n, "gains must have one entry per input");
                 HIP_CHECK(launch_set_gains(gains, m->n, m->gains.p, s));
             } else {
-                HIP_CHECK(launch_gain_feed(fs, m->tab.p, m->sa.p, m->sb.p, m->chunks.p, m->n_chunks, m->partials.p, s));
-                HIP_CHECK(launch_gain_solve(m->partials.p, m->chunks.p, m->n_chunks, m->pair_ij.p, m->N.p, m->n,
-                                            m->gains.p, s));
+                HIP_CHECK(launch_gain_norm(fs, m->tab.p, m->samples.p, m->n_samples, m->norms.p, s));
+                HIP_CHECK(launch_gain_pairs(m->norms.p, m->pair_idx.p, m->chunks.p, m->n_chunks, m->partials.p, s));
+                HIP_CHECK(launch_gain_solve(m->partials.p, m->chunks.p, m->n_chunks, m->N.p, m->n, m->gains.p, s));
             }
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -883,7 +1053,7 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
             HIP_CHECK(hipEventCreate(&e1));
             HIP_CHECK(hipEventRecord(e0, s));
         }
-        HIP_CHECK(launch_stitch(fs, m->tab.p, m->lut.p, m->W, m->H, m->gains.p, m->use_gain, out_dev,
+        HIP_CHECK(launch_stitch(fs, m->tab.p, m->tiled, m->W, m->H, m->gains.p, m->use_gain, out_dev,
                                 (int64_t)out_pitch, s));
         if (m->timing) {
             HIP_CHECK(hipEventRecord(e1, s));
@@ -909,9 +1079,11 @@ int octvr_mapper_gains(octvr_mapper* m, double* g, int n) {
 int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
     return guarded([&] {
         REQUIRE(m && bytes, "NULL argument");
-        // composite kernel: 8 B LUT entry + 1.5 B YUV420 output per output pixel, every source
-        // frame read once (1.5 B per input pixel)
-        double b = 8.0 * m->W * m->H + 1.5 * m->W * m->H;
+        // composite kernel: 4 B tiled-LUT entry (8 B in wide tiles) + 1.5 B YUV420 output per output
+        // pixel, every source frame read once (1.5 B per input pixel), tile headers/slots
+        const double tiles = (double)m->tiled.tiles_x * m->tiled.tiles_y;
+        double b = 4.0 * tiles * kTilePx + 8.0 * m->n_wide_tiles * kTilePx + 1.5 * m->W * m->H +
+                   tiles * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot));
         for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
         *bytes = b;
     });
@@ -940,6 +1112,20 @@ int octvr_mapper_kernel_time(octvr_mapper* m, double* total_ms, int* launches) {
         *launches = (int)m->events.size();
         *total_ms = t;
         m->events.clear();
+    });
+}
+
+int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
+    return guarded([&] {
+        REQUIRE(m && buf && len > 0, "bad arguments");
+        char tmp[512];
+        snprintf(tmp, sizeof tmp,
+                 "{\"inputs\": %d, \"out\": [%d, %d], \"tiles\": %d, \"wide_tiles\": %d, \"staged_bytes\": %.0f, "
+                 "\"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, \"gain_chunks\": %d}",
+                 m->n, m->W, m->H, m->tiled.tiles_x * m->tiled.tiles_y, m->n_wide_tiles, m->staged_bytes, m->use_gain,
+                 m->n_samples, m->n_entries, m->n_chunks);
+        REQUIRE(strlen(tmp) < len, "buffer too small");
+        memcpy(buf, tmp, strlen(tmp) + 1);
     });
 }
 

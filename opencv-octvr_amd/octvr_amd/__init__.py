@@ -64,6 +64,7 @@ _lib.octvr_mapper_gains.argtypes = [_VP, C.POINTER(C.c_double), C.c_int]
 _lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
 _lib.octvr_mapper_set_timing.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+_lib.octvr_mapper_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
 _lib.octvr_mapper_destroy.argtypes = [_VP]
 _lib.octvr_mapper_destroy.restype = None
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
@@ -200,6 +201,11 @@ class Mapper:
         b = C.c_double()
         _check(_lib.octvr_mapper_traffic(self._h, C.byref(b)))
         return b.value
+
+    def info(self):
+        buf = C.create_string_buffer(1024)
+        _check(_lib.octvr_mapper_info(self._h, buf, 1024))
+        return _json.loads(buf.value.decode())
 
     def set_timing(self, enable=True):
         _check(_lib.octvr_mapper_set_timing(self._h, int(enable)))
