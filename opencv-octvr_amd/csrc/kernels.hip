@@ -563,11 +563,17 @@ __device__ __forceinline__ void finish_quad(const int (&rgb)[4][3], const uint32
     outV[(int64_t)qyg * out_pitch + qxg] = (uint8_t)sat_u8_rne(vs * 0.25f);
 }
 
+__device__ __forceinline__ uint32_t rgba_of(int y, int u, int v) {
+    int r, g, b;
+    yuv_to_rgb(y, u, v, r, g, b);
+    return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
+}
+
 template <bool DWORD_STAGE>
 __global__ void __launch_bounds__(256) stitch_tiled_kernel(FrameSet frames, const int16_t* tab, TiledLut lut, int W,
                                                            int H, const double* gains, int use_gain, uint8_t* out,
                                                            int64_t out_pitch) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_src[kTileLdsBytes];
+    __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
     __shared__ short s_tab[1024 * 4];
     __shared__ float s_gain[kMaxCams];
     __shared__ TileSlot s_slot[kTileSlots];
@@ -613,54 +619,44 @@ __global__ void __launch_bounds__(256) stitch_tiled_kernel(FrameSet frames, cons
         const uint4 e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)t * kTilePx)[tid];
         __syncthreads();  // previous staged tile's LDS readers are done
         if (tid < kTileSlots) s_slot[tid] = lut.slots[(int64_t)t * kTileSlots + tid];
-        // ---- stage every slot's Y/U/V box into LDS --------------------------------------------
-        {
-            const uint32_t total = hd.stage_dwords;
-            for (uint32_t k = tid; k < total; k += 256) {
-                uint32_t kk = k;
-                int s = 0;
-                TileSlot sl = lut.slots[(int64_t)t * kTileSlots];
+        // ---- convert every slot's box to RGBA in LDS, 4 horizontally adjacent pixels per step ----
+        for (uint32_t k = tid; k < hd.stage_groups; k += 256) {
+            uint32_t kk = k;
+            TileSlot sl = lut.slots[(int64_t)t * kTileSlots];
 #pragma unroll
-                for (int q = 0; q < kTileSlots; q++) {
-                    if (q >= nslots) break;
-                    const TileSlot c = lut.slots[(int64_t)t * kTileSlots + q];
-                    const uint32_t n = 3u * c.bw * c.bh / 8u;
-                    if (kk < n) {
-                        sl = c;
-                        s = q;
-                        break;
-                    }
-                    kk -= n;
+            for (int q = 0; q < kTileSlots; q++) {
+                if (q >= nslots) break;
+                const TileSlot c = lut.slots[(int64_t)t * kTileSlots + q];
+                const uint32_t n = (uint32_t)c.bw * c.bh / 4u;
+                if (kk < n) {
+                    sl = c;
+                    break;
                 }
-                (void)s;
-                const SourceFrame& f = frames.f[sl.cam];
-                const uint32_t ydw = (uint32_t)sl.bw * sl.bh / 4u;
-                const uint8_t* src;
-                uint32_t dst;
-                if (kk < ydw) {
-                    const uint32_t rowdw = sl.bw / 4u;
-                    const uint32_t row = kk / rowdw, col = kk - row * rowdw;
-                    src = f.yuv + (int64_t)(sl.by0 + row) * f.pitch + sl.bx0 + col * 4u;
-                    dst = sl.lds_y + row * sl.bw + col * 4u;
-                } else {
-                    kk -= ydw;
-                    const uint32_t cdw = ydw / 4u;  // each chroma plane: (bw/2) x (bh/2)
-                    const bool isv = kk >= cdw;
-                    if (isv) kk -= cdw;
-                    const uint32_t rowdw = sl.bw / 8u;
-                    const uint32_t row = kk / rowdw, col = kk - row * rowdw;
-                    const uint8_t* plane = f.yuv + (int64_t)f.h * f.pitch + (isv ? (f.w >> 1) : 0);
-                    src = plane + (int64_t)((sl.by0 >> 1) + row) * f.pitch + (sl.bx0 >> 1) + col * 4u;
-                    dst = (isv ? sl.lds_v : sl.lds_u) + row * (sl.bw >> 1) + col * 4u;
-                }
-                uint32_t v;
-                if (DWORD_STAGE) {
-                    v = *reinterpret_cast<const uint32_t*>(src);
-                } else {
-                    v = (uint32_t)src[0] | ((uint32_t)src[1] << 8) | ((uint32_t)src[2] << 16) | ((uint32_t)src[3] << 24);
-                }
-                *reinterpret_cast<uint32_t*>(s_src + dst) = v;
+                kk -= n;
             }
+            const SourceFrame& f = frames.f[sl.cam];
+            const uint32_t rowg = sl.bw / 4u;
+            const uint32_t row = kk / rowg, col = kk - row * rowg;
+            const int sx = sl.bx0 + (int)col * 4, sy = sl.by0 + (int)row;
+            const uint8_t* Yp = f.yuv + (int64_t)sy * f.pitch + sx;
+            const uint8_t* Up = f.yuv + (int64_t)(f.h + (sy >> 1)) * f.pitch + (sx >> 1);
+            const uint8_t* Vp = Up + (f.w >> 1);
+            uint32_t yq, uq, vq;
+            if (DWORD_STAGE) {
+                yq = *reinterpret_cast<const uint32_t*>(Yp);
+                uq = *reinterpret_cast<const uint16_t*>(Up);
+                vq = *reinterpret_cast<const uint16_t*>(Vp);
+            } else {
+                yq = (uint32_t)Yp[0] | ((uint32_t)Yp[1] << 8) | ((uint32_t)Yp[2] << 16) | ((uint32_t)Yp[3] << 24);
+                uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8);
+                vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8);
+            }
+            uint4 px;
+            px.x = rgba_of(yq & 255u, uq & 255u, vq & 255u);
+            px.y = rgba_of((yq >> 8) & 255u, uq & 255u, vq & 255u);
+            px.z = rgba_of((yq >> 16) & 255u, (uq >> 8) & 255u, (vq >> 8) & 255u);
+            px.w = rgba_of(yq >> 24, (uq >> 8) & 255u, (vq >> 8) & 255u);
+            *reinterpret_cast<uint4*>(s_rgb + sl.lds / 4u + row * sl.bw + col * 4u) = px;
         }
         __syncthreads();
         const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
@@ -672,29 +668,18 @@ __global__ void __launch_bounds__(256) stitch_tiled_kernel(FrameSet frames, cons
             const int rx = (int)(e & 255u), ry = (int)((e >> 8) & 255u);
             const int dx = (int)(((m >> 1) | (m >> 3)) & 1u), dy = (int)(((m >> 2) | (m >> 3)) & 1u);
             const short* w = s_tab + ((e >> 16) & 1023u) * 4;
-            const int bw = sl.bw, cbw = sl.bw >> 1;
-            const uint8_t* Yl = s_src + sl.lds_y;
-            const uint8_t* Ul = s_src + sl.lds_u;
-            const uint8_t* Vl = s_src + sl.lds_v;
-            const int r0 = ry * bw, r1 = (ry + dy) * bw;
-            const int c0 = (ry >> 1) * cbw, c1 = ((ry + dy) >> 1) * cbw;
-            const int xa = rx, xb = rx + dx, ca = rx >> 1, cb = (rx + dx) >> 1;
-            Taps tp;
-            tp.y[0] = Yl[r0 + xa];
-            tp.y[1] = Yl[r0 + xb];
-            tp.y[2] = Yl[r1 + xa];
-            tp.y[3] = Yl[r1 + xb];
-            tp.u[0] = Ul[c0 + ca];
-            tp.u[1] = Ul[c0 + cb];
-            tp.u[2] = Ul[c1 + ca];
-            tp.u[3] = Ul[c1 + cb];
-            tp.v[0] = Vl[c0 + ca];
-            tp.v[1] = Vl[c0 + cb];
-            tp.v[2] = Vl[c1 + ca];
-            tp.v[3] = Vl[c1 + cb];
+            const uint32_t* box = s_rgb + sl.lds / 4u;
+            const int r0 = ry * sl.bw + rx, r1 = (ry + dy) * sl.bw + rx;
+            const uint32_t c00 = box[r0], c01 = box[r0 + dx], c10 = box[r1], c11 = box[r1 + dx];
+            const int w0 = (m & 1u) ? w[0] : 0, w1 = (m & 2u) ? w[1] : 0, w2 = (m & 4u) ? w[2] : 0,
+                      w3 = (m & 8u) ? w[3] : 0;
 #pragma unroll
-            for (int q = 0; q < 4; q++) tp.w[q] = ((m >> q) & 1u) ? (int)w[q] : 0;
-            blend_taps(tp, rgb[p][0], rgb[p][1], rgb[p][2]);
+            for (int ch = 0; ch < 3; ch++) {
+                const int sh = ch * 8;
+                const int acc = (int)((c00 >> sh) & 255u) * w0 + (int)((c01 >> sh) & 255u) * w1 +
+                                (int)((c10 >> sh) & 255u) * w2 + (int)((c11 >> sh) & 255u) * w3;
+                rgb[p][ch] = min(max((acc + (1 << 14)) >> 15, 0), 255);
+            }
             cam[p] = sl.cam;
         }
         if (x < W && y < H) finish_quad(rgb, cam, s_gain, out, outU, outV, out_pitch, x, y, x >> 1, y >> 1);
@@ -706,7 +691,7 @@ hipError_t launch_stitch(const FrameSet& frames, const int16_t* tab, const Tiled
     const int tiles = lut.tiles_x * lut.tiles_y;
     int blocks = std::min(tiles, 256 * 8);
     blocks = std::max(8, (blocks + 7) / 8 * 8);
-    // dword staging needs every source row and chroma plane start 4-byte aligned
+    // dword staging needs 4-byte aligned Y rows and 2-byte aligned chroma rows
     bool dw = true;
     for (int i = 0; i < kMaxCams; i++) {
         const SourceFrame& f = frames.f[i];

@@ -39,9 +39,10 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
 // ---- tiled composite (the per-frame hot path) -------------------------------------------------
 // The output is cut into 128 x 8 pixel tiles (one 256-lane workgroup per tile, one 2x2 quad per
 // lane).  Per tile the host pre-computes, once per rig, which cameras win inside it (<= 4 "slots")
-// and the luma bounding box of every bilinear tap of each slot.  A staged tile first copies those
-// boxes (Y plus the matching U and V boxes) into LDS with coalesced dword loads; every tap is then
-// an LDS read.  The LUT is tile-major, 4 bytes per pixel, relative to the slot's box origin:
+// and the luma bounding box of every bilinear tap of each slot.  A staged tile first converts those
+// boxes from YUV420P (coalesced dword Y + u16 U/V loads) into packed RGBA in LDS — every source
+// pixel converted once, as NPP's full-frame pass does in the reference — so a tap is one LDS dword.
+// The LUT is tile-major, 4 bytes per pixel, relative to the slot's box origin:
 //   bits 0-7 relx, 8-15 rely, 16-20 fx, 21-25 fy, 26-27 slot, 28-31 tap-valid mask (tap t = bit t;
 //   taps: 0 (x,y), 1 (x+1,y), 2 (x,y+1), 3 (x+1,y+1); all clear = black pixel).
 // Tiles that do not fit (> 4 cameras, a box > 256 px, or LDS need above kTileLdsBytes) are "wide":
@@ -52,16 +53,16 @@ constexpr int kTileLdsBytes = 24 * 1024;
 
 struct TileSlot {
     uint16_t cam;
-    uint16_t bw, bh;   // luma box size (even; bw a multiple of 8)
-    uint16_t lds_y;    // byte offsets in the tile's LDS area
+    uint16_t bw, bh;   // luma box size (bw a multiple of 8, bh even)
+    uint16_t lds;      // byte offset of the slot's RGBA box (bw * bh * 4 bytes) in the tile's LDS area
     uint16_t bx0, by0; // luma box origin (bx0 multiple of 8, by0 even)
-    uint16_t lds_u, lds_v;
+    uint16_t pad0, pad1;
 };
 
 struct TileHdr {
     uint32_t nslots_flags;  // bits 0-2: slots used; bit 8: wide
     uint32_t wide_off;      // wide tiles: first CompositeEntry of this tile in the wide array
-    uint32_t stage_dwords;  // staged tiles: dwords to copy into LDS
+    uint32_t stage_groups;  // staged tiles: 4-pixel groups to convert into LDS
     uint32_t pad_;
 };
 

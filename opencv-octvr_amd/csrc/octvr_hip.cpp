@@ -715,11 +715,9 @@ void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
                 ts[j].bh = (uint16_t)bh;
                 ts[j].bx0 = (uint16_t)bx0;
                 ts[j].by0 = (uint16_t)by0;
-                ts[j].lds_y = (uint16_t)lds;
-                ts[j].lds_u = (uint16_t)(lds + bw * bh);
-                ts[j].lds_v = (uint16_t)(lds + bw * bh + bw * bh / 4);
-                lds += (uint32_t)(bw * bh + bw * bh / 2);
-                dwords += (uint32_t)(3 * bw * bh / 8);
+                ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
+                lds += (uint32_t)(bw * bh * 4);
+                dwords += (uint32_t)(bw * bh / 4);
             }
             if (lds > (uint32_t)kTileLdsBytes) wide = true;
             if (wide) {
@@ -761,7 +759,7 @@ void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
     m.tile_wide.upload(wide.data(), wide.size());
     m.n_wide_tiles = (int)all.size();
     double sb = 0;
-    for (auto& h : hdr) sb += 4.0 * h.stage_dwords;
+    for (auto& h : hdr) sb += 6.0 * h.stage_groups;  // 4 Y + 2 U/V bytes read per 4-pixel group
     m.staged_bytes = sb;
     m.tiled = TiledLut{m.tile_hdr.p, m.tile_slots.p, m.tile_entries.p, m.tile_wide.p, tx_n, ty_n};
 }
