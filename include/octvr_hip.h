@@ -116,6 +116,11 @@ int octvr_remap_u8(const uint8_t* src_dev, int sw, int sh, size_t spitch, int cn
                    const float* map2_dev, int mw, int mh, size_t mpitch_elems, float scale_x, float scale_y,
                    uint8_t* dst_dev, size_t dpitch, void* stream);
 
+/* ---- self-test hooks (used by tests/, not by the stitching path) ---------------------------------- */
+/* Saturating float -> u8 conversion as the kernels implement it (method 0: rint + clamp in VALU,
+ * method 1: v_cvt_pk_u8_f32), for a known-answer test of round-half-even and clamping on device. */
+int octvr_selftest_sat_u8(const float* in_dev, uint8_t* out_dev, int n, int method, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,52 +11,11 @@
 #include <cstring>
 
 #include "kernels.hpp"
+#ifndef OCTVR_FEED_VARIANT
+#define OCTVR_FEED_VARIANT 0
+#endif
 
 namespace octvr {
-
-// ---------------------------------------------------------------------------------------------
-// Bilinear 15-bit weight table: initInterTab2D(INTER_LINEAR, true) (imgwarp.cpp:146-150,211-280),
-// including the sum fix-up whose min/max search walks flat indices 3..6, i.e. into the NEXT cell
-// (a positive excess can be "corrected" there and later overwritten): reproduced on a flat array.
-// ---------------------------------------------------------------------------------------------
-static short sat_s16(float v) {
-    int iv = (int)rintf(v);
-    return (short)(iv < -32768 ? -32768 : iv > 32767 ? 32767 : iv);
-}
-
-void bilinear_table(int16_t out[1024 * 4]) {
-    float tab1[64];
-    const float scale = 1.f / 32;
-    for (int i = 0; i < 32; i++) {
-        tab1[i * 2] = 1.f - i * scale;
-        tab1[i * 2 + 1] = i * scale;
-    }
-    static short flat[1024 * 4 + 8];
-    memset(flat, 0, sizeof flat);
-    short* itab = flat;
-    for (int i = 0; i < 32; i++)
-        for (int j = 0; j < 32; j++, itab += 4) {
-            int isum = 0;
-            for (int k1 = 0; k1 < 2; k1++) {
-                float vy = tab1[i * 2 + k1];
-                for (int k2 = 0; k2 < 2; k2++) {
-                    float v = vy * tab1[j * 2 + k2];
-                    isum += itab[k1 * 2 + k2] = sat_s16(v * 32768);
-                }
-            }
-            if (isum != 32768) {
-                int diff = isum - 32768, Mk1 = 1, Mk2 = 1, mk1 = 1, mk2 = 1;
-                for (int k1 = 1; k1 < 3; k1++)
-                    for (int k2 = 1; k2 < 3; k2++) {
-                        if (itab[k1 * 2 + k2] < itab[mk1 * 2 + mk2]) mk1 = k1, mk2 = k2;
-                        else if (itab[k1 * 2 + k2] > itab[Mk1 * 2 + Mk2]) Mk1 = k1, Mk2 = k2;
-                    }
-                if (diff < 0) itab[Mk1 * 2 + Mk2] = (short)(itab[Mk1 * 2 + Mk2] - diff);
-                else itab[mk1 * 2 + mk2] = (short)(itab[mk1 * 2 + mk2] - diff);
-            }
-        }
-    memcpy(out, flat, 1024 * 4 * sizeof(short));
-}
 
 // ---------------------------------------------------------------------------------------------
 // Pixel arithmetic shared by the kernels
@@ -68,81 +27,84 @@ __device__ __forceinline__ int sat_u8_rne(float v) {
     return (int)__builtin_rintf(v);
 }
 
-// Own BT.601 YUV -> RGB (stands in for NPP nppiYUV420ToRGB_8u_P3AC4R, cudaimgproc/src/color.cpp:2269;
-// NPP's arithmetic is closed, so this definition is pinned by the oracle only).
-__device__ __forceinline__ void yuv_to_rgb(int y, int u, int v, int& r, int& g, int& b) {
-    float Yf = (float)y, Uf = (float)u - 128.f, Vf = (float)v - 128.f;
-    r = sat_u8_rne(Yf + 1.140f * Vf);
-    g = sat_u8_rne(Yf - 0.394f * Uf - 0.581f * Vf);
-    b = sat_u8_rne(Yf + 2.032f * Uf);
+// The same conversion in one instruction, written into byte `sel` of `old`: v_cvt_pk_u8_f32 rounds
+// half to even and saturates (NaN -> 0); tests/test_gpu_parity.py::test_gpu_saturating_conversion_kat.
+__device__ __forceinline__ uint32_t pack_u8(float v, uint32_t sel, uint32_t old) {
+    return __builtin_amdgcn_cvt_pk_u8_f32(v, sel, old);
 }
 
-// Bilinear fixed-point sample of one camera at a composite entry: the cv::remap INTER_LINEAR /
-// BORDER_CONSTANT rule (imgwarp.cpp:3812-4030) on the RGBA image NPP would have produced.
-// Out-of-image taps contribute 0 (cval); result per channel = sat_u8((sum + 2^14) >> 15).
-// Branch-free: out-of-image taps read a clamped (in-bounds) address with weight 0, and an invalid
-// entry (no camera) gets all-zero weights, so every load of every pixel can be issued up front.
+// The library's own BT.601 YUV -> RGB (stands in for NPP nppiYUV420ToRGB_8u_P3AC4R,
+// cudaimgproc/src/color.cpp:2269, whose arithmetic is closed: pinned by the oracle only).  Same
+// operation sequence as oracle/octvr_oracle.c yuv_px_to_rgb.  Returns packed R | G << 8 | B << 16.
+__device__ __forceinline__ uint32_t yuv_to_rgba(uint32_t y, uint32_t u, uint32_t v) {
+    const float Yf = (float)y, Uf = (float)u - 128.f, Vf = (float)v - 128.f;
+    uint32_t p = pack_u8(__builtin_fmaf(1.140f, Vf, Yf), 0, 0u);
+    p = pack_u8(__builtin_fmaf(-0.581f, Vf, __builtin_fmaf(-0.394f, Uf, Yf)), 1, p);
+    return pack_u8(__builtin_fmaf(2.032f, Uf, Yf), 2, p);
+}
+
+// 15-bit bilinear weights.  initInterTab2D's table (imgwarp.cpp:211-280) holds
+// w = {(32-fx)(32-fy), fx(32-fy), (32-fx)fy, fx fy} * 32 exactly (every product is exact in f32),
+// except code 0 whose 32768 saturates to 32767 and the fix-up adds the missing unit to the
+// bottom-right tap: {32767, 0, 0, 1}.  For u8 taps that cell rounds to c00 exactly like
+// {32768, 0, 0, 0} would ((32767 c00 + c11 + 2^14) >> 15 == c00 for c00, c11 <= 255), so the
+// separable form below is bit-identical to the table — pinned by the all-codes remap KAT.
+// Out-of-image taps are passed as 0 (BORDER_CONSTANT).  Returns (sum + 2^14) >> 15 per channel.
+__device__ __forceinline__ uint32_t bilerp_ch(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t fx,
+                                              uint32_t fy) {
+    const uint32_t h0 = (32u - fx) * a + fx * b;  // <= 8160
+    const uint32_t h1 = (32u - fx) * c + fx * d;
+    return ((32u - fy) * h0 + fy * h1 + 512u) >> 10;
+}
+
+__device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint32_t fx,
+                                            uint32_t fy, uint32_t (&rgb)[3]) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const uint32_t sh = 8u * ch;
+        rgb[ch] = bilerp_ch((c00 >> sh) & 255u, (c01 >> sh) & 255u, (c10 >> sh) & 255u, (c11 >> sh) & 255u, fx, fy);
+    }
+}
+
+// Direct (global-memory) bilinear sample of one camera at an 8-byte composite entry — the gain feed
+// samples and "wide" tiles.  Every load is issued unconditionally from a clamped in-image address;
+// taps outside the image and invalid entries are zeroed afterwards.
+// wave-uniform value -> SGPR (scalar loads / branches downstream)
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
 struct Taps {
-    uint8_t y[4], u[4], v[4];
-    int w[4];
+    uint32_t c[4];  // packed RGBA of the 4 taps (0 when outside / invalid)
+    uint32_t fx, fy;
 };
 
-__device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, const short* tab,
-                                            Taps& t) {
+__device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t xy, uint32_t code, Taps& t) {
     const bool valid = (code & 0x8000u) != 0;
-    const SourceFrame& f = fs.f[(code >> 10) & 31u];
     const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
-    const short* w = tab + (code & 1023u) * 4;
     const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
-    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);  // sx <= W_in (X may round up to W)
-    const int x1 = inx ? sx + 1 : x0, y1 = iny ? sy + 1 : y0;
     const bool in0 = valid && sx < f.w && sy < f.h;
-    t.w[0] = in0 ? w[0] : 0;
-    t.w[1] = (valid && inx && sy < f.h) ? w[1] : 0;
-    t.w[2] = (valid && iny && sx < f.w) ? w[2] : 0;
-    t.w[3] = (valid && inx && iny) ? w[3] : 0;
+    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);
+    const int x1 = inx ? sx + 1 : x0, y1 = iny ? sy + 1 : y0;
     const int64_t p = f.pitch;
     const uint8_t* Y = f.yuv;
     const uint8_t* U = Y + (int64_t)f.h * p;
     const uint8_t* V = U + (f.w >> 1);
     const int64_t r0 = (int64_t)y0 * p, r1 = (int64_t)y1 * p;
-    const int64_t c0 = (int64_t)(y0 >> 1) * p, c1 = (int64_t)(y1 >> 1) * p;
-    t.y[0] = Y[r0 + x0];
-    t.y[1] = Y[r0 + x1];
-    t.y[2] = Y[r1 + x0];
-    t.y[3] = Y[r1 + x1];
-    t.u[0] = U[c0 + (x0 >> 1)];
-    t.u[1] = U[c0 + (x1 >> 1)];
-    t.u[2] = U[c1 + (x0 >> 1)];
-    t.u[3] = U[c1 + (x1 >> 1)];
-    t.v[0] = V[c0 + (x0 >> 1)];
-    t.v[1] = V[c0 + (x1 >> 1)];
-    t.v[2] = V[c1 + (x0 >> 1)];
-    t.v[3] = V[c1 + (x1 >> 1)];
+    const int64_t q0 = (int64_t)(y0 >> 1) * p, q1 = (int64_t)(y1 >> 1) * p;
+    const uint32_t ya = Y[r0 + x0], yb = Y[r0 + x1], yc = Y[r1 + x0], yd = Y[r1 + x1];
+    const uint32_t ua = U[q0 + (x0 >> 1)], ub = U[q0 + (x1 >> 1)], uc = U[q1 + (x0 >> 1)], ud = U[q1 + (x1 >> 1)];
+    const uint32_t va = V[q0 + (x0 >> 1)], vb = V[q0 + (x1 >> 1)], vc = V[q1 + (x0 >> 1)], vd = V[q1 + (x1 >> 1)];
+    t.c[0] = in0 ? yuv_to_rgba(ya, ua, va) : 0u;
+    t.c[1] = (valid && inx && sy < f.h) ? yuv_to_rgba(yb, ub, vb) : 0u;
+    t.c[2] = (valid && iny && sx < f.w) ? yuv_to_rgba(yc, uc, vc) : 0u;
+    t.c[3] = (valid && inx && iny) ? yuv_to_rgba(yd, ud, vd) : 0u;
+    t.fx = code & 31u;
+    t.fy = (code >> 5) & 31u;
 }
 
-__device__ __forceinline__ void blend_taps(const Taps& t, int& r, int& g, int& b) {
-    int ar = 0, ag = 0, ab = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        int cr, cg, cb;
-        yuv_to_rgb(t.y[k], t.u[k], t.v[k], cr, cg, cb);
-        ar += cr * t.w[k];
-        ag += cg * t.w[k];
-        ab += cb * t.w[k];
-    }
-    r = min(max((ar + (1 << 14)) >> 15, 0), 255);
-    g = min(max((ag + (1 << 14)) >> 15, 0), 255);
-    b = min(max((ab + (1 << 14)) >> 15, 0), 255);
+__device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, Taps& t) {
+    gather_taps_frame(fs.f[(code >> 10) & 31u], xy, code, t);
 }
 
-__device__ __forceinline__ void load_table_lds(const int16_t* tab, short* lds) {
-    // 8 KiB table -> LDS, 16 B per lane
-    const int4* src = reinterpret_cast<const int4*>(tab);
-    int4* dst = reinterpret_cast<int4*>(lds);
-    for (int i = threadIdx.x; i < 1024 * 4 * 2 / 16; i += blockDim.x) dst[i] = src[i];
-    __syncthreads();
-}
 
 // ---------------------------------------------------------------------------------------------
 // LUT build: MapperTemplate::add_input (template.cpp:46-133), one thread per output pixel, FP64.
@@ -231,69 +193,6 @@ hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(composite_lut_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, n, W, H, lut);
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
-// Gain feed (GainCompensatorGPU::feed, exposure_compensate.cpp:223-263).  The working-scale images
-// are nearest resizes of the warped ROIs (mapper.cpp:234-237); the host pre-resolves every working
-// pixel that lies in some pair intersection into a sample entry of its camera, so one thread per
-// sample computes the warped pixel's f32 norm (elementNorm, core/src/cuda/gpu_mat.cu:443-449).
-// ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) gain_norm_kernel(FrameSet frames, const int16_t* tab,
-                                                        const CompositeEntry* samples, int n, float* norms) {
-    __shared__ short s_tab[1024 * 4];
-    load_table_lds(tab, s_tab);
-    for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-        const CompositeEntry e = samples[k];
-        Taps t;
-        gather_taps(frames, e.xy, e.code, s_tab, t);
-        int r, g, b;
-        blend_taps(t, r, g, b);
-        norms[k] = sqrtf((float)(r * r + g * g + b * b));
-    }
-}
-
-hipError_t launch_gain_norm(const FrameSet& frames, const int16_t* tab, const CompositeEntry* samples, int n_samples,
-                            float* norms, hipStream_t s) {
-    if (n_samples <= 0) return hipSuccess;
-    const int blocks = std::min((n_samples + 255) / 256, 256 * 8);
-    hipLaunchKernelGGL(gain_norm_kernel, dim3(blocks), dim3(256), 0, s, frames, tab, samples, n_samples, norms);
-    return hipGetLastError();
-}
-
-// calcSum over the intersection mask (cudaarithm calcSum, f32 -> f64): one chunk per block, fixed
-// reduction order, partial sums stored in chunk order (deterministic, no atomics).
-__global__ void __launch_bounds__(256) gain_pairs_kernel(const float* norms, const uint2* idx, const GainChunk* chunks,
-                                                         double* partials) {
-    __shared__ double s_red[2][256];
-    const GainChunk ch = chunks[blockIdx.x];
-    double s1 = 0.0, s2 = 0.0;
-    for (int e = ch.begin + (int)threadIdx.x; e < ch.end; e += blockDim.x) {
-        const uint2 p = idx[e];
-        s1 += (double)norms[p.x];
-        s2 += (double)norms[p.y];
-    }
-    s_red[0][threadIdx.x] = s1;
-    s_red[1][threadIdx.x] = s2;
-    __syncthreads();
-    for (int off = 128; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) {
-            s_red[0][threadIdx.x] += s_red[0][threadIdx.x + off];
-            s_red[1][threadIdx.x] += s_red[1][threadIdx.x + off];
-        }
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        partials[2 * blockIdx.x] = s_red[0][0];
-        partials[2 * blockIdx.x + 1] = s_red[1][0];
-    }
-}
-
-hipError_t launch_gain_pairs(const float* norms, const uint2* pair_idx, const GainChunk* chunks, int n_chunks,
-                             double* partials, hipStream_t s) {
-    if (n_chunks <= 0) return hipSuccess;
-    hipLaunchKernelGGL(gain_pairs_kernel, dim3(n_chunks), dim3(256), 0, s, norms, pair_idx, chunks, partials);
     return hipGetLastError();
 }
 
@@ -391,38 +290,54 @@ __device__ bool solve_fixed(const double* Ain, const double* bin, double* x) {
 #undef Sd
 }
 
-// Same LUImpl on a matrix held in LDS (n = 9..16: too large to keep in registers).
-__device__ bool lu_solve_lds(double* A, double* b, int n, double* x) {
+
+// The same LUImpl with the whole workgroup: per pivot every thread finds the pivot row (same scan
+// order), one thread per column swaps, one thread per (row, column) eliminates; every element sees
+// exactly the serial operation sequence of LUImpl (matrix_decomp.cpp:50-110), so the result is
+// bit-identical to lu_solve<N>.  Used for n = 9..16 (too large for one lane's registers).
+// Call with all threads of the workgroup; returns the same flag everywhere.
+__device__ bool lu_solve_block(double* A, double* b, int n, double* x) {
     const double eps = DBL_EPSILON * 100;
+    const int tid = threadIdx.x, nt = blockDim.x;
     for (int i = 0; i < n; i++) {
         int k = i;
         for (int j = i + 1; j < n; j++)
             if (fabs(A[j * n + i]) > fabs(A[k * n + i])) k = j;
-        if (fabs(A[k * n + i]) < eps) return false;
+        if (fabs(A[k * n + i]) < eps) return false;  // uniform: every thread read the same values
+        __syncthreads();
         if (k != i) {
-            for (int j = i; j < n; j++) {
-                const double t = A[i * n + j];
-                A[i * n + j] = A[k * n + j];
-                A[k * n + j] = t;
+            for (int c = i + tid; c <= n; c += nt) {  // column n is b
+                double* ri = (c < n) ? &A[i * n + c] : &b[i];
+                double* rk = (c < n) ? &A[k * n + c] : &b[k];
+                const double t = *ri;
+                *ri = *rk;
+                *rk = t;
             }
-            const double t = b[i];
-            b[i] = b[k];
-            b[k] = t;
+            __syncthreads();
         }
         const double d = -1 / A[i * n + i];
-        for (int j = i + 1; j < n; j++) {
+        const int w = n - i;  // columns i+1 .. n (n = b)
+        for (int q = tid; q < (n - 1 - i) * w; q += nt) {
+            const int j = i + 1 + q / w, c = i + 1 + q % w;
             const double alpha = A[j * n + i] * d;
-            for (int c = i + 1; c < n; c++) A[j * n + c] += alpha * A[i * n + c];
-            b[j] += alpha * b[i];
+            if (c < n)
+                A[j * n + c] += alpha * A[i * n + c];
+            else
+                b[j] += alpha * b[i];
         }
-        A[i * n + i] = -d;
+        __syncthreads();
+        if (tid == 0) A[i * n + i] = -d;
+        __syncthreads();
     }
-    for (int i = n - 1; i >= 0; i--) {
-        double s = b[i];
-        for (int c = i + 1; c < n; c++) s -= A[i * n + c] * b[c];
-        b[i] = s * A[i * n + i];
+    if (tid == 0) {
+        for (int i = n - 1; i >= 0; i--) {
+            double s = b[i];
+            for (int c = i + 1; c < n; c++) s -= A[i * n + c] * b[c];
+            b[i] = s * A[i * n + i];
+        }
+        for (int i = 0; i < n; i++) x[i] = b[i];
     }
-    for (int i = 0; i < n; i++) x[i] = b[i];
+    __syncthreads();
     return true;
 }
 
@@ -434,86 +349,154 @@ __device__ bool solve_dispatch(double* A, double* b, int n, double* x) {
         CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE
         default:
-            return n <= 16 ? lu_solve_lds(A, b, n, x) : false;
+            return false;
     }
 }
 
-// One workgroup: the chunk partials, their pair ids and N are first staged into LDS by all lanes
-// (parallel loads instead of a dependent chain on one lane), lane p then sums pair p's partials in
-// chunk order, and lane 0 assembles I, A, b (exposure_compensate.cpp:265-296) and solves.
-constexpr int kSolveMaxChunks = 4096;
-__global__ void __launch_bounds__(256) gain_solve_kernel(const double* partials, const GainChunk* chunks, int n_chunks,
-                                                         const int32_t* N, int n, double* gains) {
-    __shared__ double s_part[2 * kSolveMaxChunks];
-    __shared__ int s_pair[kSolveMaxChunks];
-    __shared__ int s_N[16 * 16];
-    __shared__ double s_I[16 * 16];
-    __shared__ double s_A[16 * 16];
-    __shared__ double s_b[16];
-    __shared__ double s_x[16];
-    const int tid = threadIdx.x;
-    const int n_pairs = n * (n - 1) / 2;
-    const int nc = min(n_chunks, kSolveMaxChunks);
-    for (int c = tid; c < nc; c += blockDim.x) {
-        s_part[2 * c] = partials[2 * c];
-        s_part[2 * c + 1] = partials[2 * c + 1];
-        s_pair[c] = chunks[c].pair;
+// ---------------------------------------------------------------------------------------------
+// Gain feed (GainCompensatorGPU::feed, exposure_compensate.cpp:223-297) — one launch.
+// Sample s of camera i (a working-scale pixel, nearest resize of the warped ROI, mapper.cpp:234-237)
+// contributes its f32 norm (core/src/cuda/gpu_mat.cu:443-449) to the masked sum of every pair
+// (i, j) whose intersection contains it: I(i,j) = sum / N(i,j).
+//
+// Exact, order-free sums: a norm is sqrtf of an integer, so it is 0 or lies in [1, 442] and is a
+// whole multiple of 2^-23; a pair sum of fewer than 2^21 of them (the working scale holds ~1e5
+// pixels, checked on the host) is an integer below 2^53 in units of 2^-23.  Every partial sum is
+// therefore exact in f64, and the per-pair totals are kept as u64 fixed point (units of 2^-23)
+// added with device-scope integer atomics: the result equals the sequential f64 sum bit for bit,
+// whatever order the workgroups finish in.
+//
+// Completion: per-XCD tickets (blockIdx % 8), then one global ticket; the last workgroup reads the
+// totals with returning atomics (executed at the memory side, so no L2 staleness across XCDs),
+// resets them, assembles A, b and solves.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
+                                                        const uint16_t* partners, const GainChunk* chunks,
+                                                        int n_chunks, const int32_t* N, int n,
+                                                        unsigned long long* totals, uint32_t* tickets,
+                                                        double* gains) {
+    __shared__ int s_last;
+    __shared__ double s_I[kGainMaxCams * kGainMaxCams];
+    __shared__ double s_A[kGainMaxCams * kGainMaxCams];
+    __shared__ double s_b[kGainMaxCams];
+    __shared__ double s_x[kGainMaxCams];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const GainChunk ch = chunks[blockIdx.x];
+    double acc[kGainMaxCams];
+#pragma unroll
+    for (int j = 0; j < kGainMaxCams; j++) acc[j] = 0.0;
+    // kGainChunk / 256 samples per thread, all gathers issued before any arithmetic
+    constexpr int kPer = kGainChunk / 256;
+    uint32_t pm[kPer];
+    Taps t[kPer];
+    const int cam = uniform(ch.cam);  // a chunk holds one camera's samples: its frame is wave-uniform
+    const SourceFrame fr = frames.f[cam];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const int k = ch.begin + u * 256 + tid;
+        const bool in = k < ch.end;
+        const CompositeEntry e = in ? samples[k] : CompositeEntry{0u, 0u};
+        pm[u] = in ? partners[k] : 0u;
+        gather_taps_frame(fr, e.xy, e.code, t[u]);
     }
-    for (int k = tid; k < n * n; k += blockDim.x) {
-        s_N[k] = N[k];
-        s_I[k] = 0.0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        uint32_t rgb[3];
+        bilerp_rgba(t[u].c[0], t[u].c[1], t[u].c[2], t[u].c[3], t[u].fx, t[u].fy, rgb);
+        const double nv = (double)sqrtf((float)(rgb[0] * rgb[0] + rgb[1] * rgb[1] + rgb[2] * rgb[2]));
+#pragma unroll
+        for (int j = 0; j < kGainMaxCams; j++)
+            if (pm[u] & (1u << j)) acc[j] += nv;
+    }
+    // exact sums: per wave, then per workgroup, then one u64 atomic per partner
+    __shared__ double s_wsum[4][kGainMaxCams];
+    for (int j = 0; j < n; j++) {
+        double v = 0.0;
+#pragma unroll
+        for (int q = 0; q < kGainMaxCams; q++)
+            if (q == j) v = acc[q];
+        v = wave_sum(v);
+        if (lane == 0) s_wsum[tid >> 6][j] = v;
     }
     __syncthreads();
-    for (int p = tid; p < n_pairs; p += blockDim.x) {
-        int i = 0, rem = p;  // pair p = (i, j), i < j, in the constructor's loop order
-        while (rem >= n - 1 - i) {
-            rem -= n - 1 - i;
-            i++;
+    if (tid < n) {
+        const double v = (s_wsum[0][tid] + s_wsum[1][tid]) + (s_wsum[2][tid] + s_wsum[3][tid]);
+        if (v != 0.0)
+            __hip_atomic_fetch_add(&totals[(cam * kGainMaxCams + tid) * kGainTotalStride],
+                                   (unsigned long long)(v * 8388608.0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // every wave's adds have completed before the workgroup takes its ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+        const int xcd = blockIdx.x & 7;
+        const uint32_t in_xcd = (uint32_t)((n_chunks - xcd + 7) >> 3);
+        int last = 0;
+        if (__hip_atomic_fetch_add(&tickets[xcd], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_xcd - 1) {
+            const uint32_t groups = (uint32_t)min(n_chunks, 8);
+            last = __hip_atomic_fetch_add(&tickets[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
         }
-        const int j = i + 1 + rem;
-        // chunks are grouped by pair in pair order: binary search for the first chunk of p
-        int lo = 0, hi = nc;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_pair[mid] < p) lo = mid + 1;
-            else hi = mid;
-        }
-        double s1 = 0.0, s2 = 0.0;
-        bool any = false;
-        for (int c = lo; c < nc && s_pair[c] == p; c++) {
-            s1 += s_part[2 * c];
-            s2 += s_part[2 * c + 1];
-            any = true;
-        }
-        if (any) {
-            const int nij = s_N[i * n + j];
-            s_I[i * n + j] = s1 / nij;
-            s_I[j * n + i] = s2 / nij;
-        }
+        s_last = last;
     }
     __syncthreads();
-    if (tid != 0) return;
+    if (!s_last) return;
+    // ---- the last workgroup ------------------------------------------------------------------
+    __shared__ int32_t s_N[kGainMaxCams * kGainMaxCams];
+    if (tid < n * n) {
+        const int i = tid / n, j = tid - i * n;
+        const int32_t Nij = N[tid];
+        s_N[tid] = Nij;
+        const unsigned long long raw =
+            __hip_atomic_exchange(&totals[(i * kGainMaxCams + j) * kGainTotalStride], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_I[tid] = (i != j) ? ((double)raw * 0x1p-23) / Nij : 0.0;
+    }
+    if (tid < 9) __hip_atomic_exchange(&tickets[tid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+#if OCTVR_FEED_VARIANT == 1
+    if (tid < n) gains[tid] = s_I[tid];
+    return;
+#endif
     const double alpha = 0.01, beta = 100;
-    for (int k = 0; k < n * n; k++) s_A[k] = 0.0;
-    for (int i = 0; i < n; i++) s_b[i] = 0.0;
-    for (int i = 0; i < n; i++)
+    if (tid < n) {  // row i of A and b, in the reference's j order (exposure_compensate.cpp:282-294)
+        const int i = tid;
+        double bi = 0.0, aii = 0.0;
         for (int j = 0; j < n; j++) {
             const int Nij = s_N[i * n + j];
-            s_b[i] += beta * Nij;
-            s_A[i * n + i] += beta * Nij;
+            bi += beta * Nij;
+            aii += beta * Nij;
             if (j == i) continue;
-            s_A[i * n + i] += 2 * alpha * s_I[i * n + j] * s_I[i * n + j] * Nij;
-            s_A[i * n + j] -= 2 * alpha * s_I[i * n + j] * s_I[j * n + i] * Nij;
+            aii += 2 * alpha * s_I[i * n + j] * s_I[i * n + j] * Nij;
+            s_A[i * n + j] = 0.0 - 2 * alpha * s_I[i * n + j] * s_I[j * n + i] * Nij;
         }
-    if (!solve_dispatch(s_A, s_b, n, s_x))
-        for (int i = 0; i < n; i++) s_x[i] = 1.0;
-    for (int i = 0; i < n; i++) gains[i] = s_x[i];
+        s_A[i * n + i] = aii;
+        s_b[i] = bi;
+    }
+    __syncthreads();
+    // cv::solve (lapack.cpp:1050-1275): one lane with the matrix in registers for n <= 8 (closed forms
+    // n <= 3); the LU across the workgroup for 9..16
+    bool ok;
+    if (n <= 8) {
+        if (tid == 0) s_last = solve_dispatch(s_A, s_b, n, s_x) ? 1 : 0;
+        __syncthreads();
+        ok = s_last != 0;
+    } else {
+        ok = lu_solve_block(s_A, s_b, n, s_x);
+    }
+    if (tid < n) gains[tid] = ok ? s_x[tid] : 1.0;  // cv::solve failure leaves gains_ unspecified; 1 as the oracle
 }
 
-hipError_t launch_gain_solve(const double* partials, const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
-                             double* gains, hipStream_t s) {
-    if (n_chunks > kSolveMaxChunks) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gain_solve_kernel, dim3(1), dim3(256), 0, s, partials, chunks, n_chunks, N, n, gains);
+hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
+                            const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
+                            unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s) {
+    if (n_chunks <= 0 || n > kGainMaxCams) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, chunks, n_chunks,
+                       N, n, totals, tickets, gains);
     return hipGetLastError();
 }
 
@@ -533,53 +516,147 @@ hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, 
 
 // ---------------------------------------------------------------------------------------------
 // Per-frame stitch, blend = 0 (mapper.cpp:219-306 with the copy chain resolved into the tiled LUT):
-// for every 2x2 output quad the winning camera of each pixel is sampled from its YUV420P source
-// (YUV->RGB per tap, 15-bit bilinear), gain-scaled (mul_scalar_with_mask, exposure_compensate.cu:
-// 15-30: sat_u8(px * (float)g)) and written as YUV420P (own BT.601 in place of NPP RGBToYUV420).
+// for every 2x2 output quad the winning camera of each pixel is sampled (15-bit bilinear on the
+// RGBA the source converts to), gain-scaled (mul_scalar_with_mask, exposure_compensate.cu:15-30:
+// saturate_cast<uchar>(px * (float)g)) and written as YUV420P (the library's own BT.601 in place of
+// NPP RGBToYUV420, same sequence as oracle rgb_quad_to_yuv).
 // One workgroup per 128x8 tile; staged tiles read every tap from LDS (see kernels.hpp).  Tiles are
 // walked grid-stride; blocks b, b+8, ... (one XCD under round-robin dispatch) take a contiguous
 // band of tiles so their source boxes share that XCD's L2.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void finish_quad(const int (&rgb)[4][3], const uint32_t (&cam)[4], const float* s_gain,
-                                            uint8_t* out, uint8_t* outU, uint8_t* outV, int64_t out_pitch, int x,
-                                            int y, int qxg, int qyg) {
-    int Yo[4];
+__device__ __forceinline__ void finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4], uint8_t* out,
+                                            uint8_t* outU, uint8_t* outV, int64_t out_pitch, int x, int y) {
+    uint32_t y01 = 0, y23 = 0;
     float us = 0.f, vs = 0.f;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        const float gf = s_gain[cam[p]];  // a black pixel stays black under any gain
-        const int r = sat_u8_rne((float)rgb[p][0] * gf);
-        const int g = sat_u8_rne((float)rgb[p][1] * gf);
-        const int b = sat_u8_rne((float)rgb[p][2] * gf);
-        const float R = (float)r, G = (float)g, B = (float)b;
-        const float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
-        Yo[p] = sat_u8_rne(Yf);
-        us = us + (0.492f * (B - Yf) + 128.f);
-        vs = vs + (0.877f * (R - Yf) + 128.f);
+        // gain: saturate_cast<uchar>(px * g), kept as an exact float of the saturated integer
+        const float R = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][0] * gain[p]), 0.f, 255.f);
+        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain[p]), 0.f, 255.f);
+        const float B = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][2] * gain[p]), 0.f, 255.f);
+        const float Yf = __builtin_fmaf(0.114f, B, __builtin_fmaf(0.587f, G, 0.299f * R));
+        if (p < 2) y01 = pack_u8(Yf, p, y01);
+        else y23 = pack_u8(Yf, p - 2, y23);
+        us = __builtin_fmaf(0.492f, B - Yf, us);
+        vs = __builtin_fmaf(0.877f, R - Yf, vs);
     }
-    *reinterpret_cast<uint16_t*>(out + (int64_t)y * out_pitch + x) = (uint16_t)(Yo[0] | (Yo[1] << 8));
-    *reinterpret_cast<uint16_t*>(out + (int64_t)(y + 1) * out_pitch + x) = (uint16_t)(Yo[2] | (Yo[3] << 8));
-    outU[(int64_t)qyg * out_pitch + qxg] = (uint8_t)sat_u8_rne(us * 0.25f);
-    outV[(int64_t)qyg * out_pitch + qxg] = (uint8_t)sat_u8_rne(vs * 0.25f);
+    *reinterpret_cast<uint16_t*>(out + (int64_t)y * out_pitch + x) = (uint16_t)y01;
+    *reinterpret_cast<uint16_t*>(out + (int64_t)(y + 1) * out_pitch + x) = (uint16_t)y23;
+    outU[(int64_t)(y >> 1) * out_pitch + (x >> 1)] = (uint8_t)pack_u8(__builtin_fmaf(us, 0.25f, 128.f), 0, 0u);
+    outV[(int64_t)(y >> 1) * out_pitch + (x >> 1)] = (uint8_t)pack_u8(__builtin_fmaf(vs, 0.25f, 128.f), 0, 0u);
 }
 
-__device__ __forceinline__ uint32_t rgba_of(int y, int u, int v) {
-    int r, g, b;
-    yuv_to_rgb(y, u, v, r, g, b);
-    return (uint32_t)r | ((uint32_t)g << 8) | ((uint32_t)b << 16);
+
+// The tile's slot descriptors in scalar registers (the tile index is wave-uniform).
+struct SlotSet {
+    TileSlot s[kTileSlots];
+};
+
+__device__ __forceinline__ SlotSet load_slots(const TiledLut& lut, int t) {
+    SlotSet ss;
+    const uint4* p = reinterpret_cast<const uint4*>(lut.slots + (int64_t)t * kTileSlots);
+#pragma unroll
+    for (int q = 0; q < kTileSlots; q++) {
+        uint4 v = p[q];
+        v.x = (uint32_t)uniform((int)v.x);
+        v.y = (uint32_t)uniform((int)v.y);
+        v.z = (uint32_t)uniform((int)v.z);
+        v.w = (uint32_t)uniform((int)v.w);
+        memcpy(&ss.s[q], &v, sizeof(uint4));
+    }
+    return ss;
+}
+
+// One 4-pixel staging group of a tile: the YUV bytes it needs and its LDS destination.
+struct StageGroup {
+    uint32_t yq, uq, vq;  // 4 Y bytes, 2 U bytes, 2 V bytes
+    int32_t dst;          // dword index of the group's first RGBA pixel; -1 = none
+};
+
+template <bool DWORD_STAGE>
+__device__ __forceinline__ void stage_load(const SourceFrame* fs, const SlotSet& ss, int nslots, uint32_t stride,
+                                           uint32_t k, StageGroup& sg) {
+    uint32_t kk = k;
+    TileSlot sl = ss.s[0];
+#pragma unroll
+    for (int q = 1; q < kTileSlots; q++) {  // slot of group k: subtract the sizes of the slots before it
+        const uint32_t n = (uint32_t)ss.s[q - 1].bw * ss.s[q - 1].bh / 4u;
+        const bool past = q < nslots && kk >= n;
+        kk = past ? kk - n : kk;
+        if (past) sl = ss.s[q];
+        if (!past) break;
+    }
+    const SourceFrame f = fs[sl.cam];
+    const uint32_t rowg = sl.bw / 4u;
+    const uint32_t row = kk / rowg, col = kk - row * rowg;
+    const int sx = sl.bx0 + (int)col * 4, sy = sl.by0 + (int)row;
+    const uint8_t* Yp = f.yuv + (int64_t)sy * f.pitch + sx;
+    const uint8_t* Up = f.yuv + (int64_t)(f.h + (sy >> 1)) * f.pitch + (sx >> 1);
+    const uint8_t* Vp = Up + (f.w >> 1);
+    if (DWORD_STAGE) {
+        sg.yq = *reinterpret_cast<const uint32_t*>(Yp);
+        sg.uq = *reinterpret_cast<const uint16_t*>(Up);
+        sg.vq = *reinterpret_cast<const uint16_t*>(Vp);
+    } else {
+        sg.yq = (uint32_t)Yp[0] | ((uint32_t)Yp[1] << 8) | ((uint32_t)Yp[2] << 16) | ((uint32_t)Yp[3] << 24);
+        sg.uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8);
+        sg.vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8);
+    }
+    sg.dst = (int32_t)(sl.lds + row * stride + col * 4u);
+}
+
+__device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rgb) {
+    if (sg.dst < 0) return;
+    uint4 px;
+    px.x = yuv_to_rgba(sg.yq & 255u, sg.uq & 255u, sg.vq & 255u);
+    px.y = yuv_to_rgba((sg.yq >> 8) & 255u, sg.uq & 255u, sg.vq & 255u);
+    px.z = yuv_to_rgba((sg.yq >> 16) & 255u, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
+    px.w = yuv_to_rgba(sg.yq >> 24, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
+    *reinterpret_cast<uint4*>(s_rgb + sg.dst) = px;
+}
+
+constexpr int kStageRegs = 2;  // staging groups per lane loaded one tile ahead (512 per tile)
+
+struct TilePrefetch {
+    int t;
+    TileHdr hd;
+    uint4 e4;
+    StageGroup sg[kStageRegs];
+};
+
+template <bool DWORD_STAGE>
+__device__ __forceinline__ void tile_prefetch(const SourceFrame* fs, const TiledLut& lut, int t, int t_end,
+                                              TilePrefetch& pf) {
+    t = uniform(t);
+    pf.t = t;
+#pragma unroll
+    for (int r = 0; r < kStageRegs; r++) pf.sg[r].dst = -1;
+    if (t >= t_end) return;
+    const uint4 h = reinterpret_cast<const uint4*>(lut.hdr)[t];
+    pf.hd.nslots_flags = (uint32_t)uniform((int)h.x);
+    pf.hd.wide_off = (uint32_t)uniform((int)h.y);
+    pf.hd.stage_groups = (uint32_t)uniform((int)h.z);
+    pf.hd.stride = (uint32_t)uniform((int)h.w);
+    if (pf.hd.nslots_flags & 0x100u) return;  // wide tile: loaded when processed
+    const int tid = threadIdx.x;
+    pf.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)t * kTilePx)[tid];
+    const SlotSet ss = load_slots(lut, t);
+    const int nslots = (int)(pf.hd.nslots_flags & 7u);
+#pragma unroll
+    for (int r = 0; r < kStageRegs; r++) {
+        const uint32_t k = (uint32_t)(tid + r * 256);
+        if (k < pf.hd.stage_groups) stage_load<DWORD_STAGE>(fs, ss, nslots, pf.hd.stride, k, pf.sg[r]);
+    }
 }
 
 template <bool DWORD_STAGE>
-__global__ void __launch_bounds__(256) stitch_tiled_kernel(FrameSet frames, const int16_t* tab, TiledLut lut, int W,
-                                                           int H, const double* gains, int use_gain, uint8_t* out,
-                                                           int64_t out_pitch) {
+__global__ void __launch_bounds__(256, 4) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
+                                                              const double* gains, int use_gain, uint8_t* out,
+                                                              int64_t out_pitch) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
-    __shared__ short s_tab[1024 * 4];
     __shared__ float s_gain[kMaxCams];
-    __shared__ TileSlot s_slot[kTileSlots];
-    load_table_lds(tab, s_tab);
-    if (threadIdx.x < kMaxCams) s_gain[threadIdx.x] = use_gain ? (float)gains[threadIdx.x] : 1.0f;
-    __syncthreads();
+    __shared__ float s_slot_gain[kTileSlots];
+    __shared__ SourceFrame s_frames[kMaxCams];  // divergent per-lane camera lookups hit LDS, not kernarg
 
     const int n_tiles = lut.tiles_x * lut.tiles_y;
     const int groups = 8;
@@ -592,104 +669,79 @@ __global__ void __launch_bounds__(256) stitch_tiled_kernel(FrameSet frames, cons
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
 
-    for (int t = t_begin + (int)(blockIdx.x / groups); t < t_end; t += blocks_in_g) {
-        const TileHdr hd = lut.hdr[t];
+    if (tid < kMaxCams) {
+        s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
+        s_frames[tid] = frames.f[tid];
+    }
+    if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
+    __syncthreads();
+    TilePrefetch pf;
+    tile_prefetch<DWORD_STAGE>(s_frames, lut, t_begin + (int)(blockIdx.x / groups), t_end, pf);
+
+    while (pf.t < t_end) {
+        const int t = uniform(pf.t);
+        const TileHdr hd = pf.hd;
         const int tyi = t / lut.tiles_x, txi = t - tyi * lut.tiles_x;
         const int x = txi * kTileW + qx * 2, y = tyi * kTileH + qy * 2;
-        const bool wide = (hd.nslots_flags & 0x100u) != 0;
-        const int nslots = (int)(hd.nslots_flags & 7u);
-        int rgb[4][3];
-        uint32_t cam[4];
-        if (wide) {
+        uint32_t rgb[4][3];
+        float gain[4];
+        if (hd.nslots_flags & 0x100u) {  // wide tile: direct global gathers, no LDS
+            tile_prefetch<DWORD_STAGE>(s_frames, lut, t + blocks_in_g, t_end, pf);
             const uint4* wp = reinterpret_cast<const uint4*>(lut.wide + hd.wide_off) + tid * 2;
             const uint4 e0 = wp[0], e1 = wp[1];
             const uint32_t xy[4] = {e0.x, e0.z, e1.x, e1.z};
             const uint32_t cd[4] = {e0.y, e0.w, e1.y, e1.w};
             Taps tp[4];
 #pragma unroll
-            for (int p = 0; p < 4; p++) gather_taps(frames, xy[p], cd[p], s_tab, tp[p]);
+            for (int p = 0; p < 4; p++) gather_taps(frames, xy[p], cd[p], tp[p]);
 #pragma unroll
             for (int p = 0; p < 4; p++) {
-                blend_taps(tp[p], rgb[p][0], rgb[p][1], rgb[p][2]);
-                cam[p] = (cd[p] >> 10) & 31u;
+                bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
+                gain[p] = s_gain[(cd[p] >> 10) & 31u];
             }
-            if (x < W && y < H) finish_quad(rgb, cam, s_gain, out, outU, outV, out_pitch, x, y, x >> 1, y >> 1);
-            continue;  // no LDS touched: no barrier needed
+            if (x < W && y < H) finish_quad(rgb, gain, out, outU, outV, out_pitch, x, y);
+            continue;
         }
-        const uint4 e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)t * kTilePx)[tid];
-        __syncthreads();  // previous staged tile's LDS readers are done
-        if (tid < kTileSlots) s_slot[tid] = lut.slots[(int64_t)t * kTileSlots + tid];
-        // ---- convert every slot's box to RGBA in LDS, 4 horizontally adjacent pixels per step ----
-        for (uint32_t k = tid; k < hd.stage_groups; k += 256) {
-            uint32_t kk = k;
-            TileSlot sl = lut.slots[(int64_t)t * kTileSlots];
+        const uint4 e4 = pf.e4;
+        const uint32_t S = hd.stride;
+        const int nslots = (int)(hd.nslots_flags & 7u);
+        __syncthreads();  // the previous staged tile's LDS readers are done
+        if (tid < kTileSlots) s_slot_gain[tid] = s_gain[lut.slots[(int64_t)t * kTileSlots + tid].cam];
 #pragma unroll
-            for (int q = 0; q < kTileSlots; q++) {
-                if (q >= nslots) break;
-                const TileSlot c = lut.slots[(int64_t)t * kTileSlots + q];
-                const uint32_t n = (uint32_t)c.bw * c.bh / 4u;
-                if (kk < n) {
-                    sl = c;
-                    break;
-                }
-                kk -= n;
+        for (int r = 0; r < kStageRegs; r++) stage_store(pf.sg[r], s_rgb);
+        if (hd.stage_groups > (uint32_t)(kStageRegs * 256)) {  // large boxes only
+            const SlotSet ss = load_slots(lut, t);
+            for (uint32_t k = tid + kStageRegs * 256; k < hd.stage_groups; k += 256) {
+                StageGroup sg;
+                stage_load<DWORD_STAGE>(s_frames, ss, nslots, S, k, sg);
+                stage_store(sg, s_rgb);
             }
-            const SourceFrame& f = frames.f[sl.cam];
-            const uint32_t rowg = sl.bw / 4u;
-            const uint32_t row = kk / rowg, col = kk - row * rowg;
-            const int sx = sl.bx0 + (int)col * 4, sy = sl.by0 + (int)row;
-            const uint8_t* Yp = f.yuv + (int64_t)sy * f.pitch + sx;
-            const uint8_t* Up = f.yuv + (int64_t)(f.h + (sy >> 1)) * f.pitch + (sx >> 1);
-            const uint8_t* Vp = Up + (f.w >> 1);
-            uint32_t yq, uq, vq;
-            if (DWORD_STAGE) {
-                yq = *reinterpret_cast<const uint32_t*>(Yp);
-                uq = *reinterpret_cast<const uint16_t*>(Up);
-                vq = *reinterpret_cast<const uint16_t*>(Vp);
-            } else {
-                yq = (uint32_t)Yp[0] | ((uint32_t)Yp[1] << 8) | ((uint32_t)Yp[2] << 16) | ((uint32_t)Yp[3] << 24);
-                uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8);
-                vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8);
-            }
-            uint4 px;
-            px.x = rgba_of(yq & 255u, uq & 255u, vq & 255u);
-            px.y = rgba_of((yq >> 8) & 255u, uq & 255u, vq & 255u);
-            px.z = rgba_of((yq >> 16) & 255u, (uq >> 8) & 255u, (vq >> 8) & 255u);
-            px.w = rgba_of(yq >> 24, (uq >> 8) & 255u, (vq >> 8) & 255u);
-            *reinterpret_cast<uint4*>(s_rgb + sl.lds / 4u + row * sl.bw + col * 4u) = px;
         }
         __syncthreads();
+        // the next tile's global loads are in flight while this tile computes from LDS
+        tile_prefetch<DWORD_STAGE>(s_frames, lut, t + blocks_in_g, t_end, pf);
         const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint32_t e = ent[p];
-            const uint32_t m = e >> 28;
-            const TileSlot sl = s_slot[(e >> 26) & 3u];
-            const int rx = (int)(e & 255u), ry = (int)((e >> 8) & 255u);
-            const int dx = (int)(((m >> 1) | (m >> 3)) & 1u), dy = (int)(((m >> 2) | (m >> 3)) & 1u);
-            const short* w = s_tab + ((e >> 16) & 1023u) * 4;
-            const uint32_t* box = s_rgb + sl.lds / 4u;
-            const int r0 = ry * sl.bw + rx, r1 = (ry + dy) * sl.bw + rx;
-            const uint32_t c00 = box[r0], c01 = box[r0 + dx], c10 = box[r1], c11 = box[r1 + dx];
-            const int w0 = (m & 1u) ? w[0] : 0, w1 = (m & 2u) ? w[1] : 0, w2 = (m & 4u) ? w[2] : 0,
-                      w3 = (m & 8u) ? w[3] : 0;
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) {
-                const int sh = ch * 8;
-                const int acc = (int)((c00 >> sh) & 255u) * w0 + (int)((c01 >> sh) & 255u) * w1 +
-                                (int)((c10 >> sh) & 255u) * w2 + (int)((c11 >> sh) & 255u) * w3;
-                rgb[p][ch] = min(max((acc + (1 << 14)) >> 15, 0), 255);
-            }
-            cam[p] = sl.cam;
+            const uint32_t off = e & 0x1FFFu, m = (e >> 25) & 15u;
+            const uint32_t c00 = s_rgb[(m & 1u) ? off : 0u];
+            const uint32_t c01 = s_rgb[(m & 2u) ? off + 1u : 0u];
+            const uint32_t c10 = s_rgb[(m & 4u) ? off + S : 0u];
+            const uint32_t c11 = s_rgb[(m & 8u) ? off + S + 1u : 0u];
+            bilerp_rgba(c00, c01, c10, c11, (e >> 13) & 31u, (e >> 18) & 31u, rgb[p]);
+            gain[p] = s_slot_gain[(e >> 23) & 3u];
         }
-        if (x < W && y < H) finish_quad(rgb, cam, s_gain, out, outU, outV, out_pitch, x, y, x >> 1, y >> 1);
+        if (x < W && y < H) finish_quad(rgb, gain, out, outU, outV, out_pitch, x, y);
     }
 }
 
-hipError_t launch_stitch(const FrameSet& frames, const int16_t* tab, const TiledLut& lut, int W, int H,
-                         const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
+hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
+                         int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
+    // one resident wave of workgroups (256 CUs x 4 per CU at <= 128 VGPRs and < 40 KiB LDS), each
+    // walking its XCD group's tiles
     const int tiles = lut.tiles_x * lut.tiles_y;
-    int blocks = std::min(tiles, 256 * 8);
+    int blocks = std::min(tiles, 256 * 4);
     blocks = std::max(8, (blocks + 7) / 8 * 8);
     // dword staging needs 4-byte aligned Y rows and 2-byte aligned chroma rows
     bool dw = true;
@@ -699,10 +751,10 @@ hipError_t launch_stitch(const FrameSet& frames, const int16_t* tab, const Tiled
         if ((reinterpret_cast<uintptr_t>(f.yuv) & 3u) || (f.pitch & 3) || (f.w & 7)) dw = false;
     }
     if (dw)
-        hipLaunchKernelGGL(stitch_tiled_kernel<true>, dim3(blocks), dim3(256), 0, s, frames, tab, lut, W, H, gains,
+        hipLaunchKernelGGL(stitch_tiled_kernel<true>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
                            use_gain, out, out_pitch);
     else
-        hipLaunchKernelGGL(stitch_tiled_kernel<false>, dim3(blocks), dim3(256), 0, s, frames, tab, lut, W, H, gains,
+        hipLaunchKernelGGL(stitch_tiled_kernel<false>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
                            use_gain, out, out_pitch);
     return hipGetLastError();
 }
@@ -711,12 +763,10 @@ hipError_t launch_stitch(const FrameSet& frames, const int16_t* tab, const Tiled
 // Standalone cv::remap INTER_LINEAR u8 (cn = 1, 3, 4), BORDER_CONSTANT 0 — one output pixel per lane.
 // ---------------------------------------------------------------------------------------------
 template <int CN>
-__global__ void __launch_bounds__(256) remap_u8_kernel(const int16_t* tab, const uint8_t* src, int sw, int sh,
-                                                       int64_t spitch, const float* map1, const float* map2, int mw,
-                                                       int mh, int64_t mpitch, float scale_x, float scale_y,
-                                                       uint8_t* dst, int64_t dpitch) {
-    __shared__ short s_tab[1024 * 4];
-    load_table_lds(tab, s_tab);
+__global__ void __launch_bounds__(256) remap_u8_kernel(const uint8_t* src, int sw, int sh, int64_t spitch,
+                                                       const float* map1, const float* map2, int mw, int mh,
+                                                       int64_t mpitch, float scale_x, float scale_y, uint8_t* dst,
+                                                       int64_t dpitch) {
     const int64_t total = (int64_t)mw * mh;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
@@ -728,26 +778,23 @@ __global__ void __launch_bounds__(256) remap_u8_kernel(const int16_t* tab, const
         const int ix = (fx32 != fx32 || fabsf(fx32) >= 2147483648.f) ? INT32_MIN : (int)__builtin_rintf(fx32);
         const int iy = (fy32 != fy32 || fabsf(fy32) >= 2147483648.f) ? INT32_MIN : (int)__builtin_rintf(fy32);
         const int sx = min(max(ix >> 5, -32768), 32767), sy = min(max(iy >> 5, -32768), 32767);
-        const short* w = s_tab + (((iy & 31) << 5) | (ix & 31)) * 4;
-        int acc[CN];
-#pragma unroll
-        for (int k = 0; k < CN; k++) acc[k] = 0;
+        const uint32_t fx = (uint32_t)(ix & 31), fy = (uint32_t)(iy & 31);
+        uint32_t v[4][CN];
 #pragma unroll
         for (int t = 0; t < 4; t++) {
             const int tx = sx + (t & 1), ty = sy + (t >> 1);
-            if (tx >= 0 && tx < sw && ty >= 0 && ty < sh) {
-                const uint8_t* p = src + (int64_t)ty * spitch + (int64_t)tx * CN;
+            const bool in = tx >= 0 && tx < sw && ty >= 0 && ty < sh;
+            const uint8_t* p = src + (int64_t)min(max(ty, 0), sh - 1) * spitch + (int64_t)min(max(tx, 0), sw - 1) * CN;
 #pragma unroll
-                for (int k = 0; k < CN; k++) acc[k] += (int)p[k] * w[t];
-            }
+            for (int k = 0; k < CN; k++) v[t][k] = in ? p[k] : 0u;
         }
         uint8_t* d = dst + (int64_t)y * dpitch + (int64_t)x * CN;
 #pragma unroll
-        for (int k = 0; k < CN; k++) d[k] = (uint8_t)min(max((acc[k] + (1 << 14)) >> 15, 0), 255);
+        for (int k = 0; k < CN; k++) d[k] = (uint8_t)bilerp_ch(v[0][k], v[1][k], v[2][k], v[3][k], fx, fy);
     }
 }
 
-hipError_t launch_remap_u8(const int16_t* tab, const uint8_t* src, int sw, int sh, int64_t spitch, int cn,
+hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, int cn,
                            const float* map1, const float* map2, int mw, int mh, int64_t mpitch, float scale_x,
                            float scale_y, uint8_t* dst, int64_t dpitch, hipStream_t s) {
     const int64_t total = (int64_t)mw * mh;
@@ -755,20 +802,36 @@ hipError_t launch_remap_u8(const int16_t* tab, const uint8_t* src, int sw, int s
     if (blocks < 1) blocks = 1;
     switch (cn) {
         case 1:
-            hipLaunchKernelGGL(remap_u8_kernel<1>, dim3(blocks), dim3(256), 0, s, tab, src, sw, sh, spitch, map1, map2,
+            hipLaunchKernelGGL(remap_u8_kernel<1>, dim3(blocks), dim3(256), 0, s, src, sw, sh, spitch, map1, map2,
                                mw, mh, mpitch, scale_x, scale_y, dst, dpitch);
             break;
         case 3:
-            hipLaunchKernelGGL(remap_u8_kernel<3>, dim3(blocks), dim3(256), 0, s, tab, src, sw, sh, spitch, map1, map2,
+            hipLaunchKernelGGL(remap_u8_kernel<3>, dim3(blocks), dim3(256), 0, s, src, sw, sh, spitch, map1, map2,
                                mw, mh, mpitch, scale_x, scale_y, dst, dpitch);
             break;
         case 4:
-            hipLaunchKernelGGL(remap_u8_kernel<4>, dim3(blocks), dim3(256), 0, s, tab, src, sw, sh, spitch, map1, map2,
+            hipLaunchKernelGGL(remap_u8_kernel<4>, dim3(blocks), dim3(256), 0, s, src, sw, sh, spitch, map1, map2,
                                mw, mh, mpitch, scale_x, scale_y, dst, dpitch);
             break;
         default:
             return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Self-test: device saturating conversions (rint + clamp vs v_cvt_pk_u8_f32).
+// ---------------------------------------------------------------------------------------------
+__global__ void selftest_sat_kernel(const float* in, uint8_t* out, int n, int method) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = in[i];
+    out[i] = method == 0 ? (uint8_t)sat_u8_rne(v) : (uint8_t)(__builtin_amdgcn_cvt_pk_u8_f32(v, 0, 0u) & 255u);
+}
+
+hipError_t launch_selftest_sat(const float* in, uint8_t* out, int n, int method, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(selftest_sat_kernel, dim3((n + 255) / 256), dim3(256), 0, s, in, out, n, method);
     return hipGetLastError();
 }
 

@@ -39,22 +39,25 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
 // ---- tiled composite (the per-frame hot path) -------------------------------------------------
 // The output is cut into 128 x 8 pixel tiles (one 256-lane workgroup per tile, one 2x2 quad per
 // lane).  Per tile the host pre-computes, once per rig, which cameras win inside it (<= 4 "slots")
-// and the luma bounding box of every bilinear tap of each slot.  A staged tile first converts those
-// boxes from YUV420P (coalesced dword Y + u16 U/V loads) into packed RGBA in LDS — every source
-// pixel converted once, as NPP's full-frame pass does in the reference — so a tap is one LDS dword.
-// The LUT is tile-major, 4 bytes per pixel, relative to the slot's box origin:
-//   bits 0-7 relx, 8-15 rely, 16-20 fx, 21-25 fy, 26-27 slot, 28-31 tap-valid mask (tap t = bit t;
-//   taps: 0 (x,y), 1 (x+1,y), 2 (x,y+1), 3 (x+1,y+1); all clear = black pixel).
+// and the luma bounding box of every in-image bilinear tap of each slot.  A staged tile converts
+// those boxes from YUV420P (dword Y + u16 U/V loads) into packed RGBA in LDS — every source pixel
+// converted once, as NPP's full-frame pass does in the reference — at a tile-uniform row stride.
+// LDS dwords 0-3 of the tile area are zero: out-of-image taps point there (BORDER_CONSTANT).
+// The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel:
+//   bits 0-12 LDS dword offset of tap (x, y); 13-17 fx; 18-22 fy; 23-24 slot;
+//   25-28 tap-valid mask (bit t: tap t in the image; taps 0 (x,y), 1 (x+1,y), 2 (x,y+1), 3 (x+1,y+1)).
+// A pixel with no camera, or with every tap outside, has mask 0 and comes out black.
 // Tiles that do not fit (> 4 cameras, a box > 256 px, or LDS need above kTileLdsBytes) are "wide":
 // their pixels use 8-byte absolute CompositeEntry records and direct global gathers.
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
 constexpr int kTileLdsBytes = 24 * 1024;
+constexpr int kTileZeroDwords = 4;
 
 struct TileSlot {
     uint16_t cam;
     uint16_t bw, bh;   // luma box size (bw a multiple of 8, bh even)
-    uint16_t lds;      // byte offset of the slot's RGBA box (bw * bh * 4 bytes) in the tile's LDS area
+    uint16_t lds;      // dword offset of the slot's RGBA box in the tile's LDS area
     uint16_t bx0, by0; // luma box origin (bx0 multiple of 8, by0 even)
     uint16_t pad0, pad1;
 };
@@ -63,7 +66,7 @@ struct TileHdr {
     uint32_t nslots_flags;  // bits 0-2: slots used; bit 8: wide
     uint32_t wide_off;      // wide tiles: first CompositeEntry of this tile in the wide array
     uint32_t stage_groups;  // staged tiles: 4-pixel groups to convert into LDS
-    uint32_t pad_;
+    uint32_t stride;        // staged tiles: LDS row stride in dwords (max box width of the tile)
 };
 
 // One input camera as the per-frame kernels see it: a YUV420P frame in "Y over [U|V]" layout.
@@ -88,16 +91,22 @@ struct CamTemplate {
 };
 
 // Gain-feed work description (built on the host once per rig, GainCompensatorGPU ctor
-// exposure_compensate.cpp:174-221 + Mapper ctor mapper.cpp:94-114).
+// exposure_compensate.cpp:174-221 + Mapper ctor mapper.cpp:94-114).  Every working-scale pixel of
+// camera i that lies in the bitwise-AND intersection with some camera j becomes one sample: its
+// 8-byte entry plus a partner mask (bit j).  Samples are sorted by (camera, source row, column) and
+// cut into single-camera chunks of up to kGainChunk samples, one workgroup each.
+constexpr int kGainMaxCams = 16;
+#ifndef OCTVR_GAIN_CHUNK
+#define OCTVR_GAIN_CHUNK 1024
+#endif
+constexpr int kGainChunk = OCTVR_GAIN_CHUNK;
+constexpr int kGainTotalStride = 32;  // u64 words between pair totals: one 256-B line each
 struct GainChunk {
-    int32_t pair;     // index into the i<j pair list
-    int32_t begin;    // [begin, end) into the flat sample-pair arrays
+    int32_t cam;
+    int32_t begin;  // [begin, end) into the sample arrays
     int32_t end;
     int32_t pad_;
 };
-
-// initInterTab2D(INTER_LINEAR, fixpt=true) replica (imgproc/src/imgwarp.cpp:211-280), 1024 x 4.
-void bilinear_table(int16_t tab[1024 * 4]);
 
 hipError_t launch_lut_build(const CameraParams& out, const CameraParams& in, int W, int H, float* map1, float* map2,
                             uint8_t* mask, int32_t* bbox, hipStream_t s);
@@ -105,16 +114,14 @@ hipError_t launch_lut_build(const CameraParams& out, const CameraParams& in, int
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
                                 hipStream_t s);
 
-// Gain feed, three stream-ordered launches (no host sync):
-//  1. gain_norm:  every working-scale sample that lies in some pair intersection -> f32 RGB norm
-//  2. gain_pairs: per chunk of a pair's intersection, f64 sums of both cameras' norms -> partials
-//  3. gain_solve: I(i,j), A, b assembly and the cv::solve replica -> gains (device f64)
-hipError_t launch_gain_norm(const FrameSet& frames, const int16_t* tab, const CompositeEntry* samples, int n_samples,
-                            float* norms, hipStream_t s);
-hipError_t launch_gain_pairs(const float* norms, const uint2* pair_idx, const GainChunk* chunks, int n_chunks,
-                             double* partials, hipStream_t s);
-hipError_t launch_gain_solve(const double* partials, const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
-                             double* gains, hipStream_t s);
+// Gain feed in ONE launch (no host sync): each workgroup gathers its chunk's warped samples, takes
+// the f32 RGB norm (elementNorm) and adds it per partner camera into exact u64 fixed-point totals
+// (units of 2^-23, see kernels.hip); the last workgroup (per-XCD then global ticket) reads and
+// resets the totals, assembles I(i,j), A, b and solves.  `totals` (kGainMaxCams^2) and `tickets`
+// (9) must be zero before the first launch; the last workgroup leaves them zero.
+hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
+                            const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
+                            unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s);
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 
@@ -126,11 +133,13 @@ struct TiledLut {
     int tiles_x, tiles_y;
 };
 
-hipError_t launch_stitch(const FrameSet& frames_dev, const int16_t* tab, const TiledLut& lut, int W, int H,
+hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W, int H,
                          const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s);
 
-hipError_t launch_remap_u8(const int16_t* tab, const uint8_t* src, int sw, int sh, int64_t spitch, int cn, const float* map1,
+hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, int cn, const float* map1,
                            const float* map2, int mw, int mh, int64_t mpitch, float scale_x, float scale_y,
                            uint8_t* dst, int64_t dpitch, hipStream_t s);
+
+hipError_t launch_selftest_sat(const float* in, uint8_t* out, int n, int method, hipStream_t s);
 
 }  // namespace octvr

@@ -485,7 +485,6 @@ struct octvr_mapper {
     int W = 0, H = 0;
     int use_gain = 0;
     std::vector<int> in_w, in_h;
-    DevBuf<int16_t> tab;
     // tiled composite LUT (kernels.hpp)
     DevBuf<TileHdr> tile_hdr;
     DevBuf<TileSlot> tile_slots;
@@ -496,12 +495,12 @@ struct octvr_mapper {
     double staged_bytes = 0;
     DevBuf<double> gains;
     // gain feed
-    DevBuf<CompositeEntry> samples;  // unique working-scale samples used by some intersection
-    DevBuf<float> norms;
-    DevBuf<uint2> pair_idx;           // (sample of camera i, sample of camera j) per intersection pixel
-    DevBuf<GainChunk> chunks;
-    DevBuf<double> partials;
+    DevBuf<CompositeEntry> samples;  // working-scale samples that lie in some pair intersection
+    DevBuf<uint16_t> partners;       // per sample: bit j = the sample is in the (camera, j) intersection
+    DevBuf<GainChunk> chunks;        // single-camera runs of <= kGainChunk samples, one workgroup each
+    DevBuf<unsigned long long> totals;  // [kGainMaxCams][kGainMaxCams] exact pair sums, units of 2^-23
     DevBuf<int32_t> N;
+    DevBuf<uint32_t> tickets;        // 8 per-XCD + 1 global last-workgroup-done counters
     int n_chunks = 0, n_samples = 0;
     size_t n_entries = 0;
     std::vector<double> last_gains;
@@ -577,24 +576,12 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
         for (uint8_t v : smask[i]) nz += v != 0;
         N[(size_t)i * n + i] = std::max(1, nz);
     }
-    // unique samples (camera-major) and per-pair index lists
-    std::vector<std::vector<int32_t>> sample_id(n);
-    for (int i = 0; i < n; i++) sample_id[i].assign(samp[i].size(), -1);
-    std::vector<CompositeEntry> uniq;
-    auto sid = [&](int cam, size_t k) {
-        int32_t& id = sample_id[cam][k];
-        if (id < 0) {
-            id = (int32_t)uniq.size();
-            uniq.push_back(samp[cam][k]);
-        }
-        return (uint32_t)id;
-    };
-    std::vector<uint2> idx;
-    std::vector<GainChunk> chunks;
-    std::vector<std::array<int, 3>> ranges;  // (pair, begin, end) of every non-empty intersection
-    int p = 0;
+    // samples: working pixel k of camera i joins I(i,j) (exposure_compensate.cpp:262-277) for every
+    // camera j whose resized-mask intersection holds it -> one entry plus a partner bit per pixel
+    std::vector<std::vector<uint16_t>> partner(n);
+    for (int i = 0; i < n; i++) partner[i].assign(samp[i].size(), 0);
     for (int i = 0; i < n; i++)
-        for (int j = i + 1; j < n; j++, p++) {
+        for (int j = i + 1; j < n; j++) {
             const auto &a = wr[i], &b = wr[j];
             int x0 = std::max(a[0], b[0]), y0 = std::max(a[1], b[1]);
             int x1 = std::min(a[0] + a[2], b[0] + b[2]), y1 = std::min(a[1] + a[3], b[1] + b[3]);
@@ -602,37 +589,58 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
                 N[(size_t)i * n + j] = N[(size_t)j * n + i] = 1;
                 continue;
             }
-            int begin = (int)idx.size(), nz = 0;
+            int nz = 0;
             for (int y = y0; y < y1; y++)
                 for (int x = x0; x < x1; x++) {
                     size_t ka = (size_t)(y - a[1]) * a[2] + (x - a[0]);
                     size_t kb = (size_t)(y - b[1]) * b[2] + (x - b[0]);
                     if ((smask[i][ka] & smask[j][kb]) == 0) continue;
                     nz++;
-                    idx.push_back(make_uint2(sid(i, ka), sid(j, kb)));
+                    partner[i][ka] |= (uint16_t)(1u << j);
+                    partner[j][kb] |= (uint16_t)(1u << i);
                 }
             N[(size_t)i * n + j] = N[(size_t)j * n + i] = std::max(1, nz);
-            if (nz) ranges.push_back({p, begin, (int)idx.size()});
         }
-    // chunk size: ~1K entries per block, grown so the solve's partial table (<= 4096 chunks) holds all
-    int kChunk = 1024;
-    while (true) {
-        size_t cnt = 0;
-        for (auto& r : ranges) cnt += (size_t)(r[2] - r[1] + kChunk - 1) / kChunk;
-        if (cnt <= 4000) break;
-        kChunk *= 2;
+    // per camera: the samples with a partner, ordered by (source row, source column) so the lanes of
+    // a wave gather from a few neighbouring source lines; invalid (mask 0) samples read as 0 and go last
+    std::vector<CompositeEntry> uniq;
+    std::vector<uint16_t> pmask;
+    std::vector<GainChunk> chunks;
+    for (int i = 0; i < n; i++) {
+        std::vector<uint32_t> ks;
+        for (size_t k = 0; k < samp[i].size(); k++)
+            if (partner[i][k]) ks.push_back((uint32_t)k);
+        auto key = [&](uint32_t k) {
+            const CompositeEntry& e = samp[i][k];
+            const uint64_t valid = (e.code & 0x8000u) ? 0 : 1;
+            return (valid << 60) | ((uint64_t)(e.xy >> 16) << 24) | (uint64_t)(e.xy & 0xFFFFu);
+        };
+        std::stable_sort(ks.begin(), ks.end(), [&](uint32_t a, uint32_t b) { return key(a) < key(b); });
+        const int begin = (int)uniq.size();
+        for (uint32_t k : ks) {
+            CompositeEntry e = samp[i][k];
+            if (!(e.code & 0x8000u)) e.code = (uint16_t)(i << 10);  // a zero sample of camera i
+            uniq.push_back(e);
+            pmask.push_back(partner[i][k]);
+        }
+        for (int s0 = begin; s0 < (int)uniq.size(); s0 += kGainChunk)
+            chunks.push_back(GainChunk{i, s0, std::min((int)uniq.size(), s0 + kGainChunk), 0});
     }
-    for (auto& r : ranges)
-        for (int s0 = r[1]; s0 < r[2]; s0 += kChunk) chunks.push_back(GainChunk{r[0], s0, std::min(r[2], s0 + kChunk), 0});
     m.samples.upload(uniq.data(), uniq.size());
-    m.norms.alloc(std::max<size_t>(uniq.size(), 1));
-    m.pair_idx.upload(idx.data(), idx.size());
+    m.partners.upload(pmask.data(), pmask.size());
     m.chunks.upload(chunks.data(), chunks.size());
-    m.partials.alloc(std::max<size_t>(2 * chunks.size(), 2));
+    // exactness bound of the fixed-point totals (kernels.hip, gain feed): < 2^21 samples per camera
+    for (int i = 0; i < n; i++) REQUIRE(samp[i].size() < (1u << 21), "working-scale ROI too large for exact gain sums");
+    m.totals.alloc((size_t)kGainMaxCams * kGainMaxCams * kGainTotalStride);
+    HIP_CHECK(hipMemset(m.totals.p, 0, sizeof(unsigned long long) * kGainMaxCams * kGainMaxCams * kGainTotalStride));
     m.N.upload(N.data(), N.size());
+    m.tickets.alloc(9);
+    HIP_CHECK(hipMemset(m.tickets.p, 0, sizeof(uint32_t) * 9));
     m.n_chunks = (int)chunks.size();
     m.n_samples = (int)uniq.size();
-    m.n_entries = idx.size();
+    size_t pairs_px = 0;
+    for (uint16_t pm : pmask) pairs_px += (size_t)__builtin_popcount(pm);
+    m.n_entries = pairs_px;
 }
 
 // Tiled composite LUT (kernels.hpp "tiled composite") from the per-pixel winner LUT.  Once per rig.
@@ -696,45 +704,51 @@ void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
             }
             if (ns > kTileSlots) wide = true;
             TileSlot ts[kTileSlots] = {};
-            uint32_t lds = 0, dwords = 0;
+            int bws[kTileSlots] = {}, bhs[kTileSlots] = {};
+            uint32_t stride = 0, groups = 0;
             for (int j = 0; j < ns && !wide; j++) {
                 const int iw = m.in_w[cams[j]];
-                if (iw % 8) {
+                if (iw % 8) {  // dword staging of boxes needs 8-aligned box columns inside the image
                     wide = true;
                     break;
                 }
                 const int bx0 = minx[j] & ~7, by0 = miny[j] & ~1;
                 const int bx1 = (maxx[j] + 1 + 7) & ~7, by1 = (maxy[j] + 1 + 1) & ~1;
-                const int bw = bx1 - bx0, bh = by1 - by0;
-                if (bw > 256 || bh > 256) {
+                bws[j] = bx1 - bx0;
+                bhs[j] = by1 - by0;
+                if (bws[j] > 256 || bhs[j] > 256) {
                     wide = true;
                     break;
                 }
                 ts[j].cam = (uint16_t)cams[j];
-                ts[j].bw = (uint16_t)bw;
-                ts[j].bh = (uint16_t)bh;
+                ts[j].bw = (uint16_t)bws[j];
+                ts[j].bh = (uint16_t)bhs[j];
                 ts[j].bx0 = (uint16_t)bx0;
                 ts[j].by0 = (uint16_t)by0;
-                ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
-                lds += (uint32_t)(bw * bh * 4);
-                dwords += (uint32_t)(bw * bh / 4);
+                stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
+                groups += (uint32_t)(bws[j] * bhs[j] / 4);
             }
-            if (lds > (uint32_t)kTileLdsBytes) wide = true;
+            uint32_t lds = kTileZeroDwords;
+            for (int j = 0; j < ns && !wide; j++) {
+                ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
+                lds += stride * (uint32_t)bhs[j];
+            }
+            if (lds * 4 > (uint32_t)kTileLdsBytes) wide = true;
             if (wide) {
                 is_wide[t] = 1;
                 hdr[t] = TileHdr{0x100u, 0u, 0u, 0u};
                 wide_local[tid].emplace_back(t, std::vector<CompositeEntry>(raw, raw + kTilePx));
                 continue;
             }
-            hdr[t] = TileHdr{(uint32_t)ns, 0u, dwords, 0u};
+            hdr[t] = TileHdr{(uint32_t)ns, 0u, groups, stride};
             for (int j = 0; j < kTileSlots; j++) slots[(size_t)t * kTileSlots + j] = ts[j];
             uint32_t* out = entries.data() + (size_t)t * kTilePx;
             for (int k = 0; k < kTilePx; k++) {
-                if (!px[k].mask) continue;
+                if (!px[k].mask) continue;  // black
                 const TileSlot& sl = ts[px[k].slot];
-                const uint32_t rx = (uint32_t)(px[k].x0 - sl.bx0), ry = (uint32_t)(px[k].y0 - sl.by0);
-                out[k] = rx | (ry << 8) | ((uint32_t)px[k].fxy << 16) | ((uint32_t)px[k].slot << 26) |
-                         ((uint32_t)px[k].mask << 28);
+                const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
+                out[k] = off | ((uint32_t)(px[k].fxy & 31) << 13) | ((uint32_t)(px[k].fxy >> 5) << 18) |
+                         ((uint32_t)px[k].slot << 23) | ((uint32_t)px[k].mask << 25);
             }
         }
     };
@@ -759,7 +773,7 @@ void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
     m.tile_wide.upload(wide.data(), wide.size());
     m.n_wide_tiles = (int)all.size();
     double sb = 0;
-    for (auto& h : hdr) sb += 6.0 * h.stage_groups;  // 4 Y + 2 U/V bytes read per 4-pixel group
+    for (auto& h : hdr) sb += 8.0 * h.stage_groups;  // 4 Y + 2 U + 2 V bytes loaded per 4-pixel group
     m.staged_bytes = sb;
     m.tiled = TiledLut{m.tile_hdr.p, m.tile_slots.p, m.tile_entries.p, m.tile_wide.p, tx_n, ty_n};
 }
@@ -981,9 +995,6 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         m->use_gain = (enable_gain && m->n > 1) ? 1 : 0;
         REQUIRE(!m->use_gain || m->n <= 16, "gain estimation supports at most 16 inputs");
         DeviceGuard dg(device);
-        int16_t tab[4096];
-        bilinear_table(tab);
-        m->tab.upload(tab, 4096);
         // per-camera templates -> device, composite LUT, then drop the per-camera maps
         {
             std::vector<DevBuf<float>> m1(m->n), m2(m->n);
@@ -1039,10 +1050,12 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
             if (gains) {
                 REQUIRE(n_gains == m->n, "gains must have one entry per input");
                 HIP_CHECK(launch_set_gains(gains, m->n, m->gains.p, s));
+            } else if (m->n_chunks == 0) {  // no intersections: A = diag(b), every gain is 1
+                const std::vector<double> ones(m->n, 1.0);
+                HIP_CHECK(launch_set_gains(ones.data(), m->n, m->gains.p, s));
             } else {
-                HIP_CHECK(launch_gain_norm(fs, m->tab.p, m->samples.p, m->n_samples, m->norms.p, s));
-                HIP_CHECK(launch_gain_pairs(m->norms.p, m->pair_idx.p, m->chunks.p, m->n_chunks, m->partials.p, s));
-                HIP_CHECK(launch_gain_solve(m->partials.p, m->chunks.p, m->n_chunks, m->N.p, m->n, m->gains.p, s));
+                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->chunks.p, m->n_chunks, m->N.p, m->n,
+                                           m->totals.p, m->tickets.p, m->gains.p, s));
             }
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1051,8 +1064,7 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
             HIP_CHECK(hipEventCreate(&e1));
             HIP_CHECK(hipEventRecord(e0, s));
         }
-        HIP_CHECK(launch_stitch(fs, m->tab.p, m->tiled, m->W, m->H, m->gains.p, m->use_gain, out_dev,
-                                (int64_t)out_pitch, s));
+        HIP_CHECK(launch_stitch(fs, m->tiled, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
         if (m->timing) {
             HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
@@ -1142,22 +1154,15 @@ int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, co
         REQUIRE(src && map1 && map2 && dst && sw > 0 && sh > 0 && mw >= 0 && mh >= 0, "bad arguments");
         REQUIRE(cn == 1 || cn == 3 || cn == 4, "cn must be 1, 3 or 4");
         if (mw == 0 || mh == 0) return;
-        // one shared table per device (allocated on first use, never freed: 8 KiB)
-        static thread_local std::vector<std::pair<int, int16_t*>> tabs;
-        int dev = 0;
-        HIP_CHECK(hipGetDevice(&dev));
-        int16_t* t = nullptr;
-        for (auto& kv : tabs)
-            if (kv.first == dev) t = kv.second;
-        if (!t) {
-            int16_t host[4096];
-            bilinear_table(host);
-            HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&t), sizeof host));
-            HIP_CHECK(hipMemcpy(t, host, sizeof host, hipMemcpyHostToDevice));
-            tabs.emplace_back(dev, t);
-        }
-        HIP_CHECK(launch_remap_u8(t, src, sw, sh, (int64_t)spitch, cn, map1, map2, mw, mh, (int64_t)mpitch, scale_x,
+        HIP_CHECK(launch_remap_u8(src, sw, sh, (int64_t)spitch, cn, map1, map2, mw, mh, (int64_t)mpitch, scale_x,
                                   scale_y, dst, (int64_t)dpitch, (hipStream_t)stream));
+    });
+}
+
+int octvr_selftest_sat_u8(const float* in, uint8_t* out, int n, int method, void* stream) {
+    return guarded([&] {
+        REQUIRE(in && out && n >= 0 && (method == 0 || method == 1), "bad arguments");
+        HIP_CHECK(launch_selftest_sat(in, out, n, method, (hipStream_t)stream));
     });
 }
 

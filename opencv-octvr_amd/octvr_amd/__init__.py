@@ -228,6 +228,19 @@ class Mapper:
             pass
 
 
+_lib.octvr_selftest_sat_u8.argtypes = [_VP, _VP, C.c_int, C.c_int, _VP]
+
+
+def selftest_sat_u8(values, method, stream=None):
+    """Device float -> u8 saturating conversion (kernel self-test)."""
+    x = values if isinstance(values, torch.Tensor) else torch.tensor(values, dtype=torch.float32)
+    x = x.to(device="cuda", dtype=torch.float32).contiguous()
+    out = torch.empty(x.numel(), dtype=torch.uint8, device=x.device)
+    _check(_lib.octvr_selftest_sat_u8(C.c_void_p(x.data_ptr()), C.c_void_p(out.data_ptr()), x.numel(), method,
+                                      _stream_ptr(stream)))
+    return out
+
+
 def remap_u8(src, map1, map2, scale_x, scale_y, out=None, stream=None):
     """cv::remap INTER_LINEAR on cuda uint8 tensors (H x W [x cn]); maps are cuda float32 (mh x mw)."""
     cn = 1 if src.dim() == 2 else src.shape[2]

@@ -465,21 +465,38 @@ static inline uint8_t sat_u8_rne(float v) {
     return (uint8_t)lrintf(v);
 }
 
+/* The library's own BT.601 colour definitions (they stand in for NPP's closed arithmetic; parity
+ * with NPP is unpinned).  Fused multiply-adds, round half to even, saturate — kernels.hip uses the
+ * identical operation sequence. */
+static inline void yuv_px_to_rgb(int y, int u, int v, uint8_t* o) {
+    float Yf = (float)y, Uf = (float)u - 128.f, Vf = (float)v - 128.f;
+    o[0] = sat_u8_rne(fmaf(1.140f, Vf, Yf));
+    o[1] = sat_u8_rne(fmaf(-0.581f, Vf, fmaf(-0.394f, Uf, Yf)));
+    o[2] = sat_u8_rne(fmaf(2.032f, Uf, Yf));
+}
+
+/* 2x2 RGB quad -> 4 Y + 1 U + 1 V (U, V from the mean of the per-pixel chroma differences). */
+static inline void rgb_quad_to_yuv(const uint8_t* const p[4], uint8_t Y[4], uint8_t* U, uint8_t* V) {
+    float us = 0.f, vs = 0.f;
+    for (int k = 0; k < 4; k++) {
+        float R = p[k][0], G = p[k][1], B = p[k][2];
+        float Yf = fmaf(0.114f, B, fmaf(0.587f, G, 0.299f * R));
+        Y[k] = sat_u8_rne(Yf);
+        us = fmaf(0.492f, B - Yf, us);
+        vs = fmaf(0.877f, R - Yf, vs);
+    }
+    *U = sat_u8_rne(fmaf(us, 0.25f, 128.f));
+    *V = sat_u8_rne(fmaf(vs, 0.25f, 128.f));
+}
+
 void orc_yuv420_to_rgba(const uint8_t* yuv, int w, int h, size_t pitch, uint8_t* rgba, size_t rgba_pitch) {
     const uint8_t* U = yuv + (size_t)h * pitch;
     const uint8_t* V = U + w / 2;
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) {
-            float Yf = (float)yuv[(size_t)y * pitch + x];
-            float Uf = (float)U[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
-            float Vf = (float)V[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
-            float R = Yf + 1.140f * Vf;
-            float G = Yf - 0.394f * Uf - 0.581f * Vf;
-            float B = Yf + 2.032f * Uf;
             uint8_t* o = rgba + (size_t)y * rgba_pitch + (size_t)x * 4;
-            o[0] = sat_u8_rne(R);
-            o[1] = sat_u8_rne(G);
-            o[2] = sat_u8_rne(B);
+            yuv_px_to_rgb(yuv[(size_t)y * pitch + x], U[(size_t)(y >> 1) * pitch + (x >> 1)],
+                          V[(size_t)(y >> 1) * pitch + (x >> 1)], o);
             o[3] = 255;
         }
 }
@@ -489,18 +506,11 @@ void orc_rgb_to_yuv420(const uint8_t* rgb, int w, int h, size_t rgb_pitch, int c
     uint8_t* Vo = Uo + w / 2;
     for (int y = 0; y < h; y += 2)
         for (int x = 0; x < w; x += 2) {
-            float us = 0.f, vs = 0.f;
-            for (int dy = 0; dy < 2; dy++)
-                for (int dx = 0; dx < 2; dx++) {
-                    const uint8_t* p = rgb + (size_t)(y + dy) * rgb_pitch + (size_t)(x + dx) * cn;
-                    float R = p[0], G = p[1], B = p[2];
-                    float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
-                    yuv[(size_t)(y + dy) * pitch + x + dx] = sat_u8_rne(Yf);
-                    us = us + (0.492f * (B - Yf) + 128.f);
-                    vs = vs + (0.877f * (R - Yf) + 128.f);
-                }
-            Uo[(size_t)(y >> 1) * pitch + (x >> 1)] = sat_u8_rne(us * 0.25f);
-            Vo[(size_t)(y >> 1) * pitch + (x >> 1)] = sat_u8_rne(vs * 0.25f);
+            const uint8_t* p[4];
+            uint8_t Yq[4];
+            for (int k = 0; k < 4; k++) p[k] = rgb + (size_t)(y + (k >> 1)) * rgb_pitch + (size_t)(x + (k & 1)) * cn;
+            rgb_quad_to_yuv(p, Yq, &Uo[(size_t)(y >> 1) * pitch + (x >> 1)], &Vo[(size_t)(y >> 1) * pitch + (x >> 1)]);
+            for (int k = 0; k < 4; k++) yuv[(size_t)(y + (k >> 1)) * pitch + x + (k & 1)] = Yq[k];
         }
 }
 
@@ -747,13 +757,9 @@ static void yuv_rows(void* c, int y0, int y1) {
     const uint8_t* V = U + w / 2;
     for (int y = y0; y < y1; y++)
         for (int x = 0; x < w; x++) {
-            float Yf = (float)yuv[(size_t)y * pitch + x];
-            float Uf = (float)U[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
-            float Vf = (float)V[(size_t)(y >> 1) * pitch + (x >> 1)] - 128.f;
             uint8_t* o = s->rgba + ((size_t)y * w + x) * 4;
-            o[0] = sat_u8_rne(Yf + 1.140f * Vf);
-            o[1] = sat_u8_rne(Yf - 0.394f * Uf - 0.581f * Vf);
-            o[2] = sat_u8_rne(Yf + 2.032f * Uf);
+            yuv_px_to_rgb(yuv[(size_t)y * pitch + x], U[(size_t)(y >> 1) * pitch + (x >> 1)],
+                          V[(size_t)(y >> 1) * pitch + (x >> 1)], o);
             o[3] = 255;
         }
 }
@@ -809,18 +815,11 @@ static void out_rows(void* c, int q0, int q1) {
     for (int q = q0; q < q1; q++) {
         int y = 2 * q;
         for (int x = 0; x < f->out_w; x += 2) {
-            float us = 0.f, vs = 0.f;
-            for (int dy = 0; dy < 2; dy++)
-                for (int dx = 0; dx < 2; dx++) {
-                    const uint8_t* p = s->result + ((size_t)(y + dy) * W + x + dx) * 3;
-                    float R = p[0], G = p[1], B = p[2];
-                    float Yf = 0.299f * R + 0.587f * G + 0.114f * B;
-                    f->out_yuv[(size_t)(y + dy) * f->out_pitch + x + dx] = sat_u8_rne(Yf);
-                    us = us + (0.492f * (B - Yf) + 128.f);
-                    vs = vs + (0.877f * (R - Yf) + 128.f);
-                }
-            Uo[(size_t)q * f->out_pitch + (x >> 1)] = sat_u8_rne(us * 0.25f);
-            Vo[(size_t)q * f->out_pitch + (x >> 1)] = sat_u8_rne(vs * 0.25f);
+            const uint8_t* p[4];
+            uint8_t Yq[4];
+            for (int k = 0; k < 4; k++) p[k] = s->result + ((size_t)(y + (k >> 1)) * W + x + (k & 1)) * 3;
+            rgb_quad_to_yuv(p, Yq, &Uo[(size_t)q * f->out_pitch + (x >> 1)], &Vo[(size_t)q * f->out_pitch + (x >> 1)]);
+            for (int k = 0; k < 4; k++) f->out_yuv[(size_t)(y + (k >> 1)) * f->out_pitch + x + (k & 1)] = Yq[k];
         }
     }
 }

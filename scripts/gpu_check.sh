@@ -23,6 +23,10 @@ for s in $STEPS; do
     pytest) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py --steps 30 --warmup 5 ;;
+    pmc)    step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex stitch_tiled -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --pmc-child --steps 5
+            step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex stitch_tiled -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --pmc-child --steps 5
+            step pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT --kernel-include-regex stitch_tiled -d gpurun_out/pmc_sq -o run --output-format csv -- python3 bench.py --pmc-child --steps 5
+            step pmc_sq2 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE SQ_INSTS_VMEM_WR --kernel-include-regex stitch_tiled -d gpurun_out/pmc_sq2 -o run --output-format csv -- python3 bench.py --pmc-child --steps 5 ;;
     prof)   step prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
   esac
 done

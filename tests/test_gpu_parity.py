@@ -124,10 +124,43 @@ def test_gpu_stitch_fixed_gains_bit_exact(ox, name):
 def test_gpu_stitch_estimated_gains(ox, name):
     from octvr_amd import synthetic
     got, want, g_gpu, g_orc = _stitch_case(ox, name, synthetic.smooth_yuv_frame, None)
-    # deterministic block-ordered f64 sums vs the oracle's serial sums: last-bit differences only
-    np.testing.assert_allclose(g_gpu, g_orc, rtol=1e-12, atol=0)
-    if np.array_equal(g_gpu.astype(np.float32), g_orc.astype(np.float32)):
-        assert np.array_equal(got, want)
+    # the pair sums are exact (u64 fixed point on the GPU, exact f64 in the oracle): gains bit-exact
+    np.testing.assert_array_equal(g_gpu, g_orc)
+    assert np.array_equal(got, want)
+
+
+def _ring_rig(n, in_w=320, in_h=240):
+    from octvr_amd import synthetic
+    yaws = [2 * math.pi * k / n for k in range(n)]
+    pitches = [0.35 * (-1) ** k for k in range(n)]
+    return synthetic.fisheye_rig(in_w, in_h, yaws, pitches)
+
+
+@pytest.mark.parametrize("n", [4, 7, 9, 12, 16])
+def test_gpu_ring_estimated_gains_bit_exact(ox, n):
+    """n cameras in a ring: the register LU (n <= 8) and the workgroup LU (9..16) of the fused feed,
+    two frames in a row (the feed's totals and tickets must reset), gains and output vs the oracle."""
+    import torch
+    from octvr_amd import synthetic
+    rig = _ring_rig(n)
+    W, H = 512, 256
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
+    sizes = [(320, 240)] * n
+    rois, maps1, maps2, masks = [], [], [], []
+    for i in range(n):
+        roi, m1, m2, mk, _ = mt.input(i)
+        rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk)
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True)
+    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    for frame_no in range(2):
+        frames = [synthetic.smooth_yuv_frame(w, h, 100 * n + 10 * frame_no + i) for i, (w, h) in enumerate(sizes)]
+        m.stitch([_cuda(f) for f in frames], out)
+        torch.cuda.synchronize()
+        g = np.array(m.gains())
+        want, g_orc = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None)
+        np.testing.assert_array_equal(g, np.array(g_orc))
+        assert not np.all(g == 1.0)
+        assert np.array_equal(out.cpu().numpy(), want), frame_no
 
 
 def test_gpu_stitch_is_deterministic_and_stream_ordered(ox):
@@ -232,3 +265,25 @@ def test_gpu_c2_stitch_row_bands_vs_oracle(ox, c2):
         y0, y1 = band
         assert np.array_equal(got[y0:y1], want[y0:y1]), band
         assert np.array_equal(got[H + y0 // 2:H + y1 // 2], want[H + y0 // 2:H + y1 // 2]), band
+
+
+def test_gpu_saturating_conversion_kat(ox):
+    # saturate_cast<uchar>(float) = round half to even, then clamp to [0, 255]; NaN -> 0
+    vals = [-1e9, -256.0, -1.0, -0.5, -0.49, -0.0, 0.0, 0.25, 0.5, 0.5000001, 1.5, 2.5, 3.49999, 3.5, 126.5, 127.5,
+            254.4, 254.5, 254.5001, 255.0, 255.49, 255.5, 256.0, 1e9, float("inf"), float("-inf"), float("nan")]
+    want = np.array([0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 2, 2, 3, 4, 126, 128, 254, 254, 255, 255, 255, 255, 255, 255, 255,
+                     0, 0], np.uint8)
+    rng = np.random.default_rng(5)
+    extra = rng.uniform(-10, 270, 100000).astype(np.float32)
+    extra = np.concatenate([extra, (np.arange(-20, 560) / 2).astype(np.float32)])
+    ref = np.clip(np.rint(extra), 0, 255).astype(np.uint8)
+    for method in (0, 1):
+        got = ox.selftest_sat_u8(vals, method).cpu().numpy()
+        assert np.array_equal(got, want), (method, got)
+        got2 = ox.selftest_sat_u8(torch_tensor(extra), method).cpu().numpy()
+        assert np.array_equal(got2, ref), method
+
+
+def torch_tensor(a):
+    import torch
+    return torch.from_numpy(a)
