@@ -69,6 +69,12 @@ __device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t
 // Direct (global-memory) bilinear sample of one camera at an 8-byte composite entry — the gain feed
 // samples and "wide" tiles.  Every load is issued unconditionally from a clamped in-image address;
 // taps outside the image and invalid entries are zeroed afterwards.
+// global-address-space views (loads through pointers held in LDS / structs would otherwise be flat)
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(1))) uint16_t gu16;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
 // wave-uniform value -> SGPR (scalar loads / branches downstream)
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -524,8 +530,12 @@ hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, 
 // walked grid-stride; blocks b, b+8, ... (one XCD under round-robin dispatch) take a contiguous
 // band of tiles so their source boxes share that XCD's L2.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4], uint8_t* out,
-                                            uint8_t* outU, uint8_t* outV, int64_t out_pitch, int x, int y) {
+struct QuadOut {
+    uint32_t y01, y23;  // two Y bytes of each row
+    uint32_t u, v;
+};
+
+__device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
     uint32_t y01 = 0, y23 = 0;
     float us = 0.f, vs = 0.f;
 #pragma unroll
@@ -540,187 +550,276 @@ __device__ __forceinline__ void finish_quad(const uint32_t (&rgb)[4][3], const f
         us = __builtin_fmaf(0.492f, B - Yf, us);
         vs = __builtin_fmaf(0.877f, R - Yf, vs);
     }
-    *reinterpret_cast<uint16_t*>(out + (int64_t)y * out_pitch + x) = (uint16_t)y01;
-    *reinterpret_cast<uint16_t*>(out + (int64_t)(y + 1) * out_pitch + x) = (uint16_t)y23;
-    outU[(int64_t)(y >> 1) * out_pitch + (x >> 1)] = (uint8_t)pack_u8(__builtin_fmaf(us, 0.25f, 128.f), 0, 0u);
-    outV[(int64_t)(y >> 1) * out_pitch + (x >> 1)] = (uint8_t)pack_u8(__builtin_fmaf(vs, 0.25f, 128.f), 0, 0u);
+    QuadOut q;
+    q.y01 = y01;
+    q.y23 = y23;
+    q.u = pack_u8(__builtin_fmaf(us, 0.25f, 128.f), 0, 0u);
+    q.v = pack_u8(__builtin_fmaf(vs, 0.25f, 128.f), 0, 0u);
+    return q;
+}
+
+// The output frame as a buffer resource: stores of a quad outside W x H get an offset past the
+// range and are dropped by the hardware, so every lane issues the same stores (no branch) and the
+// per-iteration count of outstanding vector-memory operations is fixed.
+struct OutFrame {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t pitch;
+    uint32_t u_off, v_off;  // byte offsets of the U and V planes
+};
+constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host: frame < 2^31 - 64 B)
+
+__device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
+    const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
+    const uint32_t oc = in ? (uint32_t)(y >> 1) * o.pitch + (uint32_t)(x >> 1) : kDropOffset;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, 0);
 }
 
 
-// The tile's slot descriptors in scalar registers (the tile index is wave-uniform).
+// The tile's slot descriptors as 16 raw dwords in scalar registers (the tile index is wave-uniform).
+// Slot q: dword 4q = cam | bw << 16, 4q+1 = bh | lds << 16, 4q+2 = bx0 | by0 << 16, 4q+3 = chunk0.
+// Only static indices and explicit selects touch it, so it never lands in scratch memory.
 struct SlotSet {
-    TileSlot s[kTileSlots];
+    uint32_t w[4 * kTileSlots];
 };
+static_assert(sizeof(TileSlot) == 16, "TileSlot layout");
 
-__device__ __forceinline__ SlotSet load_slots(const TiledLut& lut, int t) {
-    SlotSet ss;
-    const uint4* p = reinterpret_cast<const uint4*>(lut.slots + (int64_t)t * kTileSlots);
-#pragma unroll
-    for (int q = 0; q < kTileSlots; q++) {
-        uint4 v = p[q];
-        v.x = (uint32_t)uniform((int)v.x);
-        v.y = (uint32_t)uniform((int)v.y);
-        v.z = (uint32_t)uniform((int)v.z);
-        v.w = (uint32_t)uniform((int)v.w);
-        memcpy(&ss.s[q], &v, sizeof(uint4));
-    }
-    return ss;
+__device__ __forceinline__ uint32_t sel4(int q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+    return q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : a3;
 }
 
-// One 4-pixel staging group of a tile: the YUV bytes it needs and its LDS destination.
+// The per-call FrameSet is the FIRST argument of the stitch kernels: index it in the kernarg
+// segment directly (a wave-uniform index gives scalar loads; indexing the by-value parameter would
+// copy it to scratch).
+typedef __attribute__((address_space(4))) const SourceFrame kSourceFrame;
+static_assert(offsetof(FrameSet, f) == 0, "FrameSet layout");
+__device__ __forceinline__ SourceFrame kernarg_frame(uint32_t cam) {
+    const kSourceFrame* kf = (const kSourceFrame*)__builtin_amdgcn_kernarg_segment_ptr();
+    SourceFrame s;
+    s.yuv = kf[cam].yuv;
+    s.w = kf[cam].w;
+    s.h = kf[cam].h;
+    s.pitch = kf[cam].pitch;
+    return s;
+}
+
+// One 8-pixel staging group of a tile: the YUV bytes it needs and its LDS destination.
 struct StageGroup {
-    uint32_t yq, uq, vq;  // 4 Y bytes, 2 U bytes, 2 V bytes
-    int32_t dst;          // dword index of the group's first RGBA pixel; -1 = none
+    uint32_t y0, y1;  // 8 Y bytes
+    uint32_t uq, vq;  // 4 U bytes, 4 V bytes
+    int32_t dst;      // dword index of the group's first RGBA pixel; -1 = none
 };
 
+// Loads of staging chunk c (wave-uniform) of a tile: 64 groups of 8 luma pixels inside one slot.
+// The slot is found with scalar compares on the slots' first chunks; a lane's group k within the
+// slot is row k / (bw/8), column k % (bw/8) of the slot's box.  Lanes past the slot's groups (and
+// chunks past the tile's) read the box origin / frame start and are marked dst = -1.  With box
+// columns 8-aligned, the Y load is 8-byte and the U / V loads 4-byte aligned (DWORD_STAGE).
 template <bool DWORD_STAGE>
-__device__ __forceinline__ void stage_load(const SourceFrame* fs, const SlotSet& ss, int nslots, uint32_t stride,
-                                           uint32_t k, StageGroup& sg) {
-    uint32_t kk = k;
-    TileSlot sl = ss.s[0];
+__device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32_t nchunks, uint32_t stride, int c,
+                                           StageGroup& sg) {
+    const int lane = threadIdx.x & 63;
+    const bool live_chunk = (uint32_t)c < nchunks;
+    int q = 0;
 #pragma unroll
-    for (int q = 1; q < kTileSlots; q++) {  // slot of group k: subtract the sizes of the slots before it
-        const uint32_t n = (uint32_t)ss.s[q - 1].bw * ss.s[q - 1].bh / 4u;
-        const bool past = q < nslots && kk >= n;
-        kk = past ? kk - n : kk;
-        if (past) sl = ss.s[q];
-        if (!past) break;
-    }
-    const SourceFrame f = fs[sl.cam];
-    const uint32_t rowg = sl.bw / 4u;
-    const uint32_t row = kk / rowg, col = kk - row * rowg;
-    const int sx = sl.bx0 + (int)col * 4, sy = sl.by0 + (int)row;
-    const uint8_t* Yp = f.yuv + (int64_t)sy * f.pitch + sx;
-    const uint8_t* Up = f.yuv + (int64_t)(f.h + (sy >> 1)) * f.pitch + (sx >> 1);
-    const uint8_t* Vp = Up + (f.w >> 1);
+    for (int j = 1; j < kTileSlots; j++) q += (j < nslots && c >= (int)(ss.w[4 * j + 3] & 0xFFFFu)) ? 1 : 0;
+    const uint32_t d0 = sel4(q, ss.w[0], ss.w[4], ss.w[8], ss.w[12]);
+    const uint32_t d1 = sel4(q, ss.w[1], ss.w[5], ss.w[9], ss.w[13]);
+    const uint32_t d2 = sel4(q, ss.w[2], ss.w[6], ss.w[10], ss.w[14]);
+    const uint32_t d3 = sel4(q, ss.w[3], ss.w[7], ss.w[11], ss.w[15]);
+    const uint32_t cam = d0 & 31u, bw = d0 >> 16, bh = d1 & 0xFFFFu, lds = d1 >> 16;
+    const uint32_t bx0 = d2 & 0xFFFFu, by0 = d2 >> 16, chunk0 = d3 & 0xFFFFu;
+    const uint32_t rowg = max(1u, bw >> 3);
+    const uint32_t groups = bw * bh >> 3;
+    const uint32_t k = (uint32_t)(c - (int)chunk0) * 64u + (uint32_t)lane;
+    const bool ok = live_chunk && k < groups;
+    // k < 2^14, rowg <= 32: (k + 0.5) / rowg is >= 1/64 away from an integer, far above f32 error
+    const float inv = __builtin_amdgcn_rcpf((float)rowg);
+    const uint32_t row_f = (uint32_t)(((float)k + 0.5f) * inv);
+    const uint32_t row = ok ? row_f : 0u, col = ok ? k - row_f * rowg : 0u;
+    const SourceFrame f = kernarg_frame(live_chunk ? cam : 0u);
+    const uint32_t p32 = (uint32_t)f.pitch;
+    const gu8* base = (const gu8*)f.yuv;
+    const gu8* Yb = base + (int64_t)by0 * f.pitch + bx0;  // by0, bx0 even: chroma rows / columns exact
+    const gu8* Ub = base + (int64_t)(f.h + (int)(by0 >> 1)) * f.pitch + (bx0 >> 1);
+    const gu8* Vb = Ub + (f.w >> 1);
+    const uint32_t oy = row * p32 + col * 8u, oc = (row >> 1) * p32 + col * 4u;
     if (DWORD_STAGE) {
-        sg.yq = *reinterpret_cast<const uint32_t*>(Yp);
-        sg.uq = *reinterpret_cast<const uint16_t*>(Up);
-        sg.vq = *reinterpret_cast<const uint16_t*>(Vp);
+        const uint64_t yy = *(const gu64*)(Yb + oy);
+        sg.y0 = (uint32_t)yy;
+        sg.y1 = (uint32_t)(yy >> 32);
+        sg.uq = *(const gu32*)(Ub + oc);
+        sg.vq = *(const gu32*)(Vb + oc);
     } else {
-        sg.yq = (uint32_t)Yp[0] | ((uint32_t)Yp[1] << 8) | ((uint32_t)Yp[2] << 16) | ((uint32_t)Yp[3] << 24);
-        sg.uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8);
-        sg.vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8);
+        const gu8* Yp = Yb + oy;
+        const gu8* Up = Ub + oc;
+        const gu8* Vp = Vb + oc;
+        sg.y0 = (uint32_t)Yp[0] | ((uint32_t)Yp[1] << 8) | ((uint32_t)Yp[2] << 16) | ((uint32_t)Yp[3] << 24);
+        sg.y1 = (uint32_t)Yp[4] | ((uint32_t)Yp[5] << 8) | ((uint32_t)Yp[6] << 16) | ((uint32_t)Yp[7] << 24);
+        sg.uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8) | ((uint32_t)Up[2] << 16) | ((uint32_t)Up[3] << 24);
+        sg.vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8) | ((uint32_t)Vp[2] << 16) | ((uint32_t)Vp[3] << 24);
     }
-    sg.dst = (int32_t)(sl.lds + row * stride + col * 4u);
+    sg.dst = ok ? (int32_t)(lds + row * stride + col * 8u) : -1;
 }
 
 __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rgb) {
     if (sg.dst < 0) return;
-    uint4 px;
-    px.x = yuv_to_rgba(sg.yq & 255u, sg.uq & 255u, sg.vq & 255u);
-    px.y = yuv_to_rgba((sg.yq >> 8) & 255u, sg.uq & 255u, sg.vq & 255u);
-    px.z = yuv_to_rgba((sg.yq >> 16) & 255u, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
-    px.w = yuv_to_rgba(sg.yq >> 24, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
-    *reinterpret_cast<uint4*>(s_rgb + sg.dst) = px;
+    uint4 a, b;
+    a.x = yuv_to_rgba(sg.y0 & 255u, sg.uq & 255u, sg.vq & 255u);
+    a.y = yuv_to_rgba((sg.y0 >> 8) & 255u, sg.uq & 255u, sg.vq & 255u);
+    a.z = yuv_to_rgba((sg.y0 >> 16) & 255u, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
+    a.w = yuv_to_rgba(sg.y0 >> 24, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
+    b.x = yuv_to_rgba(sg.y1 & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u);
+    b.y = yuv_to_rgba((sg.y1 >> 8) & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u);
+    b.z = yuv_to_rgba((sg.y1 >> 16) & 255u, sg.uq >> 24, sg.vq >> 24);
+    b.w = yuv_to_rgba(sg.y1 >> 24, sg.uq >> 24, sg.vq >> 24);
+    *reinterpret_cast<uint4*>(s_rgb + sg.dst) = a;
+    *reinterpret_cast<uint4*>(s_rgb + sg.dst + 4) = b;
 }
 
+#ifndef OCTVR_STITCH_BLOCKS_PER_CU
+#define OCTVR_STITCH_BLOCKS_PER_CU 6
+#endif
+constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
 constexpr int kStageRegs = 2;  // staging groups per lane loaded one tile ahead (512 per tile)
 
-struct TilePrefetch {
+// Software pipeline over a block's tiles (t, t + step, ...):
+//   iteration of tile t:  stage tile t's YUV (loaded during the previous iteration) into LDS,
+//                         read tile t+step's metadata (loaded one iteration earlier) into SGPRs,
+//                         issue tile t+step's entries + YUV loads and tile t+2*step's metadata load,
+//                         then compute tile t from LDS while all of those are in flight.
+// No global load is waited on in the iteration that issues it, and every iteration issues the
+// same vector-memory operations in the same order (clamped addresses instead of branches), so the
+// compiler's wait counts stay exact across the loop.
+//
+// Metadata in flight is one VGPR: lanes 0-3 hold the header's dwords, lanes 4-19 the 4 slots'.
+struct TileMeta {
     int t;
     TileHdr hd;
+    SlotSet ss;
+};
+
+__device__ __forceinline__ uint32_t meta_issue(const TiledLut& lut, int t, int t_end) {  // t: staged item
+    const int lane = threadIdx.x & 63;
+    const int tt = t < t_end ? t : 0;
+    const uint32_t* p = lane < 4 ? reinterpret_cast<const uint32_t*>(lut.hdr + tt) + lane
+                                 : reinterpret_cast<const uint32_t*>(lut.slots + (int64_t)tt * kTileSlots) +
+                                       (lane < 20 ? lane - 4 : 0);
+    return *p;
+}
+
+__device__ __forceinline__ TileMeta meta_read(uint32_t v, int t) {
+    TileMeta m;
+    m.t = t;
+    m.hd.tile = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    m.hd.nslots = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
+    m.hd.stage_groups = (uint32_t)__builtin_amdgcn_readlane((int)v, 2);
+    m.hd.stride = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
+    uint32_t w[4 * kTileSlots];
+#pragma unroll
+    for (int q = 0; q < 4 * kTileSlots; q++) w[q] = (uint32_t)__builtin_amdgcn_readlane((int)v, 4 + q);
+#pragma unroll
+    for (int q = 0; q < 4 * kTileSlots; q++) m.ss.w[q] = w[q];
+    return m;
+}
+
+struct TileData {
     uint4 e4;
     StageGroup sg[kStageRegs];
 };
 
 template <bool DWORD_STAGE>
-__device__ __forceinline__ void tile_prefetch(const SourceFrame* fs, const TiledLut& lut, int t, int t_end,
-                                              TilePrefetch& pf) {
-    t = uniform(t);
-    pf.t = t;
-#pragma unroll
-    for (int r = 0; r < kStageRegs; r++) pf.sg[r].dst = -1;
-    if (t >= t_end) return;
-    const uint4 h = reinterpret_cast<const uint4*>(lut.hdr)[t];
-    pf.hd.nslots_flags = (uint32_t)uniform((int)h.x);
-    pf.hd.wide_off = (uint32_t)uniform((int)h.y);
-    pf.hd.stage_groups = (uint32_t)uniform((int)h.z);
-    pf.hd.stride = (uint32_t)uniform((int)h.w);
-    if (pf.hd.nslots_flags & 0x100u) return;  // wide tile: loaded when processed
+__device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLut& lut, const TileMeta& m, int t_end,
+                                           TileData& d) {
+    const bool live = m.t < t_end;
     const int tid = threadIdx.x;
-    pf.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)t * kTilePx)[tid];
-    const SlotSet ss = load_slots(lut, t);
-    const int nslots = (int)(pf.hd.nslots_flags & 7u);
+    const int wave = uniform(tid >> 6);
+    d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? m.t : 0) * kTilePx)[tid];
+    const uint32_t nchunks = live ? (m.hd.nslots >> 8) : 0u;
 #pragma unroll
-    for (int r = 0; r < kStageRegs; r++) {
-        const uint32_t k = (uint32_t)(tid + r * 256);
-        if (k < pf.hd.stage_groups) stage_load<DWORD_STAGE>(fs, ss, nslots, pf.hd.stride, k, pf.sg[r]);
-    }
+    for (int r = 0; r < kStageRegs; r++)
+        stage_load<DWORD_STAGE>(m.ss, (int)(m.hd.nslots & 0xFFu), nchunks, m.hd.stride, r * 4 + wave, d.sg[r]);
 }
 
+__device__ __forceinline__ OutFrame make_out_frame(uint8_t* out, int W, int H, int64_t out_pitch) {
+    OutFrame of;
+    of.pitch = (uint32_t)out_pitch;
+    of.u_off = (uint32_t)H * (uint32_t)out_pitch;
+    of.v_off = of.u_off + (uint32_t)(W >> 1);
+    of.rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)((uint32_t)out_pitch * (uint32_t)(H + H / 2)), 0x00020000);
+    return of;
+}
+
+// Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
+// dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
 template <bool DWORD_STAGE>
-__global__ void __launch_bounds__(256, 4) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
+__global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
                                                               int64_t out_pitch) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
     __shared__ float s_gain[kMaxCams];
     __shared__ float s_slot_gain[kTileSlots];
-    __shared__ SourceFrame s_frames[kMaxCams];  // divergent per-lane camera lookups hit LDS, not kernarg
 
-    const int n_tiles = lut.tiles_x * lut.tiles_y;
     const int groups = 8;
     const int g = blockIdx.x % groups;
-    const int blocks_in_g = (gridDim.x - g + groups - 1) / groups;
-    const int t_begin = (int)((int64_t)n_tiles * g / groups);
-    const int t_end = (int)((int64_t)n_tiles * (g + 1) / groups);
-    uint8_t* outU = out + (int64_t)H * out_pitch;
-    uint8_t* outV = outU + (W >> 1);
+    const int step = (gridDim.x - g + groups - 1) / groups;
+    const int t_begin = (int)((int64_t)lut.n_items * g / groups);
+    const int t_end = (int)((int64_t)lut.n_items * (g + 1) / groups);
+    const OutFrame of = make_out_frame(out, W, H, out_pitch);
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
 
-    if (tid < kMaxCams) {
-        s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
-        s_frames[tid] = frames.f[tid];
-    }
+    if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
     if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
+    const int t0 = t_begin + (int)(blockIdx.x / groups);
+    TileMeta cur = meta_read(meta_issue(lut, t0, t_end), t0);
     __syncthreads();
-    TilePrefetch pf;
-    tile_prefetch<DWORD_STAGE>(s_frames, lut, t_begin + (int)(blockIdx.x / groups), t_end, pf);
+    TileData d;
+    data_issue<DWORD_STAGE>(frames, lut, cur, t_end, d);
+    uint32_t mv = meta_issue(lut, t0 + step, t_end);
+    // opaque copies of the prologue loads: the loop-header phis then merge a load with a non-load,
+    // so the compiler cannot fold them into one load at the header (waited on right there)
+    asm volatile("" : "+v"(mv));
+    asm volatile("" : "+v"(d.e4.x), "+v"(d.e4.y), "+v"(d.e4.z), "+v"(d.e4.w));
+#pragma unroll
+    for (int r = 0; r < kStageRegs; r++)
+        asm volatile("" : "+v"(d.sg[r].y0), "+v"(d.sg[r].y1), "+v"(d.sg[r].uq), "+v"(d.sg[r].vq));
 
-    while (pf.t < t_end) {
-        const int t = uniform(pf.t);
-        const TileHdr hd = pf.hd;
-        const int tyi = t / lut.tiles_x, txi = t - tyi * lut.tiles_x;
-        const int x = txi * kTileW + qx * 2, y = tyi * kTileH + qy * 2;
-        uint32_t rgb[4][3];
-        float gain[4];
-        if (hd.nslots_flags & 0x100u) {  // wide tile: direct global gathers, no LDS
-            tile_prefetch<DWORD_STAGE>(s_frames, lut, t + blocks_in_g, t_end, pf);
-            const uint4* wp = reinterpret_cast<const uint4*>(lut.wide + hd.wide_off) + tid * 2;
-            const uint4 e0 = wp[0], e1 = wp[1];
-            const uint32_t xy[4] = {e0.x, e0.z, e1.x, e1.z};
-            const uint32_t cd[4] = {e0.y, e0.w, e1.y, e1.w};
-            Taps tp[4];
-#pragma unroll
-            for (int p = 0; p < 4; p++) gather_taps(frames, xy[p], cd[p], tp[p]);
-#pragma unroll
-            for (int p = 0; p < 4; p++) {
-                bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
-                gain[p] = s_gain[(cd[p] >> 10) & 31u];
-            }
-            if (x < W && y < H) finish_quad(rgb, gain, out, outU, outV, out_pitch, x, y);
-            continue;
+    // the previous tile's output, stored at the top of the next iteration: every store is then
+    // older than the loads it shares the iteration with (vmcnt waits on a load that is older than
+    // a store must drain everything, as loads and stores complete out of order)
+    QuadOut prev{0u, 0u, 0u, 0u};
+    int px = 0, py = 0;
+    bool pin = false;
+    while (cur.t < t_end) {
+        const int x = (int)(cur.hd.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.hd.tile >> 16) * kTileH + qy * 2;
+        const uint32_t S = cur.hd.stride;
+        const uint4 e4 = d.e4;
+        __syncthreads();  // the previous tile's LDS readers are done
+        const TileMeta nxt = meta_read(mv, cur.t + step);
+        if (tid < kTileSlots) {
+            const uint32_t cam = sel4(tid, cur.ss.w[0], cur.ss.w[4], cur.ss.w[8], cur.ss.w[12]) & 31u;
+            s_slot_gain[tid] = s_gain[cam];
         }
-        const uint4 e4 = pf.e4;
-        const uint32_t S = hd.stride;
-        const int nslots = (int)(hd.nslots_flags & 7u);
-        __syncthreads();  // the previous staged tile's LDS readers are done
-        if (tid < kTileSlots) s_slot_gain[tid] = s_gain[lut.slots[(int64_t)t * kTileSlots + tid].cam];
 #pragma unroll
-        for (int r = 0; r < kStageRegs; r++) stage_store(pf.sg[r], s_rgb);
-        if (hd.stage_groups > (uint32_t)(kStageRegs * 256)) {  // large boxes only
-            const SlotSet ss = load_slots(lut, t);
-            for (uint32_t k = tid + kStageRegs * 256; k < hd.stage_groups; k += 256) {
+        for (int r = 0; r < kStageRegs; r++) stage_store(d.sg[r], s_rgb);
+        if ((cur.hd.nslots >> 8) > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
+            const int wave = uniform(tid >> 6);
+            for (int c = kStageRegs * 4 + wave; c < (int)(cur.hd.nslots >> 8); c += 4) {
                 StageGroup sg;
-                stage_load<DWORD_STAGE>(s_frames, ss, nslots, S, k, sg);
+                stage_load<DWORD_STAGE>(cur.ss, (int)(cur.hd.nslots & 0xFFu), cur.hd.nslots >> 8, S, c, sg);
                 stage_store(sg, s_rgb);
             }
         }
         __syncthreads();
-        // the next tile's global loads are in flight while this tile computes from LDS
-        tile_prefetch<DWORD_STAGE>(s_frames, lut, t + blocks_in_g, t_end, pf);
+        store_quad(of, prev, px, py, pin);
+        data_issue<DWORD_STAGE>(frames, lut, nxt, t_end, d);
+        mv = meta_issue(lut, cur.t + 2 * step, t_end);
         const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
+        uint32_t rgb[4][3];
+        float gain[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint32_t e = ent[p];
@@ -732,30 +831,69 @@ __global__ void __launch_bounds__(256, 4) stitch_tiled_kernel(FrameSet frames, T
             bilerp_rgba(c00, c01, c10, c11, (e >> 13) & 31u, (e >> 18) & 31u, rgb[p]);
             gain[p] = s_slot_gain[(e >> 23) & 3u];
         }
-        if (x < W && y < H) finish_quad(rgb, gain, out, outU, outV, out_pitch, x, y);
+        prev = finish_quad(rgb, gain);
+        px = x;
+        py = y;
+        pin = x < W && y < H;
+        cur = nxt;
     }
+    store_quad(of, prev, px, py, pin);
+}
+
+// Wide tiles: one workgroup per tile, 8-byte absolute entries, direct global gathers.
+__global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, TiledLut lut, int W, int H,
+                                                          const double* gains, int use_gain, uint8_t* out,
+                                                          int64_t out_pitch) {
+    __shared__ float s_gain[kMaxCams];
+    const int tid = threadIdx.x;
+    if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
+    __syncthreads();
+    const OutFrame of = make_out_frame(out, W, H, out_pitch);
+    const uint32_t tile = (uint32_t)uniform((int)lut.wide_tiles[blockIdx.x]);
+    const int x = (int)(tile & 0xFFFFu) * kTileW + (tid & 63) * 2, y = (int)(tile >> 16) * kTileH + (tid >> 6) * 2;
+    const uint4* wp = reinterpret_cast<const uint4*>(lut.wide + (int64_t)blockIdx.x * kTilePx) + tid * 2;
+    const uint4 e0 = wp[0], e1 = wp[1];
+    const uint32_t xy[4] = {e0.x, e0.z, e1.x, e1.z};
+    const uint32_t cd[4] = {e0.y, e0.w, e1.y, e1.w};
+    Taps tp[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) gather_taps(frames, xy[p], cd[p], tp[p]);
+    uint32_t rgb[4][3];
+    float gain[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
+        gain[p] = s_gain[(cd[p] >> 10) & 31u];
+    }
+    store_quad(of, finish_quad(rgb, gain), x, y, x < W && y < H);
 }
 
 hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                          int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
-    // one resident wave of workgroups (256 CUs x 4 per CU at <= 128 VGPRs and < 40 KiB LDS), each
-    // walking its XCD group's tiles
-    const int tiles = lut.tiles_x * lut.tiles_y;
-    int blocks = std::min(tiles, 256 * 4);
-    blocks = std::max(8, (blocks + 7) / 8 * 8);
-    // dword staging needs 4-byte aligned Y rows and 2-byte aligned chroma rows
-    bool dw = true;
-    for (int i = 0; i < kMaxCams; i++) {
-        const SourceFrame& f = frames.f[i];
-        if (!f.yuv) continue;
-        if ((reinterpret_cast<uintptr_t>(f.yuv) & 3u) || (f.pitch & 3) || (f.w & 7)) dw = false;
+    if (lut.n_items > 0) {
+        // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU: 25 KiB LDS each), each
+        // walking its XCD band's items
+        int blocks = std::min(lut.n_items, 256 * kStitchBlocksPerCU);
+        blocks = std::max(8, (blocks + 7) / 8 * 8);
+        // wide staging loads need 8-byte aligned Y rows (then U / V rows are 4-byte aligned)
+        bool dw = true;
+        for (int i = 0; i < kMaxCams; i++) {
+            const SourceFrame& f = frames.f[i];
+            if (!f.yuv) continue;
+            if ((reinterpret_cast<uintptr_t>(f.yuv) & 7u) || (f.pitch & 7) || (f.w & 7)) dw = false;
+        }
+        if (dw)
+            hipLaunchKernelGGL(stitch_tiled_kernel<true>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
+                               use_gain, out, out_pitch);
+        else
+            hipLaunchKernelGGL(stitch_tiled_kernel<false>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
+                               use_gain, out, out_pitch);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
     }
-    if (dw)
-        hipLaunchKernelGGL(stitch_tiled_kernel<true>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
-                           use_gain, out, out_pitch);
-    else
-        hipLaunchKernelGGL(stitch_tiled_kernel<false>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
-                           use_gain, out, out_pitch);
+    if (lut.n_wide > 0)
+        hipLaunchKernelGGL(stitch_wide_kernel, dim3(lut.n_wide), dim3(256), 0, s, frames, lut, W, H, gains, use_gain,
+                           out, out_pitch);
     return hipGetLastError();
 }
 

@@ -40,15 +40,19 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
 // The output is cut into 128 x 8 pixel tiles (one 256-lane workgroup per tile, one 2x2 quad per
 // lane).  Per tile the host pre-computes, once per rig, which cameras win inside it (<= 4 "slots")
 // and the luma bounding box of every in-image bilinear tap of each slot.  A staged tile converts
-// those boxes from YUV420P (dword Y + u16 U/V loads) into packed RGBA in LDS — every source pixel
+// those boxes from YUV420P (8-byte Y + 4-byte U/V loads per 8 pixels) into packed RGBA in LDS — every source pixel
 // converted once, as NPP's full-frame pass does in the reference — at a tile-uniform row stride.
+// Staging work is cut into chunks of 64 eight-pixel groups, each chunk inside one slot, so a wave's
+// chunk has wave-uniform slot parameters (scalar registers, no per-lane slot search).
 // LDS dwords 0-3 of the tile area are zero: out-of-image taps point there (BORDER_CONSTANT).
 // The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel:
 //   bits 0-12 LDS dword offset of tap (x, y); 13-17 fx; 18-22 fy; 23-24 slot;
 //   25-28 tap-valid mask (bit t: tap t in the image; taps 0 (x,y), 1 (x+1,y), 2 (x,y+1), 3 (x+1,y+1)).
 // A pixel with no camera, or with every tap outside, has mask 0 and comes out black.
 // Tiles that do not fit (> 4 cameras, a box > 256 px, or LDS need above kTileLdsBytes) are "wide":
-// their pixels use 8-byte absolute CompositeEntry records and direct global gathers.
+// their pixels use 8-byte absolute CompositeEntry records and direct global gathers, in a second
+// launch over the list of wide tiles.  The staged tiles form a compact item list (header, slots and
+// entries indexed by item), so the staged kernel has no per-tile branch between the two kinds.
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
 constexpr int kTileLdsBytes = 24 * 1024;
@@ -59,14 +63,15 @@ struct TileSlot {
     uint16_t bw, bh;   // luma box size (bw a multiple of 8, bh even)
     uint16_t lds;      // dword offset of the slot's RGBA box in the tile's LDS area
     uint16_t bx0, by0; // luma box origin (bx0 multiple of 8, by0 even)
-    uint16_t pad0, pad1;
+    uint16_t chunk0;   // first 64-group staging chunk of this slot (slots are chunk-aligned)
+    uint16_t pad1;
 };
 
-struct TileHdr {
-    uint32_t nslots_flags;  // bits 0-2: slots used; bit 8: wide
-    uint32_t wide_off;      // wide tiles: first CompositeEntry of this tile in the wide array
-    uint32_t stage_groups;  // staged tiles: 4-pixel groups to convert into LDS
-    uint32_t stride;        // staged tiles: LDS row stride in dwords (max box width of the tile)
+struct TileHdr {           // one staged item
+    uint32_t tile;          // tile column | tile row << 16
+    uint32_t nslots;        // bits 0-7: slots used (0..4); bits 8-15: 64-group staging chunks
+    uint32_t stage_groups;  // 4-pixel groups to convert into LDS
+    uint32_t stride;        // LDS row stride in dwords (max box width of the tile)
 };
 
 // One input camera as the per-frame kernels see it: a YUV420P frame in "Y over [U|V]" layout.
@@ -126,11 +131,13 @@ hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* sample
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 
 struct TiledLut {
-    const TileHdr* hdr;
-    const TileSlot* slots;        // kTileSlots per tile
-    const uint32_t* entries;      // kTilePx per tile, tile-major, quad-major inside the tile
+    const TileHdr* hdr;           // per staged item
+    const TileSlot* slots;        // kTileSlots per staged item
+    const uint32_t* entries;      // kTilePx per staged item, quad-major inside the tile
+    int n_items;
+    const uint32_t* wide_tiles;   // tile column | row << 16 of each wide tile
     const CompositeEntry* wide;   // kTilePx per wide tile
-    int tiles_x, tiles_y;
+    int n_wide;
 };
 
 hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W, int H,

@@ -490,6 +490,8 @@ struct octvr_mapper {
     DevBuf<TileSlot> tile_slots;
     DevBuf<uint32_t> tile_entries;
     DevBuf<CompositeEntry> tile_wide;
+    DevBuf<uint32_t> tile_wide_ids;
+    int n_tiles = 0;
     TiledLut tiled{};
     int n_wide_tiles = 0;
     double staged_bytes = 0;
@@ -728,19 +730,22 @@ void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
                 stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
                 groups += (uint32_t)(bws[j] * bhs[j] / 4);
             }
-            uint32_t lds = kTileZeroDwords;
+            uint32_t lds = kTileZeroDwords, chunks = 0;
             for (int j = 0; j < ns && !wide; j++) {
                 ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
                 lds += stride * (uint32_t)bhs[j];
+                ts[j].chunk0 = (uint16_t)chunks;
+                chunks += (uint32_t)(bws[j] * bhs[j] / 8 + 63) / 64;
             }
+            for (int j = ns; j < kTileSlots; j++) ts[j].chunk0 = (uint16_t)std::min<uint32_t>(chunks, 255u);
+            if (chunks > 255) wide = true;
             if (lds * 4 > (uint32_t)kTileLdsBytes) wide = true;
             if (wide) {
                 is_wide[t] = 1;
-                hdr[t] = TileHdr{0x100u, 0u, 0u, 0u};
                 wide_local[tid].emplace_back(t, std::vector<CompositeEntry>(raw, raw + kTilePx));
                 continue;
             }
-            hdr[t] = TileHdr{(uint32_t)ns, 0u, groups, stride};
+            hdr[t] = TileHdr{(uint32_t)tx | ((uint32_t)ty << 16), (uint32_t)ns | (chunks << 8), groups, stride};
             for (int j = 0; j < kTileSlots; j++) slots[(size_t)t * kTileSlots + j] = ts[j];
             uint32_t* out = entries.data() + (size_t)t * kTilePx;
             for (int k = 0; k < kTilePx; k++) {
@@ -755,27 +760,47 @@ void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
     std::vector<std::thread> th;
     for (int i = 0; i < T; i++) th.emplace_back(work, i);
     for (auto& x : th) x.join();
+    // staged items: the non-wide tiles in tile order, compacted in place
+    int n_items = 0;
+    double sb = 0;
+    for (int t = 0; t < n_tiles; t++) {
+        if (is_wide[t]) continue;
+        if (n_items != t) {
+            hdr[n_items] = hdr[t];
+            std::copy(slots.begin() + (size_t)t * kTileSlots, slots.begin() + (size_t)(t + 1) * kTileSlots,
+                      slots.begin() + (size_t)n_items * kTileSlots);
+            std::copy(entries.begin() + (size_t)t * kTilePx, entries.begin() + (size_t)(t + 1) * kTilePx,
+                      entries.begin() + (size_t)n_items * kTilePx);
+        }
+        sb += 8.0 * hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes loaded per 4-pixel group
+        n_items++;
+    }
     // wide tiles: 8-byte absolute entries in tile order
     std::vector<std::pair<int, std::vector<CompositeEntry>>> all;
     for (auto& v : wide_local)
         for (auto& p : v) all.push_back(std::move(p));
     std::sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
     std::vector<CompositeEntry> wide;
+    std::vector<uint32_t> wide_tiles;
     wide.reserve(all.size() * kTilePx);
     for (auto& p : all) {
-        hdr[p.first].wide_off = (uint32_t)wide.size();
+        wide_tiles.push_back((uint32_t)(p.first % tx_n) | ((uint32_t)(p.first / tx_n) << 16));
         wide.insert(wide.end(), p.second.begin(), p.second.end());
     }
-    m.tile_hdr.upload(hdr.data(), hdr.size());
-    m.tile_slots.upload(slots.data(), slots.size());
-    m.tile_entries.upload(entries.data(), entries.size());
-    if (wide.empty()) wide.push_back(CompositeEntry{0, 0});
+    m.tile_hdr.upload(hdr.data(), std::max(n_items, 1));
+    m.tile_slots.upload(slots.data(), (size_t)std::max(n_items, 1) * kTileSlots);
+    m.tile_entries.upload(entries.data(), (size_t)std::max(n_items, 1) * kTilePx);
+    if (wide.empty()) {
+        wide.push_back(CompositeEntry{0, 0});
+        wide_tiles.push_back(0u);
+    }
     m.tile_wide.upload(wide.data(), wide.size());
+    m.tile_wide_ids.upload(wide_tiles.data(), wide_tiles.size());
     m.n_wide_tiles = (int)all.size();
-    double sb = 0;
-    for (auto& h : hdr) sb += 8.0 * h.stage_groups;  // 4 Y + 2 U + 2 V bytes loaded per 4-pixel group
+    m.n_tiles = n_tiles;
     m.staged_bytes = sb;
-    m.tiled = TiledLut{m.tile_hdr.p, m.tile_slots.p, m.tile_entries.p, m.tile_wide.p, tx_n, ty_n};
+    m.tiled = TiledLut{m.tile_hdr.p, m.tile_slots.p, m.tile_entries.p, n_items,
+                       m.tile_wide_ids.p, m.tile_wide.p, m.n_wide_tiles};
 }
 
 }  // namespace
@@ -1038,6 +1063,8 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
     return guarded([&] {
         REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
         REQUIRE(out_pitch >= (size_t)m->W, "output pitch smaller than width");
+        // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
+        REQUIRE((uint64_t)out_pitch * (m->H + m->H / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
         hipStream_t s = (hipStream_t)stream;
         DeviceGuard dg(m->device);
         FrameSet fs;
@@ -1091,9 +1118,9 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
         REQUIRE(m && bytes, "NULL argument");
         // composite kernel: 4 B tiled-LUT entry (8 B in wide tiles) + 1.5 B YUV420 output per output
         // pixel, every source frame read once (1.5 B per input pixel), tile headers/slots
-        const double tiles = (double)m->tiled.tiles_x * m->tiled.tiles_y;
-        double b = 4.0 * tiles * kTilePx + 8.0 * m->n_wide_tiles * kTilePx + 1.5 * m->W * m->H +
-                   tiles * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot));
+        double b = 4.0 * m->tiled.n_items * kTilePx + 8.0 * m->n_wide_tiles * kTilePx + 1.5 * m->W * m->H +
+                   (double)m->tiled.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) +
+                   4.0 * m->n_wide_tiles;
         for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
         *bytes = b;
     });
@@ -1132,7 +1159,7 @@ int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
         snprintf(tmp, sizeof tmp,
                  "{\"inputs\": %d, \"out\": [%d, %d], \"tiles\": %d, \"wide_tiles\": %d, \"staged_bytes\": %.0f, "
                  "\"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, \"gain_chunks\": %d}",
-                 m->n, m->W, m->H, m->tiled.tiles_x * m->tiled.tiles_y, m->n_wide_tiles, m->staged_bytes, m->use_gain,
+                 m->n, m->W, m->H, m->n_tiles, m->n_wide_tiles, m->staged_bytes, m->use_gain,
                  m->n_samples, m->n_entries, m->n_chunks);
         REQUIRE(strlen(tmp) < len, "buffer too small");
         memcpy(buf, tmp, strlen(tmp) + 1);
