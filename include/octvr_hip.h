@@ -71,8 +71,13 @@ int octvr_stream_sync(void* stream);
 int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, int device, octvr_rig** rig);
 /* MapperTemplate(std::ifstream&) — VRv11 reader (template.cpp:258-314). */
 int octvr_rig_load_dat(const char* path, octvr_rig** rig);
-/* MapperTemplate::dump — VRv11 writer, byte-compatible (template.cpp:206-256).  Requires seam masks. */
-int octvr_rig_dump_dat(const octvr_rig* rig, const char* path);
+/* MapperTemplate::dump — VRv11 writer, byte-compatible (template.cpp:206-256).  Like the reference,
+ * creates the seam masks first when the rig has none (template.cpp:209-210). */
+int octvr_rig_dump_dat(octvr_rig* rig, const char* path);
+/* MapperTemplate::create_masks() without images (template.cpp:155-204): the L2 distance seam finder
+ * (DistanceSeamFinder, stitching/src/seam_finders.cpp:97-133) on masks resized to <= 960 px wide,
+ * seams resized back to each ROI.  Resizes run on `device`; replaces existing seam masks. */
+int octvr_rig_create_masks(octvr_rig* rig, int device);
 /* Build a rig from caller arrays (ROI-sized maps/masks, row-major, tightly packed). */
 int octvr_rig_create_from_arrays(int out_w, int out_h, int n_inputs, const int* rois, const float* const* map1,
                                  const float* const* map2, const uint8_t* const* masks,

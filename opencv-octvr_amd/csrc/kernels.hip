@@ -958,6 +958,49 @@ hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, i
 }
 
 // ---------------------------------------------------------------------------------------------
+// cv::resize INTER_LINEAR u8 (CPU fixed-point rule, tables from the host) — seam-mask build.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) resize_u8_kernel(const uint8_t* __restrict__ src, int sw, int sh, int64_t spitch,
+                                                        uint8_t* __restrict__ dst, int dw, int dh, int64_t dpitch,
+                                                        ResizeTables t) {
+    const int64_t total = (int64_t)dw * dh;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int y = (int)(idx / dw), x = (int)(idx - (int64_t)y * dw);
+        uint32_t v;
+        if (t.area2) {
+            const uint8_t* s0 = src + (int64_t)(2 * y) * spitch + 2 * x;
+            v = ((uint32_t)s0[0] + s0[1] + s0[spitch] + s0[spitch + 1] + 2u) >> 2;
+        } else {
+            const uint8_t* r0 = src + (int64_t)t.rows[2 * y] * spitch;
+            const uint8_t* r1 = src + (int64_t)t.rows[2 * y + 1] * spitch;
+            const int sx = t.xofs[x];
+            int h0, h1;
+            if (x < t.xmax) {
+                const int a0 = t.ax[2 * x], a1 = t.ax[2 * x + 1];
+                h0 = r0[sx] * a0 + r0[sx + 1] * a1;
+                h1 = r1[sx] * a0 + r1[sx + 1] * a1;
+            } else {
+                h0 = r0[sx] * 2048;
+                h1 = r1[sx] * 2048;
+            }
+            const int b0 = t.by[2 * y], b1 = t.by[2 * y + 1];
+            v = (uint32_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+        }
+        dst[(int64_t)y * dpitch + x] = (uint8_t)v;
+    }
+}
+
+hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, int64_t spitch, uint8_t* dst, int dw, int dh,
+                            int64_t dpitch, const ResizeTables& t, hipStream_t s) {
+    const int64_t total = (int64_t)dw * dh;
+    if (total <= 0) return hipSuccess;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(resize_u8_kernel, dim3(blocks), dim3(256), 0, s, src, sw, sh, spitch, dst, dw, dh, dpitch, t);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Self-test: device saturating conversions (rint + clamp vs v_cvt_pk_u8_f32).
 // ---------------------------------------------------------------------------------------------
 __global__ void selftest_sat_kernel(const float* in, uint8_t* out, int n, int method) {

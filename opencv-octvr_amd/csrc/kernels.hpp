@@ -147,6 +147,21 @@ hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, i
                            const float* map2, int mw, int mh, int64_t mpitch, float scale_x, float scale_y,
                            uint8_t* dst, int64_t dpitch, hipStream_t s);
 
+// cv::resize INTER_LINEAR, u8, one channel, with the CPU path's fixed-point rule
+// (imgwarp.cpp:1391-1500): per output column the source column and 11-bit weights, per output row
+// the two clipped source rows and weights — tables built on the host (seams.cpp), so the kernel
+// does integer arithmetic only.  area2: exact 1/2 downscale, (a + b + c + d + 2) >> 2 (:2349-2400).
+struct ResizeTables {
+    const int32_t* xofs;  // dw
+    const int16_t* ax;    // 2 * dw
+    const int32_t* rows;  // 2 * dh
+    const int16_t* by;    // 2 * dh
+    int32_t xmax;
+    int32_t area2;
+};
+hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, int64_t spitch, uint8_t* dst, int dw, int dh,
+                            int64_t dpitch, const ResizeTables& t, hipStream_t s);
+
 hipError_t launch_selftest_sat(const float* in, uint8_t* out, int n, int method, hipStream_t s);
 
 }  // namespace octvr

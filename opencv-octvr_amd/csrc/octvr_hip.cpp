@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "camera_math.hpp"
+#include "host_common.hpp"
 #include "json_lite.hpp"
 #include "kernels.hpp"
 
@@ -29,23 +30,6 @@ using namespace octvr;
 namespace {
 
 thread_local std::string g_last_error;
-
-struct OctvrError : std::runtime_error {
-    int code;
-    OctvrError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
-};
-
-#define HIP_CHECK(expr)                                                                                \
-    do {                                                                                               \
-        hipError_t e_ = (expr);                                                                        \
-        if (e_ != hipSuccess)                                                                          \
-            throw OctvrError(OCTVR_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
-    } while (0)
-
-#define REQUIRE(cond, msg)                                          \
-    do {                                                            \
-        if (!(cond)) throw OctvrError(OCTVR_E_INVALID, (msg));      \
-    } while (0)
 
 template <class F>
 int guarded(F&& f) {
@@ -64,63 +48,7 @@ int guarded(F&& f) {
     }
 }
 
-// Scoped device selection: restores the caller's current device.
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        HIP_CHECK(hipGetDevice(&prev));
-        if (dev != prev) HIP_CHECK(hipSetDevice(dev));
-    }
-    ~DeviceGuard() {
-        if (prev >= 0) (void)hipSetDevice(prev);
-    }
-};
-
-template <class T>
-struct DevBuf {
-    T* p = nullptr;
-    size_t n = 0;
-    DevBuf() = default;
-    DevBuf(const DevBuf&) = delete;
-    DevBuf& operator=(const DevBuf&) = delete;
-    ~DevBuf() { reset(); }
-    void alloc(size_t count) {
-        reset();
-        if (count == 0) return;
-        HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p), count * sizeof(T)));
-        n = count;
-    }
-    void upload(const T* h, size_t count) {
-        alloc(count);
-        if (count) HIP_CHECK(hipMemcpy(p, h, count * sizeof(T), hipMemcpyHostToDevice));
-    }
-    void reset() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        n = 0;
-    }
-};
-
 }  // namespace
-
-// =================================================================================================
-// Rig (vr::MapperTemplate)
-// =================================================================================================
-struct RigInput {
-    int roi[4] = {0, 0, 0, 0};
-    int in_w = 0, in_h = 0;  // input image size when known (JSON rigs)
-    std::vector<float> map1, map2;
-    std::vector<uint8_t> mask;
-    std::vector<float> vignette;
-    int vig_w = 0, vig_h = 0;
-};
-
-struct octvr_rig {
-    int out_w = 0, out_h = 0;
-    std::vector<RigInput> inputs;
-    std::vector<RigInput> overlays;
-    std::vector<std::vector<uint8_t>> seam_masks;
-};
 
 namespace {
 
@@ -859,6 +787,7 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
         auto rig = std::make_unique<octvr_rig>();
         rig->out_w = out_w;
         rig->out_h = out_h;
+        rig->device = device;
         const JsonValue& ins = doc["inputs"];
         rig->inputs.resize(ins.size());
         for (size_t i = 0; i < ins.size(); i++)
@@ -934,11 +863,19 @@ int octvr_rig_load_dat(const char* path, octvr_rig** out) {
     });
 }
 
-int octvr_rig_dump_dat(const octvr_rig* rig, const char* path) {
+int octvr_rig_create_masks(octvr_rig* rig, int device) {
+    return guarded([&] {
+        REQUIRE(rig, "rig is NULL");
+        rig->device = device;
+        rig_create_masks(*rig);
+    });
+}
+
+int octvr_rig_dump_dat(octvr_rig* rig, const char* path) {
     return guarded([&] {
         REQUIRE(rig && path, "rig/path is NULL");
-        REQUIRE(rig->seam_masks.size() == rig->inputs.size(),
-                "rig has no seam masks (create them before dumping; template.cpp:209-210)");
+        if (rig->seam_masks.empty()) rig_create_masks(*rig);  // MapperTemplate::dump (template.cpp:209-210)
+        REQUIRE(rig->seam_masks.size() == rig->inputs.size(), "seam mask count does not match the inputs");
         DatWriter w;
         w.f.open(path, std::ios::binary);
         if (!w.f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);

@@ -49,6 +49,7 @@ _VP = C.c_void_p
 _lib.octvr_rig_create_json.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]
 _lib.octvr_rig_load_dat.argtypes = [C.c_char_p, C.POINTER(_VP)]
 _lib.octvr_rig_dump_dat.argtypes = [_VP, C.c_char_p]
+_lib.octvr_rig_create_masks.argtypes = [_VP, C.c_int]
 _lib.octvr_rig_create_from_arrays.argtypes = [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(_VP),
                                               C.POINTER(_VP), C.POINTER(_VP), C.POINTER(_VP), C.POINTER(_VP)]
 _lib.octvr_rig_num_inputs.argtypes = [_VP, C.POINTER(C.c_int)]
@@ -123,7 +124,12 @@ class MapperTemplate:
         return cls(h.value)
 
     def dump(self, path):
+        """MapperTemplate::dump: VRv11 file (creates the seam masks first if there are none)."""
         _check(_lib.octvr_rig_dump_dat(self._h, os.fsencode(path)))
+
+    def create_masks(self, device=0):
+        """MapperTemplate::create_masks(): L2 distance seams (resizes on `device`)."""
+        _check(_lib.octvr_rig_create_masks(self._h, device))
 
     @property
     def out_size(self):

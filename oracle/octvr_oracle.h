@@ -111,6 +111,16 @@ void orc_resize_nearest_u8(const uint8_t* src, int sw, int sh, size_t spitch, in
 void orc_resize_linear_cuda_u8(const uint8_t* src, int sw, int sh, size_t spitch, uint8_t* dst, int dw, int dh,
                                size_t dpitch);
 
+/* ---- seam masks (octvr_oracle_seam.c) ------------------------------------------ */
+/* cv::resize INTER_LINEAR u8 on the CPU (imgwarp.cpp:3120-3480; fixed point, 11-bit coefficients). */
+void orc_resize_linear_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw, int dh,
+                          size_t dpitch);
+/* cv::distanceTransform(src, dst, DIST_L2, 3) -> f32 (distransform.cpp:48-139). */
+void orc_distance_transform_l2_3x3(const uint8_t* src, int w, int h, size_t spitch, float* dist, size_t dpitch_elems);
+/* MapperTemplate::create_masks() without images (template.cpp:155-204 -> DistanceSeamFinder,
+ * seam_finders.cpp:97-133).  masks / seams: ROI-sized u8 (tightly packed); seams are written. */
+int orc_create_masks(int n, const int* rois, const uint8_t* const* masks, int out_w, uint8_t* const* seams);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,8 +58,8 @@ def lib():
     global _LIB
     if _LIB is None:
         so = os.path.join(ORACLE_DIR, "liboctvr_oracle.so")
-        src = os.path.join(ORACLE_DIR, "octvr_oracle.c")
-        if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        srcs = [os.path.join(ORACLE_DIR, f) for f in os.listdir(ORACLE_DIR) if f.endswith((".c", ".h"))]
+        if not os.path.exists(so) or os.path.getmtime(so) < max(os.path.getmtime(f) for f in srcs):
             subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
         L = C.CDLL(so)
         L.orc_lut_build.restype = C.c_int
@@ -184,6 +184,37 @@ def yuv420_to_rgba(yuv, w, h):
     yuv = np.ascontiguousarray(yuv)
     lib().orc_yuv420_to_rgba(_p(yuv), w, h, C.c_size_t(yuv.shape[1]), _p(out), C.c_size_t(w * 4))
     return out
+
+
+def resize_linear(src, dw, dh):
+    """cv::resize INTER_LINEAR u8 on the CPU (oracle/octvr_oracle_seam.c)."""
+    src = np.ascontiguousarray(src)
+    sh, sw = src.shape[:2]
+    cn = 1 if src.ndim == 2 else src.shape[2]
+    out = np.zeros((dh, dw) + (() if cn == 1 else (cn,)), np.uint8)
+    lib().orc_resize_linear_u8(_p(src), sw, sh, C.c_size_t(sw * cn), cn, _p(out), dw, dh, C.c_size_t(dw * cn))
+    return out
+
+
+def distance_transform(src):
+    src = np.ascontiguousarray(src, dtype=np.uint8)
+    h, w = src.shape
+    out = np.zeros((h, w), np.float32)
+    lib().orc_distance_transform_l2_3x3(_p(src), w, h, C.c_size_t(w), _p(out), C.c_size_t(w))
+    return out
+
+
+def create_masks(rois, masks, out_w):
+    """MapperTemplate::create_masks() (DistanceSeamFinder): ROI-sized u8 seam masks."""
+    n = len(masks)
+    masks = [np.ascontiguousarray(m, dtype=np.uint8) for m in masks]
+    seams = [np.zeros_like(m) for m in masks]
+    r = np.ascontiguousarray(np.asarray(rois, dtype=np.int32).reshape(-1))
+    arr = C.c_void_p * n
+    rc = lib().orc_create_masks(n, _p(r), arr(*[m.ctypes.data for m in masks]), int(out_w),
+                                arr(*[s.ctypes.data for s in seams]))
+    assert rc == 0
+    return seams
 
 
 def rgb_to_yuv420(rgb):

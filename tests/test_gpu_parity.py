@@ -287,3 +287,41 @@ def test_gpu_saturating_conversion_kat(ox):
 def torch_tensor(a):
     import torch
     return torch.from_numpy(a)
+
+
+# ---- seam masks (MapperTemplate::create_masks) ----------------------------------
+@pytest.mark.parametrize("name", RIGS)
+def test_gpu_create_masks_vs_reference(ox, name, tmp_path):
+    import hashlib
+    rig, z = O.load_rig(name)
+    n = len(z["rois"])
+    W, H = (int(v) for v in z["out_size"])
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), [z[f"map1_{i}"] for i in range(n)],
+                                       [z[f"map2_{i}"] for i in range(n)], [z[f"mask_{i}"] for i in range(n)])
+    # dump without seams creates them (template.cpp:209-210): byte-identical to the reference's file
+    p = tmp_path / "rig.dat"
+    mt.dump(str(p))
+    man = json.load(open(os.path.join(O.ROOT, "tests", "golden", "manifest.json")))["rigs"][name]
+    assert hashlib.sha256(p.read_bytes()).hexdigest() == man["dat_sha256"]
+    for i in range(n):
+        assert np.array_equal(mt.input(i)[4], z[f"seam_{i}"]), i
+
+
+@pytest.mark.parametrize("out_w", [1920, 2048])
+def test_gpu_create_masks_scaled_vs_oracle(ox, out_w):
+    # out_w > 960: masks go through the 1/2 area path (1920) or the generic linear path (2048) both
+    # ways; oracle = CPU restatement pinned by the resize / distance KATs and the rig seams
+    rig, _ = O.load_rig("rigB")
+    for c in rig["inputs"]:
+        c["options"]["width"], c["options"]["height"] = 640, 360
+        c["options"]["crop"]["rect"] = [140, 500, 0, 360]
+    H = out_w // 2
+    res = O.lut_build(rig, out_w, H, use_roi=True)
+    rois = [list(r[0]) for r in res]
+    masks = [r[3] for r in res]
+    mt = ox.MapperTemplate.from_arrays(out_w, H, rois, [r[1] for r in res], [r[2] for r in res], masks)
+    mt.create_masks(0)
+    want = O.create_masks(rois, masks, out_w)
+    for i in range(len(res)):
+        got = mt.input(i)[4]
+        assert np.array_equal(got, want[i]), (i, int((got != want[i]).sum()))
