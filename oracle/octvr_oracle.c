@@ -842,7 +842,7 @@ int orc_stitch_frame(const orc_frame* f) {
         parallel_rows(T, 0, f->in_h[i], yuv_rows, &c);
         /* ROI rows the output band needs (all rows when the feed needs whole warped images) */
         int y0 = 0, y1 = r[3];
-        if (!estimate) {
+        if (!estimate && f->blend == 0) {
             y0 = rb - r[1]; y1 = re - r[1];
             if (y0 < 0) y0 = 0;
             if (y1 > r[3]) y1 = r[3];
@@ -866,12 +866,22 @@ int orc_stitch_frame(const orc_frame* f) {
         for (int i = 0; i < n; i++) gains[i] = 1.0;
     }
     if (f->gains_out) memcpy(f->gains_out, gains, sizeof(double) * n);
-    /* result = 0 (mapper.cpp:153-156), copies in camera order */
+    /* result = 0 (mapper.cpp:153-156); blend (mapper.cpp:266-278): a blender over the warped
+     * images, or the copy chain in camera order */
     uint8_t* result = (uint8_t*)calloc((size_t)f->out_w * f->out_h * 3, 1);
-    for (int i = 0; i < n; i++) {
-        const int* r = f->rois + 4 * i;
-        stage_ctx c = {f, i, NULL, warped[i], 1.f, result, rb, re};
-        parallel_rows(T, 0, r[3], copy_rows, &c);
+    const int blend = n > 1 ? f->blend : 0; /* mapper.cpp:78-82 */
+    int rc = 0;
+    if (blend > 0) {
+        rc = orc_multiband_blend(n, f->rois, f->seams, (const uint8_t* const*)warped, orc_blend_bands(blend), result,
+                                 f->out_w, f->out_h, (size_t)f->out_w * 3, T);
+    } else if (blend < 0) {
+        rc = -3; /* feather: not restated yet */
+    } else {
+        for (int i = 0; i < n; i++) {
+            const int* r = f->rois + 4 * i;
+            stage_ctx c = {f, i, NULL, warped[i], 1.f, result, rb, re};
+            parallel_rows(T, 0, r[3], copy_rows, &c);
+        }
     }
     {
         stage_ctx c = {f, 0, NULL, NULL, 1.f, result, rb, re};
@@ -879,5 +889,7 @@ int orc_stitch_frame(const orc_frame* f) {
     }
     for (int i = 0; i < n; i++) free(warped[i]);
     free(warped); free(gains); free(result);
-    return 0;
+    return rc;
 }
+
+int orc_blend_bands(int blend) { return (int)(ceil(log((double)blend) / log(2.)) - 1.); }

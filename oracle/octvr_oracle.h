@@ -102,8 +102,23 @@ typedef struct {
     double* gains_out;
     int threads;
     int row_begin, row_end;          /* restrict composite+output to a row band (cpu_baseline sample); 0,0 = all */
+    int blend;                       /* Mapper blend: 0 copy chain, > 0 multi-band (bands = ceil(log2 blend) - 1), < 0 feather */
+    const uint8_t* const* seams;     /* ROI-sized seam masks (multi-band weights); NULL unless blend > 0 */
 } orc_frame;
 int orc_stitch_frame(const orc_frame* f);
+
+/* ---- GPU blenders (octvr_oracle_blend.c) ----------------------------------- */
+void orc_fast_pyr_down_u8x4(const uint8_t* src, int sw, int sh, uint8_t* dst, int threads);           /* K2 */
+void orc_pyr_up_u8x4(const uint8_t* src, int sw, int sh, uint8_t* dst, int threads);                  /* K3 */
+void orc_pyr_up_s16x3(const int16_t* src, int sw, int sh, int16_t* dst, int threads);                 /* K3 */
+void orc_pyr_down_f32(const float* src, int sw, int sh, float* dst, int threads);                     /* K4 */
+/* MultiBandGPUBlender(seams, rois, bands).blend(warped u8x4 ROI images, result u8x3): writes the
+ * aligned result ROI of `result` (out_w x out_h, pitch bytes).  Returns 0, or < 0 on a failed
+ * reference assertion. */
+int orc_multiband_blend(int n, const int* rois, const uint8_t* const* seams, const uint8_t* const* warped, int bands,
+                        uint8_t* result, int out_w, int out_h, size_t result_pitch, int threads);
+/* Mapper's band count for blend > 0: int(ceil(log(blend) / log(2.)) - 1.) (mapper.cpp:172). */
+int orc_blend_bands(int blend);
 
 /* K13/K14 CUDA resize semantics used by the gain path (cudawarping/src/cuda/resize.cu:57-103). */
 void orc_resize_nearest_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw, int dh,

@@ -51,6 +51,8 @@ class OrcFrame(C.Structure):
         ("gains_out", C.POINTER(C.c_double)),
         ("threads", C.c_int),
         ("row_begin", C.c_int), ("row_end", C.c_int),
+        ("blend", C.c_int),
+        ("seams", C.POINTER(C.c_void_p)),
     ]
 
 
@@ -186,6 +188,37 @@ def yuv420_to_rgba(yuv, w, h):
     return out
 
 
+def _pyr(fn, src, dshape, dtype, threads=1):
+    src = np.ascontiguousarray(src)
+    out = np.zeros(dshape, dtype)
+    getattr(lib(), fn)(_p(src), src.shape[1], src.shape[0], _p(out), threads)
+    return out
+
+
+def fast_pyr_down_u8x4(src, threads=1):
+    h, w = src.shape[:2]
+    return _pyr("orc_fast_pyr_down_u8x4", src, ((h + 1) // 2, (w + 1) // 2, 4), np.uint8, threads)
+
+
+def pyr_up_u8x4(src, threads=1):
+    h, w = src.shape[:2]
+    return _pyr("orc_pyr_up_u8x4", src, (2 * h, 2 * w, 4), np.uint8, threads)
+
+
+def pyr_up_s16x3(src, threads=1):
+    h, w = src.shape[:2]
+    return _pyr("orc_pyr_up_s16x3", src.astype(np.int16), (2 * h, 2 * w, 3), np.int16, threads)
+
+
+def pyr_down_f32(src, threads=1):
+    h, w = src.shape[:2]
+    return _pyr("orc_pyr_down_f32", src.astype(np.float32), ((h + 1) // 2, (w + 1) // 2), np.float32, threads)
+
+
+def blend_bands(blend):
+    return lib().orc_blend_bands(int(blend))
+
+
 def resize_linear(src, dw, dh):
     """cv::resize INTER_LINEAR u8 on the CPU (oracle/octvr_oracle_seam.c)."""
     src = np.ascontiguousarray(src)
@@ -239,7 +272,7 @@ def gain_feed(rois, warped, masks, out_w, out_h):
 
 
 def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enable_gain=True, gains=None,
-                 threads=1, row_band=None):
+                 threads=1, row_band=None, blend=0, seams=None):
     n = len(in_yuv)
     keep = []
 
@@ -276,6 +309,11 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
     f.threads = threads
     if row_band:
         f.row_begin, f.row_end = row_band
+    f.blend = blend
+    if seams is not None:
+        seams = [np.ascontiguousarray(a, np.uint8) for a in seams]
+        keep.append(seams)
+        f.seams = arr(C.c_void_p, [a.ctypes.data for a in seams])
     rc = lib().orc_stitch_frame(C.byref(f))
     assert rc == 0
     return out, gout
