@@ -1,0 +1,166 @@
+// device_common.hpp — device-side pixel arithmetic and I/O helpers shared by the gfx950 kernels
+// (kernels.hip: remap / gain / composite; multiband.hip: pyramid blend).  Internal header.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+
+namespace octvr {
+
+// ---------------------------------------------------------------------------------------------
+// Pixel arithmetic shared by the kernels
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int sat_u8_rne(float v) {
+    // saturate_cast<uchar>(float): round half to even, clamp (NaN -> 0)
+    if (!(v > 0.f)) return 0;
+    if (v >= 255.f) return 255;
+    return (int)__builtin_rintf(v);
+}
+
+// The same conversion in one instruction, written into byte `sel` of `old`: v_cvt_pk_u8_f32 rounds
+// half to even and saturates (NaN -> 0); tests/test_gpu_parity.py::test_gpu_saturating_conversion_kat.
+__device__ __forceinline__ uint32_t pack_u8(float v, uint32_t sel, uint32_t old) {
+    return __builtin_amdgcn_cvt_pk_u8_f32(v, sel, old);
+}
+
+// The library's own BT.601 YUV -> RGB (stands in for NPP nppiYUV420ToRGB_8u_P3AC4R,
+// cudaimgproc/src/color.cpp:2269, whose arithmetic is closed: pinned by the oracle only).  Same
+// operation sequence as oracle/octvr_oracle.c yuv_px_to_rgb.  Returns packed R | G << 8 | B << 16.
+__device__ __forceinline__ uint32_t yuv_to_rgba(uint32_t y, uint32_t u, uint32_t v) {
+    const float Yf = (float)y, Uf = (float)u - 128.f, Vf = (float)v - 128.f;
+    uint32_t p = pack_u8(__builtin_fmaf(1.140f, Vf, Yf), 0, 0u);
+    p = pack_u8(__builtin_fmaf(-0.581f, Vf, __builtin_fmaf(-0.394f, Uf, Yf)), 1, p);
+    return pack_u8(__builtin_fmaf(2.032f, Uf, Yf), 2, p);
+}
+
+// 15-bit bilinear weights.  initInterTab2D's table (imgwarp.cpp:211-280) holds
+// w = {(32-fx)(32-fy), fx(32-fy), (32-fx)fy, fx fy} * 32 exactly (every product is exact in f32),
+// except code 0 whose 32768 saturates to 32767 and the fix-up adds the missing unit to the
+// bottom-right tap: {32767, 0, 0, 1}.  For u8 taps that cell rounds to c00 exactly like
+// {32768, 0, 0, 0} would ((32767 c00 + c11 + 2^14) >> 15 == c00 for c00, c11 <= 255), so the
+// separable form below is bit-identical to the table — pinned by the all-codes remap KAT.
+// Out-of-image taps are passed as 0 (BORDER_CONSTANT).  Returns (sum + 2^14) >> 15 per channel.
+__device__ __forceinline__ uint32_t bilerp_ch(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t fx,
+                                              uint32_t fy) {
+    const uint32_t h0 = (32u - fx) * a + fx * b;  // <= 8160
+    const uint32_t h1 = (32u - fx) * c + fx * d;
+    return ((32u - fy) * h0 + fy * h1 + 512u) >> 10;
+}
+
+__device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint32_t fx,
+                                            uint32_t fy, uint32_t (&rgb)[3]) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const uint32_t sh = 8u * ch;
+        rgb[ch] = bilerp_ch((c00 >> sh) & 255u, (c01 >> sh) & 255u, (c10 >> sh) & 255u, (c11 >> sh) & 255u, fx, fy);
+    }
+}
+
+// Direct (global-memory) bilinear sample of one camera at an 8-byte composite entry — the gain feed
+// samples and "wide" tiles.  Every load is issued unconditionally from a clamped in-image address;
+// taps outside the image and invalid entries are zeroed afterwards.
+// global-address-space views (loads through pointers held in LDS / structs would otherwise be flat)
+typedef __attribute__((address_space(1))) uint8_t gu8;
+typedef __attribute__((address_space(1))) uint16_t gu16;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// wave-uniform value -> SGPR (scalar loads / branches downstream)
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+struct Taps {
+    uint32_t c[4];  // packed RGBA of the 4 taps (0 when outside / invalid)
+    uint32_t fx, fy;
+};
+
+__device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t xy, uint32_t code, Taps& t) {
+    const bool valid = (code & 0x8000u) != 0;
+    const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
+    const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
+    const bool in0 = valid && sx < f.w && sy < f.h;
+    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);
+    const int x1 = inx ? sx + 1 : x0, y1 = iny ? sy + 1 : y0;
+    const int64_t p = f.pitch;
+    const uint8_t* Y = f.yuv;
+    const uint8_t* U = Y + (int64_t)f.h * p;
+    const uint8_t* V = U + (f.w >> 1);
+    const int64_t r0 = (int64_t)y0 * p, r1 = (int64_t)y1 * p;
+    const int64_t q0 = (int64_t)(y0 >> 1) * p, q1 = (int64_t)(y1 >> 1) * p;
+    const uint32_t ya = Y[r0 + x0], yb = Y[r0 + x1], yc = Y[r1 + x0], yd = Y[r1 + x1];
+    const uint32_t ua = U[q0 + (x0 >> 1)], ub = U[q0 + (x1 >> 1)], uc = U[q1 + (x0 >> 1)], ud = U[q1 + (x1 >> 1)];
+    const uint32_t va = V[q0 + (x0 >> 1)], vb = V[q0 + (x1 >> 1)], vc = V[q1 + (x0 >> 1)], vd = V[q1 + (x1 >> 1)];
+    t.c[0] = in0 ? yuv_to_rgba(ya, ua, va) : 0u;
+    t.c[1] = (valid && inx && sy < f.h) ? yuv_to_rgba(yb, ub, vb) : 0u;
+    t.c[2] = (valid && iny && sx < f.w) ? yuv_to_rgba(yc, uc, vc) : 0u;
+    t.c[3] = (valid && inx && iny) ? yuv_to_rgba(yd, ud, vd) : 0u;
+    t.fx = code & 31u;
+    t.fy = (code >> 5) & 31u;
+}
+
+__device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, Taps& t) {
+    gather_taps_frame(fs.f[(code >> 10) & 31u], xy, code, t);
+}
+
+
+struct QuadOut {
+    uint32_t y01, y23;  // two Y bytes of each row
+    uint32_t u, v;
+};
+
+__device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
+    uint32_t y01 = 0, y23 = 0;
+    float us = 0.f, vs = 0.f;
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        // gain: saturate_cast<uchar>(px * g), kept as an exact float of the saturated integer
+        const float R = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][0] * gain[p]), 0.f, 255.f);
+        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain[p]), 0.f, 255.f);
+        const float B = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][2] * gain[p]), 0.f, 255.f);
+        const float Yf = __builtin_fmaf(0.114f, B, __builtin_fmaf(0.587f, G, 0.299f * R));
+        if (p < 2) y01 = pack_u8(Yf, p, y01);
+        else y23 = pack_u8(Yf, p - 2, y23);
+        us = __builtin_fmaf(0.492f, B - Yf, us);
+        vs = __builtin_fmaf(0.877f, R - Yf, vs);
+    }
+    QuadOut q;
+    q.y01 = y01;
+    q.y23 = y23;
+    q.u = pack_u8(__builtin_fmaf(us, 0.25f, 128.f), 0, 0u);
+    q.v = pack_u8(__builtin_fmaf(vs, 0.25f, 128.f), 0, 0u);
+    return q;
+}
+
+// The output frame as a buffer resource: stores of a quad outside W x H get an offset past the
+// range and are dropped by the hardware, so every lane issues the same stores (no branch) and the
+// per-iteration count of outstanding vector-memory operations is fixed.
+struct OutFrame {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t pitch;
+    uint32_t u_off, v_off;  // byte offsets of the U and V planes
+};
+constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host: frame < 2^31 - 64 B)
+
+__device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
+    const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
+    const uint32_t oc = in ? (uint32_t)(y >> 1) * o.pitch + (uint32_t)(x >> 1) : kDropOffset;
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, 0);
+}
+
+
+__device__ __forceinline__ OutFrame make_out_frame(uint8_t* out, int W, int H, int64_t out_pitch) {
+    OutFrame of;
+    of.pitch = (uint32_t)out_pitch;
+    of.u_off = (uint32_t)H * (uint32_t)out_pitch;
+    of.v_off = of.u_off + (uint32_t)(W >> 1);
+    of.rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)((uint32_t)out_pitch * (uint32_t)(H + H / 2)), 0x00020000);
+    return of;
+}
+
+
+}  // namespace octvr

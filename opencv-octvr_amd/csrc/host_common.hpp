@@ -6,10 +6,13 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "kernels.hpp"
 #include "octvr_hip.h"
 
 namespace octvr {
@@ -94,4 +97,51 @@ struct octvr_rig {
 namespace octvr {
 // MapperTemplate::create_masks() (template.cpp:155-204) — seams.cpp
 void rig_create_masks(octvr_rig& rig);
+
+// ---- tiled composite LUT builder (tiling.cpp) ----------------------------------------------------
+struct TileJob {
+    int tx, ty;  // 128x8 tile of the output (or level-0) grid
+    int cam;     // RGBA mode: the camera whose pyramid image the tile is written to
+};
+// entry(job, x, y): the 8-byte CompositeEntry of grid pixel (x, y) for that job ({0,0} = black)
+using EntryFn = std::function<CompositeEntry(int job, int x, int y)>;
+struct TiledLutBuild {
+    std::vector<TileHdr> hdr;
+    std::vector<TileSlot> slots;
+    std::vector<uint32_t> entries;
+    std::vector<CompositeEntry> wide;
+    std::vector<uint32_t> wide_tiles;
+    std::vector<uint8_t> wide_cams;
+    int n_items = 0, n_wide = 0;
+    double staged_bytes = 0;
+};
+TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
+                              const std::vector<int>& in_h);
+struct TiledLutDev {
+    DevBuf<TileHdr> hdr;
+    DevBuf<TileSlot> slots;
+    DevBuf<uint32_t> entries;
+    DevBuf<CompositeEntry> wide;
+    DevBuf<uint32_t> wide_tiles;
+    DevBuf<uint8_t> wide_cams;
+    double staged_bytes = 0;
+    TiledLut view{};
+    void upload(const TiledLutBuild& b);
+};
+
+// ---- multi-band blend (multiband_host.cpp) ---------------------------------------------------------
+class MultiBand;
+struct MultiBandDeleter {
+    void operator()(MultiBand* p) const;
+};
+// MultiBandGPUBlender(seam_masks, rois, bands) for a mapper: everything per rig (weights, tile lists,
+// pyramid buffers) on `device`.  in_w / in_h: input frame sizes.
+MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
+                            const std::vector<int>& in_h);
+// One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P.
+void multiband_run(MultiBand& mb, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
+                   int64_t out_pitch, hipStream_t s);
+// Algorithmic bytes of one frame and a JSON fragment of build statistics.
+double multiband_traffic(const MultiBand& mb);
+std::string multiband_info(const MultiBand& mb);
 }  // namespace octvr

@@ -10,107 +10,13 @@
 #include <cstdint>
 #include <cstring>
 
+#include "device_common.hpp"
 #include "kernels.hpp"
 #ifndef OCTVR_FEED_VARIANT
 #define OCTVR_FEED_VARIANT 0
 #endif
 
 namespace octvr {
-
-// ---------------------------------------------------------------------------------------------
-// Pixel arithmetic shared by the kernels
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int sat_u8_rne(float v) {
-    // saturate_cast<uchar>(float): round half to even, clamp (NaN -> 0)
-    if (!(v > 0.f)) return 0;
-    if (v >= 255.f) return 255;
-    return (int)__builtin_rintf(v);
-}
-
-// The same conversion in one instruction, written into byte `sel` of `old`: v_cvt_pk_u8_f32 rounds
-// half to even and saturates (NaN -> 0); tests/test_gpu_parity.py::test_gpu_saturating_conversion_kat.
-__device__ __forceinline__ uint32_t pack_u8(float v, uint32_t sel, uint32_t old) {
-    return __builtin_amdgcn_cvt_pk_u8_f32(v, sel, old);
-}
-
-// The library's own BT.601 YUV -> RGB (stands in for NPP nppiYUV420ToRGB_8u_P3AC4R,
-// cudaimgproc/src/color.cpp:2269, whose arithmetic is closed: pinned by the oracle only).  Same
-// operation sequence as oracle/octvr_oracle.c yuv_px_to_rgb.  Returns packed R | G << 8 | B << 16.
-__device__ __forceinline__ uint32_t yuv_to_rgba(uint32_t y, uint32_t u, uint32_t v) {
-    const float Yf = (float)y, Uf = (float)u - 128.f, Vf = (float)v - 128.f;
-    uint32_t p = pack_u8(__builtin_fmaf(1.140f, Vf, Yf), 0, 0u);
-    p = pack_u8(__builtin_fmaf(-0.581f, Vf, __builtin_fmaf(-0.394f, Uf, Yf)), 1, p);
-    return pack_u8(__builtin_fmaf(2.032f, Uf, Yf), 2, p);
-}
-
-// 15-bit bilinear weights.  initInterTab2D's table (imgwarp.cpp:211-280) holds
-// w = {(32-fx)(32-fy), fx(32-fy), (32-fx)fy, fx fy} * 32 exactly (every product is exact in f32),
-// except code 0 whose 32768 saturates to 32767 and the fix-up adds the missing unit to the
-// bottom-right tap: {32767, 0, 0, 1}.  For u8 taps that cell rounds to c00 exactly like
-// {32768, 0, 0, 0} would ((32767 c00 + c11 + 2^14) >> 15 == c00 for c00, c11 <= 255), so the
-// separable form below is bit-identical to the table — pinned by the all-codes remap KAT.
-// Out-of-image taps are passed as 0 (BORDER_CONSTANT).  Returns (sum + 2^14) >> 15 per channel.
-__device__ __forceinline__ uint32_t bilerp_ch(uint32_t a, uint32_t b, uint32_t c, uint32_t d, uint32_t fx,
-                                              uint32_t fy) {
-    const uint32_t h0 = (32u - fx) * a + fx * b;  // <= 8160
-    const uint32_t h1 = (32u - fx) * c + fx * d;
-    return ((32u - fy) * h0 + fy * h1 + 512u) >> 10;
-}
-
-__device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint32_t fx,
-                                            uint32_t fy, uint32_t (&rgb)[3]) {
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) {
-        const uint32_t sh = 8u * ch;
-        rgb[ch] = bilerp_ch((c00 >> sh) & 255u, (c01 >> sh) & 255u, (c10 >> sh) & 255u, (c11 >> sh) & 255u, fx, fy);
-    }
-}
-
-// Direct (global-memory) bilinear sample of one camera at an 8-byte composite entry — the gain feed
-// samples and "wide" tiles.  Every load is issued unconditionally from a clamped in-image address;
-// taps outside the image and invalid entries are zeroed afterwards.
-// global-address-space views (loads through pointers held in LDS / structs would otherwise be flat)
-typedef __attribute__((address_space(1))) uint8_t gu8;
-typedef __attribute__((address_space(1))) uint16_t gu16;
-typedef __attribute__((address_space(1))) uint32_t gu32;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-
-// wave-uniform value -> SGPR (scalar loads / branches downstream)
-__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
-
-struct Taps {
-    uint32_t c[4];  // packed RGBA of the 4 taps (0 when outside / invalid)
-    uint32_t fx, fy;
-};
-
-__device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t xy, uint32_t code, Taps& t) {
-    const bool valid = (code & 0x8000u) != 0;
-    const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
-    const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
-    const bool in0 = valid && sx < f.w && sy < f.h;
-    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);
-    const int x1 = inx ? sx + 1 : x0, y1 = iny ? sy + 1 : y0;
-    const int64_t p = f.pitch;
-    const uint8_t* Y = f.yuv;
-    const uint8_t* U = Y + (int64_t)f.h * p;
-    const uint8_t* V = U + (f.w >> 1);
-    const int64_t r0 = (int64_t)y0 * p, r1 = (int64_t)y1 * p;
-    const int64_t q0 = (int64_t)(y0 >> 1) * p, q1 = (int64_t)(y1 >> 1) * p;
-    const uint32_t ya = Y[r0 + x0], yb = Y[r0 + x1], yc = Y[r1 + x0], yd = Y[r1 + x1];
-    const uint32_t ua = U[q0 + (x0 >> 1)], ub = U[q0 + (x1 >> 1)], uc = U[q1 + (x0 >> 1)], ud = U[q1 + (x1 >> 1)];
-    const uint32_t va = V[q0 + (x0 >> 1)], vb = V[q0 + (x1 >> 1)], vc = V[q1 + (x0 >> 1)], vd = V[q1 + (x1 >> 1)];
-    t.c[0] = in0 ? yuv_to_rgba(ya, ua, va) : 0u;
-    t.c[1] = (valid && inx && sy < f.h) ? yuv_to_rgba(yb, ub, vb) : 0u;
-    t.c[2] = (valid && iny && sx < f.w) ? yuv_to_rgba(yc, uc, vc) : 0u;
-    t.c[3] = (valid && inx && iny) ? yuv_to_rgba(yd, ud, vd) : 0u;
-    t.fx = code & 31u;
-    t.fy = (code >> 5) & 31u;
-}
-
-__device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, Taps& t) {
-    gather_taps_frame(fs.f[(code >> 10) & 31u], xy, code, t);
-}
-
 
 // ---------------------------------------------------------------------------------------------
 // LUT build: MapperTemplate::add_input (template.cpp:46-133), one thread per output pixel, FP64.
@@ -530,54 +436,6 @@ hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, 
 // walked grid-stride; blocks b, b+8, ... (one XCD under round-robin dispatch) take a contiguous
 // band of tiles so their source boxes share that XCD's L2.
 // ---------------------------------------------------------------------------------------------
-struct QuadOut {
-    uint32_t y01, y23;  // two Y bytes of each row
-    uint32_t u, v;
-};
-
-__device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
-    uint32_t y01 = 0, y23 = 0;
-    float us = 0.f, vs = 0.f;
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-        // gain: saturate_cast<uchar>(px * g), kept as an exact float of the saturated integer
-        const float R = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][0] * gain[p]), 0.f, 255.f);
-        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain[p]), 0.f, 255.f);
-        const float B = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][2] * gain[p]), 0.f, 255.f);
-        const float Yf = __builtin_fmaf(0.114f, B, __builtin_fmaf(0.587f, G, 0.299f * R));
-        if (p < 2) y01 = pack_u8(Yf, p, y01);
-        else y23 = pack_u8(Yf, p - 2, y23);
-        us = __builtin_fmaf(0.492f, B - Yf, us);
-        vs = __builtin_fmaf(0.877f, R - Yf, vs);
-    }
-    QuadOut q;
-    q.y01 = y01;
-    q.y23 = y23;
-    q.u = pack_u8(__builtin_fmaf(us, 0.25f, 128.f), 0, 0u);
-    q.v = pack_u8(__builtin_fmaf(vs, 0.25f, 128.f), 0, 0u);
-    return q;
-}
-
-// The output frame as a buffer resource: stores of a quad outside W x H get an offset past the
-// range and are dropped by the hardware, so every lane issues the same stores (no branch) and the
-// per-iteration count of outstanding vector-memory operations is fixed.
-struct OutFrame {
-    __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t pitch;
-    uint32_t u_off, v_off;  // byte offsets of the U and V planes
-};
-constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host: frame < 2^31 - 64 B)
-
-__device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
-    const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
-    const uint32_t oc = in ? (uint32_t)(y >> 1) * o.pitch + (uint32_t)(x >> 1) : kDropOffset;
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, 0);
-}
-
-
 // The tile's slot descriptors as 16 raw dwords in scalar registers (the tile index is wave-uniform).
 // Slot q: dword 4q = cam | bw << 16, 4q+1 = bh | lds << 16, 4q+2 = bx0 | by0 << 16, 4q+3 = chunk0.
 // Only static indices and explicit selects touch it, so it never lands in scratch memory.
@@ -737,27 +595,63 @@ __device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLu
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
     d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? m.t : 0) * kTilePx)[tid];
-    const uint32_t nchunks = live ? (m.hd.nslots >> 8) : 0u;
+    const uint32_t nchunks = live ? ((m.hd.nslots >> 8) & 0xFFu) : 0u;
 #pragma unroll
     for (int r = 0; r < kStageRegs; r++)
         stage_load<DWORD_STAGE>(m.ss, (int)(m.hd.nslots & 0xFFu), nchunks, m.hd.stride, r * 4 + wave, d.sg[r]);
 }
 
-__device__ __forceinline__ OutFrame make_out_frame(uint8_t* out, int W, int H, int64_t out_pitch) {
-    OutFrame of;
-    of.pitch = (uint32_t)out_pitch;
-    of.u_off = (uint32_t)H * (uint32_t)out_pitch;
-    of.v_off = of.u_off + (uint32_t)(W >> 1);
-    of.rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)((uint32_t)out_pitch * (uint32_t)(H + H / 2)), 0x00020000);
-    return of;
+// The composite's two sinks.  MODE 0: gain + RGB -> YUV420P into the output frame (blend = 0).
+// MODE 1: gain-applied RGBA into the camera's level-0 pyramid image (blend > 0; the warped image
+// Mapper::stitch hands to the blender, mapper.cpp:233-262); pixels outside the camera's aligned ROI
+// are dropped.  Either way a quad's result is 4 dwords.
+template <int MODE>
+__device__ __forceinline__ QuadOut finish_any(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
+    if constexpr (MODE == 0) {
+        return finish_quad(rgb, gain);
+    } else {
+        uint32_t px[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            uint32_t v = pack_u8((float)rgb[p][0] * gain[p], 0, 0u);
+            v = pack_u8((float)rgb[p][1] * gain[p], 1, v);
+            px[p] = pack_u8((float)rgb[p][2] * gain[p], 2, v);
+        }
+        return QuadOut{px[0], px[1], px[2], px[3]};
+    }
+}
+
+struct RgbaSink {
+    __amdgpu_buffer_rsrc_t rsrc;
+    const MbCamLevel* cams;
+};
+
+__device__ __forceinline__ void store_rgba(const RgbaSink& o, const QuadOut& q, uint32_t cam, int x, int y, bool in) {
+    const MbCamLevel* c = o.cams + cam;
+    const int xl = x - c->ox, yl = y - c->oy;
+    const bool ok = in && xl >= 0 && yl >= 0 && xl < c->w && yl < c->h;  // w, h even: whole quads
+    const uint32_t off = ok ? c->g_off + (uint32_t)yl * c->g_pitch + (uint32_t)xl * 4u : kDropOffset;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 r0 = {q.y01, q.y23}, r1 = {q.u, q.v};
+    __builtin_amdgcn_raw_buffer_store_b64(r0, o.rsrc, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(r1, o.rsrc, ok ? off + c->g_pitch : kDropOffset, 0, 0);
+}
+
+template <int MODE>
+__device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro, const QuadOut& q, uint32_t cam,
+                                          int x, int y, bool in) {
+    if constexpr (MODE == 0)
+        store_quad(of, q, x, y, in);
+    else
+        store_rgba(ro, q, cam, x, y, in);
 }
 
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
-template <bool DWORD_STAGE>
+template <bool DWORD_STAGE, int MODE>
 __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
-                                                              int64_t out_pitch) {
+                                                              int64_t out_pitch, RgbaOut rgba) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
     __shared__ float s_gain[kMaxCams];
     __shared__ float s_slot_gain[kTileSlots];
@@ -767,7 +661,12 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
     const int step = (gridDim.x - g + groups - 1) / groups;
     const int t_begin = (int)((int64_t)lut.n_items * g / groups);
     const int t_end = (int)((int64_t)lut.n_items * (g + 1) / groups);
-    const OutFrame of = make_out_frame(out, W, H, out_pitch);
+    OutFrame of{};
+    RgbaSink ro{};
+    if constexpr (MODE == 0)
+        of = make_out_frame(out, W, H, out_pitch);
+    else
+        ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
 
@@ -792,6 +691,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
     // a store must drain everything, as loads and stores complete out of order)
     QuadOut prev{0u, 0u, 0u, 0u};
     int px = 0, py = 0;
+    uint32_t pcam = 0;
     bool pin = false;
     while (cur.t < t_end) {
         const int x = (int)(cur.hd.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.hd.tile >> 16) * kTileH + qy * 2;
@@ -805,16 +705,17 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
         }
 #pragma unroll
         for (int r = 0; r < kStageRegs; r++) stage_store(d.sg[r], s_rgb);
-        if ((cur.hd.nslots >> 8) > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
+        const uint32_t nch = (cur.hd.nslots >> 8) & 0xFFu;
+        if (nch > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
             const int wave = uniform(tid >> 6);
-            for (int c = kStageRegs * 4 + wave; c < (int)(cur.hd.nslots >> 8); c += 4) {
+            for (int c = kStageRegs * 4 + wave; c < (int)nch; c += 4) {
                 StageGroup sg;
-                stage_load<DWORD_STAGE>(cur.ss, (int)(cur.hd.nslots & 0xFFu), cur.hd.nslots >> 8, S, c, sg);
+                stage_load<DWORD_STAGE>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sg);
                 stage_store(sg, s_rgb);
             }
         }
         __syncthreads();
-        store_quad(of, prev, px, py, pin);
+        store_any<MODE>(of, ro, prev, pcam, px, py, pin);
         data_issue<DWORD_STAGE>(frames, lut, nxt, t_end, d);
         mv = meta_issue(lut, cur.t + 2 * step, t_end);
         const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
@@ -830,25 +731,33 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
             const uint32_t c11 = s_rgb[(m & 8u) ? off + S + 1u : 0u];
             bilerp_rgba(c00, c01, c10, c11, (e >> 13) & 31u, (e >> 18) & 31u, rgb[p]);
             gain[p] = s_slot_gain[(e >> 23) & 3u];
+            if (MODE == 1 && (e & kEntryNoGain)) gain[p] = 1.0f;
         }
-        prev = finish_quad(rgb, gain);
+        prev = finish_any<MODE>(rgb, gain);
         px = x;
         py = y;
+        pcam = (cur.hd.nslots >> 16) & 31u;
         pin = x < W && y < H;
         cur = nxt;
     }
-    store_quad(of, prev, px, py, pin);
+    store_any<MODE>(of, ro, prev, pcam, px, py, pin);
 }
 
 // Wide tiles: one workgroup per tile, 8-byte absolute entries, direct global gathers.
+template <int MODE>
 __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                           const double* gains, int use_gain, uint8_t* out,
-                                                          int64_t out_pitch) {
+                                                          int64_t out_pitch, RgbaOut rgba) {
     __shared__ float s_gain[kMaxCams];
     const int tid = threadIdx.x;
     if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
     __syncthreads();
-    const OutFrame of = make_out_frame(out, W, H, out_pitch);
+    OutFrame of{};
+    RgbaSink ro{};
+    if constexpr (MODE == 0)
+        of = make_out_frame(out, W, H, out_pitch);
+    else
+        ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
     const uint32_t tile = (uint32_t)uniform((int)lut.wide_tiles[blockIdx.x]);
     const int x = (int)(tile & 0xFFFFu) * kTileW + (tid & 63) * 2, y = (int)(tile >> 16) * kTileH + (tid >> 6) * 2;
     const uint4* wp = reinterpret_cast<const uint4*>(lut.wide + (int64_t)blockIdx.x * kTilePx) + tid * 2;
@@ -863,13 +772,15 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
-        gain[p] = s_gain[(cd[p] >> 10) & 31u];
+        gain[p] = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
     }
-    store_quad(of, finish_quad(rgb, gain), x, y, x < W && y < H);
+    const uint32_t cam = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;
+    store_any<MODE>(of, ro, finish_any<MODE>(rgb, gain), cam, x, y, x < W && y < H);
 }
 
-hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
-                         int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
+template <int MODE>
+static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
+                                   int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s) {
     if (lut.n_items > 0) {
         // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU: 25 KiB LDS each), each
         // walking its XCD band's items
@@ -883,18 +794,29 @@ hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int
             if ((reinterpret_cast<uintptr_t>(f.yuv) & 7u) || (f.pitch & 7) || (f.w & 7)) dw = false;
         }
         if (dw)
-            hipLaunchKernelGGL(stitch_tiled_kernel<true>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
-                               use_gain, out, out_pitch);
+            hipLaunchKernelGGL((stitch_tiled_kernel<true, MODE>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H,
+                               gains, use_gain, out, out_pitch, rgba);
         else
-            hipLaunchKernelGGL(stitch_tiled_kernel<false>, dim3(blocks), dim3(256), 0, s, frames, lut, W, H, gains,
-                               use_gain, out, out_pitch);
+            hipLaunchKernelGGL((stitch_tiled_kernel<false, MODE>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H,
+                               gains, use_gain, out, out_pitch, rgba);
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
     if (lut.n_wide > 0)
-        hipLaunchKernelGGL(stitch_wide_kernel, dim3(lut.n_wide), dim3(256), 0, s, frames, lut, W, H, gains, use_gain,
-                           out, out_pitch);
+        hipLaunchKernelGGL(stitch_wide_kernel<MODE>, dim3(lut.n_wide), dim3(256), 0, s, frames, lut, W, H, gains,
+                           use_gain, out, out_pitch, rgba);
     return hipGetLastError();
+}
+
+hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
+                         int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
+    return launch_composite<0>(frames, lut, W, H, gains, use_gain, out, out_pitch, RgbaOut{}, s);
+}
+
+hipError_t launch_mb_remap(const FrameSet& frames, const TiledLut& lut, const double* gains, int use_gain,
+                           const RgbaOut& out, hipStream_t s) {
+    // W, H: no level-grid bound of its own (the per-camera ROI check drops what lies outside)
+    return launch_composite<1>(frames, lut, 1 << 16, 1 << 16, gains, use_gain, nullptr, 0, out, s);
 }
 
 // ---------------------------------------------------------------------------------------------

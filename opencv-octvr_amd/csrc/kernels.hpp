@@ -138,10 +138,77 @@ struct TiledLut {
     const uint32_t* wide_tiles;   // tile column | row << 16 of each wide tile
     const CompositeEntry* wide;   // kTilePx per wide tile
     int n_wide;
+    const uint8_t* wide_cams;     // RGBA mode: output camera of each wide tile
 };
+// 4-byte tiled entries: bit 29 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
+// in-image map value; mul_scalar_with_mask, exposure_compensate.cu:15-30).  8-byte CompositeEntry
+// records carry the same flag in code bit 16.  TileHdr.nslots bits 16-20: output camera (RGBA mode).
+constexpr uint32_t kEntryNoGain = 1u << 29;
+constexpr uint32_t kCodeNoGain = 1u << 16;
 
 hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W, int H,
                          const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s);
+
+// ---- multi-band blend (blend > 0): MultiBandGPUBlender (blenders.cpp:589-735) ------------------
+// Level l of the blend lives on the "level grid": align_result_roi >> l.  Each camera keeps its
+// Gaussian pyramid G (u8x4, camera-local, dense over align_roi >> l) but only the 128x8 tiles some
+// blend step reads are ever computed (tile lists built once per rig).  pyrUp is evaluated on the
+// fly from 3x3 source taps per output quad through per-row / per-column tap tables (UpQuad), which
+// encode pyr_up.cu's borders (abs, then clamp) and its 8-row-block quirk.
+constexpr int kMbMaxBands = 10;
+struct UpQuad {          // one quad row (or column) of a pyrUp output
+    uint16_t idx[3];      // source rows (cols) of the 3 union taps, clamped, local to the coarser level
+    uint8_t w0[3], w1[3]; // integer weights of the quad's first / second row (col) over them
+};
+static_assert(sizeof(UpQuad) == 12, "UpQuad layout");
+
+struct MbCamLevel {       // one camera at one level
+    uint32_t g_off;        // byte offset of the camera's G in the level's pyramid allocation
+    uint32_t g_pitch;      // bytes per row of G (4 * w)
+    int32_t ox, oy, w, h;  // camera's aligned ROI on the level grid: origin and size
+    const void* weight;    // level 0: u8 seam mask (pitch w), else f32 Gaussian weight (pitch w)
+    const UpQuad* up_rows; // pyrUp taps into this camera's next level, by level-grid quad row
+    const UpQuad* up_cols; // ... by level-grid quad column
+};
+
+// Level-0 pyramid images as the composite kernels' RGBA sink.
+struct RgbaOut {
+    uint8_t* base;
+    uint32_t bytes;        // allocation size (< 2^31)
+    const MbCamLevel* cams;
+};
+
+hipError_t launch_mb_remap(const FrameSet& frames, const TiledLut& lut, const double* gains, int use_gain,
+                           const RgbaOut& out, hipStream_t s);
+// fastPyrDown<uchar4> (fast_pyr_down.cu:17-76) of every listed (camera, tile) of level l from l - 1.
+hipError_t launch_mb_down(const uint2* items, int n_items, const MbCamLevel* cams_l, const MbCamLevel* cams_prev,
+                          const uint8_t* g_prev, uint8_t* g_l, hipStream_t s);
+struct MbBlendArgs {
+    int level, bands, n_cams;
+    int W, H;                       // level grid
+    int tiles_x;
+    const uint32_t* tile_cams;      // bit n: camera n has a non-zero weight in the tile
+    const MbCamLevel* cams;         // this level
+    const MbCamLevel* cams_next;    // level + 1 (NULL at the top)
+    const uint8_t* g;               // this level's pyramid allocation
+    const uint8_t* g_next;          // level + 1 allocation
+    const int16_t* r_next;          // collapsed level + 1 (s16x4, pitch 2 * W_next... see W_next)
+    int W_next;
+    const UpQuad* rup_rows;         // pyrUp taps of the collapse (level grid, camera independent)
+    const UpQuad* rup_cols;
+    int16_t* r_out;                 // level > 0: collapsed level (s16x4, pitch 4 * W shorts)
+    uint8_t* out;                   // level 0: YUV420P output frame
+    int64_t out_pitch;
+    int out_w, out_h;
+    int ax, ay, crop_w, crop_h;     // align_result_roi origin in the output frame, crop size
+};
+hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s);
+// Build time: K4 pyrDown<float, BrdReflect101> with nvcc's FMA contraction (pyr_down.cu:55-192).
+hipError_t launch_pyr_down_f32(const float* src, int sw, int sh, float* dst, int dw, int dh, hipStream_t s);
+// Build time: OR bit `cam` into tile_cams[] of every level-grid tile where the camera's weight is
+// non-zero (level 0: u8 seam, else f32).
+hipError_t launch_tile_activity(const void* weight, int is_u8, int w, int h, int ox, int oy, int tiles_x, int cam,
+                                uint32_t* tile_cams, hipStream_t s);
 
 hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, int cn, const float* map1,
                            const float* map2, int mw, int mh, int64_t mpitch, float scale_x, float scale_y,

@@ -1,0 +1,351 @@
+// multiband.hip — gfx950 kernels of the multi-band blend (blend > 0): MultiBandGPUBlender
+// (stitching/src/blenders.cpp:589-735) re-laid out for the level grids and per-camera tile lists
+// of kernels.hpp.  Per frame: mb_down (Gaussian levels 1..B of every camera, only the tiles some
+// later step reads) and mb_blend (per level, coarsest first: Laplacian accumulate over the tile's
+// cameras + weight normalisation + collapse with the coarser level, fused; level 0 writes YUV420P).
+//
+// All pyramid arithmetic is integer and exact (see oracle/octvr_oracle_blend.c for why the CUDA
+// f32 code is):  fastPyrDown = sat(rne(S / 256)), pyrUp = sat(rne(S / 64)) with S the integer
+// weighted tap sum.  The weight pyramid (build time) is f32 with nvcc's FMA contraction.
+// Built with -ffp-contract=off: every other f32 expression rounds as written.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+
+namespace octvr {
+
+// round half to even of S / 2^sh (S of any sign)
+template <int SH>
+__device__ __forceinline__ int rne_shr(int S) {
+    const int q = S >> SH;
+    const int r = S - (q << SH);
+    constexpr int half = 1 << (SH - 1);
+    return q + ((r > half || (r == half && (q & 1))) ? 1 : 0);
+}
+
+__device__ __forceinline__ uint32_t ch_of(uint32_t v, int c) { return (v >> (8 * c)) & 255u; }
+
+// ---------------------------------------------------------------------------------------------
+// fastPyrDown<uchar4> (fast_pyr_down.cu:17-76): out = sat(rne(sum_{j,k} w_j w_k src / 256)),
+// w = [1 4 6 4 1], texture clamp border (camera-local).  One workgroup per (camera, 128x8 tile of
+// level l): the 20 x 260 source patch of level l-1 is staged in LDS, then a vertical pass into 8
+// rows of u16 channel sums, then the horizontal pass per 2x2 output quad.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDnRows = 2 * kTileH + 4, kDnCols = 2 * kTileW + 4;
+
+__global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ items, const MbCamLevel* cams_l,
+                                                      const MbCamLevel* cams_prev, const uint8_t* __restrict__ g_prev,
+                                                      uint8_t* __restrict__ g_l) {
+    __shared__ uint32_t s_src[kDnRows * kDnCols];      // 20.3 KiB
+    __shared__ uint2 s_v[kTileH * kDnCols];             // 16.3 KiB: (c0 | c1 << 16, c2)
+    const uint2 it = items[blockIdx.x];
+    const int cam = uniform((int)it.x);
+    const int tx = uniform((int)(it.y & 0xFFFFu)), ty = uniform((int)(it.y >> 16));
+    const MbCamLevel c = cams_l[cam];
+    const MbCamLevel p = cams_prev[cam];
+    const int tid = threadIdx.x;
+    // tile origin in camera-local coordinates of level l, and its source window in level l-1
+    const int xo = tx * kTileW - c.ox, yo = ty * kTileH - c.oy;
+    const int sx0 = 2 * xo - 2, sy0 = 2 * yo - 2;
+    const uint8_t* src = g_prev + p.g_off;
+    for (int i = tid; i < kDnRows * kDnCols; i += 256) {
+        const int r = i / kDnCols, q = i - r * kDnCols;
+        const int sy = min(max(sy0 + r, 0), p.h - 1), sx = min(max(sx0 + q, 0), p.w - 1);
+        s_src[i] = *reinterpret_cast<const uint32_t*>(src + (int64_t)sy * p.g_pitch + (int64_t)sx * 4);
+    }
+    __syncthreads();
+    for (int i = tid; i < kTileH * kDnCols; i += 256) {
+        const int r = i / kDnCols, q = i - r * kDnCols;
+        const uint32_t* col = s_src + (2 * r) * kDnCols + q;
+        uint32_t acc[3] = {0u, 0u, 0u};
+        const uint32_t w[5] = {1u, 4u, 6u, 4u, 1u};
+#pragma unroll
+        for (int j = 0; j < 5; j++) {
+            const uint32_t v = col[j * kDnCols];
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) acc[ch] += w[j] * ch_of(v, ch);
+        }
+        s_v[i] = make_uint2(acc[0] | (acc[1] << 16), acc[2]);
+    }
+    __syncthreads();
+    const int qx = tid & 63, qy = tid >> 6;
+    const int xl = xo + 2 * qx, yl = yo + 2 * qy;  // quad origin, camera-local (even: whole quads)
+    if (xl < 0 || yl < 0 || xl >= c.w || yl >= c.h) return;
+    uint32_t px[4];
+#pragma unroll
+    for (int p4 = 0; p4 < 4; p4++) {
+        const int r = 2 * qy + (p4 >> 1), cx = 2 * (2 * qx + (p4 & 1));  // source column 2x-2 -> index 2x
+        const uint2* v = s_v + r * kDnCols + cx;
+        const uint32_t w[5] = {1u, 4u, 6u, 4u, 1u};
+        uint32_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            a0 += w[k] * (v[k].x & 0xFFFFu);
+            a1 += w[k] * (v[k].x >> 16);
+            a2 += w[k] * v[k].y;
+        }
+        px[p4] = (uint32_t)min(rne_shr<8>((int)a0), 255) | ((uint32_t)min(rne_shr<8>((int)a1), 255) << 8) |
+                 ((uint32_t)min(rne_shr<8>((int)a2), 255) << 16);
+    }
+    uint8_t* dst = g_l + c.g_off + (int64_t)yl * c.g_pitch + (int64_t)xl * 4;
+    *reinterpret_cast<uint2*>(dst) = make_uint2(px[0], px[1]);
+    *reinterpret_cast<uint2*>(dst + c.g_pitch) = make_uint2(px[2], px[3]);
+}
+
+hipError_t launch_mb_down(const uint2* items, int n_items, const MbCamLevel* cams_l, const MbCamLevel* cams_prev,
+                          const uint8_t* g_prev, uint8_t* g_l, hipStream_t s) {
+    if (n_items <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mb_down_kernel, dim3(n_items), dim3(256), 0, s, items, cams_l, cams_prev, g_prev, g_l);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Blend of one level (blenders.cpp:686-735 for one i, fused with the collapse step of i):
+//   D    = sum over the tile's cameras (ascending) of (short)((G_n - pyrUp(G_n,next)) * w_n)   [K5]
+//          (at the top level: (short)(G_n * w_n), K6), short adds wrapping; only where w_n != 0
+//   L    = sat_s16(rne(D * (1.0f / (1e-5f + sum_n w_n))))                                     [K11]
+//   R    = top ? L : sat_s16(L + pyrUp(R_next))                                                [add]
+//   level 0: out = sat_u8(R) as RGB -> YUV420P; otherwise R is stored (s16x4) for the next level.
+// One workgroup per 128x8 tile of the level grid, one 2x2 quad per lane.  pyrUp taps come from the
+// UpQuad tables: 3 rows x 3 columns of source per quad, per-pixel integer weights over them.
+// ---------------------------------------------------------------------------------------------
+struct Up9 {
+    int s[4][3];  // per quad pixel, per channel: the integer tap sum (scale 1/64)
+};
+
+// 9 source taps (u8x4 from G, or s16x4 from R) of a quad -> integer pyrUp sums for its 4 pixels.
+template <class LOAD>
+__device__ __forceinline__ void up_quad(const UpQuad& ur, const UpQuad& uc, LOAD load, Up9& o) {
+    int v[3][3][3];  // [row][col][ch]
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) load(ur.idx[j], uc.idx[k], v[j][k]);
+#pragma unroll
+    for (int pc = 0; pc < 2; pc++) {
+        const uint8_t* wx = pc ? uc.w1 : uc.w0;
+        int h[3][3];  // [row][ch]
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) h[j][ch] = wx[0] * v[j][0][ch] + wx[1] * v[j][1][ch] + wx[2] * v[j][2][ch];
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++) {
+            const uint8_t* wy = pr ? ur.w1 : ur.w0;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) o.s[pr * 2 + pc][ch] = wy[0] * h[0][ch] + wy[1] * h[1][ch] + wy[2] * h[2][ch];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
+    const int tid = threadIdx.x;
+    const int tile = blockIdx.x;
+    const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+    const int x = tx * kTileW + 2 * (tid & 63), y = ty * kTileH + 2 * (tid >> 6);  // quad origin (even)
+    const bool top = a.level == a.bands;
+    bool valid[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) valid[p] = (x + (p & 1)) < a.W && (y + (p >> 1)) < a.H;
+    int D[4][3];
+    float wsum[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        wsum[p] = 1e-5f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) D[p][ch] = 0;
+    }
+    uint32_t m = (uint32_t)uniform((int)a.tile_cams[tile]);
+    while (m) {
+        const int n = __builtin_ctz(m);
+        m &= m - 1;
+        const MbCamLevel c = a.cams[n];
+        const int xl = x - c.ox, yl = y - c.oy;  // camera-local quad origin (any parity)
+        float w[4];
+        bool any = false;
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int px = xl + (p & 1), py = yl + (p >> 1);
+            const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
+            float wv = 0.f;
+            if (in) {
+                const int64_t k = (int64_t)py * c.w + px;
+                // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
+                wv = a.level == 0 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
+                                  : static_cast<const float*>(c.weight)[k];
+            }
+            w[p] = wv;
+            any |= wv != 0.f;
+        }
+        if (!any) continue;
+        int g[4][3];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int px = min(max(xl + (p & 1), 0), c.w - 1), py = min(max(yl + (p >> 1), 0), c.h - 1);
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)py * c.g_pitch + px * 4);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) g[p][ch] = (int)ch_of(v, ch);
+        }
+        if (!top) {
+            const MbCamLevel cn = a.cams_next[n];
+            const uint8_t* gn = a.g_next + cn.g_off;
+            Up9 u;
+            up_quad(c.up_rows[y >> 1], c.up_cols[x >> 1],
+                    [&](int r, int col, int (&o)[3]) {
+                        const uint32_t v = *reinterpret_cast<const uint32_t*>(gn + (int64_t)r * cn.g_pitch + col * 4);
+#pragma unroll
+                        for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
+                    },
+                    u);
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) g[p][ch] -= min(max(rne_shr<6>(u.s[p][ch]), 0), 255);  // sat u8
+        }
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            if (w[p] == 0.f) continue;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                const int sub = (int)__builtin_truncf((float)g[p][ch] * w[p]);  // (short) of a small value
+                D[p][ch] = (int)(int16_t)(D[p][ch] + sub);                      // short += short wraps
+            }
+            wsum[p] = wsum[p] + w[p];
+        }
+    }
+    int R[4][3];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        const float rcp = 1.0f / wsum[p];  // correctly rounded (hipcc default), as CUDA's 1.0f / b
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++)
+            R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf((float)D[p][ch] * rcp), -32768.f, 32767.f);
+    }
+    if (!top) {
+        Up9 u;
+        const int16_t* rn = a.r_next;
+        const int wn = a.W_next;
+        up_quad(a.rup_rows[y >> 1], a.rup_cols[x >> 1],
+                [&](int r, int col, int (&o)[3]) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(rn + ((int64_t)r * wn + col) * 4);
+                    o[0] = (int)(int16_t)(v.x & 0xFFFFu);
+                    o[1] = (int)(int16_t)(v.x >> 16);
+                    o[2] = (int)(int16_t)(v.y & 0xFFFFu);
+                },
+                u);
+#pragma unroll
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                const int up = min(max(rne_shr<6>(u.s[p][ch]), -32768), 32767);
+                R[p][ch] = min(max(R[p][ch] + up, -32768), 32767);
+            }
+    }
+    if (a.level > 0) {
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            if (!valid[p]) continue;
+            const uint2 v = make_uint2(((uint32_t)R[p][0] & 0xFFFFu) | ((uint32_t)R[p][1] << 16), (uint32_t)R[p][2] & 0xFFFFu);
+            *reinterpret_cast<uint2*>(a.r_out + ((int64_t)(y + (p >> 1)) * a.W + x + (p & 1)) * 4) = v;
+        }
+        return;
+    }
+    // level 0: convertTo(CV_8UC3) into result(align_result_roi.tl, crop) and RGB -> YUV420P
+    uint32_t rgb[4][3];
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) rgb[p][ch] = (uint32_t)min(max(R[p][ch], 0), 255);
+    const float one[4] = {1.f, 1.f, 1.f, 1.f};
+    const OutFrame of = make_out_frame(a.out, a.out_w, a.out_h, a.out_pitch);
+    const int ox = a.ax + x, oy = a.ay + y;
+    store_quad(of, finish_quad(rgb, one), ox, oy, x < a.crop_w && y < a.crop_h && ox < a.out_w && oy < a.out_h);
+}
+
+hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s) {
+    const int tiles_y = (a.H + kTileH - 1) / kTileH;
+    const int n = a.tiles_x * tiles_y;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(mb_blend_kernel, dim3(n), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// Build time: K4 pyrDown<float, BrdReflect101> (pyr_down.cu:55-192).  Column sums first (5 rows,
+// reflect-101), then the row sum of 5 column sums; nvcc contracts `sum + w * v` into fmaf.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int refl101(int v, int last) {
+    v = abs(last - abs(last - v)) % (last + 1);
+    return abs(v) % (last + 1);
+}
+__device__ __forceinline__ float sum5(float a, float b, float c, float d, float e) {
+    float s = 0.0625f * a;
+    s = __builtin_fmaf(0.25f, b, s);
+    s = __builtin_fmaf(0.375f, c, s);
+    s = __builtin_fmaf(0.25f, d, s);
+    return __builtin_fmaf(0.0625f, e, s);
+}
+
+__global__ void __launch_bounds__(256) pyr_down_f32_kernel(const float* __restrict__ src, int sw, int sh,
+                                                           float* __restrict__ dst, int dw, int dh) {
+    const int64_t total = (int64_t)dw * dh;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int y = (int)(i / dw), x = (int)(i - (int64_t)y * dw);
+        const float* r[5];
+#pragma unroll
+        for (int j = 0; j < 5; j++) r[j] = src + (int64_t)refl101(2 * y + j - 2, sh - 1) * sw;
+        float cs[5];
+#pragma unroll
+        for (int k = 0; k < 5; k++) {
+            const int cx = refl101(2 * x + k - 2, sw - 1);
+            cs[k] = sum5(r[0][cx], r[1][cx], r[2][cx], r[3][cx], r[4][cx]);
+        }
+        dst[i] = sum5(cs[0], cs[1], cs[2], cs[3], cs[4]);
+    }
+}
+
+hipError_t launch_pyr_down_f32(const float* src, int sw, int sh, float* dst, int dw, int dh, hipStream_t s) {
+    const int64_t total = (int64_t)dw * dh;
+    if (total <= 0) return hipSuccess;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(pyr_down_f32_kernel, dim3(blocks), dim3(256), 0, s, src, sw, sh, dst, dw, dh);
+    return hipGetLastError();
+}
+
+// Build time: which level-grid tiles hold a non-zero weight of camera `cam`.  A lane scans 8
+// pixels of one row that share a tile (level-grid x multiple of 8) and sets the bit once.
+__global__ void __launch_bounds__(256) tile_activity_kernel(const void* weight, int is_u8, int w, int h, int ox, int oy,
+                                                            int tiles_x, int cam, uint32_t* tile_cams) {
+    const int gx_n = (w + 7 + (ox & 7)) / 8 + 1;  // 8-pixel groups per row on the level grid
+    const int64_t total = (int64_t)gx_n * h;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+        const int yl = (int)(i / gx_n), gi = (int)(i - (int64_t)yl * gx_n);
+        const int gx0 = ((ox >> 3) + gi) * 8;  // level-grid x of the group
+        bool nz = false;
+        for (int q = 0; q < 8; q++) {
+            const int xl = gx0 + q - ox;
+            if (xl < 0 || xl >= w) continue;
+            const int64_t k = (int64_t)yl * w + xl;
+            nz |= is_u8 ? static_cast<const uint8_t*>(weight)[k] != 0 : static_cast<const float*>(weight)[k] != 0.f;
+        }
+        if (nz) {
+            const int gy = yl + oy;
+            atomicOr(&tile_cams[(gy / kTileH) * tiles_x + gx0 / kTileW], 1u << cam);
+        }
+    }
+}
+
+hipError_t launch_tile_activity(const void* weight, int is_u8, int w, int h, int ox, int oy, int tiles_x, int cam,
+                                uint32_t* tile_cams, hipStream_t s) {
+    if (w <= 0 || h <= 0) return hipSuccess;
+    const int64_t total = (int64_t)((w + 7 + (ox & 7)) / 8 + 1) * h;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(tile_activity_kernel, dim3(blocks), dim3(256), 0, s, weight, is_u8, w, h, ox, oy, tiles_x, cam,
+                       tile_cams);
+    return hipGetLastError();
+}
+
+}  // namespace octvr

@@ -1,0 +1,498 @@
+// multiband_host.cpp — host orchestration of the multi-band blend (Mapper blend > 0):
+// MultiBandGPUBlender (stitching/src/blenders.cpp:589-735) laid out for the MI355X.
+//
+// Build (once per rig, all on `device`):
+//   * rectangles exactly as the reference: result ROI, align_result_roi (multiples of 2^B), per
+//     camera align_rois with the 5 * 2^B gap (blenders.cpp:595-618);
+//   * weights: level 0 = seam / 255 (kept as the u8 seam, converted in-kernel bit-exactly), levels
+//     1..B = K4 pyrDown in f32 (multiband.hip); per level and tile the set of cameras with a non-zero
+//     weight (tile_cams);
+//   * pyrUp tap tables (UpQuad) per camera and level, and for the collapse;
+//   * "required" tile sets per camera and level: a camera's Gaussian level is computed only on the
+//     tiles that its blend reads (its weight tiles, the pyrUp support of its finer level's weight
+//     tiles) and, transitively, the pyrDown support of its coarser required tiles.  For a rig whose
+//     seams split the panorama, this is ~1.2-1.5 cameras per pixel instead of every camera
+//     everywhere (the reference computes all pyramids over every align_roi);
+//   * the level-0 remap as a tiled composite LUT over (camera, required tile) jobs (tiling.cpp).
+// Per frame: remap (+gain) -> pyrDown levels -> blend + collapse from the top level to level 0.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "host_common.hpp"
+#include "kernels.hpp"
+
+namespace octvr {
+
+namespace {
+struct Rect {
+    int x = 0, y = 0, w = 0, h = 0;
+};
+}  // namespace
+
+class MultiBand {
+   public:
+    int n = 0, B = 0, device = 0;
+    int out_w = 0, out_h = 0;
+    Rect arr;
+    std::vector<Rect> ar;
+    struct Level {
+        int W = 0, H = 0, tx_n = 0, ty_n = 0;
+        DevBuf<uint8_t> g;              // all cameras' Gaussian level (u8x4)
+        size_t g_bytes = 0;
+        std::vector<MbCamLevel> cams_h;
+        DevBuf<MbCamLevel> cams;
+        DevBuf<uint8_t> seam0;          // level 0: u8 seams over each align_roi
+        DevBuf<float> wts;              // level > 0: f32 weights over each align_roi >> l
+        DevBuf<uint32_t> tile_cams;
+        std::vector<uint32_t> tile_cams_h;
+        DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
+        DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
+        int rup_rows = 0;
+        DevBuf<uint2> down_items;       // level > 0
+        int n_down = 0;
+        DevBuf<int16_t> R;              // level > 0: collapsed level, s16x4
+        size_t req_tiles = 0;           // sum over cameras of required tiles
+    };
+    std::vector<Level> lv;
+    TiledLutDev remap;
+    bool full_cover = true;
+    int crop_w = 0, crop_h = 0;
+};
+
+void MultiBandDeleter::operator()(MultiBand* p) const { delete p; }
+
+namespace {
+
+int round_down(int x, int b) { return (x >> b) << b; }
+int round_up(int x, int b) {
+    const int m = 1 << b;
+    return x + (m - (x % m)) % m;
+}
+
+// pyrUp (pyr_up.cu:55-166) source taps of one output row (col) `o` of a level of size n_out, from a
+// source of size n_src: unclamped indices + weights (1,6,1 | 4,4), the 8-row block quirk for rows.
+int up_taps(int o, bool rows, int* u, int* w) {
+    if (!(o & 1)) {
+        const int q = o >> 1;
+        u[0] = q - 1;
+        u[1] = q;
+        u[2] = (rows && (o & 7) == 6) ? q + 2 : q + 1;
+        w[0] = 1, w[1] = 6, w[2] = 1;
+        return 3;
+    }
+    u[0] = (o - 1) >> 1;
+    u[1] = (rows && (o & 7) == 7) ? ((o + 1) >> 1) + 1 : (o + 1) >> 1;
+    w[0] = 4, w[1] = 4;
+    return 2;
+}
+
+// Tap table over the level grid's quad rows (cols): grid index g -> local index g - off, valid in
+// [0, n_local); sources clamped to [0, n_src) after abs (pyr_up.cu:72-79).
+std::vector<UpQuad> up_table(int n_grid, int off, int n_local, int n_src, bool rows) {
+    std::vector<UpQuad> t((n_grid + 1) / 2);
+    for (size_t q = 0; q < t.size(); q++) {
+        int uni[6], nu = 0;
+        int us[2][3], ws[2][3], nt[2] = {0, 0};
+        for (int p = 0; p < 2; p++) {
+            const int o = (int)(2 * q) + p - off;
+            if (o < 0 || o >= n_local) continue;
+            nt[p] = up_taps(o, rows, us[p], ws[p]);
+            for (int k = 0; k < nt[p]; k++) {
+                bool seen = false;
+                for (int j = 0; j < nu; j++) seen |= uni[j] == us[p][k];
+                if (!seen) uni[nu++] = us[p][k];
+            }
+        }
+        UpQuad& e = t[q];
+        memset(&e, 0, sizeof e);
+        REQUIRE(nu <= 3, "pyrUp quad needs more than 3 source rows");
+        std::sort(uni, uni + nu);
+        for (int j = nu; j < 3; j++) uni[j] = nu ? uni[0] : 0;
+        for (int j = 0; j < 3; j++) e.idx[j] = (uint16_t)std::min(n_src - 1, std::abs(uni[j]));
+        for (int p = 0; p < 2; p++) {
+            uint8_t* w = p ? e.w1 : e.w0;
+            for (int k = 0; k < nt[p]; k++)
+                for (int j = 0; j < nu; j++)
+                    if (uni[j] == us[p][k]) w[j] = (uint8_t)ws[p][k];
+        }
+    }
+    return t;
+}
+
+struct Bitmap {
+    int tx_n = 0, ty_n = 0;
+    std::vector<uint8_t> b;
+    void init(int tx, int ty) {
+        tx_n = tx, ty_n = ty;
+        b.assign((size_t)tx * ty, 0);
+    }
+    // mark every tile overlapping grid rectangle [x0, x1] x [y0, y1] (inclusive)
+    void mark(int x0, int y0, int x1, int y1) {
+        x0 = std::max(x0, 0), y0 = std::max(y0, 0);
+        x1 = std::min(x1, tx_n * kTileW - 1), y1 = std::min(y1, ty_n * kTileH - 1);
+        for (int ty = y0 / kTileH; ty <= y1 / kTileH; ty++)
+            for (int tx = x0 / kTileW; tx <= x1 / kTileW; tx++) b[(size_t)ty * tx_n + tx] = 1;
+    }
+};
+
+}  // namespace
+
+MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
+                            const std::vector<int>& in_h) {
+    auto mb = std::unique_ptr<MultiBand>(new MultiBand);
+    MultiBand& M = *mb;
+    const int n = (int)rig.inputs.size();
+    M.n = n;
+    M.B = bands;
+    M.device = device;
+    M.out_w = rig.out_w;
+    M.out_h = rig.out_h;
+    const int B = bands;
+    REQUIRE(B >= 1 && B <= kMbMaxBands, "multi-band blend: band count out of range (blend must be >= 3)");
+    REQUIRE(rig.seam_masks.size() == (size_t)n,
+            "multi-band blend needs seam masks (octvr_rig_create_masks or a .dat with seams)");
+    // ---- rectangles (blenders.cpp:479-486, 595-618) ------------------------------------------
+    int x0 = INT32_MAX, y0 = INT32_MAX, x1 = INT32_MIN, y1 = INT32_MIN;
+    for (auto& in : rig.inputs) {
+        x0 = std::min(x0, in.roi[0]);
+        y0 = std::min(y0, in.roi[1]);
+        x1 = std::max(x1, in.roi[0] + in.roi[2]);
+        y1 = std::max(y1, in.roi[1] + in.roi[3]);
+    }
+    M.arr = Rect{round_down(x0, B), round_down(y0, B), 0, 0};
+    M.arr.w = round_up(x1, B) - M.arr.x;
+    M.arr.h = round_up(y1, B) - M.arr.y;
+    const int gap = 5 * (1 << B);
+    for (auto& in : rig.inputs) {
+        const int l = std::max(M.arr.x, round_down(in.roi[0], B) - gap);
+        const int t = std::max(M.arr.y, round_down(in.roi[1], B) - gap);
+        const int r = std::min(M.arr.x + M.arr.w, round_up(in.roi[0] + in.roi[2], B) + gap);
+        const int b = std::min(M.arr.y + M.arr.h, round_up(in.roi[1] + in.roi[3], B) + gap);
+        REQUIRE(((r - l) >> B) > 0 && ((b - t) >> B) > 0, "multi-band: aligned ROI too small (blenders.cpp:614-615)");
+        M.ar.push_back(Rect{l, t, r - l, b - t});
+    }
+    const double max_len = std::max(M.arr.w, M.arr.h);
+    REQUIRE(B <= (int)std::ceil(std::log(max_len) / std::log(2.0)), "multi-band: too many bands (blenders.cpp:621)");
+    M.crop_w = std::min(M.arr.w, rig.out_w);
+    M.crop_h = std::min(M.arr.h, rig.out_h);
+    REQUIRE(M.arr.x + M.crop_w <= rig.out_w && M.arr.y + M.crop_h <= rig.out_h,
+            "multi-band: aligned result ROI leaves the output frame (blenders.cpp:727-729)");
+    M.full_cover = M.arr.x == 0 && M.arr.y == 0 && M.crop_w == rig.out_w && M.crop_h == rig.out_h;
+
+    DeviceGuard dg(device);
+    M.lv.resize(B + 1);
+    for (int l = 0; l <= B; l++) {
+        auto& L = M.lv[l];
+        L.W = M.arr.w >> l;
+        L.H = M.arr.h >> l;
+        L.tx_n = (L.W + kTileW - 1) / kTileW;
+        L.ty_n = (L.H + kTileH - 1) / kTileH;
+        L.cams_h.resize(n);
+        size_t off = 0;
+        for (int i = 0; i < n; i++) {
+            MbCamLevel& c = L.cams_h[i];
+            memset(&c, 0, sizeof c);
+            c.ox = (M.ar[i].x - M.arr.x) >> l;
+            c.oy = (M.ar[i].y - M.arr.y) >> l;
+            c.w = M.ar[i].w >> l;
+            c.h = M.ar[i].h >> l;
+            c.g_pitch = (uint32_t)c.w * 4;
+            c.g_off = (uint32_t)off;
+            off += ((size_t)c.g_pitch * c.h + 255) & ~(size_t)255;
+        }
+        REQUIRE(off < 0x7FFFFF00u, "multi-band: pyramid level larger than 2 GiB");
+        L.g_bytes = off;
+        L.g.alloc(off);
+    }
+    // ---- weights: level 0 = seam (u8), levels >= 1 = K4 pyrDown of seam/255 ------------------
+    {
+        auto& L0 = M.lv[0];
+        size_t tot = 0;
+        std::vector<size_t> woff(n);
+        for (int i = 0; i < n; i++) woff[i] = tot, tot += (size_t)L0.cams_h[i].w * L0.cams_h[i].h;
+        std::vector<uint8_t> s0(tot, 0);
+        std::vector<float> f0(tot, 0.f);
+        const float inv255 = (float)(1. / 255);
+        for (int i = 0; i < n; i++) {
+            const RigInput& in = rig.inputs[i];
+            const Rect& a = M.ar[i];
+            for (int y = 0; y < in.roi[3]; y++)
+                for (int x = 0; x < in.roi[2]; x++) {
+                    const uint8_t v = rig.seam_masks[i][(size_t)y * in.roi[2] + x];
+                    const size_t d = woff[i] + (size_t)(in.roi[1] - a.y + y) * a.w + (in.roi[0] - a.x + x);
+                    s0[d] = v;
+                    f0[d] = inv255 * (float)v;
+                }
+        }
+        L0.seam0.upload(s0.data(), s0.size());
+        for (int i = 0; i < n; i++) L0.cams_h[i].weight = L0.seam0.p + woff[i];
+        DevBuf<float> prev;
+        prev.upload(f0.data(), f0.size());
+        std::vector<size_t> poff = woff;
+        for (int l = 1; l <= B; l++) {
+            auto& L = M.lv[l];
+            size_t t2 = 0;
+            std::vector<size_t> o2(n);
+            for (int i = 0; i < n; i++) o2[i] = t2, t2 += (size_t)L.cams_h[i].w * L.cams_h[i].h;
+            L.wts.alloc(t2);
+            for (int i = 0; i < n; i++) {
+                const auto& pc = M.lv[l - 1].cams_h[i];
+                HIP_CHECK(launch_pyr_down_f32(prev.p + poff[i], pc.w, pc.h, L.wts.p + o2[i], L.cams_h[i].w,
+                                              L.cams_h[i].h, nullptr));
+                L.cams_h[i].weight = L.wts.p + o2[i];
+            }
+            HIP_CHECK(hipDeviceSynchronize());
+            if (l < B) {  // next level's source: a copy (L.wts stays owned by the level)
+                prev.alloc(t2);
+                HIP_CHECK(hipMemcpy(prev.p, L.wts.p, t2 * sizeof(float), hipMemcpyDeviceToDevice));
+                poff = o2;
+            }
+        }
+    }
+    // ---- tile activity ----------------------------------------------------------------------
+    for (int l = 0; l <= B; l++) {
+        auto& L = M.lv[l];
+        const size_t nt = (size_t)L.tx_n * L.ty_n;
+        L.tile_cams.alloc(nt);
+        HIP_CHECK(hipMemset(L.tile_cams.p, 0, nt * sizeof(uint32_t)));
+        for (int i = 0; i < n; i++) {
+            const auto& c = L.cams_h[i];
+            HIP_CHECK(launch_tile_activity(c.weight, l == 0, c.w, c.h, c.ox, c.oy, L.tx_n, i, L.tile_cams.p, nullptr));
+        }
+        HIP_CHECK(hipDeviceSynchronize());
+        L.tile_cams_h.resize(nt);
+        HIP_CHECK(hipMemcpy(L.tile_cams_h.data(), L.tile_cams.p, nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    }
+    // ---- pyrUp tap tables -------------------------------------------------------------------
+    std::vector<std::vector<std::vector<UpQuad>>> ur(B), uc(B);  // [level][camera]
+    for (int l = 0; l < B; l++) {
+        auto& L = M.lv[l];
+        const auto& Ln = M.lv[l + 1];
+        std::vector<UpQuad> all;
+        ur[l].resize(n);
+        uc[l].resize(n);
+        std::vector<size_t> ro(n), co(n);
+        for (int i = 0; i < n; i++) {
+            const auto& c = L.cams_h[i];
+            ur[l][i] = up_table(L.H, c.oy, c.h, Ln.cams_h[i].h, true);
+            uc[l][i] = up_table(L.W, c.ox, c.w, Ln.cams_h[i].w, false);
+            ro[i] = all.size();
+            all.insert(all.end(), ur[l][i].begin(), ur[l][i].end());
+            co[i] = all.size();
+            all.insert(all.end(), uc[l][i].begin(), uc[l][i].end());
+        }
+        L.up.upload(all.data(), all.size());
+        for (int i = 0; i < n; i++) {
+            L.cams_h[i].up_rows = L.up.p + ro[i];
+            L.cams_h[i].up_cols = L.up.p + co[i];
+        }
+        std::vector<UpQuad> rr = up_table(L.H, 0, L.H, Ln.H, true), rc = up_table(L.W, 0, L.W, Ln.W, false);
+        L.rup_rows = (int)rr.size();
+        rr.insert(rr.end(), rc.begin(), rc.end());
+        L.rup.upload(rr.data(), rr.size());
+    }
+    // ---- required tiles per camera and level ---------------------------------------------------
+    std::vector<std::vector<Bitmap>> req(B + 1, std::vector<Bitmap>(n));
+    for (int l = B; l >= 0; l--) {
+        auto& L = M.lv[l];
+        for (int i = 0; i < n; i++) {
+            Bitmap& R = req[l][i];
+            R.init(L.tx_n, L.ty_n);
+            const auto& c = L.cams_h[i];
+            for (size_t t = 0; t < R.b.size(); t++)
+                if (L.tile_cams_h[t] >> i & 1u) R.b[t] = 1;
+            if (l >= 1) {  // pyrUp support of the finer level's weight tiles
+                const auto& Lf = M.lv[l - 1];
+                for (int ty = 0; ty < Lf.ty_n; ty++)
+                    for (int tx = 0; tx < Lf.tx_n; tx++) {
+                        if (!(Lf.tile_cams_h[(size_t)ty * Lf.tx_n + tx] >> i & 1u)) continue;
+                        int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
+                        for (int q = ty * kTileH / 2; q < std::min((ty + 1) * kTileH / 2, (int)ur[l - 1][i].size()); q++)
+                            for (int j = 0; j < 3; j++) {
+                                r0 = std::min(r0, (int)ur[l - 1][i][q].idx[j]);
+                                r1 = std::max(r1, (int)ur[l - 1][i][q].idx[j]);
+                            }
+                        for (int q = tx * kTileW / 2; q < std::min((tx + 1) * kTileW / 2, (int)uc[l - 1][i].size()); q++)
+                            for (int j = 0; j < 3; j++) {
+                                c0 = std::min(c0, (int)uc[l - 1][i][q].idx[j]);
+                                c1 = std::max(c1, (int)uc[l - 1][i][q].idx[j]);
+                            }
+                        if (r1 >= 0 && c1 >= 0) R.mark(c0 + c.ox, r0 + c.oy, c1 + c.ox, r1 + c.oy);
+                    }
+            }
+            if (l < B) {  // pyrDown support of the coarser level's required tiles
+                const auto& Lc = M.lv[l + 1];
+                const auto& cc = Lc.cams_h[i];
+                const Bitmap& Rc = req[l + 1][i];
+                for (int ty = 0; ty < Lc.ty_n; ty++)
+                    for (int tx = 0; tx < Lc.tx_n; tx++) {
+                        if (!Rc.b[(size_t)ty * Lc.tx_n + tx]) continue;
+                        const int xa = std::max(tx * kTileW - cc.ox, 0), xb = std::min((tx + 1) * kTileW - 1 - cc.ox, cc.w - 1);
+                        const int ya = std::max(ty * kTileH - cc.oy, 0), yb = std::min((ty + 1) * kTileH - 1 - cc.oy, cc.h - 1);
+                        if (xa > xb || ya > yb) continue;
+                        const int sx0 = std::max(2 * xa - 2, 0), sx1 = std::min(2 * xb + 2, c.w - 1);
+                        const int sy0 = std::max(2 * ya - 2, 0), sy1 = std::min(2 * yb + 2, c.h - 1);
+                        R.mark(sx0 + c.ox, sy0 + c.oy, sx1 + c.ox, sy1 + c.oy);
+                    }
+            }
+            // only tiles that intersect the camera's aligned ROI
+            for (int ty = 0; ty < L.ty_n; ty++)
+                for (int tx = 0; tx < L.tx_n; tx++) {
+                    uint8_t& v = R.b[(size_t)ty * L.tx_n + tx];
+                    if (!v) continue;
+                    const bool hit = tx * kTileW < c.ox + c.w && (tx + 1) * kTileW > c.ox && ty * kTileH < c.oy + c.h &&
+                                     (ty + 1) * kTileH > c.oy;
+                    if (!hit) v = 0;
+                    else L.req_tiles++;
+                }
+        }
+    }
+    // ---- per-level device tables, down items, collapse buffers ----------------------------------
+    for (int l = 0; l <= B; l++) {
+        auto& L = M.lv[l];
+        L.cams.upload(L.cams_h.data(), n);
+        if (l >= 1) {
+            std::vector<uint2> items;
+            for (int i = 0; i < n; i++)
+                for (int ty = 0; ty < L.ty_n; ty++)
+                    for (int tx = 0; tx < L.tx_n; tx++)
+                        if (req[l][i].b[(size_t)ty * L.tx_n + tx])
+                            items.push_back(make_uint2((uint32_t)i, (uint32_t)tx | ((uint32_t)ty << 16)));
+            L.n_down = (int)items.size();
+            L.down_items.upload(items.data(), items.size());
+            L.R.alloc((size_t)L.W * L.H * 4);
+        }
+    }
+    // ---- level-0 remap jobs (camera, required tile) -------------------------------------------
+    {
+        auto& L0 = M.lv[0];
+        std::vector<TileJob> jobs;
+        for (int i = 0; i < n; i++)
+            for (int ty = 0; ty < L0.ty_n; ty++)
+                for (int tx = 0; tx < L0.tx_n; tx++)
+                    if (req[0][i].b[(size_t)ty * L0.tx_n + tx]) jobs.push_back(TileJob{tx, ty, i});
+        std::atomic<bool> bad{false};
+        const Rect arr = M.arr;
+        auto entry = [&](int job, int x, int y) -> CompositeEntry {
+            const int i = jobs[job].cam;
+            const RigInput& in = rig.inputs[i];
+            const int X = x + arr.x, Y = y + arr.y;
+            const int rx = X - in.roi[0], ry = Y - in.roi[1];
+            if (rx < 0 || ry < 0 || rx >= in.roi[2] || ry >= in.roi[3]) return CompositeEntry{0u, 0u};
+            const size_t k = (size_t)ry * in.roi[2] + rx;
+            const float m1 = in.map1[k], m2 = in.map2[k];
+            if (in.mask[k]) return make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
+            // LUT mask 0: the remap still runs there, without gain (mul_scalar_with_mask)
+            if (m1 >= 0.f && m1 < 1.f && m2 >= 0.f && m2 < 1.f) {
+                CompositeEntry e = make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
+                e.code |= kCodeNoGain;
+                return e;
+            }
+            const float X32 = m1 * (float)in_w[i] * 32.f, Y32 = m2 * (float)in_h[i] * 32.f;
+            if (X32 == X32 && Y32 == Y32 && std::fabs(X32) < 1e9f && std::fabs(Y32) < 1e9f) {
+                const int sx = (int)std::lrint(X32) >> 5, sy = (int)std::lrint(Y32) >> 5;
+                if (sx >= -1 && sx < in_w[i] && sy >= -1 && sy < in_h[i]) bad = true;
+            }
+            return CompositeEntry{0u, 0u};
+        };
+        TiledLutBuild tb = build_tiled_lut(jobs, entry, in_w, in_h);
+        REQUIRE(!bad, "multi-band: a LUT-mask-0 pixel maps into the image just outside [0,1) (unsupported)");
+        M.remap.upload(tb);
+    }
+    return mb.release();
+}
+
+void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
+                   int64_t out_pitch, hipStream_t s) {
+    auto& L0 = M.lv[0];
+    HIP_CHECK(launch_mb_remap(frames, M.remap.view, gains_dev, use_gain,
+                              RgbaOut{L0.g.p, (uint32_t)L0.g_bytes, L0.cams.p}, s));
+    for (int l = 1; l <= M.B; l++) {
+        auto& L = M.lv[l];
+        HIP_CHECK(launch_mb_down(L.down_items.p, L.n_down, L.cams.p, M.lv[l - 1].cams.p, M.lv[l - 1].g.p, L.g.p, s));
+    }
+    if (!M.full_cover) {  // result pixels outside the blended ROI stay 0 (mapper.cpp:155): Y 0, U = V = 128
+        HIP_CHECK(hipMemset2DAsync(out, out_pitch, 0, M.out_w, M.out_h, s));
+        HIP_CHECK(hipMemset2DAsync(out + (int64_t)M.out_h * out_pitch, out_pitch, 128, M.out_w, M.out_h / 2, s));
+    }
+    for (int l = M.B; l >= 0; l--) {
+        auto& L = M.lv[l];
+        MbBlendArgs a{};
+        a.level = l;
+        a.bands = M.B;
+        a.n_cams = M.n;
+        a.W = L.W;
+        a.H = L.H;
+        a.tiles_x = L.tx_n;
+        a.tile_cams = L.tile_cams.p;
+        a.cams = L.cams.p;
+        a.g = L.g.p;
+        if (l < M.B) {
+            auto& Ln = M.lv[l + 1];
+            a.cams_next = Ln.cams.p;
+            a.g_next = Ln.g.p;
+            a.r_next = Ln.R.p;
+            a.W_next = Ln.W;
+            a.rup_rows = L.rup.p;
+            a.rup_cols = L.rup.p + L.rup_rows;
+        }
+        if (l > 0) {
+            a.r_out = L.R.p;
+        } else {
+            a.out = out;
+            a.out_pitch = out_pitch;
+            a.out_w = M.out_w;
+            a.out_h = M.out_h;
+            a.ax = M.arr.x;
+            a.ay = M.arr.y;
+            a.crop_w = M.crop_w;
+            a.crop_h = M.crop_h;
+        }
+        HIP_CHECK(launch_mb_blend(a, s));
+    }
+}
+
+double multiband_traffic(const MultiBand& M) {
+    // remap: tiled entries + level-0 pyramid writes; pyrDown: source reads + writes; blend: per
+    // (camera, pixel) of every weight tile G + weight + 9/4 coarser taps, R reads/writes, output
+    const auto& L0 = M.lv[0];
+    const TiledLut& t = M.remap.view;
+    double b = (4.0 + 4.0) * t.n_items * kTilePx + (8.0 + 4.0) * t.n_wide * kTilePx;
+    for (int l = 1; l <= M.B; l++) b += (double)M.lv[l].n_down * kTilePx * (16.0 + 4.0);
+    for (int l = 0; l <= M.B; l++) {
+        const auto& L = M.lv[l];
+        size_t cam_tiles = 0;
+        for (uint32_t m : L.tile_cams_h) cam_tiles += (size_t)__builtin_popcount(m);
+        b += (double)cam_tiles * kTilePx * (4.0 + (l ? 4.0 : 1.0) + (l < M.B ? 1.0 : 0.0));
+        if (l > 0) b += 8.0 * L.W * L.H * 1.25;  // R written, read back by the finer level's pyrUp
+    }
+    b += 1.5 * M.out_w * M.out_h;
+    (void)L0;
+    return b;
+}
+
+std::string multiband_info(const MultiBand& M) {
+    std::string s = "\"bands\": " + std::to_string(M.B) + ", \"align_result_roi\": [" + std::to_string(M.arr.x) + ", " +
+                    std::to_string(M.arr.y) + ", " + std::to_string(M.arr.w) + ", " + std::to_string(M.arr.h) +
+                    "], \"remap_items\": " + std::to_string(M.remap.view.n_items) +
+                    ", \"remap_wide\": " + std::to_string(M.remap.view.n_wide) + ", \"level_tiles\": [";
+    for (int l = 0; l <= M.B; l++) {
+        const auto& L = M.lv[l];
+        size_t cam_tiles = 0;
+        for (uint32_t m : L.tile_cams_h) cam_tiles += (size_t)__builtin_popcount(m);
+        char buf[160];
+        snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d}",
+                 l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down);
+        s += buf;
+    }
+    return s + "]";
+}
+
+}  // namespace octvr

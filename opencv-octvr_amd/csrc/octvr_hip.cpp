@@ -413,16 +413,12 @@ struct octvr_mapper {
     int W = 0, H = 0;
     int use_gain = 0;
     std::vector<int> in_w, in_h;
-    // tiled composite LUT (kernels.hpp)
-    DevBuf<TileHdr> tile_hdr;
-    DevBuf<TileSlot> tile_slots;
-    DevBuf<uint32_t> tile_entries;
-    DevBuf<CompositeEntry> tile_wide;
-    DevBuf<uint32_t> tile_wide_ids;
+    // tiled composite LUT (kernels.hpp), blend = 0
+    TiledLutDev tiles;
     int n_tiles = 0;
-    TiledLut tiled{};
-    int n_wide_tiles = 0;
-    double staged_bytes = 0;
+    // multi-band blend state, blend > 0 (multiband_host.cpp)
+    std::unique_ptr<MultiBand, MultiBandDeleter> mb;
+    int blend = 0;
     DevBuf<double> gains;
     // gain feed
     DevBuf<CompositeEntry> samples;  // working-scale samples that lie in some pair intersection
@@ -571,164 +567,6 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
     size_t pairs_px = 0;
     for (uint16_t pm : pmask) pairs_px += (size_t)__builtin_popcount(pm);
     m.n_entries = pairs_px;
-}
-
-// Tiled composite LUT (kernels.hpp "tiled composite") from the per-pixel winner LUT.  Once per rig.
-void build_tiles(octvr_mapper& m, const std::vector<CompositeEntry>& lut8) {
-    const int W = m.W, H = m.H;
-    const int tx_n = (W + kTileW - 1) / kTileW, ty_n = (H + kTileH - 1) / kTileH;
-    const int n_tiles = tx_n * ty_n;
-    std::vector<TileHdr> hdr(n_tiles);
-    std::vector<TileSlot> slots((size_t)n_tiles * kTileSlots);
-    std::vector<uint32_t> entries((size_t)n_tiles * kTilePx, 0u);
-    std::vector<std::vector<CompositeEntry>> wide_parts;
-    std::vector<uint8_t> is_wide(n_tiles, 0);
-    const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<std::vector<std::pair<int, std::vector<CompositeEntry>>>> wide_local(T);
-    auto work = [&](int tid) {
-        for (int t = tid; t < n_tiles; t += T) {
-            const int ty = t / tx_n, tx = t % tx_n;
-            struct Px {
-                int slot, x0, y0, fxy, mask;
-            };
-            Px px[kTilePx];
-            CompositeEntry raw[kTilePx];
-            int cams[8], ns = 0;
-            int minx[8], maxx[8], miny[8], maxy[8];
-            bool wide = false;
-            for (int k = 0; k < kTilePx; k++) {
-                const int q = k >> 2, p = k & 3;
-                const int x = tx * kTileW + (q & 63) * 2 + (p & 1), y = ty * kTileH + (q >> 6) * 2 + (p >> 1);
-                CompositeEntry e{0, 0};
-                if (x < W && y < H) e = lut8[(size_t)y * W + x];
-                raw[k] = e;
-                px[k].mask = 0;
-                if (!(e.code & 0x8000u)) continue;
-                const int cam = (int)((e.code >> 10) & 31u);
-                const int sx = (int)(e.xy & 0xFFFFu), sy = (int)(e.xy >> 16);
-                const int iw = m.in_w[cam], ih = m.in_h[cam];
-                const bool inx = sx + 1 < iw, iny = sy + 1 < ih;
-                const int mask = ((sx < iw && sy < ih) ? 1 : 0) | ((inx && sy < ih) ? 2 : 0) |
-                                 ((iny && sx < iw) ? 4 : 0) | ((inx && iny) ? 8 : 0);
-                if (!mask) continue;
-                const int x0 = std::min(sx, iw - 1), y0 = std::min(sy, ih - 1);
-                const int x1 = x0 + (((mask >> 1) | (mask >> 3)) & 1), y1 = y0 + (((mask >> 2) | (mask >> 3)) & 1);
-                int sl = -1;
-                for (int j = 0; j < ns; j++)
-                    if (cams[j] == cam) sl = j;
-                if (sl < 0) {
-                    if (ns == 8) {
-                        wide = true;
-                        continue;
-                    }
-                    sl = ns++;
-                    cams[sl] = cam;
-                    minx[sl] = miny[sl] = INT32_MAX;
-                    maxx[sl] = maxy[sl] = -1;
-                }
-                minx[sl] = std::min(minx[sl], x0);
-                maxx[sl] = std::max(maxx[sl], x1);
-                miny[sl] = std::min(miny[sl], y0);
-                maxy[sl] = std::max(maxy[sl], y1);
-                px[k] = Px{sl, x0, y0, (int)(e.code & 1023u), mask};
-            }
-            if (ns > kTileSlots) wide = true;
-            TileSlot ts[kTileSlots] = {};
-            int bws[kTileSlots] = {}, bhs[kTileSlots] = {};
-            uint32_t stride = 0, groups = 0;
-            for (int j = 0; j < ns && !wide; j++) {
-                const int iw = m.in_w[cams[j]];
-                if (iw % 8) {  // dword staging of boxes needs 8-aligned box columns inside the image
-                    wide = true;
-                    break;
-                }
-                const int bx0 = minx[j] & ~7, by0 = miny[j] & ~1;
-                const int bx1 = (maxx[j] + 1 + 7) & ~7, by1 = (maxy[j] + 1 + 1) & ~1;
-                bws[j] = bx1 - bx0;
-                bhs[j] = by1 - by0;
-                if (bws[j] > 256 || bhs[j] > 256) {
-                    wide = true;
-                    break;
-                }
-                ts[j].cam = (uint16_t)cams[j];
-                ts[j].bw = (uint16_t)bws[j];
-                ts[j].bh = (uint16_t)bhs[j];
-                ts[j].bx0 = (uint16_t)bx0;
-                ts[j].by0 = (uint16_t)by0;
-                stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
-                groups += (uint32_t)(bws[j] * bhs[j] / 4);
-            }
-            uint32_t lds = kTileZeroDwords, chunks = 0;
-            for (int j = 0; j < ns && !wide; j++) {
-                ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
-                lds += stride * (uint32_t)bhs[j];
-                ts[j].chunk0 = (uint16_t)chunks;
-                chunks += (uint32_t)(bws[j] * bhs[j] / 8 + 63) / 64;
-            }
-            for (int j = ns; j < kTileSlots; j++) ts[j].chunk0 = (uint16_t)std::min<uint32_t>(chunks, 255u);
-            if (chunks > 255) wide = true;
-            if (lds * 4 > (uint32_t)kTileLdsBytes) wide = true;
-            if (wide) {
-                is_wide[t] = 1;
-                wide_local[tid].emplace_back(t, std::vector<CompositeEntry>(raw, raw + kTilePx));
-                continue;
-            }
-            hdr[t] = TileHdr{(uint32_t)tx | ((uint32_t)ty << 16), (uint32_t)ns | (chunks << 8), groups, stride};
-            for (int j = 0; j < kTileSlots; j++) slots[(size_t)t * kTileSlots + j] = ts[j];
-            uint32_t* out = entries.data() + (size_t)t * kTilePx;
-            for (int k = 0; k < kTilePx; k++) {
-                if (!px[k].mask) continue;  // black
-                const TileSlot& sl = ts[px[k].slot];
-                const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
-                out[k] = off | ((uint32_t)(px[k].fxy & 31) << 13) | ((uint32_t)(px[k].fxy >> 5) << 18) |
-                         ((uint32_t)px[k].slot << 23) | ((uint32_t)px[k].mask << 25);
-            }
-        }
-    };
-    std::vector<std::thread> th;
-    for (int i = 0; i < T; i++) th.emplace_back(work, i);
-    for (auto& x : th) x.join();
-    // staged items: the non-wide tiles in tile order, compacted in place
-    int n_items = 0;
-    double sb = 0;
-    for (int t = 0; t < n_tiles; t++) {
-        if (is_wide[t]) continue;
-        if (n_items != t) {
-            hdr[n_items] = hdr[t];
-            std::copy(slots.begin() + (size_t)t * kTileSlots, slots.begin() + (size_t)(t + 1) * kTileSlots,
-                      slots.begin() + (size_t)n_items * kTileSlots);
-            std::copy(entries.begin() + (size_t)t * kTilePx, entries.begin() + (size_t)(t + 1) * kTilePx,
-                      entries.begin() + (size_t)n_items * kTilePx);
-        }
-        sb += 8.0 * hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes loaded per 4-pixel group
-        n_items++;
-    }
-    // wide tiles: 8-byte absolute entries in tile order
-    std::vector<std::pair<int, std::vector<CompositeEntry>>> all;
-    for (auto& v : wide_local)
-        for (auto& p : v) all.push_back(std::move(p));
-    std::sort(all.begin(), all.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-    std::vector<CompositeEntry> wide;
-    std::vector<uint32_t> wide_tiles;
-    wide.reserve(all.size() * kTilePx);
-    for (auto& p : all) {
-        wide_tiles.push_back((uint32_t)(p.first % tx_n) | ((uint32_t)(p.first / tx_n) << 16));
-        wide.insert(wide.end(), p.second.begin(), p.second.end());
-    }
-    m.tile_hdr.upload(hdr.data(), std::max(n_items, 1));
-    m.tile_slots.upload(slots.data(), (size_t)std::max(n_items, 1) * kTileSlots);
-    m.tile_entries.upload(entries.data(), (size_t)std::max(n_items, 1) * kTilePx);
-    if (wide.empty()) {
-        wide.push_back(CompositeEntry{0, 0});
-        wide_tiles.push_back(0u);
-    }
-    m.tile_wide.upload(wide.data(), wide.size());
-    m.tile_wide_ids.upload(wide_tiles.data(), wide_tiles.size());
-    m.n_wide_tiles = (int)all.size();
-    m.n_tiles = n_tiles;
-    m.staged_bytes = sb;
-    m.tiled = TiledLut{m.tile_hdr.p, m.tile_slots.p, m.tile_entries.p, n_items,
-                       m.tile_wide_ids.p, m.tile_wide.p, m.n_wide_tiles};
 }
 
 }  // namespace
@@ -936,7 +774,6 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         REQUIRE(n_inputs == (int)(rig->inputs.size() + rig->overlays.size()), "in_sizes must cover inputs + overlays");
         REQUIRE(rig->overlays.empty(), "overlay inputs are not implemented in this ABI version");
         REQUIRE((int)rig->inputs.size() <= kMaxCams, "too many inputs");
-        if (blend != 0) throw OctvrError(OCTVR_E_UNSUPPORTED, "multi-band / feather blend is not implemented in this ABI version");
         REQUIRE((scale_w == 0 && scale_h == 0) || (scale_w == rig->out_w && scale_h == rig->out_h),
                 "scaled output is not implemented in this ABI version");
         REQUIRE(rig->out_w % 2 == 0 && rig->out_h % 2 == 0, "YUV420 output needs even width/height");
@@ -955,10 +792,16 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
                     "input sizes must be even and < 65536");
         // mapper.cpp:78-82: a single input disables gain (and blend)
         m->use_gain = (enable_gain && m->n > 1) ? 1 : 0;
+        m->blend = m->n > 1 ? blend : 0;
+        if (m->blend < 0) throw OctvrError(OCTVR_E_UNSUPPORTED, "feather blend is not implemented in this ABI version");
         REQUIRE(!m->use_gain || m->n <= 16, "gain estimation supports at most 16 inputs");
         DeviceGuard dg(device);
-        // per-camera templates -> device, composite LUT, then drop the per-camera maps
-        {
+        if (m->blend > 0) {
+            // MultiBandGPUBlender(seam_masks, rois, bands), bands = ceil(log2(blend)) - 1 (mapper.cpp:171-176)
+            const int bands = (int)(std::ceil(std::log((double)m->blend) / std::log(2.)) - 1.);
+            m->mb.reset(multiband_create(*rig, device, bands, m->in_w, m->in_h));
+        } else {
+            // per-camera templates -> device, composite LUT, then drop the per-camera maps
             std::vector<DevBuf<float>> m1(m->n), m2(m->n);
             std::vector<DevBuf<uint8_t>> mk(m->n);
             std::vector<CamTemplate> ct(m->n);
@@ -984,7 +827,16 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
                 m2[i].reset();
                 mk[i].reset();
             }
-            build_tiles(*m, lut8);
+            const int tx_n = (m->W + kTileW - 1) / kTileW, ty_n = (m->H + kTileH - 1) / kTileH;
+            std::vector<TileJob> jobs;
+            jobs.reserve((size_t)tx_n * ty_n);
+            for (int ty = 0; ty < ty_n; ty++)
+                for (int tx = 0; tx < tx_n; tx++) jobs.push_back(TileJob{tx, ty, 0});
+            const int W = m->W, H = m->H;
+            m->tiles.upload(build_tiled_lut(jobs, [&](int, int x, int y) {
+                return (x < W && y < H) ? lut8[(size_t)y * W + x] : CompositeEntry{0u, 0u};
+            }, m->in_w, m->in_h));
+            m->n_tiles = tx_n * ty_n;
         }
         m->gains.alloc(kMaxCams);
         std::vector<double> ones(kMaxCams, 1.0);
@@ -1028,7 +880,10 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
             HIP_CHECK(hipEventCreate(&e1));
             HIP_CHECK(hipEventRecord(e0, s));
         }
-        HIP_CHECK(launch_stitch(fs, m->tiled, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
+        if (m->mb)
+            multiband_run(*m->mb, fs, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s);
+        else
+            HIP_CHECK(launch_stitch(fs, m->tiles.view, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
         if (m->timing) {
             HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
@@ -1055,9 +910,15 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
         REQUIRE(m && bytes, "NULL argument");
         // composite kernel: 4 B tiled-LUT entry (8 B in wide tiles) + 1.5 B YUV420 output per output
         // pixel, every source frame read once (1.5 B per input pixel), tile headers/slots
-        double b = 4.0 * m->tiled.n_items * kTilePx + 8.0 * m->n_wide_tiles * kTilePx + 1.5 * m->W * m->H +
-                   (double)m->tiled.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) +
-                   4.0 * m->n_wide_tiles;
+        if (m->mb) {
+            double b = multiband_traffic(*m->mb);
+            for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
+            *bytes = b;
+            return;
+        }
+        const TiledLut& t = m->tiles.view;
+        double b = 4.0 * t.n_items * kTilePx + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
+                   (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide;
         for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
         *bytes = b;
     });
@@ -1094,12 +955,16 @@ int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
         REQUIRE(m && buf && len > 0, "bad arguments");
         char tmp[512];
         snprintf(tmp, sizeof tmp,
-                 "{\"inputs\": %d, \"out\": [%d, %d], \"tiles\": %d, \"wide_tiles\": %d, \"staged_bytes\": %.0f, "
-                 "\"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, \"gain_chunks\": %d}",
-                 m->n, m->W, m->H, m->n_tiles, m->n_wide_tiles, m->staged_bytes, m->use_gain,
-                 m->n_samples, m->n_entries, m->n_chunks);
-        REQUIRE(strlen(tmp) < len, "buffer too small");
-        memcpy(buf, tmp, strlen(tmp) + 1);
+                 "{\"inputs\": %d, \"out\": [%d, %d], \"blend\": %d, \"tiles\": %d, \"wide_tiles\": %d, "
+                 "\"staged_bytes\": %.0f, \"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, "
+                 "\"gain_chunks\": %d",
+                 m->n, m->W, m->H, m->blend, m->n_tiles, m->tiles.view.n_wide,
+                 m->mb ? 0.0 : m->tiles.staged_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks);
+        std::string js = tmp;
+        if (m->mb) js += ", " + multiband_info(*m->mb);
+        js += "}";
+        REQUIRE(js.size() < len, "buffer too small");
+        memcpy(buf, js.c_str(), js.size() + 1);
     });
 }
 

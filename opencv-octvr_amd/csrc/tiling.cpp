@@ -1,0 +1,175 @@
+// tiling.cpp — the tiled composite LUT (kernels.hpp "tiled composite"), built once per rig.
+//
+// A job is one 128x8 output tile written by one launch item: for blend = 0 every tile of the output
+// frame (each pixel's entry = the winning camera of the copy chain), for blend > 0 every level-0
+// tile a camera's Gaussian pyramid needs (each pixel's entry = that camera's map).  Per job the
+// builder finds the cameras (<= 4 "slots") and their even-aligned luma boxes, and encodes each
+// pixel as a 4-byte box-relative LDS offset + fractions + slot + tap-valid mask; jobs that do not
+// fit (> 4 cameras, a box > 256 px, or LDS above kTileLdsBytes) become "wide" with 8-byte entries.
+#include <algorithm>
+#include <thread>
+#include <vector>
+
+#include "host_common.hpp"
+#include "kernels.hpp"
+
+namespace octvr {
+
+TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
+                              const std::vector<int>& in_h) {
+    const int n_jobs = (int)jobs.size();
+    TiledLutBuild b;
+    b.hdr.resize(n_jobs);
+    b.slots.resize((size_t)n_jobs * kTileSlots);
+    b.entries.assign((size_t)n_jobs * kTilePx, 0u);
+    std::vector<uint8_t> is_wide(n_jobs, 0);
+    std::vector<std::vector<CompositeEntry>> wide_raw(n_jobs);
+    const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    auto work = [&](int tid) {
+        struct Px {
+            int slot, x0, y0, fxy, mask, nogain;
+        };
+        std::vector<Px> px(kTilePx);
+        std::vector<CompositeEntry> raw(kTilePx);
+        for (int t = tid; t < n_jobs; t += T) {
+            const TileJob& J = jobs[t];
+            int cams[8], ns = 0;
+            int minx[8], maxx[8], miny[8], maxy[8];
+            bool wide = false;
+            for (int k = 0; k < kTilePx; k++) {
+                const int q = k >> 2, p = k & 3;
+                const int x = J.tx * kTileW + (q & 63) * 2 + (p & 1), y = J.ty * kTileH + (q >> 6) * 2 + (p >> 1);
+                const CompositeEntry e = entry(t, x, y);
+                raw[k] = e;
+                px[k].mask = 0;
+                if (!(e.code & 0x8000u)) continue;
+                const int cam = (int)((e.code >> 10) & 31u);
+                const int sx = (int)(e.xy & 0xFFFFu), sy = (int)(e.xy >> 16);
+                const int iw = in_w[cam], ih = in_h[cam];
+                const bool inx = sx + 1 < iw, iny = sy + 1 < ih;
+                const int mask = ((sx < iw && sy < ih) ? 1 : 0) | ((inx && sy < ih) ? 2 : 0) |
+                                 ((iny && sx < iw) ? 4 : 0) | ((inx && iny) ? 8 : 0);
+                if (!mask) continue;
+                const int x0 = std::min(sx, iw - 1), y0 = std::min(sy, ih - 1);
+                const int x1 = x0 + (((mask >> 1) | (mask >> 3)) & 1), y1 = y0 + (((mask >> 2) | (mask >> 3)) & 1);
+                int sl = -1;
+                for (int j = 0; j < ns; j++)
+                    if (cams[j] == cam) sl = j;
+                if (sl < 0) {
+                    if (ns == 8) {
+                        wide = true;
+                        continue;
+                    }
+                    sl = ns++;
+                    cams[sl] = cam;
+                    minx[sl] = miny[sl] = INT32_MAX;
+                    maxx[sl] = maxy[sl] = -1;
+                }
+                minx[sl] = std::min(minx[sl], x0);
+                maxx[sl] = std::max(maxx[sl], x1);
+                miny[sl] = std::min(miny[sl], y0);
+                maxy[sl] = std::max(maxy[sl], y1);
+                px[k] = Px{sl, x0, y0, (int)(e.code & 1023u), mask, (e.code & kCodeNoGain) ? 1 : 0};
+            }
+            if (ns > kTileSlots) wide = true;
+            TileSlot ts[kTileSlots] = {};
+            int bws[kTileSlots] = {}, bhs[kTileSlots] = {};
+            uint32_t stride = 0, groups = 0;
+            for (int j = 0; j < ns && !wide; j++) {
+                if (in_w[cams[j]] % 8) {  // dword staging of boxes needs 8-aligned box columns inside the image
+                    wide = true;
+                    break;
+                }
+                const int bx0 = minx[j] & ~7, by0 = miny[j] & ~1;
+                const int bx1 = (maxx[j] + 1 + 7) & ~7, by1 = (maxy[j] + 1 + 1) & ~1;
+                bws[j] = bx1 - bx0;
+                bhs[j] = by1 - by0;
+                if (bws[j] > 256 || bhs[j] > 256) {
+                    wide = true;
+                    break;
+                }
+                ts[j].cam = (uint16_t)cams[j];
+                ts[j].bw = (uint16_t)bws[j];
+                ts[j].bh = (uint16_t)bhs[j];
+                ts[j].bx0 = (uint16_t)bx0;
+                ts[j].by0 = (uint16_t)by0;
+                stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
+                groups += (uint32_t)(bws[j] * bhs[j] / 4);
+            }
+            uint32_t lds = kTileZeroDwords, chunks = 0;
+            for (int j = 0; j < ns && !wide; j++) {
+                ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
+                lds += stride * (uint32_t)bhs[j];
+                ts[j].chunk0 = (uint16_t)chunks;
+                chunks += (uint32_t)(bws[j] * bhs[j] / 8 + 63) / 64;
+            }
+            for (int j = ns; j < kTileSlots; j++) ts[j].chunk0 = (uint16_t)std::min<uint32_t>(chunks, 255u);
+            if (chunks > 255) wide = true;
+            if (lds * 4 > (uint32_t)kTileLdsBytes) wide = true;
+            if (wide) {
+                is_wide[t] = 1;
+                wide_raw[t] = raw;
+                continue;
+            }
+            b.hdr[t] = TileHdr{(uint32_t)J.tx | ((uint32_t)J.ty << 16),
+                               (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16), groups, stride};
+            for (int j = 0; j < kTileSlots; j++) b.slots[(size_t)t * kTileSlots + j] = ts[j];
+            uint32_t* out = b.entries.data() + (size_t)t * kTilePx;
+            for (int k = 0; k < kTilePx; k++) {
+                if (!px[k].mask) continue;  // black
+                const TileSlot& sl = ts[px[k].slot];
+                const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
+                out[k] = off | ((uint32_t)(px[k].fxy & 31) << 13) | ((uint32_t)(px[k].fxy >> 5) << 18) |
+                         ((uint32_t)px[k].slot << 23) | ((uint32_t)px[k].mask << 25) |
+                         (px[k].nogain ? kEntryNoGain : 0u);
+            }
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 0; i < T; i++) th.emplace_back(work, i);
+    for (auto& x : th) x.join();
+    // staged items: the non-wide jobs in job order, compacted in place; wide jobs in job order
+    int n_items = 0;
+    for (int t = 0; t < n_jobs; t++) {
+        if (is_wide[t]) {
+            const TileJob& J = jobs[t];
+            b.wide_tiles.push_back((uint32_t)J.tx | ((uint32_t)J.ty << 16));
+            b.wide_cams.push_back((uint8_t)J.cam);
+            b.wide.insert(b.wide.end(), wide_raw[t].begin(), wide_raw[t].end());
+            continue;
+        }
+        if (n_items != t) {
+            b.hdr[n_items] = b.hdr[t];
+            std::copy(b.slots.begin() + (size_t)t * kTileSlots, b.slots.begin() + (size_t)(t + 1) * kTileSlots,
+                      b.slots.begin() + (size_t)n_items * kTileSlots);
+            std::copy(b.entries.begin() + (size_t)t * kTilePx, b.entries.begin() + (size_t)(t + 1) * kTilePx,
+                      b.entries.begin() + (size_t)n_items * kTilePx);
+        }
+        b.staged_bytes += 8.0 * b.hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes per 4-pixel group
+        n_items++;
+    }
+    b.n_items = n_items;
+    b.n_wide = (int)b.wide_tiles.size();
+    b.hdr.resize(std::max(n_items, 1));
+    b.slots.resize((size_t)std::max(n_items, 1) * kTileSlots);
+    b.entries.resize((size_t)std::max(n_items, 1) * kTilePx);
+    if (b.wide.empty()) {
+        b.wide.push_back(CompositeEntry{0, 0});
+        b.wide_tiles.push_back(0u);
+        b.wide_cams.push_back(0);
+    }
+    return b;
+}
+
+void TiledLutDev::upload(const TiledLutBuild& b) {
+    hdr.upload(b.hdr.data(), b.hdr.size());
+    slots.upload(b.slots.data(), b.slots.size());
+    entries.upload(b.entries.data(), b.entries.size());
+    wide.upload(b.wide.data(), b.wide.size());
+    wide_tiles.upload(b.wide_tiles.data(), b.wide_tiles.size());
+    wide_cams.upload(b.wide_cams.data(), b.wide_cams.size());
+    staged_bytes = b.staged_bytes;
+    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p};
+}
+
+}  // namespace octvr

@@ -89,7 +89,7 @@ def test_gpu_remap_edges(ox):
     assert np.array_equal(got, want)
 
 
-def _stitch_case(ox, name, frames_fn, gains):
+def _stitch_case(ox, name, frames_fn, gains, blend=0):
     rig, z = O.load_rig(name)
     W, H = (int(v) for v in z["out_size"])
     n = len(z["rois"])
@@ -98,15 +98,16 @@ def _stitch_case(ox, name, frames_fn, gains):
     maps1 = [z[f"map1_{i}"] for i in range(n)]
     maps2 = [z[f"map2_{i}"] for i in range(n)]
     masks = [z[f"mask_{i}"] for i in range(n)]
-    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks)
-    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True)
+    seams = [z[f"seam_{i}"] for i in range(n)]
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks, seams)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True)
     import torch
     out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
     m.stitch([_cuda(f) for f in frames], out, gains=gains)
     torch.cuda.synchronize()
     g_gpu = m.gains()
     want, g_orc = O.stitch_frame(frames, sizes, z["rois"].tolist(), maps1, maps2, masks, W, H, enable_gain=True,
-                                 gains=gains)
+                                 gains=gains, blend=blend, seams=seams, threads=8)
     return out.cpu().numpy(), want, np.array(g_gpu), g_orc
 
 
@@ -325,3 +326,17 @@ def test_gpu_create_masks_scaled_vs_oracle(ox, out_w):
     for i in range(len(res)):
         got = mt.input(i)[4]
         assert np.array_equal(got, want[i]), (i, int((got != want[i]).sum()))
+
+
+# ---- multi-band blend (MultiBandGPUBlender): bit-exact against the oracle -----------
+@pytest.mark.parametrize("blend", [4, 16, 128])
+@pytest.mark.parametrize("name", RIGS)
+def test_gpu_multiband_bit_exact(ox, name, blend):
+    from octvr_amd import synthetic
+    n = len(O.load_rig(name)[1]["rois"])
+    gains = [1.0 + 0.011 * k * (-1) ** k for k in range(n)]
+    for frames_fn, g in ((lambda w, h, s: O.rand_img(w, h * 3 // 2, 1, s), gains), (synthetic.smooth_yuv_frame, None)):
+        got, want, g_gpu, g_orc = _stitch_case(ox, name, frames_fn, g, blend=blend)
+        np.testing.assert_array_equal(g_gpu, g_orc)
+        d = got != want
+        assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
