@@ -15,6 +15,7 @@ timed on this host).
 """
 import argparse
 import json
+import math
 import os
 import subprocess
 import sys
@@ -57,22 +58,25 @@ def host_threads():
     return max(1, min(int(n) if n else avail, avail, 64))
 
 
-def cpu_baseline(mt, frames_np, sizes, W, H):
+def cpu_baseline(mt, frames_np, sizes, W, H, blend=0):
     """The reference CPU path restated by the oracle (YUV->RGBA, fixed-point cv::remap of every
-    camera over its full ROI, gain feed + apply, copyTo(mask), RGB->YUV420P) on this host."""
+    camera over its full ROI, gain feed + apply, copyTo(mask) or the multi-band blender,
+    RGB->YUV420P) on this host."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O  # test infrastructure: used only as the timed CPU baseline
-    rois, m1s, m2s, masks = [], [], [], []
+    rois, m1s, m2s, masks, seams = [], [], [], [], []
     for i in range(len(sizes)):
-        roi, m1, m2, mk, _ = mt.input(i)
-        rois.append(roi); m1s.append(m1); m2s.append(m2); masks.append(mk)
+        roi, m1, m2, mk, sm = mt.input(i)
+        rois.append(roi); m1s.append(m1); m2s.append(m2); masks.append(mk); seams.append(sm)
     T = host_threads()
     t0 = time.perf_counter()
-    O.stitch_frame(frames_np, sizes, rois, m1s, m2s, masks, W, H, enable_gain=True, gains=None, threads=T)
+    O.stitch_frame(frames_np, sizes, rois, m1s, m2s, masks, W, H, enable_gain=True, gains=None, threads=T,
+                   blend=blend, seams=seams if blend > 0 else None)
     dt = time.perf_counter() - t0
     return {"value": round(W * H / 1e6 / dt, 3), "unit": "MP/s", "cores": T, "kind": "port",
-            "sample": "one full %dx%d frame (%d cameras, gain estimated) through oracle/octvr_oracle.c, %.2f s, "
-                      "host CPU: %s" % (W, H, len(sizes), dt, cpu_model())}
+            "sample": "one full %dx%d frame (%d cameras, gain estimated%s) through the oracle (oracle/*.c), "
+                      "%.2f s, host CPU: %s" % (W, H, len(sizes), ", multi-band blend=%d" % blend if blend else "",
+                                                 dt, cpu_model())}
 
 
 def main():
@@ -94,8 +98,11 @@ def main():
     dev = local_rank
 
     rig, W, H, sizes = synthetic.CONFIGS[args.config]()
+    blend = synthetic.BLEND[args.config]
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=True, device=dev)
-    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True, device=dev)
+    if blend > 0:
+        mt.create_masks(dev)  # MapperTemplate::create_masks (DistanceSeamFinder), as octvr_dump does
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, device=dev)
     # each rank stitches an independent rig instance: frames seeded by (rank, camera)
     frames_np = [synthetic.yuv_frame(w, h, 1000 * (rank + 1) + i) for i, (w, h) in enumerate(sizes)]
     frames = [torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]
@@ -140,6 +147,9 @@ def main():
     for i in range(len(sizes)):
         n_valid += int((mt.input(i)[3] > 0).sum())
     survey_b_alg = 1.5 * sum(w * h for w, h in sizes) + 9.0 * n_valid + 1.5 * frame_px
+    if blend > 0:  # SURVEY.md §8d multi-band term: s16x3 Laplacian levels 1..B + f32 weight pyramids
+        f = sum(4.0 ** -l for l in range(1, int(math.ceil(math.log(blend) / math.log(2.)) - 1) + 1))
+        survey_b_alg += 12.0 * f * frame_px + 4.0 * f * n_valid
 
     result = {
         "metric": "stitched megapixels/sec (6x4K->8K equirect)",
@@ -155,12 +165,15 @@ def main():
         "dtype": "u8",
         "data": "synthetic (splitmix64 YUV420P frames, SURVEY.md §8d rig)",
         "config": {"workload": "%s: %d x %dx%d fullframe_fisheye -> %dx%d equirect, remap + gain (estimated per "
-                               "frame) + no-blend composite, YUV420P in/out" % (
-                                   args.config, len(sizes), sizes[0][0], sizes[0][1], W, H),
+                               "frame) + %s, YUV420P in/out" % (
+                                   args.config, len(sizes), sizes[0][0], sizes[0][1], W, H,
+                                   "multi-band blend=%d (%d bands)" % (blend, int(math.ceil(math.log(blend) / math.log(2.)) - 1))
+                                   if blend > 0 else "no-blend composite"),
                    "rigs_per_gpu": 1, "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                     "kernel": "stitch_kernel", "kernel_us": round(avg_kernel_s * 1e6, 2),
+                     "kernel": "multiband sequence (remap, pyrDown, blend levels)" if blend > 0 else "stitch_kernel",
+                     "kernel_us": round(avg_kernel_s * 1e6, 2),
                      "bytes_per_launch": bytes_per_launch,
                      "survey_b_alg_bytes": survey_b_alg,
                      "survey_b_alg_frac_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
@@ -168,7 +181,7 @@ def main():
         "mapper": m.info(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H)
+        result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:

@@ -156,6 +156,9 @@ hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W,
 // fly from 3x3 source taps per output quad through per-row / per-column tap tables (UpQuad), which
 // encode pyr_up.cu's borders (abs, then clamp) and its 8-row-block quirk.
 constexpr int kMbMaxBands = 10;
+// pyrUp source patch of one 128x8 tile: <= 8 rows (4 quad rows, the row quirk, any block phase)
+// by <= 72 columns (64 quad columns + borders), staged in LDS
+constexpr int kUpPatchRows = 8, kUpPatchCols = 72;
 struct UpQuad {          // one quad row (or column) of a pyrUp output
     uint16_t idx[3];      // source rows (cols) of the 3 union taps, clamped, local to the coarser level
     uint8_t w0[3], w1[3]; // integer weights of the quad's first / second row (col) over them
@@ -169,6 +172,8 @@ struct MbCamLevel {       // one camera at one level
     const void* weight;    // level 0: u8 seam mask (pitch w), else f32 Gaussian weight (pitch w)
     const UpQuad* up_rows; // pyrUp taps into this camera's next level, by level-grid quad row
     const UpQuad* up_cols; // ... by level-grid quad column
+    const int32_t* up_r0;  // per tile row / column: origin of the tile's staged source patch
+    const int32_t* up_c0;
 };
 
 // Level-0 pyramid images as the composite kernels' RGBA sink.
@@ -192,10 +197,12 @@ struct MbBlendArgs {
     const MbCamLevel* cams_next;    // level + 1 (NULL at the top)
     const uint8_t* g;               // this level's pyramid allocation
     const uint8_t* g_next;          // level + 1 allocation
-    const int16_t* r_next;          // collapsed level + 1 (s16x4, pitch 2 * W_next... see W_next)
-    int W_next;
+    const int16_t* r_next;          // collapsed level + 1 (s16x4, W_next x H_next)
+    int W_next, H_next;
     const UpQuad* rup_rows;         // pyrUp taps of the collapse (level grid, camera independent)
     const UpQuad* rup_cols;
+    const int32_t* rup_r0;          // per tile row / column: origin of the staged collapse patch
+    const int32_t* rup_c0;
     int16_t* r_out;                 // level > 0: collapsed level (s16x4, pitch 4 * W shorts)
     uint8_t* out;                   // level 0: YUV420P output frame
     int64_t out_pitch;
@@ -205,10 +212,10 @@ struct MbBlendArgs {
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s);
 // Build time: K4 pyrDown<float, BrdReflect101> with nvcc's FMA contraction (pyr_down.cu:55-192).
 hipError_t launch_pyr_down_f32(const float* src, int sw, int sh, float* dst, int dw, int dh, hipStream_t s);
-// Build time: OR bit `cam` into tile_cams[] of every level-grid tile where the camera's weight is
-// non-zero (level 0: u8 seam, else f32).
-hipError_t launch_tile_activity(const void* weight, int is_u8, int w, int h, int ox, int oy, int tiles_x, int cam,
-                                uint32_t* tile_cams, hipStream_t s);
+// Build time: blocks[by * bx_n + bx] = 1 for every 8x8 block of the level grid where the camera's
+// weight is non-zero (level 0: u8 seam, else f32).
+hipError_t launch_block_activity(const void* weight, int is_u8, int w, int h, int ox, int oy, int bx_n, uint8_t* blocks,
+                                 hipStream_t s);
 
 hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, int cn, const float* map1,
                            const float* map2, int mw, int mh, int64_t mpitch, float scale_x, float scale_y,

@@ -51,29 +51,46 @@ __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ 
     const int xo = tx * kTileW - c.ox, yo = ty * kTileH - c.oy;
     const int sx0 = 2 * xo - 2, sy0 = 2 * yo - 2;
     const uint8_t* src = g_prev + p.g_off;
-    for (int i = tid; i < kDnRows * kDnCols; i += 256) {
-        const int r = i / kDnCols, q = i - r * kDnCols;
-        const int sy = min(max(sy0 + r, 0), p.h - 1), sx = min(max(sx0 + q, 0), p.w - 1);
-        s_src[i] = *reinterpret_cast<const uint32_t*>(src + (int64_t)sy * p.g_pitch + (int64_t)sx * 4);
+    // staging: lane t loads column t of each of the 20 rows (lanes 0-3 also columns 256-259), all
+    // loads in flight before the first LDS write
+    {
+        const int sxa = min(max(sx0 + tid, 0), p.w - 1), sxb = min(max(sx0 + kDnCols - 4 + (tid & 3), 0), p.w - 1);
+        uint32_t va[kDnRows], vb[kDnRows];
+#pragma unroll
+        for (int r = 0; r < kDnRows; r++) {
+            const uint8_t* row = src + (int64_t)min(max(sy0 + r, 0), p.h - 1) * p.g_pitch;
+            va[r] = *reinterpret_cast<const uint32_t*>(row + (int64_t)sxa * 4);
+            vb[r] = *reinterpret_cast<const uint32_t*>(row + (int64_t)sxb * 4);
+        }
+#pragma unroll
+        for (int r = 0; r < kDnRows; r++) {
+            s_src[r * kDnCols + tid] = va[r];
+            if (tid < 4) s_src[r * kDnCols + kDnCols - 4 + tid] = vb[r];
+        }
     }
     __syncthreads();
-    for (int i = tid; i < kTileH * kDnCols; i += 256) {
-        const int r = i / kDnCols, q = i - r * kDnCols;
-        const uint32_t* col = s_src + (2 * r) * kDnCols + q;
-        uint32_t acc[3] = {0u, 0u, 0u};
-        const uint32_t w[5] = {1u, 4u, 6u, 4u, 1u};
+    const uint32_t w5[5] = {1u, 4u, 6u, 4u, 1u};
 #pragma unroll
-        for (int j = 0; j < 5; j++) {
-            const uint32_t v = col[j * kDnCols];
+    for (int r = 0; r < kTileH; r++) {
 #pragma unroll
-            for (int ch = 0; ch < 3; ch++) acc[ch] += w[j] * ch_of(v, ch);
+        for (int half = 0; half < 2; half++) {
+            const int q = half ? kDnCols - 4 + (tid & 3) : tid;
+            if (half && tid >= 4) continue;
+            const uint32_t* col = s_src + (2 * r) * kDnCols + q;
+            uint32_t acc[3] = {0u, 0u, 0u};
+#pragma unroll
+            for (int j = 0; j < 5; j++) {
+                const uint32_t v = col[j * kDnCols];
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) acc[ch] += w5[j] * ch_of(v, ch);
+            }
+            s_v[r * kDnCols + q] = make_uint2(acc[0] | (acc[1] << 16), acc[2]);
         }
-        s_v[i] = make_uint2(acc[0] | (acc[1] << 16), acc[2]);
     }
     __syncthreads();
     const int qx = tid & 63, qy = tid >> 6;
-    const int xl = xo + 2 * qx, yl = yo + 2 * qy;  // quad origin, camera-local (even: whole quads)
-    if (xl < 0 || yl < 0 || xl >= c.w || yl >= c.h) return;
+    const int xl = xo + 2 * qx, yl = yo + 2 * qy;  // quad origin, camera-local (any parity at the top level)
+    if (xl + 1 < 0 || yl + 1 < 0 || xl >= c.w || yl >= c.h) return;
     uint32_t px[4];
 #pragma unroll
     for (int p4 = 0; p4 < 4; p4++) {
@@ -90,9 +107,12 @@ __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ 
         px[p4] = (uint32_t)min(rne_shr<8>((int)a0), 255) | ((uint32_t)min(rne_shr<8>((int)a1), 255) << 8) |
                  ((uint32_t)min(rne_shr<8>((int)a2), 255) << 16);
     }
-    uint8_t* dst = g_l + c.g_off + (int64_t)yl * c.g_pitch + (int64_t)xl * 4;
-    *reinterpret_cast<uint2*>(dst) = make_uint2(px[0], px[1]);
-    *reinterpret_cast<uint2*>(dst + c.g_pitch) = make_uint2(px[2], px[3]);
+#pragma unroll
+    for (int p4 = 0; p4 < 4; p4++) {  // per pixel: odd-sized top levels end mid-quad
+        const int px_ = xl + (p4 & 1), py_ = yl + (p4 >> 1);
+        if (px_ < 0 || py_ < 0 || px_ >= c.w || py_ >= c.h) continue;
+        *reinterpret_cast<uint32_t*>(g_l + c.g_off + (int64_t)py_ * c.g_pitch + (int64_t)px_ * 4) = px[p4];
+    }
 }
 
 hipError_t launch_mb_down(const uint2* items, int n_items, const MbCamLevel* cams_l, const MbCamLevel* cams_prev,
@@ -116,14 +136,21 @@ struct Up9 {
     int s[4][3];  // per quad pixel, per channel: the integer tap sum (scale 1/64)
 };
 
-// 9 source taps (u8x4 from G, or s16x4 from R) of a quad -> integer pyrUp sums for its 4 pixels.
-template <class LOAD>
-__device__ __forceinline__ void up_quad(const UpQuad& ur, const UpQuad& uc, LOAD load, Up9& o) {
+// pyrUp sums of a quad from a staged LDS patch (rows r0.., cols c0.. of the coarser level):
+// 3 x 3 union taps, per-pixel integer weights over them (UpQuad).
+template <class T, class UNPACK>
+__device__ __forceinline__ void up_quad_lds(const UpQuad& ur, const UpQuad& uc, int r0, int c0, const T* patch,
+                                            UNPACK unpack, Up9& o) {
     int v[3][3][3];  // [row][col][ch]
 #pragma unroll
-    for (int j = 0; j < 3; j++)
+    for (int j = 0; j < 3; j++) {
+        const int pr = min(max((int)ur.idx[j] - r0, 0), kUpPatchRows - 1);  // zero-weight taps may lie outside
 #pragma unroll
-        for (int k = 0; k < 3; k++) load(ur.idx[j], uc.idx[k], v[j][k]);
+        for (int k = 0; k < 3; k++) {
+            const int pc = min(max((int)uc.idx[k] - c0, 0), kUpPatchCols - 1);
+            unpack(patch[pr * kUpPatchCols + pc], v[j][k]);
+        }
+    }
 #pragma unroll
     for (int pc = 0; pc < 2; pc++) {
         const uint8_t* wx = pc ? uc.w1 : uc.w0;
@@ -141,7 +168,35 @@ __device__ __forceinline__ void up_quad(const UpQuad& ur, const UpQuad& uc, LOAD
     }
 }
 
+// Cooperative load of an 8 x 72 patch (rows r0.., cols c0.., clamped to the source) into registers:
+// entries tid, tid + 256, tid + 512 (< 576).
+constexpr int kPatchN = kUpPatchRows * kUpPatchCols;
+template <class T>
+struct PatchRegs {
+    T v[3];
+};
+template <class T>
+__device__ __forceinline__ void patch_issue(const uint8_t* base, int64_t pitch, int rows, int cols, int r0, int c0,
+                                            PatchRegs<T>& o) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int i = min((int)threadIdx.x + 256 * k, kPatchN - 1);
+        const int r = min(r0 + i / kUpPatchCols, rows - 1), c = min(c0 + i % kUpPatchCols, cols - 1);
+        o.v[k] = *reinterpret_cast<const T*>(base + (int64_t)r * pitch + (int64_t)c * sizeof(T));
+    }
+}
+template <class T>
+__device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const int i = (int)threadIdx.x + 256 * k;
+        if (i < kPatchN) lds[i] = o.v[k];
+    }
+}
+
 __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
+    __shared__ uint2 s_r[kPatchN];     // collapsed coarser level (s16x4)
+    __shared__ uint32_t s_g[kPatchN];  // the current camera's coarser Gaussian level (u8x4)
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
     const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
@@ -150,6 +205,15 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
     bool valid[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) valid[p] = (x + (p & 1)) < a.W && (y + (p >> 1)) < a.H;
+    // the collapse patch first: its loads overlap the camera loop
+    PatchRegs<uint2> rp;
+    int rr0 = 0, rc0 = 0;
+    if (!top) {
+        rr0 = a.rup_r0[ty];
+        rc0 = a.rup_c0[tx];
+        patch_issue<uint2>(reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, a.H_next, a.W_next, rr0,
+                           rc0, rp);
+    }
     int D[4][3];
     float wsum[4];
 #pragma unroll
@@ -164,42 +228,45 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
         m &= m - 1;
         const MbCamLevel c = a.cams[n];
         const int xl = x - c.ox, yl = y - c.oy;  // camera-local quad origin (any parity)
+        // all of this camera's loads at once: weights, G, and the coarser-level patch
         float w[4];
-        bool any = false;
+        uint32_t gv[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const int px = xl + (p & 1), py = yl + (p >> 1);
             const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
-            float wv = 0.f;
-            if (in) {
-                const int64_t k = (int64_t)py * c.w + px;
-                // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
-                wv = a.level == 0 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
-                                  : static_cast<const float*>(c.weight)[k];
-            }
-            w[p] = wv;
-            any |= wv != 0.f;
+            const int cx = min(max(px, 0), c.w - 1), cy = min(max(py, 0), c.h - 1);
+            const int64_t k = (int64_t)cy * c.w + cx;
+            // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
+            const float wv = a.level == 0 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
+                                          : static_cast<const float*>(c.weight)[k];
+            w[p] = in ? wv : 0.f;
+            gv[p] = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + cx * 4);
         }
-        if (!any) continue;
-        int g[4][3];
-#pragma unroll
-        for (int p = 0; p < 4; p++) {
-            const int px = min(max(xl + (p & 1), 0), c.w - 1), py = min(max(yl + (p >> 1), 0), c.h - 1);
-            const uint32_t v = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)py * c.g_pitch + px * 4);
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) g[p][ch] = (int)ch_of(v, ch);
-        }
+        PatchRegs<uint32_t> gp;
+        int gr0 = 0, gc0 = 0;
         if (!top) {
             const MbCamLevel cn = a.cams_next[n];
-            const uint8_t* gn = a.g_next + cn.g_off;
-            Up9 u;
-            up_quad(c.up_rows[y >> 1], c.up_cols[x >> 1],
-                    [&](int r, int col, int (&o)[3]) {
-                        const uint32_t v = *reinterpret_cast<const uint32_t*>(gn + (int64_t)r * cn.g_pitch + col * 4);
+            gr0 = c.up_r0[ty];
+            gc0 = c.up_c0[tx];
+            patch_issue<uint32_t>(a.g_next + cn.g_off, cn.g_pitch, cn.h, cn.w, gr0, gc0, gp);
+            __syncthreads();  // the previous camera's patch readers are done
+            patch_store(gp, s_g);
+            __syncthreads();
+        }
+        int g[4][3];
 #pragma unroll
-                        for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
-                    },
-                    u);
+        for (int p = 0; p < 4; p++)
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) g[p][ch] = (int)ch_of(gv[p], ch);
+        if (!top) {
+            Up9 u;
+            up_quad_lds(c.up_rows[y >> 1], c.up_cols[x >> 1], gr0, gc0, s_g,
+                        [](uint32_t v, int (&o)[3]) {
+#pragma unroll
+                            for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
+                        },
+                        u);
 #pragma unroll
             for (int p = 0; p < 4; p++)
 #pragma unroll
@@ -225,17 +292,16 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
             R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf((float)D[p][ch] * rcp), -32768.f, 32767.f);
     }
     if (!top) {
+        patch_store(rp, s_r);
+        __syncthreads();
         Up9 u;
-        const int16_t* rn = a.r_next;
-        const int wn = a.W_next;
-        up_quad(a.rup_rows[y >> 1], a.rup_cols[x >> 1],
-                [&](int r, int col, int (&o)[3]) {
-                    const uint2 v = *reinterpret_cast<const uint2*>(rn + ((int64_t)r * wn + col) * 4);
-                    o[0] = (int)(int16_t)(v.x & 0xFFFFu);
-                    o[1] = (int)(int16_t)(v.x >> 16);
-                    o[2] = (int)(int16_t)(v.y & 0xFFFFu);
-                },
-                u);
+        up_quad_lds(a.rup_rows[y >> 1], a.rup_cols[x >> 1], rr0, rc0, s_r,
+                    [](uint2 v, int (&o)[3]) {
+                        o[0] = (int)(int16_t)(v.x & 0xFFFFu);
+                        o[1] = (int)(int16_t)(v.x >> 16);
+                        o[2] = (int)(int16_t)(v.y & 0xFFFFu);
+                    },
+                    u);
 #pragma unroll
         for (int p = 0; p < 4; p++)
 #pragma unroll
@@ -315,10 +381,10 @@ hipError_t launch_pyr_down_f32(const float* src, int sw, int sh, float* dst, int
     return hipGetLastError();
 }
 
-// Build time: which level-grid tiles hold a non-zero weight of camera `cam`.  A lane scans 8
-// pixels of one row that share a tile (level-grid x multiple of 8) and sets the bit once.
-__global__ void __launch_bounds__(256) tile_activity_kernel(const void* weight, int is_u8, int w, int h, int ox, int oy,
-                                                            int tiles_x, int cam, uint32_t* tile_cams) {
+// Build time: which 8x8 blocks of the level grid hold a non-zero weight of one camera.  A lane
+// scans the 8 pixels of one block row and marks the block (benign duplicate stores of 1).
+__global__ void __launch_bounds__(256) block_activity_kernel(const void* weight, int is_u8, int w, int h, int ox,
+                                                             int oy, int bx_n, uint8_t* blocks) {
     const int gx_n = (w + 7 + (ox & 7)) / 8 + 1;  // 8-pixel groups per row on the level grid
     const int64_t total = (int64_t)gx_n * h;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
@@ -331,20 +397,16 @@ __global__ void __launch_bounds__(256) tile_activity_kernel(const void* weight, 
             const int64_t k = (int64_t)yl * w + xl;
             nz |= is_u8 ? static_cast<const uint8_t*>(weight)[k] != 0 : static_cast<const float*>(weight)[k] != 0.f;
         }
-        if (nz) {
-            const int gy = yl + oy;
-            atomicOr(&tile_cams[(gy / kTileH) * tiles_x + gx0 / kTileW], 1u << cam);
-        }
+        if (nz) blocks[(int64_t)((yl + oy) >> 3) * bx_n + (gx0 >> 3)] = 1;
     }
 }
 
-hipError_t launch_tile_activity(const void* weight, int is_u8, int w, int h, int ox, int oy, int tiles_x, int cam,
-                                uint32_t* tile_cams, hipStream_t s) {
+hipError_t launch_block_activity(const void* weight, int is_u8, int w, int h, int ox, int oy, int bx_n, uint8_t* blocks,
+                                 hipStream_t s) {
     if (w <= 0 || h <= 0) return hipSuccess;
     const int64_t total = (int64_t)((w + 7 + (ox & 7)) / 8 + 1) * h;
-    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 8);
-    hipLaunchKernelGGL(tile_activity_kernel, dim3(blocks), dim3(256), 0, s, weight, is_u8, w, h, ox, oy, tiles_x, cam,
-                       tile_cams);
+    const int blocks_n = (int)std::min<int64_t>((total + 255) / 256, 256 * 8);
+    hipLaunchKernelGGL(block_activity_kernel, dim3(blocks_n), dim3(256), 0, s, weight, is_u8, w, h, ox, oy, bx_n, blocks);
     return hipGetLastError();
 }
 

@@ -55,6 +55,8 @@ class MultiBand {
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
         int rup_rows = 0;
+        DevBuf<int32_t> up_org;         // per camera: staged-patch origins per tile row, then per tile col
+        DevBuf<int32_t> rup_org;        // collapse: the same
         DevBuf<uint2> down_items;       // level > 0
         int n_down = 0;
         DevBuf<int16_t> R;              // level > 0: collapsed level, s16x4
@@ -124,6 +126,22 @@ std::vector<UpQuad> up_table(int n_grid, int off, int n_local, int n_src, bool r
         }
     }
     return t;
+}
+
+// Origin of each tile's staged pyrUp patch (kernels.hpp kUpPatchRows x kUpPatchCols): the smallest
+// source index any weighted tap of the tile's quads reads; the span must fit the patch.
+std::vector<int32_t> patch_origins(const std::vector<UpQuad>& t, int quads_per_tile, int n_tiles, int limit) {
+    std::vector<int32_t> o(n_tiles, 0);
+    for (int k = 0; k < n_tiles; k++) {
+        int lo = INT32_MAX, hi = -1;
+        for (int q = k * quads_per_tile; q < std::min((k + 1) * quads_per_tile, (int)t.size()); q++)
+            for (int j = 0; j < 3; j++)
+                if (t[q].w0[j] | t[q].w1[j]) lo = std::min(lo, (int)t[q].idx[j]), hi = std::max(hi, (int)t[q].idx[j]);
+        if (hi < 0) continue;
+        REQUIRE(hi - lo < limit, "pyrUp patch of a tile exceeds the staged size");
+        o[k] = lo;
+    }
+    return o;
 }
 
 struct Bitmap {
@@ -256,19 +274,28 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             }
         }
     }
-    // ---- tile activity ----------------------------------------------------------------------
+    // ---- weight activity per 8x8 block, then per tile (bit n: camera n) -------------------------
+    constexpr int kBlk = 8;
+    std::vector<std::vector<std::vector<uint8_t>>> act(B + 1);  // [level][camera][block]
     for (int l = 0; l <= B; l++) {
         auto& L = M.lv[l];
-        const size_t nt = (size_t)L.tx_n * L.ty_n;
-        L.tile_cams.alloc(nt);
-        HIP_CHECK(hipMemset(L.tile_cams.p, 0, nt * sizeof(uint32_t)));
+        const int bx_n = (L.W + kBlk - 1) / kBlk, by_n = (L.H + kBlk - 1) / kBlk;
+        DevBuf<uint8_t> blk;
+        blk.alloc((size_t)bx_n * by_n);
+        act[l].resize(n);
+        L.tile_cams_h.assign((size_t)L.tx_n * L.ty_n, 0u);
         for (int i = 0; i < n; i++) {
             const auto& c = L.cams_h[i];
-            HIP_CHECK(launch_tile_activity(c.weight, l == 0, c.w, c.h, c.ox, c.oy, L.tx_n, i, L.tile_cams.p, nullptr));
+            HIP_CHECK(hipMemset(blk.p, 0, blk.n));
+            HIP_CHECK(launch_block_activity(c.weight, l == 0, c.w, c.h, c.ox, c.oy, bx_n, blk.p, nullptr));
+            act[l][i].resize(blk.n);
+            HIP_CHECK(hipMemcpy(act[l][i].data(), blk.p, blk.n, hipMemcpyDeviceToHost));
+            for (int by = 0; by < by_n; by++)
+                for (int bx = 0; bx < bx_n; bx++)
+                    if (act[l][i][(size_t)by * bx_n + bx])
+                        L.tile_cams_h[(size_t)(by * kBlk / kTileH) * L.tx_n + bx * kBlk / kTileW] |= 1u << i;
         }
-        HIP_CHECK(hipDeviceSynchronize());
-        L.tile_cams_h.resize(nt);
-        HIP_CHECK(hipMemcpy(L.tile_cams_h.data(), L.tile_cams.p, nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        L.tile_cams.upload(L.tile_cams_h.data(), L.tile_cams_h.size());
     }
     // ---- pyrUp tap tables -------------------------------------------------------------------
     std::vector<std::vector<std::vector<UpQuad>>> ur(B), uc(B);  // [level][camera]
@@ -281,77 +308,110 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         std::vector<size_t> ro(n), co(n);
         for (int i = 0; i < n; i++) {
             const auto& c = L.cams_h[i];
-            ur[l][i] = up_table(L.H, c.oy, c.h, Ln.cams_h[i].h, true);
-            uc[l][i] = up_table(L.W, c.ox, c.w, Ln.cams_h[i].w, false);
+            // tables cover the whole tile grid: lanes of the last tile row / column past the level
+            // size index them too (their weights are 0, their taps clamped in range)
+            ur[l][i] = up_table(L.ty_n * kTileH, c.oy, c.h, Ln.cams_h[i].h, true);
+            uc[l][i] = up_table(L.tx_n * kTileW, c.ox, c.w, Ln.cams_h[i].w, false);
             ro[i] = all.size();
             all.insert(all.end(), ur[l][i].begin(), ur[l][i].end());
             co[i] = all.size();
             all.insert(all.end(), uc[l][i].begin(), uc[l][i].end());
         }
         L.up.upload(all.data(), all.size());
+        std::vector<int32_t> org;
+        std::vector<size_t> oo(n);
         for (int i = 0; i < n; i++) {
             L.cams_h[i].up_rows = L.up.p + ro[i];
             L.cams_h[i].up_cols = L.up.p + co[i];
+            oo[i] = org.size();
+            auto r0 = patch_origins(ur[l][i], kTileH / 2, L.ty_n, kUpPatchRows);
+            auto c0 = patch_origins(uc[l][i], kTileW / 2, L.tx_n, kUpPatchCols);
+            org.insert(org.end(), r0.begin(), r0.end());
+            org.insert(org.end(), c0.begin(), c0.end());
         }
-        std::vector<UpQuad> rr = up_table(L.H, 0, L.H, Ln.H, true), rc = up_table(L.W, 0, L.W, Ln.W, false);
+        L.up_org.upload(org.data(), org.size());
+        for (int i = 0; i < n; i++) {
+            L.cams_h[i].up_r0 = L.up_org.p + oo[i];
+            L.cams_h[i].up_c0 = L.up_org.p + oo[i] + L.ty_n;
+        }
+        std::vector<UpQuad> rr = up_table(L.ty_n * kTileH, 0, L.H, Ln.H, true),
+                            rc = up_table(L.tx_n * kTileW, 0, L.W, Ln.W, false);
+        {
+            auto r0 = patch_origins(rr, kTileH / 2, L.ty_n, kUpPatchRows);
+            auto c0 = patch_origins(rc, kTileW / 2, L.tx_n, kUpPatchCols);
+            r0.insert(r0.end(), c0.begin(), c0.end());
+            L.rup_org.upload(r0.data(), r0.size());
+        }
         L.rup_rows = (int)rr.size();
         rr.insert(rr.end(), rc.begin(), rc.end());
         L.rup.upload(rr.data(), rr.size());
     }
-    // ---- required tiles per camera and level ---------------------------------------------------
-    std::vector<std::vector<Bitmap>> req(B + 1, std::vector<Bitmap>(n));
+    // ---- required 8x8 blocks per camera and level, then tiles ------------------------------------
+    // need(l) = weight blocks(l) + pyrUp support of weight blocks(l-1) + pyrDown support of need(l+1)
+    std::vector<std::vector<Bitmap>> req(B + 1, std::vector<Bitmap>(n));  // tiles
+    std::vector<std::vector<uint8_t>> need_next(n);                       // blocks of level l + 1
     for (int l = B; l >= 0; l--) {
         auto& L = M.lv[l];
+        const int bx_n = (L.W + kBlk - 1) / kBlk, by_n = (L.H + kBlk - 1) / kBlk;
         for (int i = 0; i < n; i++) {
-            Bitmap& R = req[l][i];
-            R.init(L.tx_n, L.ty_n);
             const auto& c = L.cams_h[i];
-            for (size_t t = 0; t < R.b.size(); t++)
-                if (L.tile_cams_h[t] >> i & 1u) R.b[t] = 1;
-            if (l >= 1) {  // pyrUp support of the finer level's weight tiles
+            std::vector<uint8_t> need = act[l][i];
+            auto mark = [&](int x0, int y0, int x1, int y1) {  // level-grid pixel rectangle, inclusive
+                x0 = std::max(x0, 0), y0 = std::max(y0, 0);
+                x1 = std::min(x1, bx_n * kBlk - 1), y1 = std::min(y1, by_n * kBlk - 1);
+                for (int by = y0 / kBlk; by <= y1 / kBlk; by++)
+                    for (int bx = x0 / kBlk; bx <= x1 / kBlk; bx++) need[(size_t)by * bx_n + bx] = 1;
+            };
+            if (l >= 1) {  // pyrUp support of the finer level's weight blocks (8x8 px = 4x4 quads)
                 const auto& Lf = M.lv[l - 1];
-                for (int ty = 0; ty < Lf.ty_n; ty++)
-                    for (int tx = 0; tx < Lf.tx_n; tx++) {
-                        if (!(Lf.tile_cams_h[(size_t)ty * Lf.tx_n + tx] >> i & 1u)) continue;
+                const int fbx = (Lf.W + kBlk - 1) / kBlk, fby = (Lf.H + kBlk - 1) / kBlk;
+                for (int by = 0; by < fby; by++)
+                    for (int bx = 0; bx < fbx; bx++) {
+                        if (!act[l - 1][i][(size_t)by * fbx + bx]) continue;
                         int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
-                        for (int q = ty * kTileH / 2; q < std::min((ty + 1) * kTileH / 2, (int)ur[l - 1][i].size()); q++)
-                            for (int j = 0; j < 3; j++) {
-                                r0 = std::min(r0, (int)ur[l - 1][i][q].idx[j]);
-                                r1 = std::max(r1, (int)ur[l - 1][i][q].idx[j]);
-                            }
-                        for (int q = tx * kTileW / 2; q < std::min((tx + 1) * kTileW / 2, (int)uc[l - 1][i].size()); q++)
-                            for (int j = 0; j < 3; j++) {
-                                c0 = std::min(c0, (int)uc[l - 1][i][q].idx[j]);
-                                c1 = std::max(c1, (int)uc[l - 1][i][q].idx[j]);
-                            }
-                        if (r1 >= 0 && c1 >= 0) R.mark(c0 + c.ox, r0 + c.oy, c1 + c.ox, r1 + c.oy);
+                        for (int q = by * kBlk / 2; q < (by + 1) * kBlk / 2; q++) {
+                            const UpQuad& u = ur[l - 1][i][q];
+                            for (int j = 0; j < 3; j++)
+                                if (u.w0[j] | u.w1[j]) r0 = std::min(r0, (int)u.idx[j]), r1 = std::max(r1, (int)u.idx[j]);
+                        }
+                        for (int q = bx * kBlk / 2; q < (bx + 1) * kBlk / 2; q++) {
+                            const UpQuad& u = uc[l - 1][i][q];
+                            for (int j = 0; j < 3; j++)
+                                if (u.w0[j] | u.w1[j]) c0 = std::min(c0, (int)u.idx[j]), c1 = std::max(c1, (int)u.idx[j]);
+                        }
+                        if (r1 >= 0 && c1 >= 0) mark(c0 + c.ox, r0 + c.oy, c1 + c.ox, r1 + c.oy);
                     }
             }
-            if (l < B) {  // pyrDown support of the coarser level's required tiles
+            if (l < B) {  // pyrDown support of the coarser level's required blocks
                 const auto& Lc = M.lv[l + 1];
                 const auto& cc = Lc.cams_h[i];
-                const Bitmap& Rc = req[l + 1][i];
-                for (int ty = 0; ty < Lc.ty_n; ty++)
-                    for (int tx = 0; tx < Lc.tx_n; tx++) {
-                        if (!Rc.b[(size_t)ty * Lc.tx_n + tx]) continue;
-                        const int xa = std::max(tx * kTileW - cc.ox, 0), xb = std::min((tx + 1) * kTileW - 1 - cc.ox, cc.w - 1);
-                        const int ya = std::max(ty * kTileH - cc.oy, 0), yb = std::min((ty + 1) * kTileH - 1 - cc.oy, cc.h - 1);
+                const int cbx = (Lc.W + kBlk - 1) / kBlk, cby = (Lc.H + kBlk - 1) / kBlk;
+                for (int by = 0; by < cby; by++)
+                    for (int bx = 0; bx < cbx; bx++) {
+                        if (!need_next[i][(size_t)by * cbx + bx]) continue;
+                        const int xa = std::max(bx * kBlk - cc.ox, 0), xb = std::min((bx + 1) * kBlk - 1 - cc.ox, cc.w - 1);
+                        const int ya = std::max(by * kBlk - cc.oy, 0), yb = std::min((by + 1) * kBlk - 1 - cc.oy, cc.h - 1);
                         if (xa > xb || ya > yb) continue;
                         const int sx0 = std::max(2 * xa - 2, 0), sx1 = std::min(2 * xb + 2, c.w - 1);
                         const int sy0 = std::max(2 * ya - 2, 0), sy1 = std::min(2 * yb + 2, c.h - 1);
-                        R.mark(sx0 + c.ox, sy0 + c.oy, sx1 + c.ox, sy1 + c.oy);
+                        mark(sx0 + c.ox, sy0 + c.oy, sx1 + c.ox, sy1 + c.oy);
                     }
             }
-            // only tiles that intersect the camera's aligned ROI
-            for (int ty = 0; ty < L.ty_n; ty++)
-                for (int tx = 0; tx < L.tx_n; tx++) {
-                    uint8_t& v = R.b[(size_t)ty * L.tx_n + tx];
-                    if (!v) continue;
-                    const bool hit = tx * kTileW < c.ox + c.w && (tx + 1) * kTileW > c.ox && ty * kTileH < c.oy + c.h &&
-                                     (ty + 1) * kTileH > c.oy;
-                    if (!hit) v = 0;
-                    else L.req_tiles++;
+            // blocks outside the camera's aligned ROI hold nothing of it
+            for (int by = 0; by < by_n; by++)
+                for (int bx = 0; bx < bx_n; bx++) {
+                    uint8_t& v = need[(size_t)by * bx_n + bx];
+                    if (v && !(bx * kBlk < c.ox + c.w && (bx + 1) * kBlk > c.ox && by * kBlk < c.oy + c.h &&
+                               (by + 1) * kBlk > c.oy))
+                        v = 0;
                 }
+            Bitmap& R = req[l][i];
+            R.init(L.tx_n, L.ty_n);
+            for (int by = 0; by < by_n; by++)
+                for (int bx = 0; bx < bx_n; bx++)
+                    if (need[(size_t)by * bx_n + bx]) R.b[(size_t)(by * kBlk / kTileH) * L.tx_n + bx * kBlk / kTileW] = 1;
+            for (uint8_t v : R.b) L.req_tiles += v;
+            need_next[i] = std::move(need);
         }
     }
     // ---- per-level device tables, down items, collapse buffers ----------------------------------
@@ -440,8 +500,11 @@ void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev
             a.g_next = Ln.g.p;
             a.r_next = Ln.R.p;
             a.W_next = Ln.W;
+            a.H_next = Ln.H;
             a.rup_rows = L.rup.p;
             a.rup_cols = L.rup.p + L.rup_rows;
+            a.rup_r0 = L.rup_org.p;
+            a.rup_c0 = L.rup_org.p + L.ty_n;
         }
         if (l > 0) {
             a.r_out = L.R.p;

@@ -28,10 +28,16 @@ CONFIGS = {
     # name: (rig json, out_w, out_h, in sizes)
     "C1": lambda: (fisheye_rig(1920, 1080, [0.0, math.pi]), 4096, 2048, [(1920, 1080)] * 2),
     "C2": lambda: (fisheye_rig(3840, 2160, [k * math.pi / 3 for k in range(6)]), 7680, 3840, [(3840, 2160)] * 6),
+    # C3 = C2 + multi-band blend=16 (3 bands), seams from the L2 distance seam finder
+    "C3": lambda: (fisheye_rig(3840, 2160, [k * math.pi / 3 for k in range(6)]), 7680, 3840, [(3840, 2160)] * 6),
     "C4": lambda: (fisheye_rig(3840, 2160, [k * math.pi / 3 for k in range(6)] + [k * math.pi / 3 + math.pi / 6 for k in range(6)],
                                [0.6108652381980153] * 6 + [-0.6108652381980153] * 6, hfov=2.6179938779914944),
                    15360, 7680, [(3840, 2160)] * 12),
 }
+
+
+# Mapper blend mode per configuration (mapper.cpp:171-184: 0 copy chain, > 0 multi-band)
+BLEND = {"C1": 0, "C2": 0, "C3": 16, "C4": 0}
 
 
 def splitmix_bytes(seed, n):

@@ -192,7 +192,10 @@ def test_gpu_mapper_argument_errors(ox):
     with pytest.raises(ox.OctvrError):
         ox.Mapper(mt, [(256, 144)])  # wrong input count
     with pytest.raises(ox.OctvrError) as e:
-        ox.Mapper(mt, [(256, 144)] * 2, blend=16)
+        ox.Mapper(mt, [(256, 144)] * 2, blend=16)  # multi-band needs seam masks
+    assert e.value.code == -1 and "seam" in str(e.value)
+    with pytest.raises(ox.OctvrError) as e:
+        ox.Mapper(mt, [(256, 144)] * 2, blend=-20)  # feather: not in this ABI version
     assert e.value.code == -4
     with pytest.raises(ox.OctvrError):
         ox.Mapper(mt, [(255, 144)] * 2)  # odd size: not YUV420
