@@ -97,6 +97,8 @@ struct octvr_rig {
 namespace octvr {
 // MapperTemplate::create_masks() (template.cpp:155-204) — seams.cpp
 void rig_create_masks(octvr_rig& rig);
+// cv::distanceTransform(src, dst, DIST_L2, 3) on the host (distransform.cpp:48-139); w x h, packed
+void chamfer_l2_3x3(const uint8_t* src, int w, int h, float* dist);
 
 // ---- tiled composite LUT builder (tiling.cpp) ----------------------------------------------------
 struct TileJob {
@@ -136,8 +138,10 @@ struct MultiBandDeleter {
 };
 // MultiBandGPUBlender(seam_masks, rois, bands) for a mapper: everything per rig (weights, tile lists,
 // pyramid buffers) on `device`.  in_w / in_h: input frame sizes.
+// feather_border > 0 instead builds FeatherGPUBlender(masks, rois, border) (blenders.cpp:531-586):
+// a single level whose weights are the normalised feather weights.
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
-                            const std::vector<int>& in_h);
+                            const std::vector<int>& in_h, int feather_border = 0);
 // One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P.
 void multiband_run(MultiBand& mb, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
                    int64_t out_pitch, hipStream_t s);

@@ -190,6 +190,9 @@ hipError_t launch_mb_down(const uint2* items, int n_items, const MbCamLevel* cam
                           const uint8_t* g_prev, uint8_t* g_l, hipStream_t s);
 struct MbBlendArgs {
     int level, bands, n_cams;
+    int w_u8;                       // weights are the u8 seam mask (multi-band level 0), else f32
+    int feather;                    // FeatherGPUBlender: out = sat_u8(out_scale * D), no normalisation
+    float out_scale;                // (float)(1.0 / n) (convertTo alpha, blenders.cpp:579)
     int W, H;                       // level grid
     int tiles_x;
     const uint32_t* tile_cams;      // bit n: camera n has a non-zero weight in the tile

@@ -238,8 +238,8 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
             const int cx = min(max(px, 0), c.w - 1), cy = min(max(py, 0), c.h - 1);
             const int64_t k = (int64_t)cy * c.w + cx;
             // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
-            const float wv = a.level == 0 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
-                                          : static_cast<const float*>(c.weight)[k];
+            const float wv = a.w_u8 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
+                                    : static_cast<const float*>(c.weight)[k];
             w[p] = in ? wv : 0.f;
             gv[p] = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + cx * 4);
         }
@@ -286,7 +286,9 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
     int R[4][3];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        const float rcp = 1.0f / wsum[p];  // correctly rounded (hipcc default), as CUDA's 1.0f / b
+        // feather: convertTo(CV_8UC3, 1/n) = sat_u8(alpha * D) (clamped to u8 below); multi-band:
+        // DivOpSpecial<short3> with the correctly rounded reciprocal (hipcc default, as CUDA's 1.0f / b)
+        const float rcp = a.feather ? a.out_scale : 1.0f / wsum[p];
 #pragma unroll
         for (int ch = 0; ch < 3; ch++)
             R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf((float)D[p][ch] * rcp), -32768.f, 32767.f);

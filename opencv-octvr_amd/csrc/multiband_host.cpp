@@ -23,6 +23,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "host_common.hpp"
@@ -64,6 +65,7 @@ class MultiBand {
     };
     std::vector<Level> lv;
     TiledLutDev remap;
+    bool feather = false;  // FeatherGPUBlender instead of MultiBandGPUBlender
     bool full_cover = true;
     int crop_w = 0, crop_h = 0;
 };
@@ -163,7 +165,7 @@ struct Bitmap {
 }  // namespace
 
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
-                            const std::vector<int>& in_h) {
+                            const std::vector<int>& in_h, int feather_border) {
     auto mb = std::unique_ptr<MultiBand>(new MultiBand);
     MultiBand& M = *mb;
     const int n = (int)rig.inputs.size();
@@ -172,10 +174,14 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     M.device = device;
     M.out_w = rig.out_w;
     M.out_h = rig.out_h;
+    M.feather = feather_border > 0;
+    if (M.feather) M.B = bands = 0;
     const int B = bands;
-    REQUIRE(B >= 1 && B <= kMbMaxBands, "multi-band blend: band count out of range (blend must be >= 3)");
-    REQUIRE(rig.seam_masks.size() == (size_t)n,
-            "multi-band blend needs seam masks (octvr_rig_create_masks or a .dat with seams)");
+    if (!M.feather) {
+        REQUIRE(B >= 1 && B <= kMbMaxBands, "multi-band blend: band count out of range (blend must be >= 3)");
+        REQUIRE(rig.seam_masks.size() == (size_t)n,
+                "multi-band blend needs seam masks (octvr_rig_create_masks or a .dat with seams)");
+    }
     // ---- rectangles (blenders.cpp:479-486, 595-618) ------------------------------------------
     int x0 = INT32_MAX, y0 = INT32_MAX, x1 = INT32_MIN, y1 = INT32_MIN;
     for (auto& in : rig.inputs) {
@@ -187,7 +193,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     M.arr = Rect{round_down(x0, B), round_down(y0, B), 0, 0};
     M.arr.w = round_up(x1, B) - M.arr.x;
     M.arr.h = round_up(y1, B) - M.arr.y;
-    const int gap = 5 * (1 << B);
+    const int gap = M.feather ? 0 : 5 * (1 << B);  // feather: the ROIs themselves
     for (auto& in : rig.inputs) {
         const int l = std::max(M.arr.x, round_down(in.roi[0], B) - gap);
         const int t = std::max(M.arr.y, round_down(in.roi[1], B) - gap);
@@ -197,7 +203,8 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         M.ar.push_back(Rect{l, t, r - l, b - t});
     }
     const double max_len = std::max(M.arr.w, M.arr.h);
-    REQUIRE(B <= (int)std::ceil(std::log(max_len) / std::log(2.0)), "multi-band: too many bands (blenders.cpp:621)");
+    REQUIRE(M.feather || B <= (int)std::ceil(std::log(max_len) / std::log(2.0)),
+            "multi-band: too many bands (blenders.cpp:621)");
     M.crop_w = std::min(M.arr.w, rig.out_w);
     M.crop_h = std::min(M.arr.h, rig.out_h);
     REQUIRE(M.arr.x + M.crop_w <= rig.out_w && M.arr.y + M.crop_h <= rig.out_h,
@@ -229,8 +236,52 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         L.g_bytes = off;
         L.g.alloc(off);
     }
+    // ---- feather weights (FeatherGPUBlender ctor, blenders.cpp:531-568) -----------------------
+    //   w_i = max(distanceTransform(mask_i, L2, 3) - border, 0); W = 1e-5f + sum_i w_i (camera order);
+    //   w_i = n * w_i / W (DivScaleOp, div_mat.cu:82-91; plain a / b when n == 1)
+    if (M.feather) {
+        auto& L0 = M.lv[0];
+        std::vector<std::vector<float>> w(n);
+        std::vector<std::thread> th;
+        for (int i = 0; i < n; i++)
+            th.emplace_back([&, i] {
+                const RigInput& in = rig.inputs[i];
+                w[i].resize((size_t)in.roi[2] * in.roi[3]);
+                chamfer_l2_3x3(in.mask.data(), in.roi[2], in.roi[3], w[i].data());
+                for (float& v : w[i]) {
+                    const float d = v - (float)feather_border;
+                    v = d > 0.f ? d : 0.f;  // threshold(THRESH_TOZERO, 0)
+                }
+            });
+        for (auto& t : th) t.join();
+        std::vector<float> W((size_t)M.arr.w * M.arr.h, 1e-5f);
+        for (int i = 0; i < n; i++) {
+            const RigInput& in = rig.inputs[i];
+            for (int y = 0; y < in.roi[3]; y++)
+                for (int x = 0; x < in.roi[2]; x++) {
+                    float& d = W[(size_t)(in.roi[1] - M.arr.y + y) * M.arr.w + (in.roi[0] - M.arr.x + x)];
+                    d = w[i][(size_t)y * in.roi[2] + x] + d;
+                }
+        }
+        size_t tot = 0;
+        std::vector<size_t> woff(n);
+        for (int i = 0; i < n; i++) woff[i] = tot, tot += w[i].size();
+        std::vector<float> all(tot);
+        const float sc = (float)n;
+        for (int i = 0; i < n; i++) {
+            const RigInput& in = rig.inputs[i];
+            for (int y = 0; y < in.roi[3]; y++)
+                for (int x = 0; x < in.roi[2]; x++) {
+                    const float a = w[i][(size_t)y * in.roi[2] + x];
+                    const float b = W[(size_t)(in.roi[1] - M.arr.y + y) * M.arr.w + (in.roi[0] - M.arr.x + x)];
+                    all[woff[i] + (size_t)y * in.roi[2] + x] = b != 0 ? (n == 1 ? a / b : sc * a / b) : 0.f;
+                }
+        }
+        L0.wts.upload(all.data(), all.size());
+        for (int i = 0; i < n; i++) L0.cams_h[i].weight = L0.wts.p + woff[i];
+    }
     // ---- weights: level 0 = seam (u8), levels >= 1 = K4 pyrDown of seam/255 ------------------
-    {
+    if (!M.feather) {
         auto& L0 = M.lv[0];
         size_t tot = 0;
         std::vector<size_t> woff(n);
@@ -287,7 +338,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         for (int i = 0; i < n; i++) {
             const auto& c = L.cams_h[i];
             HIP_CHECK(hipMemset(blk.p, 0, blk.n));
-            HIP_CHECK(launch_block_activity(c.weight, l == 0, c.w, c.h, c.ox, c.oy, bx_n, blk.p, nullptr));
+            HIP_CHECK(launch_block_activity(c.weight, l == 0 && !M.feather, c.w, c.h, c.ox, c.oy, bx_n, blk.p, nullptr));
             act[l][i].resize(blk.n);
             HIP_CHECK(hipMemcpy(act[l][i].data(), blk.p, blk.n, hipMemcpyDeviceToHost));
             for (int by = 0; by < by_n; by++)
@@ -488,6 +539,9 @@ void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev
         a.level = l;
         a.bands = M.B;
         a.n_cams = M.n;
+        a.w_u8 = l == 0 && !M.feather;
+        a.feather = M.feather;
+        a.out_scale = (float)(1.0 / M.n);
         a.W = L.W;
         a.H = L.H;
         a.tiles_x = L.tx_n;
@@ -542,7 +596,7 @@ double multiband_traffic(const MultiBand& M) {
 }
 
 std::string multiband_info(const MultiBand& M) {
-    std::string s = "\"bands\": " + std::to_string(M.B) + ", \"align_result_roi\": [" + std::to_string(M.arr.x) + ", " +
+    std::string s = std::string(M.feather ? "\"feather\": 1, " : "") + "\"bands\": " + std::to_string(M.B) + ", \"align_result_roi\": [" + std::to_string(M.arr.x) + ", " +
                     std::to_string(M.arr.y) + ", " + std::to_string(M.arr.w) + ", " + std::to_string(M.arr.h) +
                     "], \"remap_items\": " + std::to_string(M.remap.view.n_items) +
                     ", \"remap_wide\": " + std::to_string(M.remap.view.n_wide) + ", \"level_tiles\": [";

@@ -793,13 +793,15 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         // mapper.cpp:78-82: a single input disables gain (and blend)
         m->use_gain = (enable_gain && m->n > 1) ? 1 : 0;
         m->blend = m->n > 1 ? blend : 0;
-        if (m->blend < 0) throw OctvrError(OCTVR_E_UNSUPPORTED, "feather blend is not implemented in this ABI version");
         REQUIRE(!m->use_gain || m->n <= 16, "gain estimation supports at most 16 inputs");
         DeviceGuard dg(device);
         if (m->blend > 0) {
             // MultiBandGPUBlender(seam_masks, rois, bands), bands = ceil(log2(blend)) - 1 (mapper.cpp:171-176)
             const int bands = (int)(std::ceil(std::log((double)m->blend) / std::log(2.)) - 1.);
             m->mb.reset(multiband_create(*rig, device, bands, m->in_w, m->in_h));
+        } else if (m->blend < 0) {
+            // FeatherGPUBlender(masks, rois, border = -blend) (mapper.cpp:177-182)
+            m->mb.reset(multiband_create(*rig, device, 0, m->in_w, m->in_h, -m->blend));
         } else {
             // per-camera templates -> device, composite LUT, then drop the per-camera maps
             std::vector<DevBuf<float>> m1(m->n), m2(m->n);

@@ -104,9 +104,11 @@ std::vector<uint8_t> resize_on_device(const uint8_t* src, int sw, int sh, int dw
     return out;
 }
 
+}  // namespace
+
 // distanceTransform(DIST_L2, 3x3) -> f32 (distransform.cpp:48-139): integer chamfer distances in
 // 16.16 fixed point, metrics a = 0.955, b = 1.3693 (:402-420), one forward and one backward pass.
-void chamfer_l2(const uint8_t* src, int w, int h, float* dist) {
+void chamfer_l2_3x3(const uint8_t* src, int w, int h, float* dist) {
     constexpr int kFar = 0x7FFFFFFF >> 2;
     const int a = (int)std::lrint(0.955f * 65536.0), b = (int)std::lrint(1.3693f * 65536.0);
     const int stride = w + 2;
@@ -138,7 +140,6 @@ void chamfer_l2(const uint8_t* src, int w, int h, float* dist) {
     }
 }
 
-}  // namespace
 
 void rig_create_masks(octvr_rig& rig) {
     const int n = (int)rig.inputs.size();
@@ -181,11 +182,11 @@ void rig_create_masks(octvr_rig& rig) {
                     for (int c = 0; c < 3; c++)
                         memcpy(&tri[((size_t)y * 3 + c) * k.w], &k.mask[(size_t)y * k.w], k.w);
                 std::vector<float> d3(tri.size());
-                chamfer_l2(tri.data(), 3 * k.w, k.h, d3.data());
+                chamfer_l2_3x3(tri.data(), 3 * k.w, k.h, d3.data());
                 for (int y = 0; y < k.h; y++)
                     memcpy(&k.dist[(size_t)y * k.w], &d3[((size_t)y * 3 + 1) * k.w], sizeof(float) * k.w);
             } else {
-                chamfer_l2(k.mask.data(), k.w, k.h, k.dist.data());
+                chamfer_l2_3x3(k.mask.data(), k.w, k.h, k.dist.data());
             }
         });
     for (auto& t : th) t.join();

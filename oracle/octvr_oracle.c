@@ -875,7 +875,8 @@ int orc_stitch_frame(const orc_frame* f) {
         rc = orc_multiband_blend(n, f->rois, f->seams, (const uint8_t* const*)warped, orc_blend_bands(blend), result,
                                  f->out_w, f->out_h, (size_t)f->out_w * 3, T);
     } else if (blend < 0) {
-        rc = -3; /* feather: not restated yet */
+        rc = orc_feather_blend(n, f->rois, f->masks, (const uint8_t* const*)warped, -blend, result, f->out_w, f->out_h,
+                               (size_t)f->out_w * 3);
     } else {
         for (int i = 0; i < n; i++) {
             const int* r = f->rois + 4 * i;

@@ -117,6 +117,9 @@ void orc_pyr_down_f32(const float* src, int sw, int sh, float* dst, int threads)
  * reference assertion. */
 int orc_multiband_blend(int n, const int* rois, const uint8_t* const* seams, const uint8_t* const* warped, int bands,
                         uint8_t* result, int out_w, int out_h, size_t result_pitch, int threads);
+/* FeatherGPUBlender(masks, rois, border).blend(warped, result): blend < 0 with border = -blend. */
+int orc_feather_blend(int n, const int* rois, const uint8_t* const* masks, const uint8_t* const* warped, int border,
+                      uint8_t* result, int out_w, int out_h, size_t result_pitch);
 /* Mapper's band count for blend > 0: int(ceil(log(blend) / log(2.)) - 1.) (mapper.cpp:172). */
 int orc_blend_bands(int blend);
 

@@ -363,3 +363,74 @@ int orc_multiband_blend(int n, const int* rois, const uint8_t* const* seams, con
     free(m.w); free(m.g); free(m.up); free(m.bw); free(m.lap); free(m.ar);
     return 0;
 }
+
+/* ---- FeatherGPUBlender (blenders.cpp:531-586) ------------------------------------------------- */
+/* ctor: w_i = threshold_tozero(distanceTransform(mask_i, L2, 3) - border), W = 1e-5f + sum_i w_i
+ * over the result ROI (camera order), w_i = N * w_i / W (DivScaleOp, div_mat.cu:82-91);
+ * do_blend: D = sum_i (short)(A_i * w_i) where w_i != 0 (K6, short wrap), result(result_roi) =
+ * saturate_cast<uchar>((float)(1.0 / N) * D) (convertTo with alpha). */
+int orc_feather_blend(int n, const int* rois, const uint8_t* const* masks, const uint8_t* const* warped, int border,
+                      uint8_t* result, int out_w, int out_h, size_t result_pitch) {
+    int x0 = rois[0], y0 = rois[1], x1 = rois[0] + rois[2], y1 = rois[1] + rois[3];
+    for (int i = 1; i < n; i++) {
+        const int* r = rois + 4 * i;
+        if (r[0] < x0) x0 = r[0];
+        if (r[1] < y0) y0 = r[1];
+        if (r[0] + r[2] > x1) x1 = r[0] + r[2];
+        if (r[1] + r[3] > y1) y1 = r[1] + r[3];
+    }
+    const int RW = x1 - x0, RH = y1 - y0;
+    float* W = (float*)malloc(sizeof(float) * (size_t)RW * RH);
+    for (size_t k = 0; k < (size_t)RW * RH; k++) W[k] = 1e-5f;
+    float** w = (float**)calloc(n, sizeof(void*));
+    for (int i = 0; i < n; i++) {
+        const int* r = rois + 4 * i;
+        w[i] = (float*)malloc(sizeof(float) * (size_t)r[2] * r[3]);
+        orc_distance_transform_l2_3x3(masks[i], r[2], r[3], (size_t)r[2], w[i], (size_t)r[2]);
+        for (size_t k = 0; k < (size_t)r[2] * r[3]; k++) {
+            float v = w[i][k] - (float)border;
+            w[i][k] = v > 0.f ? v : 0.f;
+        }
+        for (int y = 0; y < r[3]; y++)
+            for (int x = 0; x < r[2]; x++) {
+                float* d = &W[(size_t)(r[1] - y0 + y) * RW + (r[0] - x0 + x)];
+                *d = w[i][(size_t)y * r[2] + x] + *d;
+            }
+    }
+    const float sc = (float)n;
+    for (int i = 0; i < n; i++) {
+        const int* r = rois + 4 * i;
+        for (int y = 0; y < r[3]; y++)
+            for (int x = 0; x < r[2]; x++) {
+                float* a = &w[i][(size_t)y * r[2] + x];
+                float b = W[(size_t)(r[1] - y0 + y) * RW + (r[0] - x0 + x)];
+                *a = b != 0 ? (n == 1 ? *a / b : sc * *a / b) : 0.f;
+            }
+    }
+    int16_t* D = (int16_t*)calloc((size_t)RW * RH * 3, sizeof(int16_t));
+    for (int i = 0; i < n; i++) {
+        const int* r = rois + 4 * i;
+        for (int y = 0; y < r[3]; y++)
+            for (int x = 0; x < r[2]; x++) {
+                const size_t k = (size_t)y * r[2] + x;
+                const float we = w[i][k];
+                if (we == 0) continue;
+                int16_t* d = D + ((size_t)(r[1] - y0 + y) * RW + (r[0] - x0 + x)) * 3;
+                for (int ch = 0; ch < 3; ch++) {
+                    int16_t sub = (int16_t)(int)truncf((float)warped[i][4 * k + ch] * we);
+                    d[ch] = (int16_t)(d[ch] + sub);
+                }
+            }
+    }
+    const float alpha = (float)(1.0 / n);
+    for (int y = 0; y < RH; y++)
+        for (int x = 0; x < RW; x++) {
+            if (y0 + y >= out_h || x0 + x >= out_w) continue;
+            uint8_t* o = result + (size_t)(y0 + y) * result_pitch + (size_t)(x0 + x) * 3;
+            const int16_t* s = D + ((size_t)y * RW + x) * 3;
+            for (int q = 0; q < 3; q++) o[q] = (uint8_t)clampi((int)lrintf(alpha * (float)s[q]), 0, 255);
+        }
+    for (int i = 0; i < n; i++) free(w[i]);
+    free(w); free(W); free(D);
+    return 0;
+}

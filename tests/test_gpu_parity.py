@@ -194,9 +194,12 @@ def test_gpu_mapper_argument_errors(ox):
     with pytest.raises(ox.OctvrError) as e:
         ox.Mapper(mt, [(256, 144)] * 2, blend=16)  # multi-band needs seam masks
     assert e.value.code == -1 and "seam" in str(e.value)
+    seams = [np.full(z["mask_0"].shape, 255, np.uint8)] * 2
+    mt2 = ox.MapperTemplate.from_arrays(512, 256, z["rois"].tolist(), [z["map1_0"], z["map1_1"]],
+                                        [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]], seams)
     with pytest.raises(ox.OctvrError) as e:
-        ox.Mapper(mt, [(256, 144)] * 2, blend=-20)  # feather: not in this ABI version
-    assert e.value.code == -4
+        ox.Mapper(mt2, [(256, 144)] * 2, blend=2)  # ceil(log2 2) - 1 = 0 bands (blenders.cpp:594)
+    assert e.value.code == -1
     with pytest.raises(ox.OctvrError):
         ox.Mapper(mt, [(255, 144)] * 2)  # odd size: not YUV420
 
@@ -332,9 +335,10 @@ def test_gpu_create_masks_scaled_vs_oracle(ox, out_w):
 
 
 # ---- multi-band blend (MultiBandGPUBlender): bit-exact against the oracle -----------
-@pytest.mark.parametrize("blend", [4, 16, 128])
+@pytest.mark.parametrize("blend", [4, 16, 128, -5, -20])
 @pytest.mark.parametrize("name", RIGS)
 def test_gpu_multiband_bit_exact(ox, name, blend):
+    # blend > 0: MultiBandGPUBlender; blend < 0: FeatherGPUBlender
     from octvr_amd import synthetic
     n = len(O.load_rig(name)[1]["rois"])
     gains = [1.0 + 0.011 * k * (-1) ** k for k in range(n)]
