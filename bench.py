@@ -151,8 +151,19 @@ def main():
         f = sum(4.0 ** -l for l in range(1, int(math.ceil(math.log(blend) / math.log(2.)) - 1) + 1))
         survey_b_alg += 12.0 * f * frame_px + 4.0 * f * n_valid
 
+    # HBM traffic of the dominant kernel from the committed PMC summary of this configuration
+    # (scripts/pmc.sh + scripts/pmc_summary.py; rocprofv3 cannot wrap the process that reads it)
+    traffic = None
+    import glob
+    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % args.config)))
+    if pmc and blend == 0:
+        tb = json.load(open(pmc[-1])).get("traffic_bytes", {})
+        hit = [v for k, v in tb.items() if "stitch_tiled_kernel" in k]
+        traffic = round(hit[0]) if hit else None
+    ncam = len(sizes)
     result = {
-        "metric": "stitched megapixels/sec (6x4K->8K equirect)",
+        "metric": "stitched megapixels/sec (6x4K->8K equirect)" if args.config in ("C2", "C3") else
+                  "stitched megapixels/sec (%dx%dx%d->%dx%d equirect)" % (ncam, sizes[0][0], sizes[0][1], W, H),
         "value": round(value, 1),
         "unit": "MP/s",
         "n_gpus": world,
@@ -171,7 +182,7 @@ def main():
                                    if blend > 0 else "no-blend composite"),
                    "rigs_per_gpu": 1, "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": "multiband sequence (remap, pyrDown, blend levels)" if blend > 0 else "stitch_kernel",
                      "kernel_us": round(avg_kernel_s * 1e6, 2),
                      "bytes_per_launch": bytes_per_launch,
