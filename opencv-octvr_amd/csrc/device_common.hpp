@@ -36,6 +36,15 @@ __device__ __forceinline__ uint32_t yuv_to_rgba(uint32_t y, uint32_t u, uint32_t
     return pack_u8(__builtin_fmaf(2.032f, Uf, Yf), 2, p);
 }
 
+// Vignette correction of a source pixel: multiply(rgba, vignette_map) = MulOpSpecial_c4
+// (cudaarithm/src/cuda/mul_mat.cu:198-214): saturate_cast<uchar>(c * g) per channel.
+__device__ __forceinline__ uint32_t vig_mul(uint32_t rgba, float g) {
+    uint32_t v = pack_u8((float)(rgba & 255u) * g, 0, 0u);
+    v = pack_u8((float)((rgba >> 8) & 255u) * g, 1, v);
+    v = pack_u8((float)((rgba >> 16) & 255u) * g, 2, v);
+    return pack_u8((float)(rgba >> 24) * g, 3, v);
+}
+
 // 15-bit bilinear weights.  initInterTab2D's table (imgwarp.cpp:211-280) holds
 // w = {(32-fx)(32-fy), fx(32-fy), (32-fx)fy, fx fy} * 32 exactly (every product is exact in f32),
 // except code 0 whose 32768 saturates to 32767 and the fix-up adds the missing unit to the
@@ -92,10 +101,20 @@ __device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t
     const uint32_t ya = Y[r0 + x0], yb = Y[r0 + x1], yc = Y[r1 + x0], yd = Y[r1 + x1];
     const uint32_t ua = U[q0 + (x0 >> 1)], ub = U[q0 + (x1 >> 1)], uc = U[q1 + (x0 >> 1)], ud = U[q1 + (x1 >> 1)];
     const uint32_t va = V[q0 + (x0 >> 1)], vb = V[q0 + (x1 >> 1)], vc = V[q1 + (x0 >> 1)], vd = V[q1 + (x1 >> 1)];
-    t.c[0] = in0 ? yuv_to_rgba(ya, ua, va) : 0u;
-    t.c[1] = (valid && inx && sy < f.h) ? yuv_to_rgba(yb, ub, vb) : 0u;
-    t.c[2] = (valid && iny && sx < f.w) ? yuv_to_rgba(yc, uc, vc) : 0u;
-    t.c[3] = (valid && inx && iny) ? yuv_to_rgba(yd, ud, vd) : 0u;
+    uint32_t ca = yuv_to_rgba(ya, ua, va), cb = yuv_to_rgba(yb, ub, vb);
+    uint32_t cc = yuv_to_rgba(yc, uc, vc), cd = yuv_to_rgba(yd, ud, vd);
+    if (f.vig) {
+        const float* g0 = f.vig + (int64_t)y0 * f.w;
+        const float* g1 = f.vig + (int64_t)y1 * f.w;
+        ca = vig_mul(ca, g0[x0]);
+        cb = vig_mul(cb, g0[x1]);
+        cc = vig_mul(cc, g1[x0]);
+        cd = vig_mul(cd, g1[x1]);
+    }
+    t.c[0] = in0 ? ca : 0u;
+    t.c[1] = (valid && inx && sy < f.h) ? cb : 0u;
+    t.c[2] = (valid && iny && sx < f.w) ? cc : 0u;
+    t.c[3] = (valid && inx && iny) ? cd : 0u;
     t.fx = code & 31u;
     t.fy = (code >> 5) & 31u;
 }

@@ -460,6 +460,7 @@ __device__ __forceinline__ SourceFrame kernarg_frame(uint32_t cam) {
     s.w = kf[cam].w;
     s.h = kf[cam].h;
     s.pitch = kf[cam].pitch;
+    s.vig = kf[cam].vig;
     return s;
 }
 
@@ -468,6 +469,7 @@ struct StageGroup {
     uint32_t y0, y1;  // 8 Y bytes
     uint32_t uq, vq;  // 4 U bytes, 4 V bytes
     int32_t dst;      // dword index of the group's first RGBA pixel; -1 = none
+    float4 g0, g1;    // VIG: vignette gains of the 8 pixels
 };
 
 // Loads of staging chunk c (wave-uniform) of a tile: 64 groups of 8 luma pixels inside one slot.
@@ -475,7 +477,7 @@ struct StageGroup {
 // slot is row k / (bw/8), column k % (bw/8) of the slot's box.  Lanes past the slot's groups (and
 // chunks past the tile's) read the box origin / frame start and are marked dst = -1.  With box
 // columns 8-aligned, the Y load is 8-byte and the U / V loads 4-byte aligned (DWORD_STAGE).
-template <bool DWORD_STAGE>
+template <bool DWORD_STAGE, bool VIG>
 __device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32_t nchunks, uint32_t stride, int c,
                                            StageGroup& sg) {
     const int lane = threadIdx.x & 63;
@@ -520,8 +522,14 @@ __device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32
         sg.vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8) | ((uint32_t)Vp[2] << 16) | ((uint32_t)Vp[3] << 24);
     }
     sg.dst = ok ? (int32_t)(lds + row * stride + col * 8u) : -1;
+    if (VIG) {  // 8 gains (32-byte aligned: w % 8 == 0); a camera without vignette reads 1.0 gains
+        const float* gv = f.vig ? f.vig + (int64_t)(by0 + row) * f.w + bx0 + col * 8u : nullptr;
+        sg.g0 = gv ? *reinterpret_cast<const float4*>(gv) : make_float4(1.f, 1.f, 1.f, 1.f);
+        sg.g1 = gv ? *reinterpret_cast<const float4*>(gv + 4) : make_float4(1.f, 1.f, 1.f, 1.f);
+    }
 }
 
+template <bool VIG>
 __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rgb) {
     if (sg.dst < 0) return;
     uint4 a, b;
@@ -533,6 +541,16 @@ __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rg
     b.y = yuv_to_rgba((sg.y1 >> 8) & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u);
     b.z = yuv_to_rgba((sg.y1 >> 16) & 255u, sg.uq >> 24, sg.vq >> 24);
     b.w = yuv_to_rgba(sg.y1 >> 24, sg.uq >> 24, sg.vq >> 24);
+    if (VIG) {
+        a.x = vig_mul(a.x, sg.g0.x);
+        a.y = vig_mul(a.y, sg.g0.y);
+        a.z = vig_mul(a.z, sg.g0.z);
+        a.w = vig_mul(a.w, sg.g0.w);
+        b.x = vig_mul(b.x, sg.g1.x);
+        b.y = vig_mul(b.y, sg.g1.y);
+        b.z = vig_mul(b.z, sg.g1.z);
+        b.w = vig_mul(b.w, sg.g1.w);
+    }
     *reinterpret_cast<uint4*>(s_rgb + sg.dst) = a;
     *reinterpret_cast<uint4*>(s_rgb + sg.dst + 4) = b;
 }
@@ -588,7 +606,7 @@ struct TileData {
     StageGroup sg[kStageRegs];
 };
 
-template <bool DWORD_STAGE>
+template <bool DWORD_STAGE, bool VIG>
 __device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLut& lut, const TileMeta& m, int t_end,
                                            TileData& d) {
     const bool live = m.t < t_end;
@@ -598,7 +616,7 @@ __device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLu
     const uint32_t nchunks = live ? ((m.hd.nslots >> 8) & 0xFFu) : 0u;
 #pragma unroll
     for (int r = 0; r < kStageRegs; r++)
-        stage_load<DWORD_STAGE>(m.ss, (int)(m.hd.nslots & 0xFFu), nchunks, m.hd.stride, r * 4 + wave, d.sg[r]);
+        stage_load<DWORD_STAGE, VIG>(m.ss, (int)(m.hd.nslots & 0xFFu), nchunks, m.hd.stride, r * 4 + wave, d.sg[r]);
 }
 
 // The composite's two sinks.  MODE 0: gain + RGB -> YUV420P into the output frame (blend = 0).
@@ -648,7 +666,7 @@ __device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro
 
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
-template <bool DWORD_STAGE, int MODE>
+template <bool DWORD_STAGE, int MODE, bool VIG>
 __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
                                                               int64_t out_pitch, RgbaOut rgba) {
@@ -676,7 +694,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
     TileMeta cur = meta_read(meta_issue(lut, t0, t_end), t0);
     __syncthreads();
     TileData d;
-    data_issue<DWORD_STAGE>(frames, lut, cur, t_end, d);
+    data_issue<DWORD_STAGE, VIG>(frames, lut, cur, t_end, d);
     uint32_t mv = meta_issue(lut, t0 + step, t_end);
     // opaque copies of the prologue loads: the loop-header phis then merge a load with a non-load,
     // so the compiler cannot fold them into one load at the header (waited on right there)
@@ -704,19 +722,19 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
             s_slot_gain[tid] = s_gain[cam];
         }
 #pragma unroll
-        for (int r = 0; r < kStageRegs; r++) stage_store(d.sg[r], s_rgb);
+        for (int r = 0; r < kStageRegs; r++) stage_store<VIG>(d.sg[r], s_rgb);
         const uint32_t nch = (cur.hd.nslots >> 8) & 0xFFu;
         if (nch > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
             const int wave = uniform(tid >> 6);
             for (int c = kStageRegs * 4 + wave; c < (int)nch; c += 4) {
                 StageGroup sg;
-                stage_load<DWORD_STAGE>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sg);
-                stage_store(sg, s_rgb);
+                stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sg);
+                stage_store<VIG>(sg, s_rgb);
             }
         }
         __syncthreads();
         store_any<MODE>(of, ro, prev, pcam, px, py, pin);
-        data_issue<DWORD_STAGE>(frames, lut, nxt, t_end, d);
+        data_issue<DWORD_STAGE, VIG>(frames, lut, nxt, t_end, d);
         mv = meta_issue(lut, cur.t + 2 * step, t_end);
         const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
         uint32_t rgb[4][3];
@@ -787,18 +805,25 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
         int blocks = std::min(lut.n_items, 256 * kStitchBlocksPerCU);
         blocks = std::max(8, (blocks + 7) / 8 * 8);
         // wide staging loads need 8-byte aligned Y rows (then U / V rows are 4-byte aligned)
-        bool dw = true;
+        bool dw = true, vig = false;
         for (int i = 0; i < kMaxCams; i++) {
             const SourceFrame& f = frames.f[i];
             if (!f.yuv) continue;
             if ((reinterpret_cast<uintptr_t>(f.yuv) & 7u) || (f.pitch & 7) || (f.w & 7)) dw = false;
+            vig |= f.vig != nullptr;
         }
-        if (dw)
-            hipLaunchKernelGGL((stitch_tiled_kernel<true, MODE>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H,
-                               gains, use_gain, out, out_pitch, rgba);
+#define OCTVR_LAUNCH_TILED(DW, V)                                                                          \
+    hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H, \
+                       gains, use_gain, out, out_pitch, rgba)
+        if (dw && !vig)
+            OCTVR_LAUNCH_TILED(true, false);
+        else if (dw)
+            OCTVR_LAUNCH_TILED(true, true);
+        else if (!vig)
+            OCTVR_LAUNCH_TILED(false, false);
         else
-            hipLaunchKernelGGL((stitch_tiled_kernel<false, MODE>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H,
-                               gains, use_gain, out, out_pitch, rgba);
+            OCTVR_LAUNCH_TILED(false, true);
+#undef OCTVR_LAUNCH_TILED
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

@@ -79,6 +79,7 @@ struct SourceFrame {
     const uint8_t* yuv;
     int32_t w, h;
     int64_t pitch;
+    const float* vig;  // vignette gain per source pixel (w x h, packed) or NULL (mapper.cpp:108-112,230-231)
 };
 
 // All camera frames of one stitch call, passed by value as a kernel argument (no per-frame H2D copy).

@@ -430,6 +430,7 @@ struct octvr_mapper {
     int n_chunks = 0, n_samples = 0;
     size_t n_entries = 0;
     std::vector<double> last_gains;
+    std::vector<DevBuf<float>> vig;  // per camera: vignette map resized to the input size, or empty
     hipStream_t last_stream = nullptr;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -467,6 +468,28 @@ std::vector<uint8_t> resize_linear_u8(const uint8_t* src, int sw, int sh, int dw
             out = fmaf((float)src[(size_t)y2r * sw + x2r], (src_x - x1) * (src_y - y1), out);
             int v = !(out > 0.f) ? 0 : out >= 255.f ? 255 : (int)rintf(out);
             dst[(size_t)y * dw + x] = (uint8_t)v;
+        }
+    return dst;
+}
+
+// cuda::resize INTER_LINEAR on f32 (the texture LinearFilter path, filters.hpp:79-117, taken for an
+// upscale without a stream): same taps and weights as resize_linear with clamped borders; nvcc's FMA
+// contraction of `out + src * w` reproduced with explicit fmaf.
+std::vector<float> resize_linear_f32(const float* src, int sw, int sh, int dw, int dh) {
+    std::vector<float> dst((size_t)dw * dh);
+    float fx = resize_inv_scale(dw, sw), fy = resize_inv_scale(dh, sh);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float src_x = x * fx, src_y = y * fy;
+            int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+            int x2 = x1 + 1, y2 = y1 + 1;
+            int x2r = std::min(x2, sw - 1), y2r = std::min(y2, sh - 1);
+            float out = 0.f;
+            out = fmaf(src[(size_t)y1 * sw + x1], (x2 - src_x) * (y2 - src_y), out);
+            out = fmaf(src[(size_t)y1 * sw + x2r], (src_x - x1) * (y2 - src_y), out);
+            out = fmaf(src[(size_t)y2r * sw + x1], (x2 - src_x) * (src_y - y1), out);
+            out = fmaf(src[(size_t)y2r * sw + x2r], (src_x - x1) * (src_y - y1), out);
+            dst[(size_t)y * dw + x] = out;
         }
     return dst;
 }
@@ -777,8 +800,6 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         REQUIRE((scale_w == 0 && scale_h == 0) || (scale_w == rig->out_w && scale_h == rig->out_h),
                 "scaled output is not implemented in this ABI version");
         REQUIRE(rig->out_w % 2 == 0 && rig->out_h % 2 == 0, "YUV420 output needs even width/height");
-        for (auto& in : rig->inputs)
-            REQUIRE(in.vignette.empty(), "vignette correction is not implemented in this ABI version");
         auto m = std::make_unique<octvr_mapper>();
         m->device = device;
         m->n = (int)rig->inputs.size();
@@ -795,6 +816,15 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         m->blend = m->n > 1 ? blend : 0;
         REQUIRE(!m->use_gain || m->n <= 16, "gain estimation supports at most 16 inputs");
         DeviceGuard dg(device);
+        // vignette: cv::cuda::resize(vignette, vignette_maps[i], in_size) (mapper.cpp:108-112), applied to
+        // every source pixel before the remap (mapper.cpp:230-231)
+        m->vig.resize(m->n);
+        for (int i = 0; i < m->n; i++) {
+            const RigInput& in = rig->inputs[i];
+            if (in.vignette.empty()) continue;
+            const std::vector<float> v = resize_linear_f32(in.vignette.data(), in.vig_w, in.vig_h, m->in_w[i], m->in_h[i]);
+            m->vig[i].upload(v.data(), v.size());
+        }
         if (m->blend > 0) {
             // MultiBandGPUBlender(seam_masks, rois, bands), bands = ceil(log2(blend)) - 1 (mapper.cpp:171-176)
             const int bands = (int)(std::ceil(std::log((double)m->blend) / std::log(2.)) - 1.);
@@ -862,7 +892,7 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
         memset(&fs, 0, sizeof fs);
         for (int i = 0; i < m->n; i++) {
             REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
-            fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i]};
+            fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
         }
         if (m->use_gain) {
             if (gains) {

@@ -158,6 +158,16 @@ class MapperTemplate:
                 arr(v.map2, C.c_float, np.float32), arr(v.mask, C.c_uint8, np.uint8),
                 arr(v.seam_mask, C.c_uint8, np.uint8))
 
+    def vignette(self, i):
+        """The input's vignette map (Vignette::getMap, vignette.cpp:39-54) or None."""
+        v = InputView()
+        _check(_lib.octvr_rig_get_input(self._h, i, C.byref(v)))
+        if not v.vignette:
+            return None
+        k = v.vignette_w * v.vignette_h
+        return np.ctypeslib.as_array(C.cast(v.vignette, C.POINTER(C.c_float)), shape=(k,)).copy().reshape(
+            v.vignette_h, v.vignette_w)
+
     def close(self):
         if self._h and self._h.value:
             _lib.octvr_rig_destroy(self._h)

@@ -761,6 +761,10 @@ static void yuv_rows(void* c, int y0, int y1) {
             yuv_px_to_rgb(yuv[(size_t)y * pitch + x], U[(size_t)(y >> 1) * pitch + (x >> 1)],
                           V[(size_t)(y >> 1) * pitch + (x >> 1)], o);
             o[3] = 255;
+            if (f->vig && f->vig[i]) { /* multiply(rgba, vignette) = MulOpSpecial_c4 (mul_mat.cu:198-214) */
+                const float g = f->vig[i][(size_t)y * w + x];
+                for (int ch = 0; ch < 4; ch++) o[ch] = sat_u8_rne((float)o[ch] * g);
+            }
         }
 }
 
@@ -894,3 +898,30 @@ int orc_stitch_frame(const orc_frame* f) {
 }
 
 int orc_blend_bands(int blend) { return (int)(ceil(log((double)blend) / log(2.)) - 1.); }
+
+void orc_vignette_map(double a, double b, double c, double d, int width, int height, float* out) {
+    for (int j = 0; j < height; j++)
+        for (int i = 0; i < width; i++) {
+            float dx = (float)(i - width / 2), dy = (float)(j - height / 2);
+            float hx = (float)(width / 2), hy = (float)(height / 2);
+            float r = sqrtf(dx * dx + dy * dy) / sqrtf(hx * hx + hy * hy);
+            out[(size_t)j * width + i] = (float)(1.0 / (a + r * r * (b + r * r * (c + d * r * r))));
+        }
+}
+
+void orc_resize_linear_cuda_f32(const float* src, int sw, int sh, float* dst, int dw, int dh) {
+    float fx = resize_inv_scale(dw, sw), fy = resize_inv_scale(dh, sh);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float src_x = x * fx, src_y = y * fy;
+            int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+            int x2 = x1 + 1, y2 = y1 + 1;
+            int x2r = x2 < sw - 1 ? x2 : sw - 1, y2r = y2 < sh - 1 ? y2 : sh - 1;
+            float o = 0.f;
+            o = fmaf(src[(size_t)y1 * sw + x1], (x2 - src_x) * (y2 - src_y), o);
+            o = fmaf(src[(size_t)y1 * sw + x2r], (src_x - x1) * (y2 - src_y), o);
+            o = fmaf(src[(size_t)y2r * sw + x1], (x2 - src_x) * (src_y - y1), o);
+            o = fmaf(src[(size_t)y2r * sw + x2r], (src_x - x1) * (src_y - y1), o);
+            dst[(size_t)y * dw + x] = o;
+        }
+}

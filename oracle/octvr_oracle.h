@@ -104,6 +104,7 @@ typedef struct {
     int row_begin, row_end;          /* restrict composite+output to a row band (cpu_baseline sample); 0,0 = all */
     int blend;                       /* Mapper blend: 0 copy chain, > 0 multi-band (bands = ceil(log2 blend) - 1), < 0 feather */
     const uint8_t* const* seams;     /* ROI-sized seam masks (multi-band weights); NULL unless blend > 0 */
+    const float* const* vig;         /* per camera: vignette gains at input size (in_w x in_h) or NULL; may be NULL */
 } orc_frame;
 int orc_stitch_frame(const orc_frame* f);
 
@@ -122,6 +123,12 @@ int orc_feather_blend(int n, const int* rois, const uint8_t* const* masks, const
                       uint8_t* result, int out_w, int out_h, size_t result_pitch);
 /* Mapper's band count for blend > 0: int(ceil(log(blend) / log(2.)) - 1.) (mapper.cpp:172). */
 int orc_blend_bands(int blend);
+
+/* Vignette::getMap (vignette.cpp:39-54): w x h f32 map of 1 / (a + r^2 (b + r^2 (c + d r^2))); the
+ * coefficients already divided by 2^exposure in float (vignette.cpp:26-33) by the caller. */
+void orc_vignette_map(double a, double b, double c, double d, int w, int h, float* out);
+/* cuda::resize INTER_LINEAR on f32 (texture LinearFilter path, filters.hpp:79-117; FMA-contracted). */
+void orc_resize_linear_cuda_f32(const float* src, int sw, int sh, float* dst, int dw, int dh);
 
 /* K13/K14 CUDA resize semantics used by the gain path (cudawarping/src/cuda/resize.cu:57-103). */
 void orc_resize_nearest_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw, int dh,

@@ -53,6 +53,7 @@ class OrcFrame(C.Structure):
         ("row_begin", C.c_int), ("row_end", C.c_int),
         ("blend", C.c_int),
         ("seams", C.POINTER(C.c_void_p)),
+        ("vig", C.POINTER(C.c_void_p)),
     ]
 
 
@@ -215,6 +216,26 @@ def pyr_down_f32(src, threads=1):
     return _pyr("orc_pyr_down_f32", src.astype(np.float32), ((h + 1) // 2, (w + 1) // 2), np.float32, threads)
 
 
+def vignette_map(opts, w=512, h=512):
+    """Vignette(options).getMap(w, h) (vignette.cpp:18-54); None without a "vignette" option."""
+    if "vignette" not in opts:
+        return None
+    a, b, c, d = (float(v) for v in opts["vignette"])
+    if "exposure" in opts:
+        ev = float(np.float32(2.0 ** float(opts["exposure"])))
+        a, b, c, d = a / ev, b / ev, c / ev, d / ev
+    out = np.zeros((h, w), np.float32)
+    lib().orc_vignette_map(C.c_double(a), C.c_double(b), C.c_double(c), C.c_double(d), w, h, _p(out))
+    return out
+
+
+def resize_linear_cuda_f32(src, dw, dh):
+    src = np.ascontiguousarray(src, np.float32)
+    out = np.zeros((dh, dw), np.float32)
+    lib().orc_resize_linear_cuda_f32(_p(src), src.shape[1], src.shape[0], _p(out), dw, dh)
+    return out
+
+
 def blend_bands(blend):
     return lib().orc_blend_bands(int(blend))
 
@@ -272,7 +293,7 @@ def gain_feed(rois, warped, masks, out_w, out_h):
 
 
 def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enable_gain=True, gains=None,
-                 threads=1, row_band=None, blend=0, seams=None):
+                 threads=1, row_band=None, blend=0, seams=None, vig=None):
     n = len(in_yuv)
     keep = []
 
@@ -314,6 +335,10 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
         seams = [np.ascontiguousarray(a, np.uint8) for a in seams]
         keep.append(seams)
         f.seams = arr(C.c_void_p, [a.ctypes.data for a in seams])
+    if vig is not None:
+        vig = [None if v is None else np.ascontiguousarray(v, np.float32) for v in vig]
+        keep.append(vig)
+        f.vig = arr(C.c_void_p, [None if v is None else v.ctypes.data for v in vig])
     rc = lib().orc_stitch_frame(C.byref(f))
     assert rc == 0
     return out, gout
