@@ -142,9 +142,10 @@ struct MultiBandDeleter {
 // a single level whose weights are the normalised feather weights.
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
                             const std::vector<int>& in_h, int feather_border = 0);
-// One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P.
+// One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P
+// (or, with `rgba`, the RGB result as RGBA for a scaled output).
 void multiband_run(MultiBand& mb, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
-                   int64_t out_pitch, hipStream_t s);
+                   int64_t out_pitch, hipStream_t s, uint8_t* rgba = nullptr, int64_t rgba_pitch = 0);
 // Algorithmic bytes of one frame and a JSON fragment of build statistics.
 double multiband_traffic(const MultiBand& mb);
 std::string multiband_info(const MultiBand& mb);

@@ -948,6 +948,64 @@ hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, int64_t spitch, 
 }
 
 // ---------------------------------------------------------------------------------------------
+// Scaled output (Mapper with scale_output != template size, mapper.cpp:290-306): the stitched RGB
+// result is resized with cuda::resize INTER_LINEAR (the glob kernel, resize.cu:71-103, which a
+// 3-channel image always takes) and converted to YUV420P.  Source: the composite's RGBA frame
+// (alpha ignored).  One lane per 2x2 output quad: 4 bilinear samples, then the same RGB -> YUV420P
+// quad conversion as the fused path.  nvcc contracts `out + src * w` into an FMA: explicit fmaf.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) resize_rgba_yuv420_kernel(const uint8_t* __restrict__ rgba, int sw, int sh,
+                                                                 int64_t spitch, float fx, float fy, uint8_t* out,
+                                                                 int dw, int dh, int64_t out_pitch) {
+    const OutFrame of = make_out_frame(out, dw, dh, out_pitch);
+    const int qw = dw >> 1, qh = dh >> 1;
+    const int64_t total = (int64_t)qw * qh;
+    const float one[4] = {1.f, 1.f, 1.f, 1.f};
+    for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
+        const int qy = (int)(q / qw), qx = (int)(q - (int64_t)qy * qw);
+        uint32_t rgb[4][3];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const int x = 2 * qx + (p & 1), y = 2 * qy + (p >> 1);
+            const float src_x = (float)x * fx, src_y = (float)y * fy;
+            const int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+            const int x2 = x1 + 1, y2 = y1 + 1;
+            const int x2r = min(x2, sw - 1), y2r = min(y2, sh - 1);
+            const uint32_t* r1 = reinterpret_cast<const uint32_t*>(rgba + (int64_t)y1 * spitch);
+            const uint32_t* r2 = reinterpret_cast<const uint32_t*>(rgba + (int64_t)y2r * spitch);
+            const uint32_t c00 = r1[x1], c01 = r1[x2r], c10 = r2[x1], c11 = r2[x2r];
+            const float w00 = ((float)x2 - src_x) * ((float)y2 - src_y);
+            const float w01 = (src_x - (float)x1) * ((float)y2 - src_y);
+            const float w10 = ((float)x2 - src_x) * (src_y - (float)y1);
+            const float w11 = (src_x - (float)x1) * (src_y - (float)y1);
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++) {
+                const uint32_t sh8 = 8u * ch;
+                float o = 0.f;
+                o = __builtin_fmaf((float)((c00 >> sh8) & 255u), w00, o);
+                o = __builtin_fmaf((float)((c01 >> sh8) & 255u), w01, o);
+                o = __builtin_fmaf((float)((c10 >> sh8) & 255u), w10, o);
+                o = __builtin_fmaf((float)((c11 >> sh8) & 255u), w11, o);
+                rgb[p][ch] = (uint32_t)sat_u8_rne(o);
+            }
+        }
+        store_quad(of, finish_quad(rgb, one), 2 * qx, 2 * qy, true);
+    }
+}
+
+hipError_t launch_resize_rgba_yuv420(const uint8_t* rgba, int sw, int sh, int64_t spitch, uint8_t* out, int dw, int dh,
+                                     int64_t out_pitch, hipStream_t s) {
+    if (dw <= 0 || dh <= 0 || (dw & 1) || (dh & 1)) return hipErrorInvalidValue;
+    // resize.cpp:82-83,105: the kernel gets (float)(1.0 / (double(dsize) / src))
+    const float fx = (float)(1.0 / ((double)dw / sw)), fy = (float)(1.0 / ((double)dh / sh));
+    const int64_t total = (int64_t)(dw / 2) * (dh / 2);
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(resize_rgba_yuv420_kernel, dim3(blocks), dim3(256), 0, s, rgba, sw, sh, spitch, fx, fy, out, dw,
+                       dh, out_pitch);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
 // Self-test: device saturating conversions (rint + clamp vs v_cvt_pk_u8_f32).
 // ---------------------------------------------------------------------------------------------
 __global__ void selftest_sat_kernel(const float* in, uint8_t* out, int n, int method) {

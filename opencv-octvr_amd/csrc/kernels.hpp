@@ -212,6 +212,8 @@ struct MbBlendArgs {
     int64_t out_pitch;
     int out_w, out_h;
     int ax, ay, crop_w, crop_h;     // align_result_roi origin in the output frame, crop size
+    uint8_t* rgba;                  // level 0, scaled output: the RGB result as RGBA (out_w x out_h) instead of YUV
+    int64_t rgba_pitch;
 };
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s);
 // Build time: K4 pyrDown<float, BrdReflect101> with nvcc's FMA contraction (pyr_down.cu:55-192).
@@ -239,6 +241,11 @@ struct ResizeTables {
 };
 hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, int64_t spitch, uint8_t* dst, int dw, int dh,
                             int64_t dpitch, const ResizeTables& t, hipStream_t s);
+
+// Scaled output (mapper.cpp:290-306): cuda::resize INTER_LINEAR of the RGB(A) result (sw x sh,
+// pitch spitch bytes, 4 bytes per pixel) to dw x dh (even), then RGB -> YUV420P into `out`.
+hipError_t launch_resize_rgba_yuv420(const uint8_t* rgba, int sw, int sh, int64_t spitch, uint8_t* out, int dw, int dh,
+                                     int64_t out_pitch, hipStream_t s);
 
 hipError_t launch_selftest_sat(const float* in, uint8_t* out, int n, int method, hipStream_t s);
 

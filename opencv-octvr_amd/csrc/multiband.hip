@@ -327,10 +327,22 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
     for (int p = 0; p < 4; p++)
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) rgb[p][ch] = (uint32_t)min(max(R[p][ch], 0), 255);
+    const int ox = a.ax + x, oy = a.ay + y;
+    const bool in = x < a.crop_w && y < a.crop_h && ox < a.out_w && oy < a.out_h;
+    if (a.rgba) {  // scaled output: the result image itself (resized + converted afterwards)
+        if (!in) return;
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            uint2 v;
+            v.x = rgb[2 * r][0] | (rgb[2 * r][1] << 8) | (rgb[2 * r][2] << 16);
+            v.y = rgb[2 * r + 1][0] | (rgb[2 * r + 1][1] << 8) | (rgb[2 * r + 1][2] << 16);
+            *reinterpret_cast<uint2*>(a.rgba + (int64_t)(oy + r) * a.rgba_pitch + (int64_t)ox * 4) = v;
+        }
+        return;
+    }
     const float one[4] = {1.f, 1.f, 1.f, 1.f};
     const OutFrame of = make_out_frame(a.out, a.out_w, a.out_h, a.out_pitch);
-    const int ox = a.ax + x, oy = a.ay + y;
-    store_quad(of, finish_quad(rgb, one), ox, oy, x < a.crop_w && y < a.crop_h && ox < a.out_w && oy < a.out_h);
+    store_quad(of, finish_quad(rgb, one), ox, oy, in);
 }
 
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s) {

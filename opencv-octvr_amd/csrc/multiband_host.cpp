@@ -521,7 +521,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
 }
 
 void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
-                   int64_t out_pitch, hipStream_t s) {
+                   int64_t out_pitch, hipStream_t s, uint8_t* rgba, int64_t rgba_pitch) {
     auto& L0 = M.lv[0];
     HIP_CHECK(launch_mb_remap(frames, M.remap.view, gains_dev, use_gain,
                               RgbaOut{L0.g.p, (uint32_t)L0.g_bytes, L0.cams.p}, s));
@@ -530,8 +530,12 @@ void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev
         HIP_CHECK(launch_mb_down(L.down_items.p, L.n_down, L.cams.p, M.lv[l - 1].cams.p, M.lv[l - 1].g.p, L.g.p, s));
     }
     if (!M.full_cover) {  // result pixels outside the blended ROI stay 0 (mapper.cpp:155): Y 0, U = V = 128
-        HIP_CHECK(hipMemset2DAsync(out, out_pitch, 0, M.out_w, M.out_h, s));
-        HIP_CHECK(hipMemset2DAsync(out + (int64_t)M.out_h * out_pitch, out_pitch, 128, M.out_w, M.out_h / 2, s));
+        if (rgba) {
+            HIP_CHECK(hipMemset2DAsync(rgba, rgba_pitch, 0, (size_t)M.out_w * 4, M.out_h, s));
+        } else {
+            HIP_CHECK(hipMemset2DAsync(out, out_pitch, 0, M.out_w, M.out_h, s));
+            HIP_CHECK(hipMemset2DAsync(out + (int64_t)M.out_h * out_pitch, out_pitch, 128, M.out_w, M.out_h / 2, s));
+        }
     }
     for (int l = M.B; l >= 0; l--) {
         auto& L = M.lv[l];
@@ -571,6 +575,8 @@ void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev
             a.ay = M.arr.y;
             a.crop_w = M.crop_w;
             a.crop_h = M.crop_h;
+            a.rgba = rgba;
+            a.rgba_pitch = rgba_pitch;
         }
         HIP_CHECK(launch_mb_blend(a, s));
     }

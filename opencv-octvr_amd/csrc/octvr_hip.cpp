@@ -431,6 +431,12 @@ struct octvr_mapper {
     size_t n_entries = 0;
     std::vector<double> last_gains;
     std::vector<DevBuf<float>> vig;  // per camera: vignette map resized to the input size, or empty
+    // scaled output (scaled_output_size != stitch size, mapper.cpp:69,153-155,290-306): the RGB result
+    // as an RGBA frame, resized + converted to YUV420P by a second kernel
+    int SW = 0, SH = 0;
+    bool scaled = false;
+    DevBuf<uint8_t> result;
+    DevBuf<MbCamLevel> result_view;  // the result frame as a one-entry RGBA sink of the composite
     hipStream_t last_stream = nullptr;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
@@ -797,14 +803,19 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         REQUIRE(n_inputs == (int)(rig->inputs.size() + rig->overlays.size()), "in_sizes must cover inputs + overlays");
         REQUIRE(rig->overlays.empty(), "overlay inputs are not implemented in this ABI version");
         REQUIRE((int)rig->inputs.size() <= kMaxCams, "too many inputs");
-        REQUIRE((scale_w == 0 && scale_h == 0) || (scale_w == rig->out_w && scale_h == rig->out_h),
-                "scaled output is not implemented in this ABI version");
+        REQUIRE(scale_w >= 0 && scale_h >= 0 && (scale_w == 0) == (scale_h == 0), "bad scaled output size");
         REQUIRE(rig->out_w % 2 == 0 && rig->out_h % 2 == 0, "YUV420 output needs even width/height");
         auto m = std::make_unique<octvr_mapper>();
         m->device = device;
         m->n = (int)rig->inputs.size();
         m->W = rig->out_w;
         m->H = rig->out_h;
+        // scaled_output_size = scale_output.area() == 0 ? mt.out_size : scale_output (mapper.cpp:69)
+        m->SW = scale_w ? scale_w : m->W;
+        m->SH = scale_h ? scale_h : m->H;
+        REQUIRE(m->SW % 2 == 0 && m->SH % 2 == 0, "YUV420 output needs even width/height");
+        m->scaled = m->SW != m->W || m->SH != m->H;
+        REQUIRE(!m->scaled || (uint64_t)m->W * m->H * 4 < 0x7FFFFF80ull, "stitch frame larger than 2 GiB as RGBA");
         m->in_w.assign(in_w, in_w + n_inputs);
         m->in_h.assign(in_h, in_h + n_inputs);
         for (int i = 0; i < m->n; i++)
@@ -870,6 +881,17 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             }, m->in_w, m->in_h));
             m->n_tiles = tx_n * ty_n;
         }
+        if (m->scaled) {
+            // result = 0 (mapper.cpp:156): pixels no camera writes stay black in every frame
+            m->result.alloc((size_t)m->W * m->H * 4);
+            HIP_CHECK(hipMemset(m->result.p, 0, m->result.n));
+            MbCamLevel v{};
+            v.g_off = 0;
+            v.g_pitch = (uint32_t)m->W * 4;
+            v.w = m->W;
+            v.h = m->H;
+            m->result_view.upload(&v, 1);
+        }
         m->gains.alloc(kMaxCams);
         std::vector<double> ones(kMaxCams, 1.0);
         HIP_CHECK(hipMemcpy(m->gains.p, ones.data(), kMaxCams * sizeof(double), hipMemcpyHostToDevice));
@@ -883,9 +905,9 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream) {
     return guarded([&] {
         REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
-        REQUIRE(out_pitch >= (size_t)m->W, "output pitch smaller than width");
+        REQUIRE(out_pitch >= (size_t)m->SW, "output pitch smaller than width");
         // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
-        REQUIRE((uint64_t)out_pitch * (m->H + m->H / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
+        REQUIRE((uint64_t)out_pitch * (m->SH + m->SH / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
         hipStream_t s = (hipStream_t)stream;
         DeviceGuard dg(m->device);
         FrameSet fs;
@@ -912,10 +934,20 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
             HIP_CHECK(hipEventCreate(&e1));
             HIP_CHECK(hipEventRecord(e0, s));
         }
-        if (m->mb)
+        if (m->scaled) {
+            // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
+            if (m->mb)
+                multiband_run(*m->mb, fs, m->gains.p, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
+            else
+                HIP_CHECK(launch_mb_remap(fs, m->tiles.view, m->gains.p, m->use_gain,
+                                          RgbaOut{m->result.p, (uint32_t)m->result.n, m->result_view.p}, s));
+            HIP_CHECK(launch_resize_rgba_yuv420(m->result.p, m->W, m->H, (int64_t)m->W * 4, out_dev, m->SW, m->SH,
+                                                (int64_t)out_pitch, s));
+        } else if (m->mb) {
             multiband_run(*m->mb, fs, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s);
-        else
+        } else {
             HIP_CHECK(launch_stitch(fs, m->tiles.view, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
+        }
         if (m->timing) {
             HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
@@ -989,9 +1021,9 @@ int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
         snprintf(tmp, sizeof tmp,
                  "{\"inputs\": %d, \"out\": [%d, %d], \"blend\": %d, \"tiles\": %d, \"wide_tiles\": %d, "
                  "\"staged_bytes\": %.0f, \"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, "
-                 "\"gain_chunks\": %d",
+                 "\"gain_chunks\": %d, \"scaled_out\": [%d, %d]",
                  m->n, m->W, m->H, m->blend, m->n_tiles, m->tiles.view.n_wide,
-                 m->mb ? 0.0 : m->tiles.staged_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks);
+                 m->mb ? 0.0 : m->tiles.staged_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks, m->SW, m->SH);
         std::string js = tmp;
         if (m->mb) js += ", " + multiband_info(*m->mb);
         js += "}";

@@ -193,7 +193,8 @@ class Mapper:
         self._h = hd
         self.n = n
         self.device = device
-        self.out_size = mt.out_size
+        # output frame size: scale_output, or the template's out_size (mapper.cpp:69)
+        self.out_size = tuple(scale_output) if scale_output[0] else mt.out_size
 
     def stitch(self, inputs, output, gains=None, stream=None):
         """inputs: list of uint8 cuda tensors (1.5H x W "Y over [U|V]"); output likewise."""

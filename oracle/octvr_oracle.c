@@ -626,6 +626,28 @@ void orc_resize_linear_cuda_u8(const uint8_t* src, int sw, int sh, size_t spitch
         }
 }
 
+void orc_resize_linear_cuda_u8c(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw,
+                                int dh, size_t dpitch) {
+    float fx = resize_inv_scale(dw, sw), fy = resize_inv_scale(dh, sh);
+    for (int y = 0; y < dh; y++)
+        for (int x = 0; x < dw; x++) {
+            float src_x = x * fx, src_y = y * fy;
+            int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+            int x2 = x1 + 1, y2 = y1 + 1;
+            int x2r = x2 < sw - 1 ? x2 : sw - 1, y2r = y2 < sh - 1 ? y2 : sh - 1;
+            float w00 = (x2 - src_x) * (y2 - src_y), w01 = (src_x - x1) * (y2 - src_y);
+            float w10 = (x2 - src_x) * (src_y - y1), w11 = (src_x - x1) * (src_y - y1);
+            for (int c = 0; c < cn; c++) {
+                float out = 0.f;
+                out = fmaf((float)src[(size_t)y1 * spitch + (size_t)x1 * cn + c], w00, out);
+                out = fmaf((float)src[(size_t)y1 * spitch + (size_t)x2r * cn + c], w01, out);
+                out = fmaf((float)src[(size_t)y2r * spitch + (size_t)x1 * cn + c], w10, out);
+                out = fmaf((float)src[(size_t)y2r * spitch + (size_t)x2r * cn + c], w11, out);
+                dst[(size_t)y * dpitch + (size_t)x * cn + c] = sat_u8_rne(out);
+            }
+        }
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Gain compensator (stitching/src/exposure_compensate.cpp:174-297; mapper.cpp:94-114)         */
 /* ------------------------------------------------------------------------------------------ */
@@ -888,7 +910,18 @@ int orc_stitch_frame(const orc_frame* f) {
             parallel_rows(T, 0, r[3], copy_rows, &c);
         }
     }
-    {
+    if (f->scale_w > 0 && (f->scale_w != f->out_w || f->scale_h != f->out_h)) {
+        /* cuda::resize(result, result_scaled, scaled_output_size, INTER_LINEAR) + RGB -> YUV420P (mapper.cpp:290-306) */
+        uint8_t* scaled = (uint8_t*)malloc((size_t)f->scale_w * f->scale_h * 3);
+        orc_resize_linear_cuda_u8c(result, f->out_w, f->out_h, (size_t)f->out_w * 3, 3, scaled, f->scale_w, f->scale_h,
+                                   (size_t)f->scale_w * 3);
+        orc_frame g = *f;
+        g.out_w = f->scale_w;
+        g.out_h = f->scale_h;
+        stage_ctx c = {&g, 0, NULL, NULL, 1.f, scaled, 0, f->scale_h};
+        parallel_rows(T, 0, f->scale_h / 2, out_rows, &c);
+        free(scaled);
+    } else {
         stage_ctx c = {f, 0, NULL, NULL, 1.f, result, rb, re};
         parallel_rows(T, rb / 2, re / 2, out_rows, &c);
     }

@@ -105,6 +105,8 @@ typedef struct {
     int blend;                       /* Mapper blend: 0 copy chain, > 0 multi-band (bands = ceil(log2 blend) - 1), < 0 feather */
     const uint8_t* const* seams;     /* ROI-sized seam masks (multi-band weights); NULL unless blend > 0 */
     const float* const* vig;         /* per camera: vignette gains at input size (in_w x in_h) or NULL; may be NULL */
+    int scale_w, scale_h;            /* scaled output size (mapper.cpp:69, 290-306); 0,0 = out_w x out_h.  When
+                                        set, out_yuv / out_pitch describe the scaled frame and row_begin/end are ignored */
 } orc_frame;
 int orc_stitch_frame(const orc_frame* f);
 
@@ -135,6 +137,9 @@ void orc_resize_nearest_u8(const uint8_t* src, int sw, int sh, size_t spitch, in
                            size_t dpitch);
 void orc_resize_linear_cuda_u8(const uint8_t* src, int sw, int sh, size_t spitch, uint8_t* dst, int dw, int dh,
                                size_t dpitch);
+/* The same kernel on cn interleaved u8 channels (resize_linear<uchar3>, the scaled output's resize). */
+void orc_resize_linear_cuda_u8c(const uint8_t* src, int sw, int sh, size_t spitch, int cn, uint8_t* dst, int dw,
+                                int dh, size_t dpitch);
 
 /* ---- seam masks (octvr_oracle_seam.c) ------------------------------------------ */
 /* cv::resize INTER_LINEAR u8 on the CPU (imgwarp.cpp:3120-3480; fixed point, 11-bit coefficients). */

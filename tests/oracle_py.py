@@ -54,6 +54,7 @@ class OrcFrame(C.Structure):
         ("blend", C.c_int),
         ("seams", C.POINTER(C.c_void_p)),
         ("vig", C.POINTER(C.c_void_p)),
+        ("scale_w", C.c_int), ("scale_h", C.c_int),
     ]
 
 
@@ -293,7 +294,7 @@ def gain_feed(rois, warped, masks, out_w, out_h):
 
 
 def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enable_gain=True, gains=None,
-                 threads=1, row_band=None, blend=0, seams=None, vig=None):
+                 threads=1, row_band=None, blend=0, seams=None, vig=None, scale=None):
     n = len(in_yuv)
     keep = []
 
@@ -306,9 +307,12 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
     map1s = [np.ascontiguousarray(a, np.float32) for a in map1s]
     map2s = [np.ascontiguousarray(a, np.float32) for a in map2s]
     masks = [np.ascontiguousarray(a, np.uint8) for a in masks]
-    out = np.zeros((out_h * 3 // 2, out_w), np.uint8)
+    ow, oh = scale if scale else (out_w, out_h)
+    out = np.zeros((oh * 3 // 2, ow), np.uint8)
     gout = np.zeros(n)
     f = OrcFrame()
+    if scale:
+        f.scale_w, f.scale_h = scale
     f.n = n
     f.in_w = arr(C.c_int, [s[0] for s in in_sizes])
     f.in_h = arr(C.c_int, [s[1] for s in in_sizes])
@@ -320,7 +324,7 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
     f.masks = arr(C.c_void_p, [a.ctypes.data for a in masks])
     f.out_w, f.out_h = out_w, out_h
     f.out_yuv = out.ctypes.data
-    f.out_pitch = out_w
+    f.out_pitch = ow
     f.enable_gain = int(enable_gain)
     gin = None
     if gains is not None:
