@@ -114,6 +114,33 @@ int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launch
 int octvr_mapper_info(const octvr_mapper* mapper, char* buf, size_t len);
 void octvr_mapper_destroy(octvr_mapper* mapper);
 
+/* ---- vr::AsyncMultiMapper -------------------------------------------------------------------- */
+/* AsyncMultiMapper::New(mts, in_sizes, out_size, blend_modes, gain_modes, output_regions, preview)
+ * (modules/octvr/src/async.cpp:195-350, octvr.hpp:103-121): one vr::Mapper per rig, all fed the same
+ * n_inputs camera frames, each writing the region output_regions[4*i .. 4*i+3] = (x, y, w, h) (fractions
+ * of out_w x out_h, async.cpp:20-30) of one merged YUV420P output.  gain_modes[i]: -1 = no gain, i = estimate,
+ * j in [0, i) = use mapper j's gains of the same frame (async.cpp:78-86).  A 3-deep pipeline of pinned host
+ * and device buffers overlaps the host copies, the H2D upload, the stitch and the D2H download of
+ * consecutive frames (async.cpp:32-172); the preview output (Qt shared memory) is not part of the ABI. */
+typedef struct octvr_async octvr_async;
+int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
+                       const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
+                       const double* output_regions, octvr_async** async);
+/* push(inputs, output) (async.cpp:174-189): in_planes[3*i+0/1/2] = Y, U, V host planes of input i
+ * (W x H, W/2 x H/2, W/2 x H/2) with row pitches in_pitches[3*i+k]; out_planes[0/1/2] / out_pitches: the
+ * merged output's Y (out_w x out_h), U and V (out_w/2 x out_h/2) planes.  Returns once the frame is queued;
+ * all planes must stay valid until the matching pop. */
+int octvr_async_push(octvr_async* async, const uint8_t* const* in_planes, const size_t* in_pitches,
+                     uint8_t* const* out_planes, const size_t* out_pitches);
+/* pop() (async.cpp:191-193): blocks until the oldest pushed frame has been written to its output planes;
+ * returns that frame's status (OCTVR_E_INVALID if nothing is pending). */
+int octvr_async_pop(octvr_async* async);
+/* Frames pushed and not yet popped. */
+int octvr_async_pending(const octvr_async* async, int* n);
+/* Drains the frames in flight and joins the pipeline's worker threads (the reference leaves its five
+ * threads running forever, async.cpp:337-349). */
+void octvr_async_destroy(octvr_async* async);
+
 /* ---- standalone kernels --------------------------------------------------------------------- */
 /* cv::remap(src, dst, map1*sx, map2*sy, INTER_LINEAR, BORDER_CONSTANT) on u8 with cn in {1,3,4}
  * channels: 5-bit coordinates, 15-bit weights (imgwarp.cpp:211-280, 3812-4030, 4246-4497). */

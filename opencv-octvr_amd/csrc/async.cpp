@@ -1,0 +1,407 @@
+// async.cpp — vr::AsyncMultiMapper (modules/octvr/src/async.cpp:32-350) on one device.
+//
+// Same five-stage pipeline as the reference — host planes -> pinned staging -> device upload ->
+// stitch of every mapper -> device download -> pinned -> host output planes — over a ring of
+// kSlots buffer sets, so consecutive frames overlap (frame k+2 is copied in while k+1 uploads and
+// k is stitched).  Differences from the reference, all deliberate:
+//   * one HIP stream per stage (upload, compute, download), never the legacy default stream;
+//   * gain chaining (gain_modes[i] = j < i) copies mapper j's device gains on the compute stream
+//     instead of round-tripping them through the host (async.cpp:78-86);
+//   * worker threads are joinable and exit when the object is destroyed (the reference's five
+//     threads loop forever and its destructor clears joinable std::threads, async.cpp:87-90,337-349);
+//   * a failing frame carries its status to pop() instead of asserting.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host_common.hpp"
+
+using namespace octvr;
+
+namespace {
+
+constexpr int kSlots = 3;  // BUF_SIZE (async.cpp:261)
+
+template <class T>
+class Channel {  // blocking FIFO; close() wakes every waiter, pop() then drains what is left
+public:
+    void push(T v) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(std::move(v));
+        }
+        cv_.notify_one();
+    }
+    bool pop(T& out) {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !q_.empty() || closed_; });
+        if (q_.empty()) return false;
+        out = std::move(q_.front());
+        q_.pop_front();
+        return true;
+    }
+    void close() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            closed_ = true;
+        }
+        cv_.notify_all();
+    }
+
+private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<T> q_;
+    bool closed_ = false;
+};
+
+struct Rect {
+    int x, y, w, h;
+};
+
+// _rect_mul_size (async.cpp:20-30)
+Rect rect_mul_size(const double* r, int W, int H) {
+    Rect o{(int)std::round(r[0] * W), (int)std::round(r[1] * H), (int)std::round(r[2] * W), (int)std::round(r[3] * H)};
+    if (o.x + o.w >= W) o.w = W - o.x;
+    if (o.y + o.h >= H) o.h = H - o.y;
+    return o;
+}
+
+struct PinnedBuf {
+    uint8_t* p = nullptr;
+    size_t n = 0;
+    PinnedBuf() = default;
+    PinnedBuf(const PinnedBuf&) = delete;
+    PinnedBuf& operator=(const PinnedBuf&) = delete;
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+    void alloc(size_t bytes) {
+        HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&p), bytes, hipHostMallocDefault));
+        n = bytes;
+    }
+};
+
+struct Slot {  // one frame's staging buffers ("Y over [U|V]" YUV420P, packed rows)
+    std::vector<std::unique_ptr<PinnedBuf>> in_host, out_host;
+    std::vector<DevBuf<uint8_t>> in_dev, out_dev;
+};
+
+struct Job {
+    std::vector<const uint8_t*> in_planes;
+    std::vector<size_t> in_pitches;
+    uint8_t* out_planes[3] = {nullptr, nullptr, nullptr};
+    size_t out_pitches[3] = {0, 0, 0};
+    int slot = -1;
+    int status = OCTVR_OK;
+    std::string error;
+};
+
+template <class F>
+void stage(Job& j, F&& f) {  // run a stage unless the frame already failed; record the first failure
+    if (j.status != OCTVR_OK) return;
+    try {
+        f();
+    } catch (const OctvrError& e) {
+        j.status = e.code;
+        j.error = e.what();
+    } catch (const std::exception& e) {
+        j.status = OCTVR_E_HIP;
+        j.error = e.what();
+    }
+}
+
+}  // namespace
+
+struct octvr_async {
+    int device = 0;
+    int n_in = 0;
+    int out_w = 0, out_h = 0;
+    std::vector<int> in_w, in_h;
+    std::vector<octvr_mapper*> mappers;
+    std::vector<int> gain_modes;
+    std::vector<Rect> regions, regions_uv;  // per mapper: its rectangle in the Y and in the U / V planes
+    Slot slots[kSlots];
+    hipStream_t up = nullptr, comp = nullptr, down = nullptr;
+    Channel<std::shared_ptr<Job>> q_in, q_up, q_map, q_down, q_out, q_done;
+    Channel<int> free_slots;
+    std::vector<std::thread> threads;
+    int pending = 0;  // pushed, not popped (caller thread only)
+
+    ~octvr_async() {
+        q_in.close();
+        for (auto& t : threads)
+            if (t.joinable()) t.join();
+        int prev = -1;
+        (void)hipGetDevice(&prev);
+        (void)hipSetDevice(device);
+        for (hipStream_t s : {up, comp, down})
+            if (s) (void)hipStreamDestroy(s);
+        for (auto& sl : slots) {
+            sl.in_dev.clear();
+            sl.out_dev.clear();
+            sl.in_host.clear();
+            sl.out_host.clear();
+        }
+        for (auto* m : mappers) octvr_mapper_destroy(m);
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+
+    // run_copy_inputs_mat_to_hostmem (async.cpp:32-56)
+    void copy_in(Job& j) {
+        int s = -1;
+        if (!free_slots.pop(s)) throw OctvrError(OCTVR_E_INVALID, "pipeline closed");
+        j.slot = s;
+        stage(j, [&] {
+            for (int i = 0; i < n_in; i++) {
+                const int w = in_w[i], h = in_h[i];
+                uint8_t* dst = slots[s].in_host[i]->p;
+                const uint8_t *Y = j.in_planes[3 * i], *U = j.in_planes[3 * i + 1], *V = j.in_planes[3 * i + 2];
+                for (int y = 0; y < h; y++) memcpy(dst + (size_t)y * w, Y + (size_t)y * j.in_pitches[3 * i], w);
+                for (int y = 0; y < h / 2; y++) {
+                    uint8_t* row = dst + (size_t)(h + y) * w;
+                    memcpy(row, U + (size_t)y * j.in_pitches[3 * i + 1], w / 2);
+                    memcpy(row + w / 2, V + (size_t)y * j.in_pitches[3 * i + 2], w / 2);
+                }
+            }
+        });
+    }
+
+    // run_upload_inputs_hostmem_to_gpumat (async.cpp:58-68)
+    void upload(Job& j) {
+        stage(j, [&] {
+            DeviceGuard dg(device);
+            Slot& sl = slots[j.slot];
+            for (int i = 0; i < n_in; i++)
+                HIP_CHECK(hipMemcpyAsync(sl.in_dev[i].p, sl.in_host[i]->p, sl.in_host[i]->n, hipMemcpyHostToDevice, up));
+            HIP_CHECK(hipStreamSynchronize(up));
+        });
+    }
+
+    // run_do_mapping (async.cpp:70-91)
+    void map(Job& j) {
+        stage(j, [&] {
+            DeviceGuard dg(device);
+            Slot& sl = slots[j.slot];
+            std::vector<const uint8_t*> in(n_in);
+            std::vector<size_t> pitch(n_in);
+            for (int i = 0; i < n_in; i++) {
+                in[i] = sl.in_dev[i].p;
+                pitch[i] = (size_t)in_w[i];
+            }
+            for (size_t k = 0; k < mappers.size(); k++) {
+                const int gm = gain_modes[k];
+                const double* chained = nullptr;
+                if (gm >= 0 && gm < (int)k && mapper_has_gain(mappers[gm])) chained = mapper_gains_dev(mappers[gm]);
+                mapper_stitch(mappers[k], in.data(), pitch.data(), sl.out_dev[k].p, (size_t)regions[k].w, nullptr, 0,
+                              chained, comp);
+            }
+            HIP_CHECK(hipStreamSynchronize(comp));
+        });
+    }
+
+    // run_download_outputs_gpumat_to_hostmem (async.cpp:93-111)
+    void download(Job& j) {
+        stage(j, [&] {
+            DeviceGuard dg(device);
+            Slot& sl = slots[j.slot];
+            for (size_t k = 0; k < mappers.size(); k++)
+                HIP_CHECK(hipMemcpyAsync(sl.out_host[k]->p, sl.out_dev[k].p, sl.out_host[k]->n, hipMemcpyDeviceToHost,
+                                         down));
+            HIP_CHECK(hipStreamSynchronize(down));
+        });
+    }
+
+    // run_copy_outputs_hostmem_to_mat (async.cpp:113-172)
+    void copy_out(Job& j) {
+        stage(j, [&] {
+            Slot& sl = slots[j.slot];
+            for (size_t k = 0; k < mappers.size(); k++) {
+                const Rect& r = regions[k];
+                const Rect& c = regions_uv[k];
+                const uint8_t* src = sl.out_host[k]->p;
+                for (int y = 0; y < r.h; y++)
+                    memcpy(j.out_planes[0] + (size_t)(r.y + y) * j.out_pitches[0] + r.x, src + (size_t)y * r.w, r.w);
+                for (int y = 0; y < c.h; y++) {
+                    const uint8_t* row = src + (size_t)(r.h + y) * r.w;
+                    memcpy(j.out_planes[1] + (size_t)(c.y + y) * j.out_pitches[1] + c.x, row, c.w);
+                    memcpy(j.out_planes[2] + (size_t)(c.y + y) * j.out_pitches[2] + c.x, row + r.w / 2, c.w);
+                }
+            }
+        });
+    }
+
+    template <class F>
+    void worker(Channel<std::shared_ptr<Job>>& in, Channel<std::shared_ptr<Job>>& out, F f) {
+        std::shared_ptr<Job> j;
+        while (in.pop(j)) {
+            f(*j);
+            out.push(std::move(j));
+        }
+        out.close();
+    }
+
+    void start() {
+        threads.emplace_back([this] {
+            std::shared_ptr<Job> j;
+            while (q_in.pop(j)) {
+                try {
+                    copy_in(*j);
+                } catch (const OctvrError& e) {
+                    j->status = e.code;
+                    j->error = e.what();
+                }
+                q_up.push(std::move(j));
+            }
+            q_up.close();
+        });
+        threads.emplace_back([this] { worker(q_up, q_map, [this](Job& j) { upload(j); }); });
+        threads.emplace_back([this] { worker(q_map, q_down, [this](Job& j) { map(j); }); });
+        threads.emplace_back([this] { worker(q_down, q_out, [this](Job& j) { download(j); }); });
+        threads.emplace_back([this] {
+            std::shared_ptr<Job> j;
+            while (q_out.pop(j)) {
+                copy_out(*j);
+                if (j->slot >= 0) free_slots.push(j->slot);
+                q_done.push(std::move(j));
+            }
+            free_slots.close();
+            q_done.close();
+        });
+    }
+};
+
+extern "C" {
+
+int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
+                       const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
+                       const double* output_regions, octvr_async** out) {
+    try {
+        REQUIRE(rigs && n_rigs > 0 && in_w && in_h && blend_modes && gain_modes && output_regions && out,
+                "NULL argument");
+        REQUIRE(n_inputs > 0 && out_w > 0 && out_h > 0 && out_w % 2 == 0 && out_h % 2 == 0, "bad sizes");
+        auto a = std::make_unique<octvr_async>();
+        a->device = device;
+        a->n_in = n_inputs;
+        a->out_w = out_w;
+        a->out_h = out_h;
+        a->in_w.assign(in_w, in_w + n_inputs);
+        a->in_h.assign(in_h, in_h + n_inputs);
+        a->gain_modes.assign(gain_modes, gain_modes + n_rigs);
+        for (int i = 0; i < n_inputs; i++)
+            REQUIRE(in_w[i] > 0 && in_h[i] > 0 && in_w[i] % 2 == 0 && in_h[i] % 2 == 0, "input sizes must be even");
+        for (int k = 0; k < n_rigs; k++) {
+            REQUIRE(rigs[k], "NULL rig");
+            const Rect r = rect_mul_size(output_regions + 4 * k, out_w, out_h);
+            const Rect c = rect_mul_size(output_regions + 4 * k, out_w / 2, out_h / 2);
+            REQUIRE(r.x >= 0 && r.y >= 0 && r.w > 0 && r.h > 0 && r.w % 2 == 0 && r.h % 2 == 0,
+                    "output region must be a non-empty even-sized rectangle inside the output");
+            // the reference copies the mapper's U / V planes into the region of the output's U / V planes
+            // (async.cpp:133-135); a size mismatch would reallocate the destination instead
+            REQUIRE(c.w == r.w / 2 && c.h == r.h / 2, "output region's chroma rectangle is not half its luma rectangle");
+            a->regions.push_back(r);
+            a->regions_uv.push_back(c);
+            octvr_mapper* m = nullptr;
+            // Mapper(mts[i], in_sizes, blend_modes[i], gain_modes[i] >= 0, r.size()) (async.cpp:250-255)
+            const int rc = octvr_mapper_create(rigs[k], device, n_inputs, in_w, in_h, blend_modes[k],
+                                               gain_modes[k] >= 0 ? 1 : 0, r.w, r.h, &m);
+            if (rc != OCTVR_OK) throw OctvrError(rc, std::string("mapper ") + std::to_string(k) + ": " + octvr_last_error());
+            a->mappers.push_back(m);
+            REQUIRE(mapper_num_inputs(m) == n_inputs, "every rig must have n_inputs inputs (no overlays)");
+        }
+        DeviceGuard dg(device);
+        HIP_CHECK(hipStreamCreateWithFlags(&a->up, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&a->comp, hipStreamNonBlocking));
+        HIP_CHECK(hipStreamCreateWithFlags(&a->down, hipStreamNonBlocking));
+        for (auto& sl : a->slots) {
+            for (int i = 0; i < n_inputs; i++) {
+                const size_t bytes = (size_t)in_w[i] * (in_h[i] / 2 * 3);
+                sl.in_host.emplace_back(new PinnedBuf());
+                sl.in_host.back()->alloc(bytes);
+                sl.in_dev.emplace_back();
+                sl.in_dev.back().alloc(bytes);
+            }
+            for (int k = 0; k < n_rigs; k++) {
+                const size_t bytes = (size_t)a->regions[k].w * (a->regions[k].h / 2 * 3);
+                sl.out_host.emplace_back(new PinnedBuf());
+                sl.out_host.back()->alloc(bytes);
+                sl.out_dev.emplace_back();
+                sl.out_dev.back().alloc(bytes);
+            }
+        }
+        for (int s = 0; s < kSlots; s++) a->free_slots.push(s);
+        a->start();
+        *out = a.release();
+        return OCTVR_OK;
+    } catch (const OctvrError& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return OCTVR_E_HIP;
+    }
+}
+
+int octvr_async_push(octvr_async* a, const uint8_t* const* in_planes, const size_t* in_pitches,
+                     uint8_t* const* out_planes, const size_t* out_pitches) {
+    if (!a || !in_planes || !in_pitches || !out_planes || !out_pitches) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    auto j = std::make_shared<Job>();
+    j->in_planes.assign(in_planes, in_planes + 3 * a->n_in);
+    j->in_pitches.assign(in_pitches, in_pitches + 3 * a->n_in);
+    for (int i = 0; i < a->n_in; i++)
+        if (!in_planes[3 * i] || !in_planes[3 * i + 1] || !in_planes[3 * i + 2] || in_pitches[3 * i] < (size_t)a->in_w[i] ||
+            in_pitches[3 * i + 1] < (size_t)a->in_w[i] / 2 || in_pitches[3 * i + 2] < (size_t)a->in_w[i] / 2) {
+            set_last_error("bad input plane");
+            return OCTVR_E_INVALID;
+        }
+    for (int k = 0; k < 3; k++) {
+        j->out_planes[k] = out_planes[k];
+        j->out_pitches[k] = out_pitches[k];
+        if (!out_planes[k] || out_pitches[k] < (size_t)(k ? a->out_w / 2 : a->out_w)) {
+            set_last_error("bad output plane");
+            return OCTVR_E_INVALID;
+        }
+    }
+    a->q_in.push(std::move(j));
+    a->pending++;
+    return OCTVR_OK;
+}
+
+int octvr_async_pop(octvr_async* a) {
+    if (!a || a->pending <= 0) {
+        set_last_error("no frame pending");
+        return OCTVR_E_INVALID;
+    }
+    std::shared_ptr<Job> j;
+    if (!a->q_done.pop(j)) {
+        set_last_error("pipeline closed");
+        return OCTVR_E_INVALID;
+    }
+    a->pending--;
+    if (j->status != OCTVR_OK) set_last_error(j->error);
+    return j->status;
+}
+
+int octvr_async_pending(const octvr_async* a, int* n) {
+    if (!a || !n) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    *n = a->pending;
+    return OCTVR_OK;
+}
+
+void octvr_async_destroy(octvr_async* a) { delete a; }
+
+}  // extern "C"

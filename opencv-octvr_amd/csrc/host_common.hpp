@@ -34,6 +34,9 @@ struct OctvrError : std::runtime_error {
         if (!(cond)) throw ::octvr::OctvrError(OCTVR_E_INVALID, (msg));     \
     } while (0)
 
+// octvr_last_error() text of the calling thread (octvr_hip.cpp).
+void set_last_error(const std::string& msg);
+
 // Scoped device selection: restores the caller's current device.
 struct DeviceGuard {
     int prev = -1;
@@ -99,6 +102,14 @@ namespace octvr {
 void rig_create_masks(octvr_rig& rig);
 // cv::distanceTransform(src, dst, DIST_L2, 3) on the host (distransform.cpp:48-139); w x h, packed
 void chamfer_l2_3x3(const uint8_t* src, int w, int h, float* dist);
+
+// ---- mapper internals used by the AsyncMultiMapper pipeline (octvr_hip.cpp, async.cpp) -----------
+void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch, uint8_t* out_dev,
+                   size_t out_pitch, const double* gains, int n_gains, const double* gains_dev, hipStream_t s);
+int mapper_num_inputs(const octvr_mapper* m);
+bool mapper_has_gain(const octvr_mapper* m);
+const double* mapper_gains_dev(const octvr_mapper* m);
+void mapper_out_size(const octvr_mapper* m, int* w, int* h);
 
 // ---- tiled composite LUT builder (tiling.cpp) ----------------------------------------------------
 struct TileJob {

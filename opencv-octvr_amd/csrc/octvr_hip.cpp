@@ -50,6 +50,8 @@ int guarded(F&& f) {
 
 }  // namespace
 
+void octvr::set_last_error(const std::string& msg) { g_last_error = msg; }
+
 namespace {
 
 // ---- camera setup from JSON (camera.cpp:49-136 and the per-type constructors) ------------------
@@ -603,6 +605,77 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
 // =================================================================================================
 // extern "C" entry points
 // =================================================================================================
+namespace octvr {
+
+// Mapper::stitch (mapper.cpp:193-323).  gains_dev (device, n doubles): gains of another mapper of the
+// same inputs, copied stream-ordered (AsyncMultiMapper's gain_modes chaining, async.cpp:78-86).
+void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch, uint8_t* out_dev,
+                   size_t out_pitch, const double* gains, int n_gains, const double* gains_dev, hipStream_t s) {
+    {
+        REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
+        REQUIRE(out_pitch >= (size_t)m->SW, "output pitch smaller than width");
+        // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
+        REQUIRE((uint64_t)out_pitch * (m->SH + m->SH / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
+        DeviceGuard dg(m->device);
+        FrameSet fs;
+        memset(&fs, 0, sizeof fs);
+        for (int i = 0; i < m->n; i++) {
+            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
+            fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
+        }
+        if (m->use_gain) {
+            if (gains_dev) {
+                HIP_CHECK(hipMemcpyAsync(m->gains.p, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
+            } else if (gains) {
+                REQUIRE(n_gains == m->n, "gains must have one entry per input");
+                HIP_CHECK(launch_set_gains(gains, m->n, m->gains.p, s));
+            } else if (m->n_chunks == 0) {  // no intersections: A = diag(b), every gain is 1
+                const std::vector<double> ones(m->n, 1.0);
+                HIP_CHECK(launch_set_gains(ones.data(), m->n, m->gains.p, s));
+            } else {
+                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->chunks.p, m->n_chunks, m->N.p, m->n,
+                                           m->totals.p, m->tickets.p, m->gains.p, s));
+            }
+        }
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (m->timing) {
+            HIP_CHECK(hipEventCreate(&e0));
+            HIP_CHECK(hipEventCreate(&e1));
+            HIP_CHECK(hipEventRecord(e0, s));
+        }
+        if (m->scaled) {
+            // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
+            if (m->mb)
+                multiband_run(*m->mb, fs, m->gains.p, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
+            else
+                HIP_CHECK(launch_mb_remap(fs, m->tiles.view, m->gains.p, m->use_gain,
+                                          RgbaOut{m->result.p, (uint32_t)m->result.n, m->result_view.p}, s));
+            HIP_CHECK(launch_resize_rgba_yuv420(m->result.p, m->W, m->H, (int64_t)m->W * 4, out_dev, m->SW, m->SH,
+                                                (int64_t)out_pitch, s));
+        } else if (m->mb) {
+            multiband_run(*m->mb, fs, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s);
+        } else {
+            HIP_CHECK(launch_stitch(fs, m->tiles.view, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
+        }
+        if (m->timing) {
+            HIP_CHECK(hipEventRecord(e1, s));
+            m->events.emplace_back(e0, e1);
+        }
+        m->last_stream = s;
+    }
+}
+
+int mapper_num_inputs(const octvr_mapper* m) { return m->n; }
+bool mapper_has_gain(const octvr_mapper* m) { return m->use_gain != 0; }
+const double* mapper_gains_dev(const octvr_mapper* m) { return m->gains.p; }
+void mapper_out_size(const octvr_mapper* m, int* w, int* h) {
+    *w = m->SW;
+    *h = m->SH;
+}
+
+
+}  // namespace octvr
+
 extern "C" {
 
 int octvr_abi_version(void) { return OCTVR_HIP_ABI_VERSION; }
@@ -904,55 +977,7 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
 int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch,
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream) {
     return guarded([&] {
-        REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
-        REQUIRE(out_pitch >= (size_t)m->SW, "output pitch smaller than width");
-        // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
-        REQUIRE((uint64_t)out_pitch * (m->SH + m->SH / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
-        hipStream_t s = (hipStream_t)stream;
-        DeviceGuard dg(m->device);
-        FrameSet fs;
-        memset(&fs, 0, sizeof fs);
-        for (int i = 0; i < m->n; i++) {
-            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
-            fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
-        }
-        if (m->use_gain) {
-            if (gains) {
-                REQUIRE(n_gains == m->n, "gains must have one entry per input");
-                HIP_CHECK(launch_set_gains(gains, m->n, m->gains.p, s));
-            } else if (m->n_chunks == 0) {  // no intersections: A = diag(b), every gain is 1
-                const std::vector<double> ones(m->n, 1.0);
-                HIP_CHECK(launch_set_gains(ones.data(), m->n, m->gains.p, s));
-            } else {
-                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->chunks.p, m->n_chunks, m->N.p, m->n,
-                                           m->totals.p, m->tickets.p, m->gains.p, s));
-            }
-        }
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (m->timing) {
-            HIP_CHECK(hipEventCreate(&e0));
-            HIP_CHECK(hipEventCreate(&e1));
-            HIP_CHECK(hipEventRecord(e0, s));
-        }
-        if (m->scaled) {
-            // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
-            if (m->mb)
-                multiband_run(*m->mb, fs, m->gains.p, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
-            else
-                HIP_CHECK(launch_mb_remap(fs, m->tiles.view, m->gains.p, m->use_gain,
-                                          RgbaOut{m->result.p, (uint32_t)m->result.n, m->result_view.p}, s));
-            HIP_CHECK(launch_resize_rgba_yuv420(m->result.p, m->W, m->H, (int64_t)m->W * 4, out_dev, m->SW, m->SH,
-                                                (int64_t)out_pitch, s));
-        } else if (m->mb) {
-            multiband_run(*m->mb, fs, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s);
-        } else {
-            HIP_CHECK(launch_stitch(fs, m->tiles.view, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
-        }
-        if (m->timing) {
-            HIP_CHECK(hipEventRecord(e1, s));
-            m->events.emplace_back(e0, e1);
-        }
-        m->last_stream = s;
+        mapper_stitch(m, in_dev, in_pitch, out_dev, out_pitch, gains, n_gains, nullptr, (hipStream_t)stream);
     });
 }
 

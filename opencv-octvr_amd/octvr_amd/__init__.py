@@ -68,6 +68,14 @@ _lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(
 _lib.octvr_mapper_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
 _lib.octvr_mapper_destroy.argtypes = [_VP]
 _lib.octvr_mapper_destroy.restype = None
+_lib.octvr_async_create.argtypes = [C.POINTER(_VP), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                    C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
+                                    C.POINTER(_VP)]
+_lib.octvr_async_push.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), C.POINTER(_VP), C.POINTER(C.c_size_t)]
+_lib.octvr_async_pop.argtypes = [_VP]
+_lib.octvr_async_pending.argtypes = [_VP, C.POINTER(C.c_int)]
+_lib.octvr_async_destroy.argtypes = [_VP]
+_lib.octvr_async_destroy.restype = None
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
                                 C.c_float, C.c_float, _VP, C.c_size_t, _VP]
 
@@ -237,6 +245,67 @@ class Mapper:
         if self._h and self._h.value:
             _lib.octvr_mapper_destroy(self._h)
             self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class AsyncMultiMapper:
+    """vr::AsyncMultiMapper (modules/octvr/src/async.cpp): host YUV420P planes in, host planes out, through
+    a 3-deep pinned-buffer pipeline (copy-in, H2D, stitch, D2H, copy-out overlap across frames).
+
+    templates: list of MapperTemplate (all with the same inputs); output_regions: list of (x, y, w, h)
+    fractions of out_size; gain_modes[i]: -1 no gain, i estimate, j < i reuse mapper j's gains."""
+
+    def __init__(self, templates, in_sizes, out_size, blend_modes, gain_modes, output_regions, device=0):
+        k, n = len(templates), len(in_sizes)
+        rigs = (_VP * k)(*[t._h.value for t in templates])
+        w = (C.c_int * n)(*[s[0] for s in in_sizes])
+        h = (C.c_int * n)(*[s[1] for s in in_sizes])
+        bm = (C.c_int * k)(*blend_modes)
+        gm = (C.c_int * k)(*gain_modes)
+        rg = (C.c_double * (4 * k))(*[float(v) for r in output_regions for v in r])
+        hd = _VP()
+        _check(_lib.octvr_async_create(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg, C.byref(hd)))
+        self._h = hd
+        self._templates = list(templates)  # the mappers copy what they need; kept for symmetry with the reference
+        self.n = n
+        self.out_size = tuple(out_size)
+        self._inflight = []
+
+    def push(self, inputs, output):
+        """inputs: list of (Y, U, V) uint8 numpy planes per camera; output: (Y, U, V) planes of the merged
+        frame.  The arrays are kept alive until the matching pop()."""
+        planes = [p if p.strides[1] == 1 else np.ascontiguousarray(p) for tri in inputs for p in tri]
+        for p in list(planes) + list(output):
+            assert p.dtype == np.uint8 and p.ndim == 2 and p.strides[1] == 1, "uint8 2-D planes with unit column stride"
+        ip = (_VP * len(planes))(*[p.ctypes.data for p in planes])
+        ipt = (C.c_size_t * len(planes))(*[p.strides[0] for p in planes])
+        op = (_VP * 3)(*[p.ctypes.data for p in output])
+        opt = (C.c_size_t * 3)(*[p.strides[0] for p in output])
+        _check(_lib.octvr_async_push(self._h, ip, ipt, op, opt))
+        self._inflight.append((planes, output))
+
+    def pop(self):
+        """Blocks until the oldest pushed frame is written; returns its output planes."""
+        rc = _lib.octvr_async_pop(self._h)
+        output = self._inflight.pop(0)[1] if self._inflight else None
+        _check(rc)
+        return output
+
+    def pending(self):
+        n = C.c_int()
+        _check(_lib.octvr_async_pending(self._h, C.byref(n)))
+        return n.value
+
+    def close(self):
+        if self._h and self._h.value:
+            _lib.octvr_async_destroy(self._h)
+            self._h = C.c_void_p(0)
+            self._inflight = []
 
     def __del__(self):
         try:
