@@ -3,11 +3,18 @@
 // __host__ __device__ so the same arithmetic runs in the gfx950 LUT kernel and in host-side setup.
 // The order of every floating-point operation follows the reference so results agree bit-for-bit
 // with it wherever the libm calls agree (the translation unit is built with -ffp-contract=off):
-//   sphere helpers          modules/octvr/src/camera.cpp:189-210
+//   sphere helpers            modules/octvr/src/camera.cpp:189-210
 //   obj_to_image/image_to_obj camera.cpp:212-253, 296-315
-//   equirectangular         modules/octvr/src/cameras/equirectangular.cpp:25-35
-//   fullframe_fisheye       modules/octvr/src/cameras/fullframe_fisheye_cam.cpp:146-221
-//   fisheye (OpenCV KB)     modules/octvr/src/cameras/pinhole_cam.cpp:32-50 + calib3d/src/fisheye.cpp:95-146
+//   equirectangular           modules/octvr/src/cameras/equirectangular.cpp:25-35
+//   fullframe_fisheye         modules/octvr/src/cameras/fullframe_fisheye_cam.cpp:146-221
+//   fisheye (OpenCV KB)       modules/octvr/src/cameras/pinhole_cam.cpp:32-50 + calib3d/src/fisheye.cpp:95-146
+//   pinhole (projectPoints)   pinhole_cam.cpp:32-57 + calib3d/src/calibration.cpp:759-793
+//   normal                    modules/octvr/src/cameras/normal.cpp:24-39
+//   perspective               modules/octvr/src/cameras/perspective.cpp:21-33
+//   ocam_fisheye              modules/octvr/src/cameras/ocam_fisheye.cpp:135-244
+//   stupidoval                modules/octvr/src/cameras/stupidoval.hpp:24-36
+//   cubic                     modules/octvr/src/cameras/cubic.hpp:19-103
+//   eqareanorthpole / -south  modules/octvr/src/cameras/eqareanorthpole.hpp:24-41, eqareasouthpole.hpp:23-40
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -16,22 +23,46 @@
 
 namespace octvr {
 
-enum CameraType : int32_t { CAM_EQUIRECT = 0, CAM_FULLFRAME_FISHEYE = 1, CAM_FISHEYE = 2 };
+enum CameraType : int32_t {
+    CAM_EQUIRECT = 0,
+    CAM_FULLFRAME_FISHEYE = 1,
+    CAM_FISHEYE = 2,
+    CAM_PINHOLE = 3,
+    CAM_NORMAL = 4,
+    CAM_PERSPECTIVE = 5,
+    CAM_OCAM = 6,
+    CAM_STUPIDOVAL = 7,
+    CAM_CUBIC = 8,
+    CAM_EQAREA_NORTH = 9,
+    CAM_EQAREA_SOUTH = 10,
+};
 
-// Plain-old-data camera description, copied to the device by value as a kernel argument.
+constexpr int kOcamMaxPol = 64;  // MAX_POL_LENGTH (ocam_fisheye.hpp:21)
+
+// Plain-old-data camera description; the LUT kernel reads it from device memory.
 struct CameraParams {
     int32_t type;
-    int32_t width, height;                      // input image size (fisheye models)
+    int32_t width, height;                      // input image size (fisheye / pinhole / ocam / masks)
     int32_t crop_x, crop_y, crop_w, crop_h;     // fullframe_fisheye crop rect
     int32_t crop_circular;
-    int32_t pad_;
+    int32_t sel;                                // `selection` present: exclude everything outside sel_*
+    int32_t sel_l, sel_r, sel_t, sel_b;         // selection rectangle (camera.cpp:96-112)
+    int32_t len_pol, len_invpol;                // ocam polynomial lengths
     double R[9];                                // rotate_matrix (camera.cpp:57-70)
     double Rinv[9];                             // rotate_matrix.inv() (camera.cpp:205)
     double min_lon, max_lon;                    // longitude_selection (camera.cpp:125-135)
-    double min_lat, max_lat, scale_lon;         // equirectangular.hpp:61-62
+    double min_lat, max_lat, scale_lon;         // equirectangular.hpp:26-27
     double hfov, center_dx, center_dy;          // fullframe_fisheye_cam.cpp:128-130
     double rad[6];                              // radial_distortion[0..5] (fullframe_fisheye_cam.cpp:133-138)
-    double fx, fy, cx, cy, k[4];                // pinhole_cam.cpp:13-30
+    double fx, fy, cx, cy, k[4];                // fisheye / pinhole intrinsics (pinhole_cam.cpp:13-30)
+    double dist[14];                            // pinhole: projectPoints distortion k1..tauY (zero padded)
+    double tilt[9];                             // pinhole: matTilt (identity unless tauX / tauY != 0)
+    double aspect;                              // normal / perspective aspect_ratio
+    double cam_x, cam_y, cam_z;                 // normal.cpp:16-19
+    double sf;                                  // perspective.cpp:16
+    double circle;                              // eqarea: arctic_circle / antarctic_circle
+    double xc, yc, oc, od, oe;                  // ocam: center and affine parameters c, d, e
+    double pol[kOcamMaxPol], invpol[kOcamMaxPol];
 };
 
 #define OCTVR_HD __host__ __device__ inline
@@ -55,12 +86,17 @@ OCTVR_HD void rotate_rows(const double* r, const double* p, double* q) {
     }
 }
 
+// sphere_xyz_to_lonlat: p = xyz * (1 / norm(xyz)) (camera.cpp:189-192)
 OCTVR_HD void xyz_to_lonlat(const double* xyz, double* lon, double* lat) {
     double n = sqrt(xyz[0] * xyz[0] + xyz[1] * xyz[1] + xyz[2] * xyz[2]);
     double inv = 1.0 / n;
     double px = xyz[0] * inv, py = xyz[1] * inv, pz = xyz[2] * inv;
     *lon = atan2(-pz, px);
     *lat = asin(py);
+}
+OCTVR_HD void xyz3_to_lonlat(double x, double y, double z, double* lon, double* lat) {
+    const double p[3] = {x, y, z};
+    xyz_to_lonlat(p, lon, lat);
 }
 
 OCTVR_HD bool valid_longitude(const CameraParams& c, double l) {
@@ -69,11 +105,126 @@ OCTVR_HD bool valid_longitude(const CameraParams& c, double l) {
            between(l - 4 * kPi);
 }
 
+// ---- image_to_obj_single (output cameras) -------------------------------------------------------
 OCTVR_HD void equirect_image_to_obj(const CameraParams& c, double x, double y, double* lon, double* lat) {
     *lon = (x - 0.5) * kPi * 2.0;
     *lat = (c.min_lat - c.max_lat) * y + c.max_lat;
 }
 
+// cam2world (ocam_fisheye.cpp:135-166); point2D = (row, col)
+OCTVR_HD void ocam_cam2world(const CameraParams& c, const double* p2, double* p3) {
+    double invdet = 1 / (c.oc - c.od * c.oe);
+    double xp = invdet * ((p2[0] - c.xc) - c.od * (p2[1] - c.yc));
+    double yp = invdet * (-c.oe * (p2[0] - c.xc) + c.oc * (p2[1] - c.yc));
+    double r = sqrt(xp * xp + yp * yp);
+    double zp = c.pol[0];
+    double r_i = 1;
+    for (int i = 1; i < c.len_pol; i++) {
+        r_i *= r;
+        zp += r_i * c.pol[i];
+    }
+    double invnorm = 1 / sqrt(xp * xp + yp * yp + zp * zp);
+    p3[0] = invnorm * xp;
+    p3[1] = invnorm * yp;
+    p3[2] = invnorm * zp;
+}
+
+// world2cam (ocam_fisheye.cpp:183-225)
+OCTVR_HD void ocam_world2cam(const CameraParams& c, const double* p3, double* p2) {
+    double norm = sqrt(p3[0] * p3[0] + p3[1] * p3[1]);
+    double theta = atan(p3[2] / norm);
+    if (norm != 0) {
+        double invnorm = 1 / norm;
+        double t = theta;
+        double rho = c.invpol[0];
+        double t_i = 1;
+        for (int i = 1; i < c.len_invpol; i++) {
+            t_i *= t;
+            rho += t_i * c.invpol[i];
+        }
+        double x = p3[0] * invnorm * rho;
+        double y = p3[1] * invnorm * rho;
+        p2[0] = x * c.oc + y * c.od + c.xc;
+        p2[1] = x * c.oe + y + c.yc;
+    } else {
+        p2[0] = c.xc;
+        p2[1] = c.yc;
+    }
+}
+
+// Output camera: (x, y) in [0,1)^2 -> lonlat before the output rotation; NaN when undefined.
+OCTVR_HD void image_to_obj_single(const CameraParams& c, double x, double y, double* lon, double* lat) {
+    switch (c.type) {
+        case CAM_NORMAL: {
+            double xx = c.cam_x;
+            double yy = c.cam_y - y * 2.0 * c.cam_y;
+            double zz = c.cam_z - x * 2.0 * c.cam_z;
+            xyz3_to_lonlat(xx, yy, zz, lon, lat);
+            return;
+        }
+        case CAM_PERSPECTIVE: {
+            double z = (0.5 - x) * c.aspect;
+            double yy = 0.5 - y;
+            double xx = 1.0 / c.sf;
+            xyz3_to_lonlat(xx, yy, z, lon, lat);
+            return;
+        }
+        case CAM_OCAM: {
+            double p2[2] = {y * c.height, x * c.width}, p3[3];
+            ocam_cam2world(c, p2, p3);
+            xyz3_to_lonlat(-p3[2], -p3[0], -p3[1], lon, lat);
+            return;
+        }
+        case CAM_STUPIDOVAL: {
+            double la = (0.5 - y) * kPi;
+            double lo = (x - 0.5) * kPi * 2.0 / cos(la);
+            if (lo < -kPi || lo > kPi) {
+                *lon = *lat = NAN;
+                return;
+            }
+            *lon = lo;
+            *lat = la;
+            return;
+        }
+        case CAM_CUBIC: {
+            int ix = 0, iy = 0;
+            if (y >= 0.5) iy = 1;
+            if (x >= 2.0 / 3.0)
+                ix = 2;
+            else if (x >= 1.0 / 3.0)
+                ix = 1;
+            double px = (x - ix * 1.0 / 3.0) * 3.0 * 2.0 - 1.0;
+            double py = (y - iy * 1.0 / 2.0) * 2.0 * 2.0 - 1.0;
+            switch (iy * 3 + ix) {
+                case 0: xyz3_to_lonlat(1.0, py, px, lon, lat); return;
+                case 1: xyz3_to_lonlat(-1., py, -px, lon, lat); return;
+                case 2: xyz3_to_lonlat(px, -1., -py, lon, lat); return;
+                case 3: xyz3_to_lonlat(px, 1.0, py, lon, lat); return;
+                case 4: xyz3_to_lonlat(px, py, -1.0, lon, lat); return;
+                default: xyz3_to_lonlat(-px, py, 1.0, lon, lat); return;
+            }
+        }
+        case CAM_EQAREA_NORTH: {
+            double dx = x - 0.5, dy = y - 0.5;
+            double rho = sqrt(dx * dx + dy * dy) * 2;
+            *lat = kPi / 2 - (kPi / 2 - c.circle) * rho;
+            *lon = atan2(-dx, -dy);
+            return;
+        }
+        case CAM_EQAREA_SOUTH: {
+            double dx = x - 0.5, dy = y - 0.5;
+            double rho = sqrt(dx * dx + dy * dy) * 2;
+            *lat = -kPi / 2 + (c.circle + kPi / 2) * rho;
+            *lon = atan2(dx, -dy);
+            return;
+        }
+        default:
+            equirect_image_to_obj(c, x, y, lon, lat);
+            return;
+    }
+}
+
+// ---- obj_to_image_single (input cameras) --------------------------------------------------------
 OCTVR_HD void equirect_obj_to_image(const CameraParams& c, double lon, double lat, double* x, double* y) {
     *x = lon / (kPi * 2.0) + 0.5;
     *y = (lat - c.max_lat) / (c.min_lat - c.max_lat);
@@ -111,6 +262,129 @@ OCTVR_HD void fullframe_fisheye_obj_to_image(const CameraParams& c, double lon, 
     *oy = ry;
 }
 
+OCTVR_HD void cubic_face_to_img(int index, double x, double y, double* ox, double* oy) {
+    double rx = (index % 3) * 1.0 / 3.0, ry = (index / 3) * 1.0 / 2.0;
+    rx += (x + 1.0) / 2.0 / 3.0;
+    ry += (y + 1.0) / 2.0 / 2.0;
+    *ox = rx;
+    *oy = ry;
+}
+
+OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat, double* ox, double* oy) {
+    switch (c.type) {
+        case CAM_FULLFRAME_FISHEYE:
+            fullframe_fisheye_obj_to_image(c, lon, lat, ox, oy);
+            return;
+        case CAM_NORMAL: {
+            double p[3];
+            lonlat_to_xyz(lon, lat, p);
+            if (p[0] < 0) {
+                *ox = *oy = NAN;
+                return;
+            }
+            const double t = p[0] / c.cam_x;  // xxyyzz /= (xxyyzz.x / cam_x)
+            p[0] /= t;
+            p[1] /= t;
+            p[2] /= t;
+            *ox = (c.cam_z - p[2]) / 2.0 / c.cam_z;
+            *oy = (c.cam_y - p[1]) / 2.0 / c.cam_y;
+            return;
+        }
+        case CAM_PERSPECTIVE: {
+            double p[3];
+            lonlat_to_xyz(lon, lat, p);
+            double y_ = p[1] * (1.0 / c.sf / p[0]);
+            double z_ = p[2] * (1.0 / c.sf / p[0]);
+            *ox = 0.5 - z_ / c.aspect;
+            *oy = 0.5 - y_;
+            return;
+        }
+        case CAM_OCAM: {
+            double p[3];
+            lonlat_to_xyz(lon, lat, p);
+            const double q[3] = {-p[1], -p[2], -p[0]};
+            double p2[2];
+            ocam_world2cam(c, q, p2);
+            *ox = p2[1] / c.width;
+            *oy = p2[0] / c.height;
+            return;
+        }
+        case CAM_STUPIDOVAL:
+            *ox = cos(lat) * lon / (kPi * 2.0) + 0.5;
+            *oy = -lat / kPi + 0.5;
+            return;
+        case CAM_CUBIC: {
+            double p[3], s[3];
+            lonlat_to_xyz(lon, lat, p);
+            auto within = [](double a, double b) { return a >= -1.0 && a <= 1.0 && b >= -1.0 && b <= 1.0; };
+            if (fabs(p[0]) > 1e-2) {  // intersect with x = 1 / x = -1
+                const double f = fabs(p[0]);
+                s[0] = p[0] / f;
+                s[1] = p[1] / f;
+                s[2] = p[2] / f;
+                if (within(s[1], s[2])) {
+                    if (s[0] < 0)
+                        cubic_face_to_img(1, -s[2], s[1], ox, oy);
+                    else
+                        cubic_face_to_img(0, s[2], s[1], ox, oy);
+                    return;
+                }
+            }
+            if (fabs(p[2]) > 1e-2) {
+                const double f = fabs(p[2]);
+                s[0] = p[0] / f;
+                s[1] = p[1] / f;
+                s[2] = p[2] / f;
+                if (within(s[0], s[1])) {
+                    if (s[2] < 0)
+                        cubic_face_to_img(4, s[0], s[1], ox, oy);
+                    else
+                        cubic_face_to_img(5, -s[0], s[1], ox, oy);
+                    return;
+                }
+            }
+            if (fabs(p[1]) > 1e-2) {
+                const double f = fabs(p[1]);
+                s[0] = p[0] / f;
+                s[1] = p[1] / f;
+                s[2] = p[2] / f;
+                if (within(s[0], s[2])) {
+                    if (s[1] < 0)
+                        cubic_face_to_img(2, s[0], -s[2], ox, oy);
+                    else
+                        cubic_face_to_img(3, s[0], s[2], ox, oy);
+                    return;
+                }
+            }
+            *ox = *oy = NAN;
+            return;
+        }
+        case CAM_EQAREA_NORTH: {
+            if (lat < c.circle) {
+                *ox = *oy = NAN;
+                return;
+            }
+            double rho = (kPi / 2 - lat) / (kPi / 2 - c.circle);
+            *ox = -rho * sin(lon) / 2 + 0.5;
+            *oy = -rho * cos(lon) / 2 + 0.5;
+            return;
+        }
+        case CAM_EQAREA_SOUTH: {
+            if (lat > c.circle) {
+                *ox = *oy = NAN;
+                return;
+            }
+            double rho = (lat + kPi / 2) / (c.circle + kPi / 2);
+            *ox = rho * sin(lon) / 2 + 0.5;
+            *oy = -rho * cos(lon) / 2 + 0.5;
+            return;
+        }
+        default:
+            equirect_obj_to_image(c, lon, lat, ox, oy);
+            return;
+    }
+}
+
 // Y is the rotated sphere point; Kannala-Brandt projection with zero rvec/tvec and alpha = 0.
 OCTVR_HD void fisheye_project(const CameraParams& c, const double* Y, double* ox, double* oy) {
     if (Y[2] <= 0) {
@@ -134,14 +408,63 @@ OCTVR_HD void fisheye_project(const CameraParams& c, const double* Y, double* ox
     *oy = 1.0 - v / c.height;
 }
 
+// cvProjectPoints2 for one point with rvec = tvec = 0 (R = I, t = 0) (calibration.cpp:759-793).
+// Y is the rotated sphere point (z <= 0 was mapped to NaN by PinholeCamera::obj_to_image).
+OCTVR_HD void pinhole_project(const CameraParams& c, const double* Y, double* ox, double* oy) {
+    double X = Y[0], Yy = Y[1], Z = Y[2];
+    if (Z <= 0) X = Yy = Z = NAN;
+    const double* k = c.dist;
+    double x = 1.0 * X + 0.0 * Yy + 0.0 * Z + 0.0;
+    double y = 0.0 * X + 1.0 * Yy + 0.0 * Z + 0.0;
+    double z = 0.0 * X + 0.0 * Yy + 1.0 * Z + 0.0;
+    z = z ? 1. / z : 1;
+    x *= z;
+    y *= z;
+    double r2 = x * x + y * y;
+    double r4 = r2 * r2;
+    double r6 = r4 * r2;
+    double a1 = 2 * x * y;
+    double a2 = r2 + 2 * x * x;
+    double a3 = r2 + 2 * y * y;
+    double cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
+    double icdist2 = 1. / (1 + k[5] * r2 + k[6] * r4 + k[7] * r6);
+    double xd0 = x * cdist * icdist2 + k[2] * a1 + k[3] * a2 + k[8] * r2 + k[9] * r4;
+    double yd0 = y * cdist * icdist2 + k[2] * a3 + k[3] * a1 + k[10] * r2 + k[11] * r4;
+    // vecTilt = matTilt * Vec3d(xd0, yd0, 1) (Matx product: s = 0; s += a(i,k) * b(k))
+    double v[3];
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        s += c.tilt[i * 3 + 0] * xd0;
+        s += c.tilt[i * 3 + 1] * yd0;
+        s += c.tilt[i * 3 + 2] * 1.0;
+        v[i] = s;
+    }
+    double invProj = v[2] ? 1. / v[2] : 1;
+    double xd = invProj * v[0];
+    double yd = invProj * v[1];
+    double u = xd * c.fx + c.cx, vv = yd * c.fy + c.cy;
+    *ox = u / c.width;
+    *oy = 1.0 - vv / c.height;
+}
+
+// Camera::obj_to_image exclude-mask test for a `selection` rectangle (camera.cpp:96-112, 239-246):
+// the mask is 255 outside the filled rectangle [l, r-1] x [t, b-1] of the width x height image.
+OCTVR_HD bool selection_excludes(const CameraParams& c, double x, double y) {
+    if (!c.sel) return false;
+    const int W = (int)(x * c.width), H = (int)(y * c.height);
+    return !(W >= c.sel_l && W <= c.sel_r - 1 && H >= c.sel_t && H <= c.sel_b - 1);
+}
+
 // Output pixel (u, v) in [0,1)^2 -> input camera normalized image point (x, y) or NaN.
 OCTVR_HD void project_output_to_input(const CameraParams& out, const CameraParams& in, double u, double v,
                                       double* x, double* y) {
     double lon, lat, p[3], q[3];
-    equirect_image_to_obj(out, u, v, &lon, &lat);
+    // out->image_to_obj (camera.cpp:296-315)
+    image_to_obj_single(out, u, v, &lon, &lat);
     lonlat_to_xyz(lon, lat, p);
     rotate_rows(out.Rinv, p, q);
     xyz_to_lonlat(q, &lon, &lat);
+    // in->obj_to_image (camera.cpp:212-253; PinholeCamera overrides it, pinhole_cam.cpp:32-50)
     lonlat_to_xyz(lon, lat, p);
     bool lon_ok = valid_longitude(in, lon);
     rotate_rows(in.R, p, q);
@@ -149,15 +472,15 @@ OCTVR_HD void project_output_to_input(const CameraParams& out, const CameraParam
         fisheye_project(in, q, x, y);
         return;
     }
+    if (in.type == CAM_PINHOLE) {
+        pinhole_project(in, q, x, y);
+        return;
+    }
     double ll, la;
     xyz_to_lonlat(q, &ll, &la);
     double px = NAN, py = NAN;
-    if (lon_ok) {
-        if (in.type == CAM_FULLFRAME_FISHEYE)
-            fullframe_fisheye_obj_to_image(in, ll, la, &px, &py);
-        else
-            equirect_obj_to_image(in, ll, la, &px, &py);
-    }
+    if (lon_ok) obj_to_image_single(in, ll, la, &px, &py);
+    if (px >= 0 && px < 1 && py >= 0 && py < 1 && selection_excludes(in, px, py)) px = py = NAN;
     *x = px;
     *y = py;
 }

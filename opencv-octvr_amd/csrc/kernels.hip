@@ -22,8 +22,10 @@ namespace octvr {
 // LUT build: MapperTemplate::add_input (template.cpp:46-133), one thread per output pixel, FP64.
 // bbox = {min_w, min_h, max_w, max_h} of valid pixels (int atomics, initialised by the host).
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) lut_build_kernel(CameraParams out, CameraParams in, int W, int H, float* map1,
-                                                        float* map2, uint8_t* mask, int32_t* bbox) {
+__global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __restrict__ cams, int W, int H,
+                                                        float* map1, float* map2, uint8_t* mask, int32_t* bbox) {
+    const CameraParams& out = cams[0];
+    const CameraParams& in = cams[1];
     __shared__ int s_bb[4];
     if (threadIdx.x < 4) s_bb[threadIdx.x] = (threadIdx.x < 2) ? INT32_MAX : -1;
     __syncthreads();
@@ -64,12 +66,12 @@ __global__ void __launch_bounds__(256) lut_build_kernel(CameraParams out, Camera
     }
 }
 
-hipError_t launch_lut_build(const CameraParams& out, const CameraParams& in, int W, int H, float* map1, float* map2,
-                            uint8_t* mask, int32_t* bbox, hipStream_t s) {
+hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
+                            int32_t* bbox, hipStream_t s) {
     const int64_t total = (int64_t)W * H;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(lut_build_kernel, dim3(blocks), dim3(256), 0, s, out, in, W, H, map1, map2, mask, bbox);
+    hipLaunchKernelGGL(lut_build_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, W, H, map1, map2, mask, bbox);
     return hipGetLastError();
 }
 

@@ -114,8 +114,9 @@ struct GainChunk {
     int32_t pad_;
 };
 
-hipError_t launch_lut_build(const CameraParams& out, const CameraParams& in, int W, int H, float* map1, float* map2,
-                            uint8_t* mask, int32_t* bbox, hipStream_t s);
+// cams_dev: {output camera, input camera} in device memory (CameraParams holds the ocam polynomials).
+hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
+                            int32_t* bbox, hipStream_t s);
 
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
                                 hipStream_t s);

@@ -159,10 +159,62 @@ double correction_radius(const double* coeff) {
 }
 
 void reject_unsupported_options(const JsonValue& o, const std::string& type) {
-    for (const char* k : {"selection", "exclude_masks", "include_masks"})
+    // polygon / PNG masks need cv::fillPoly / cv::imdecode on the host (camera.cpp:114-123,146-187)
+    for (const char* k : {"exclude_masks", "include_masks"})
         if (o.has(k))
             throw OctvrError(OCTVR_E_UNSUPPORTED, std::string("camera option '") + k + "' (" + type +
                                                       ") is not implemented in this ABI version");
+}
+
+// computeTiltProjectionMatrix (imgproc/detail/distortion_model.hpp:74-94), Matx products s += a*b.
+void tilt_matrix(double tauX, double tauY, double* T) {
+    auto mul = [](const double* a, const double* b, double* d) {
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) {
+                double v = 0;
+                for (int k = 0; k < 3; k++) v += a[i * 3 + k] * b[k * 3 + j];
+                d[i * 3 + j] = v;
+            }
+    };
+    const double cX = cos(tauX), sX = sin(tauX), cY = cos(tauY), sY = sin(tauY);
+    const double rx[9] = {1, 0, 0, 0, cX, sX, 0, -sX, cX};
+    const double ry[9] = {cY, 0, -sY, 0, 1, 0, sY, 0, cY};
+    double rxy[9];
+    mul(ry, rx, rxy);
+    const double pz[9] = {rxy[8], 0, -rxy[2], 0, rxy[8], -rxy[5], 0, 0, 1};
+    mul(pz, rxy, T);
+}
+
+// get_ocam_model (ocam_fisheye.cpp:19-80): the calibration TXT file of the OCamCalib toolbox.
+void read_ocam_file(const std::string& path, CameraParams& c) {
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) throw OctvrError(OCTVR_E_IO, "ocam_fisheye: cannot open " + path);
+    char buf[1024];
+    int ok = 1;
+    auto line = [&] { ok &= fgets(buf, sizeof buf, f) != nullptr; };
+    line();
+    ok &= fscanf(f, "\n") >= 0;
+    ok &= fscanf(f, "%d", &c.len_pol) == 1;
+    ok &= c.len_pol > 0 && c.len_pol <= kOcamMaxPol;
+    for (int i = 0; ok && i < c.len_pol; i++) ok &= fscanf(f, " %lf", &c.pol[i]) == 1;
+    ok &= fscanf(f, "\n") >= 0;
+    line();
+    ok &= fscanf(f, "\n") >= 0;
+    ok &= fscanf(f, "%d", &c.len_invpol) == 1;
+    ok &= c.len_invpol > 0 && c.len_invpol <= kOcamMaxPol;
+    for (int i = 0; ok && i < c.len_invpol; i++) ok &= fscanf(f, " %lf", &c.invpol[i]) == 1;
+    ok &= fscanf(f, "\n") >= 0;
+    line();
+    ok &= fscanf(f, "\n") >= 0;
+    ok &= fscanf(f, "%lf %lf\n", &c.xc, &c.yc) == 2;
+    line();
+    ok &= fscanf(f, "\n") >= 0;
+    ok &= fscanf(f, "%lf %lf %lf\n", &c.oc, &c.od, &c.oe) == 3;
+    line();
+    ok &= fscanf(f, "\n") >= 0;
+    ok &= fscanf(f, "%d %d", &c.height, &c.width) == 2;
+    fclose(f);
+    if (!ok) throw OctvrError(OCTVR_E_PARSE, "ocam_fisheye: malformed calibration file " + path);
 }
 
 CameraParams camera_from_json(const JsonValue& cam) {
@@ -243,23 +295,100 @@ CameraParams camera_from_json(const JsonValue& cam) {
         for (int k = 0; k < 4; k++) c.k[k] = o["dist_coeffs"][k].as_double();
         c.width = o["width"].as_int();
         c.height = o["height"].as_int();
+    } else if (type == "pinhole") {  // PinholeCamera (pinhole_cam.cpp:13-30) + cv::projectPoints
+        c.type = CAM_PINHOLE;
+        c.fx = o["fx"].as_double();
+        c.fy = o["fy"].as_double();
+        c.cx = o["cx"].as_double();
+        c.cy = o["cy"].as_double();
+        const size_t nd = o.has("dist_coeffs") ? o["dist_coeffs"].size() : 0;
+        REQUIRE(nd == 0 || nd == 4 || nd == 5 || nd == 8 || nd == 12 || nd == 14,
+                "pinhole: dist_coeffs must have 4, 5, 8, 12 or 14 entries (calibration.cpp:644-655)");
+        for (size_t k = 0; k < nd; k++) c.dist[k] = o["dist_coeffs"][k].as_double();
+        for (int k = 0; k < 9; k++) c.tilt[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        if (c.dist[12] != 0 || c.dist[13] != 0) tilt_matrix(c.dist[12], c.dist[13], c.tilt);
+        c.width = o["width"].as_int();
+        c.height = o["height"].as_int();
+    } else if (type == "normal") {  // normal.cpp:13-22
+        c.type = CAM_NORMAL;
+        c.aspect = o["aspect_ratio"].as_double();
+        c.cam_x = o["cam_opt"].as_double();
+        c.cam_z = sqrt((1.0 - c.cam_x * c.cam_x) / (1.0 + 1.0 / c.aspect / c.aspect));
+        c.cam_y = c.cam_z / c.aspect;
+    } else if (type == "perspective") {  // perspective.cpp:14-19
+        c.type = CAM_PERSPECTIVE;
+        c.aspect = o["aspect_ratio"].as_double();
+        c.sf = o["sf"].as_double();
+    } else if (type == "ocam_fisheye") {  // ocam_fisheye.cpp:82-110
+        c.type = CAM_OCAM;
+        if (o.has("file")) {
+            read_ocam_file(o["file"].as_string(), c);
+        } else {
+            const JsonValue& pol = o["pol"];
+            const JsonValue& inv = o["invpol"];
+            c.len_pol = (int)pol.size();
+            c.len_invpol = (int)inv.size();
+            REQUIRE(c.len_pol > 0 && c.len_pol <= kOcamMaxPol && c.len_invpol > 0 && c.len_invpol <= kOcamMaxPol,
+                    "ocam_fisheye: pol / invpol must have 1..64 entries");
+            for (int i = 0; i < c.len_pol; i++) c.pol[i] = pol[i].as_double();
+            for (int i = 0; i < c.len_invpol; i++) c.invpol[i] = inv[i].as_double();
+            c.xc = o["xc"].as_double();
+            c.yc = o["yc"].as_double();
+            c.oc = o["c"].as_double();
+            c.od = o["d"].as_double();
+            c.oe = o["e"].as_double();
+            c.width = o["width"].as_int();
+            c.height = o["height"].as_int();
+        }
+    } else if (type == "stupidoval") {
+        c.type = CAM_STUPIDOVAL;
+    } else if (type == "cubic") {
+        c.type = CAM_CUBIC;
+    } else if (type == "eqareanorthpole") {  // eqareanorthpole.hpp:11-18
+        c.type = CAM_EQAREA_NORTH;
+        c.circle = o.get("arctic_circle", kPi / 3);
+    } else if (type == "eqareasouthpole") {  // eqareasouthpole.hpp:10-17
+        c.type = CAM_EQAREA_SOUTH;
+        c.circle = o.get("antarctic_circle", -kPi / 3);
     } else {
         throw OctvrError(OCTVR_E_UNSUPPORTED, "camera type '" + type + "' is not implemented in this ABI version");
+    }
+    if (o.has("selection")) {  // exclude everything outside the rectangle (camera.cpp:96-112)
+        REQUIRE(o.has("width") && o.has("height"), "selection needs the camera's width and height");
+        c.sel = 1;
+        c.width = o["width"].as_int();
+        c.height = o["height"].as_int();
+        c.sel_l = o["selection"][0].as_int();
+        c.sel_r = o["selection"][1].as_int();
+        c.sel_t = o["selection"][2].as_int();
+        c.sel_b = o["selection"][3].as_int();
     }
     return c;
 }
 
 double aspect_ratio(const JsonValue& cam) {
-    // Camera::get_aspect_ratio overrides (equirectangular.hpp:67-69, fullframe_fisheye_cam.cpp:142-144,
-    // pinhole_cam.hpp get_aspect_ratio)
-    const std::string& t = cam["type"].as_string();
-    const JsonValue& o = cam["options"];
-    if (t == "equirectangular") {
-        double mn = o.get("min_lat", -kPi / 2), mx = o.get("max_lat", kPi / 2), sl = o.get("scale_lon", 1.0);
-        return (2.0f * sl) / ((mx - mn) / kPi);
+    // Camera::get_aspect_ratio overrides (equirectangular.hpp:32-34, fullframe_fisheye_cam.cpp:142-144,
+    // pinhole_cam.hpp:32-34, normal.hpp:26-28, perspective.hpp:24-26, ocam_fisheye.cpp:112-114,
+    // stupidoval.hpp:21-23, cubic.hpp:43-45, eqarea*.hpp: 1)
+    const CameraParams c = camera_from_json(cam);
+    switch (c.type) {
+        case CAM_EQUIRECT:
+            return (2.0f * c.scale_lon) / ((c.max_lat - c.min_lat) / kPi);
+        case CAM_FULLFRAME_FISHEYE:
+        case CAM_FISHEYE:
+        case CAM_PINHOLE:
+        case CAM_OCAM:
+            return double(c.width) / c.height;
+        case CAM_NORMAL:
+        case CAM_PERSPECTIVE:
+            return c.aspect;
+        case CAM_STUPIDOVAL:
+            return 2.0;
+        case CAM_CUBIC:
+            return 3.0 / 2.0;
+        default:
+            return 1.0;
     }
-    if (t == "fullframe_fisheye" || t == "fisheye") return double(o["width"].as_int()) / o["height"].as_int();
-    return 1.0;
 }
 
 // Vignette::getMap (vignette.cpp:18-54) at 512x512.
@@ -299,7 +428,10 @@ void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H
     bb.alloc(4);
     int32_t init[4] = {INT32_MAX, INT32_MAX, -1, -1};
     HIP_CHECK(hipMemcpy(bb.p, init, sizeof init, hipMemcpyHostToDevice));
-    HIP_CHECK(launch_lut_build(out_cam, c, W, H, m1.p, m2.p, mk.p, bb.p, nullptr));
+    const CameraParams both[2] = {out_cam, c};
+    DevBuf<CameraParams> cams;
+    cams.upload(both, 2);
+    HIP_CHECK(launch_lut_build(cams.p, W, H, m1.p, m2.p, mk.p, bb.p, nullptr));
     HIP_CHECK(hipDeviceSynchronize());
     int32_t b[4];
     HIP_CHECK(hipMemcpy(b, bb.p, sizeof b, hipMemcpyDeviceToHost));
@@ -723,7 +855,10 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
         double ar = aspect_ratio(oc);
         if (out_h <= 0) out_h = int(double(out_w) / ar);
         if (out_w <= 0) out_w = int(double(out_h) * ar);
-        REQUIRE(out_cam.type == CAM_EQUIRECT, "only equirectangular output is implemented in this ABI version");
+        // the output camera needs image_to_obj_single: fisheye / pinhole throw NotImplemented (camera.hpp:101-103);
+        // fullframe_fisheye's needs cv::solvePoly (fullframe_fisheye_cam.cpp:160-184), not provided here
+        if (out_cam.type == CAM_FULLFRAME_FISHEYE || out_cam.type == CAM_FISHEYE || out_cam.type == CAM_PINHOLE)
+            throw OctvrError(OCTVR_E_UNSUPPORTED, "output camera type '" + oc["type"].as_string() + "' is not supported");
         auto rig = std::make_unique<octvr_rig>();
         rig->out_w = out_w;
         rig->out_h = out_h;

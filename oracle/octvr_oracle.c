@@ -193,6 +193,75 @@ void orc_camera_fisheye(orc_camera* c, int width, int height, double fx, double 
     for (int i = 0; i < 4; i++) c->k[i] = k[i];
 }
 
+/* computeTiltProjectionMatrix (imgproc/include/opencv2/imgproc/detail/distortion_model.hpp:74-94);
+ * Matx products accumulate s = 0; s += a(i,k) * b(k,j). */
+static void matx33_mul(const double* a, const double* b, double* d) {
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            double s = 0;
+            for (int k = 0; k < 3; k++) s += a[i * 3 + k] * b[k * 3 + j];
+            d[i * 3 + j] = s;
+        }
+}
+static void tilt_projection(double tauX, double tauY, double* T) {
+    double cTauX = cos(tauX), sTauX = sin(tauX), cTauY = cos(tauY), sTauY = sin(tauY);
+    double rotX[9] = {1, 0, 0, 0, cTauX, sTauX, 0, -sTauX, cTauX};
+    double rotY[9] = {cTauY, 0, -sTauY, 0, 1, 0, sTauY, 0, cTauY};
+    double rotXY[9];
+    matx33_mul(rotY, rotX, rotXY);
+    double projZ[9] = {rotXY[8], 0, -rotXY[2], 0, rotXY[8], -rotXY[5], 0, 0, 1};
+    matx33_mul(projZ, rotXY, T);
+}
+
+void orc_camera_pinhole(orc_camera* c, int width, int height, double fx, double fy, double cx, double cy,
+                        const double* dist, int nd) {
+    camera_defaults(c, ORC_PINHOLE);
+    c->width = width;
+    c->height = height;
+    c->fx = fx; c->fy = fy; c->cx = cx; c->cy = cy;
+    for (int i = 0; i < nd && i < 14; i++) c->dist[i] = dist[i];
+    for (int i = 0; i < 9; i++) c->tilt[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    if (c->dist[12] != 0 || c->dist[13] != 0) tilt_projection(c->dist[12], c->dist[13], c->tilt);
+}
+
+void orc_camera_normal(orc_camera* c, double aspect_ratio, double cam_opt) {
+    camera_defaults(c, ORC_NORMAL);
+    c->aspect = aspect_ratio;
+    c->cam_x = cam_opt;
+    c->cam_z = sqrt((1.0 - c->cam_x * c->cam_x) / (1.0 + 1.0 / c->aspect / c->aspect));
+    c->cam_y = c->cam_z / c->aspect;
+}
+
+void orc_camera_perspective(orc_camera* c, double aspect_ratio, double sf) {
+    camera_defaults(c, ORC_PERSPECTIVE);
+    c->aspect = aspect_ratio;
+    c->sf = sf;
+}
+
+void orc_camera_ocam(orc_camera* c, const double* pol, int len_pol, const double* invpol, int len_invpol, double xc,
+                     double yc, double cc, double d, double e, int width, int height) {
+    camera_defaults(c, ORC_OCAM);
+    c->len_pol = len_pol;
+    c->len_invpol = len_invpol;
+    for (int i = 0; i < len_pol && i < 64; i++) c->pol[i] = pol[i];
+    for (int i = 0; i < len_invpol && i < 64; i++) c->invpol[i] = invpol[i];
+    c->xc = xc; c->yc = yc; c->oc = cc; c->od = d; c->oe = e;
+    c->width = width;
+    c->height = height;
+}
+
+void orc_camera_simple(orc_camera* c, int type, double circle) {
+    camera_defaults(c, type);
+    c->circle = circle;
+}
+
+void orc_camera_set_selection(orc_camera* c, int width, int height, int l, int r, int t, int b) {
+    c->sel = 1;
+    c->width = width;
+    c->height = height;
+    c->sel_l = l; c->sel_r = r; c->sel_t = t; c->sel_b = b;
+}
+
 /* ------------------------------------------------------------------------------------------ */
 /* Sphere helpers (camera.cpp:189-210)                                                         */
 /* ------------------------------------------------------------------------------------------ */
@@ -295,11 +364,226 @@ static void fisheye_project(const orc_camera* c, const double* Y, double* ox, do
     *oy = 1.0 - v / c->height;
 }
 
+/* cv::projectPoints (calibration.cpp:759-793) of one rotated point with rvec = tvec = 0 (R = I). */
+static void pinhole_project(const orc_camera* c, const double* P, double* ox, double* oy) {
+    double X = P[0], Y = P[1], Z = P[2];
+    if (Z <= 0) X = Y = Z = NAN; /* pinhole_cam.cpp:38-40 */
+    const double* k = c->dist;
+    const double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, t[3] = {0, 0, 0};
+    double x = R[0] * X + R[1] * Y + R[2] * Z + t[0];
+    double y = R[3] * X + R[4] * Y + R[5] * Z + t[1];
+    double z = R[6] * X + R[7] * Y + R[8] * Z + t[2];
+    z = z ? 1. / z : 1;
+    x *= z; y *= z;
+    double r2 = x * x + y * y, r4 = r2 * r2, r6 = r4 * r2;
+    double a1 = 2 * x * y, a2 = r2 + 2 * x * x, a3 = r2 + 2 * y * y;
+    double cdist = 1 + k[0] * r2 + k[1] * r4 + k[4] * r6;
+    double icdist2 = 1. / (1 + k[5] * r2 + k[6] * r4 + k[7] * r6);
+    double xd0 = x * cdist * icdist2 + k[2] * a1 + k[3] * a2 + k[8] * r2 + k[9] * r4;
+    double yd0 = y * cdist * icdist2 + k[2] * a3 + k[3] * a1 + k[10] * r2 + k[11] * r4;
+    double vec[3] = {xd0, yd0, 1}, vt[3];
+    for (int i = 0; i < 3; i++) {
+        double s = 0;
+        for (int j = 0; j < 3; j++) s += c->tilt[i * 3 + j] * vec[j];
+        vt[i] = s;
+    }
+    double invProj = vt[2] ? 1. / vt[2] : 1;
+    double xd = invProj * vt[0], yd = invProj * vt[1];
+    double u = xd * c->fx + c->cx, v = yd * c->fy + c->cy;
+    *ox = u / c->width;           /* pinhole_cam.cpp:48 */
+    *oy = 1.0 - v / c->height;
+}
+
+/* OCamCalib cam2world / world2cam (ocam_fisheye.cpp:135-225). */
+static void ocam_cam2world(const orc_camera* m, const double* p2, double* p3) {
+    double invdet = 1 / (m->oc - m->od * m->oe);
+    double xp = invdet * ((p2[0] - m->xc) - m->od * (p2[1] - m->yc));
+    double yp = invdet * (-m->oe * (p2[0] - m->xc) + m->oc * (p2[1] - m->yc));
+    double r = sqrt(xp * xp + yp * yp);
+    double zp = m->pol[0], r_i = 1;
+    for (int i = 1; i < m->len_pol; i++) { r_i *= r; zp += r_i * m->pol[i]; }
+    double invnorm = 1 / sqrt(xp * xp + yp * yp + zp * zp);
+    p3[0] = invnorm * xp; p3[1] = invnorm * yp; p3[2] = invnorm * zp;
+}
+static void ocam_world2cam(const orc_camera* m, const double* p3, double* p2) {
+    double norm = sqrt(p3[0] * p3[0] + p3[1] * p3[1]);
+    double theta = atan(p3[2] / norm);
+    if (norm != 0) {
+        double invnorm = 1 / norm, t = theta, rho = m->invpol[0], t_i = 1;
+        for (int i = 1; i < m->len_invpol; i++) { t_i *= t; rho += t_i * m->invpol[i]; }
+        double x = p3[0] * invnorm * rho, y = p3[1] * invnorm * rho;
+        p2[0] = x * m->oc + y * m->od + m->xc;
+        p2[1] = x * m->oe + y + m->yc;
+    } else {
+        p2[0] = m->xc;
+        p2[1] = m->yc;
+    }
+}
+
+static void lonlat_of(double x, double y, double z, double* lon, double* lat) {
+    double p[3] = {x, y, z};
+    xyz_to_lonlat(p, lon, lat);
+}
+
+/* image_to_obj_single of the output camera types (the cameras/ files cited in octvr_oracle.h). */
+static void image_to_obj_single(const orc_camera* c, double x, double y, double* lon, double* lat) {
+    switch (c->type) {
+    case ORC_NORMAL: /* normal.cpp:24-30 */
+        lonlat_of(c->cam_x, c->cam_y - y * 2.0 * c->cam_y, c->cam_z - x * 2.0 * c->cam_z, lon, lat);
+        return;
+    case ORC_PERSPECTIVE: /* perspective.cpp:21-26 */
+        lonlat_of(1.0 / c->sf, 0.5 - y, (0.5 - x) * c->aspect, lon, lat);
+        return;
+    case ORC_OCAM: { /* ocam_fisheye.cpp:237-244 */
+        double p2[2] = {y * c->height, x * c->width}, p3[3];
+        ocam_cam2world(c, p2, p3);
+        lonlat_of(-p3[2], -p3[0], -p3[1], lon, lat);
+        return;
+    }
+    case ORC_STUPIDOVAL: { /* stupidoval.hpp:30-36 */
+        double la = (0.5 - y) * M_PI;
+        double lo = (x - 0.5) * M_PI * 2.0 / cos(la);
+        if (lo < -M_PI || lo > M_PI) { *lon = *lat = NAN; return; }
+        *lon = lo; *lat = la;
+        return;
+    }
+    case ORC_CUBIC: { /* cubic.hpp:26-37, 86-103 */
+        int index_x = 0, index_y = 0;
+        if (y >= 0.5) index_y = 1;
+        if (x >= 2.0 / 3.0) index_x = 2;
+        else if (x >= 1.0 / 3.0) index_x = 1;
+        double fx = (x - index_x * 1.0 / 3.0) * 3.0 * 2.0 - 1.0;
+        double fy = (y - index_y * 1.0 / 2.0) * 2.0 * 2.0 - 1.0;
+        int face = index_y * 3 + index_x;
+        if (face == 0) lonlat_of(1.0, fy, fx, lon, lat);
+        else if (face == 1) lonlat_of(-1., fy, -fx, lon, lat);
+        else if (face == 2) lonlat_of(fx, -1., -fy, lon, lat);
+        else if (face == 3) lonlat_of(fx, 1.0, fy, lon, lat);
+        else if (face == 4) lonlat_of(fx, fy, -1.0, lon, lat);
+        else lonlat_of(-fx, fy, 1.0, lon, lat);
+        return;
+    }
+    case ORC_EQAREA_NORTH: { /* eqareanorthpole.hpp:35-41 */
+        double dx = x - 0.5, dy = y - 0.5;
+        double rho = sqrt(dx * dx + dy * dy) * 2;
+        *lat = M_PI / 2 - (M_PI / 2 - c->circle) * rho;
+        *lon = atan2(-dx, -dy);
+        return;
+    }
+    case ORC_EQAREA_SOUTH: { /* eqareasouthpole.hpp:34-40 */
+        double dx = x - 0.5, dy = y - 0.5;
+        double rho = sqrt(dx * dx + dy * dy) * 2;
+        *lat = -M_PI / 2 + (c->circle + M_PI / 2) * rho;
+        *lon = atan2(dx, -dy);
+        return;
+    }
+    default:
+        equirect_i2o(c, x, y, lon, lat);
+    }
+}
+
+static void cubic_face_to_img(int index, double x, double y, double* ox, double* oy) {
+    double rx = (index % 3) * 1.0 / 3.0, ry = (index / 3) * 1.0 / 2.0;
+    rx += (x + 1.0) / 2.0 / 3.0;
+    ry += (y + 1.0) / 2.0 / 2.0;
+    *ox = rx; *oy = ry;
+}
+
+/* obj_to_image_single of the non-fisheye input camera types. */
+static void obj_to_image_single(const orc_camera* c, double lon, double lat, double* ox, double* oy) {
+    double p[3];
+    switch (c->type) {
+    case ORC_FULLFRAME_FISHEYE:
+        ffisheye_o2i(c, lon, lat, ox, oy);
+        return;
+    case ORC_NORMAL: { /* normal.cpp:32-39 */
+        lonlat_to_xyz(lon, lat, p);
+        if (p[0] < 0) { *ox = *oy = NAN; return; }
+        double div = p[0] / c->cam_x;
+        p[0] = p[0] / div; p[1] = p[1] / div; p[2] = p[2] / div;
+        *ox = (c->cam_z - p[2]) / 2.0 / c->cam_z;
+        *oy = (c->cam_y - p[1]) / 2.0 / c->cam_y;
+        return;
+    }
+    case ORC_PERSPECTIVE: { /* perspective.cpp:28-33 */
+        lonlat_to_xyz(lon, lat, p);
+        double y_ = p[1] * (1.0 / c->sf / p[0]);
+        double z_ = p[2] * (1.0 / c->sf / p[0]);
+        *ox = 0.5 - z_ / c->aspect;
+        *oy = 0.5 - y_;
+        return;
+    }
+    case ORC_OCAM: { /* ocam_fisheye.cpp:227-235 */
+        lonlat_to_xyz(lon, lat, p);
+        double p3[3] = {-p[1], -p[2], -p[0]}, p2[2];
+        ocam_world2cam(c, p3, p2);
+        *ox = p2[1] / c->width;
+        *oy = p2[0] / c->height;
+        return;
+    }
+    case ORC_STUPIDOVAL: /* stupidoval.hpp:24-29 */
+        *ox = cos(lat) * lon / (M_PI * 2.0) + 0.5;
+        *oy = -lat / M_PI + 0.5;
+        return;
+    case ORC_CUBIC: { /* cubic.hpp:47-84 */
+        lonlat_to_xyz(lon, lat, p);
+        double sp[3], f;
+#define WITHIN(a, b) ((a) >= -1.0 && (a) <= 1.0 && (b) >= -1.0 && (b) <= 1.0)
+        if (fabs(p[0]) > 1e-2) {
+            f = fabs(p[0]);
+            sp[0] = p[0] / f; sp[1] = p[1] / f; sp[2] = p[2] / f;
+            if (WITHIN(sp[1], sp[2])) {
+                if (sp[0] < 0) cubic_face_to_img(1, -sp[2], sp[1], ox, oy);
+                else cubic_face_to_img(0, sp[2], sp[1], ox, oy);
+                return;
+            }
+        }
+        if (fabs(p[2]) > 1e-2) {
+            f = fabs(p[2]);
+            sp[0] = p[0] / f; sp[1] = p[1] / f; sp[2] = p[2] / f;
+            if (WITHIN(sp[0], sp[1])) {
+                if (sp[2] < 0) cubic_face_to_img(4, sp[0], sp[1], ox, oy);
+                else cubic_face_to_img(5, -sp[0], sp[1], ox, oy);
+                return;
+            }
+        }
+        if (fabs(p[1]) > 1e-2) {
+            f = fabs(p[1]);
+            sp[0] = p[0] / f; sp[1] = p[1] / f; sp[2] = p[2] / f;
+            if (WITHIN(sp[0], sp[2])) {
+                if (sp[1] < 0) cubic_face_to_img(2, sp[0], -sp[2], ox, oy);
+                else cubic_face_to_img(3, sp[0], sp[2], ox, oy);
+                return;
+            }
+        }
+#undef WITHIN
+        *ox = *oy = NAN;
+        return;
+    }
+    case ORC_EQAREA_NORTH: { /* eqareanorthpole.hpp:24-33 */
+        if (lat < c->circle) { *ox = *oy = NAN; return; }
+        double rho = (M_PI / 2 - lat) / (M_PI / 2 - c->circle);
+        *ox = -rho * sin(lon) / 2 + 0.5;
+        *oy = -rho * cos(lon) / 2 + 0.5;
+        return;
+    }
+    case ORC_EQAREA_SOUTH: { /* eqareasouthpole.hpp:23-32 */
+        if (lat > c->circle) { *ox = *oy = NAN; return; }
+        double rho = (lat + M_PI / 2) / (c->circle + M_PI / 2);
+        *ox = rho * sin(lon) / 2 + 0.5;
+        *oy = -rho * cos(lon) / 2 + 0.5;
+        return;
+    }
+    default:
+        equirect_o2i(c, lon, lat, ox, oy);
+    }
+}
+
 /* One output pixel through out->image_to_obj then in->obj_to_image (camera.cpp:212-253, 296-315). */
 static void project_pixel(const orc_camera* out, const orc_camera* in, double u, double v, double* x, double* y) {
     double lon, lat, p[3], q[3];
     /* output: image_to_obj */
-    equirect_i2o(out, u, v, &lon, &lat);
+    image_to_obj_single(out, u, v, &lon, &lat);
     lonlat_to_xyz(lon, lat, p);
     rotate(out->Rinv, p, q);
     xyz_to_lonlat(q, &lon, &lat);
@@ -311,12 +595,19 @@ static void project_pixel(const orc_camera* out, const orc_camera* in, double u,
         fisheye_project(in, q, x, y);
         return;
     }
+    if (in->type == ORC_PINHOLE) {
+        pinhole_project(in, q, x, y);
+        return;
+    }
     double ll, la;
     xyz_to_lonlat(q, &ll, &la);
     double px = NAN, py = NAN;
-    if (lon_ok) {
-        if (in->type == ORC_FULLFRAME_FISHEYE) ffisheye_o2i(in, ll, la, &px, &py);
-        else equirect_o2i(in, ll, la, &px, &py);
+    if (lon_ok) obj_to_image_single(in, ll, la, &px, &py);
+    if (px >= 0 && px < 1 && py >= 0 && py < 1 && in->sel) {
+        /* exclude_mask.at(int(p.y * rows), int(p.x * cols)) (camera.cpp:239-246): 255 outside the
+         * fillPoly'd selection rectangle [l, r-1] x [t, b-1] (camera.cpp:96-112) */
+        int W = (int)(px * in->width), H = (int)(py * in->height);
+        if (!(W >= in->sel_l && W <= in->sel_r - 1 && H >= in->sel_t && H <= in->sel_b - 1)) px = py = NAN;
     }
     *x = px;
     *y = py;

@@ -19,7 +19,10 @@
 extern "C" {
 #endif
 
-enum { ORC_EQUIRECT = 0, ORC_FULLFRAME_FISHEYE = 1, ORC_FISHEYE = 2 };
+enum {
+    ORC_EQUIRECT = 0, ORC_FULLFRAME_FISHEYE = 1, ORC_FISHEYE = 2, ORC_PINHOLE = 3, ORC_NORMAL = 4,
+    ORC_PERSPECTIVE = 5, ORC_OCAM = 6, ORC_STUPIDOVAL = 7, ORC_CUBIC = 8, ORC_EQAREA_NORTH = 9, ORC_EQAREA_SOUTH = 10
+};
 
 typedef struct {
     int type;
@@ -35,6 +38,16 @@ typedef struct {
     double rad[6];
     /* pinhole_cam.cpp:13-30 (OpenCV fisheye model) */
     double fx, fy, cx, cy, k[4];
+    /* camera.cpp:96-112 `selection` rectangle (an exclude mask that is 255 outside it) */
+    int sel, sel_l, sel_r, sel_t, sel_b;
+    /* cv::projectPoints distortion k1..tauY (calibration.cpp:644-665) and the tilt matrix */
+    double dist[14], tilt[9];
+    double aspect, cam_x, cam_y, cam_z; /* normal.cpp:13-19 */
+    double sf;                          /* perspective.cpp:16 */
+    double circle;                      /* eqarea{north,south}pole.hpp arctic / antarctic circle */
+    int len_pol, len_invpol;            /* ocam_fisheye.hpp:23-35 */
+    double xc, yc, oc, od, oe;
+    double pol[64], invpol[64];
 } orc_camera;
 
 /* Type initialisers reset rotation to identity and longitude range to [-pi, pi]; call
@@ -51,6 +64,17 @@ void orc_camera_fullframe_fisheye(orc_camera* c, int width, int height, int crop
                                   double center_dy, const double radial[3]);
 void orc_camera_fisheye(orc_camera* c, int width, int height, double fx, double fy, double cx, double cy,
                         const double k[4]);
+
+/* PinholeCamera (pinhole_cam.cpp:13-30): nd in {0,4,5,8,12,14} distortion coefficients. */
+void orc_camera_pinhole(orc_camera* c, int width, int height, double fx, double fy, double cx, double cy,
+                        const double* dist, int nd);
+void orc_camera_normal(orc_camera* c, double aspect_ratio, double cam_opt);           /* normal.cpp:13-22 */
+void orc_camera_perspective(orc_camera* c, double aspect_ratio, double sf);           /* perspective.cpp:14-19 */
+void orc_camera_ocam(orc_camera* c, const double* pol, int len_pol, const double* invpol, int len_invpol, double xc,
+                     double yc, double cc, double d, double e, int width, int height); /* ocam_fisheye.cpp:82-110 */
+/* stupidoval / cubic / eqareanorthpole / eqareasouthpole (circle: arctic / antarctic latitude) */
+void orc_camera_simple(orc_camera* c, int type, double circle);
+void orc_camera_set_selection(orc_camera* c, int width, int height, int l, int r, int t, int b);
 
 /* MapperTemplate::add_input LUT loop (template.cpp:46-133) for one input camera.
  * map1/map2/mask are FULL output-size buffers (W*H); roi[4] = x,y,w,h (±8 pad, or full if !use_roi). */

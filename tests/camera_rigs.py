@@ -1,0 +1,64 @@
+"""Synthetic rigs exercising every camera model of modules/octvr/src/cameras/ (SURVEY.md §8f row 3).
+No reference fixtures exist for these models (parity unpinned): the oracle restatement is checked by
+round-trip / analytic properties (test_oracle_cameras.py) and the GPU LUT against the oracle."""
+import math
+
+OCAM = {"pol": [-180.0, 0.0, 0.0018, -1.2e-6, 3e-9], "invpol": [260.0, 150.0, -12.0, 20.0, 9.0, -3.0, 1.0],
+        "xc": 240.5, "yc": 320.25, "c": 1.0003, "d": 0.0002, "e": -0.0001, "width": 640, "height": 480}
+
+# models usable as the output camera (they implement image_to_obj_single)
+OUTPUT_MODELS = {
+    "normal": {"aspect_ratio": 1.5, "cam_opt": 0.8},
+    "perspective": {"aspect_ratio": 1.25, "sf": 1.3},
+    "stupidoval": {},
+    "cubic": {},
+    "eqareanorthpole": {},
+    "eqareasouthpole": {"antarctic_circle": -0.9},
+    "ocam_fisheye": OCAM,
+}
+
+
+def _rot(yaw, pitch=0.0, roll=0.0):
+    return {"rotation": {"roll": roll, "yaw": yaw, "pitch": pitch}}
+
+
+def input_rigs():
+    """name -> rig with an equirectangular output and the model under test as inputs."""
+    eq = {"type": "equirectangular", "options": _rot(0.1, 0.05)}
+    ff = {"width": 640, "height": 360, "hfov": 3.4906585, "center_dx": 3.0, "center_dy": -2.0,
+          "radial": [0.01, -0.02, 0.005], "crop": {"rect": [140, 500, 0, 360], "is_circular": True}}
+    pin = {"width": 640, "height": 480, "fx": 380.0, "fy": 372.0, "cx": 318.5, "cy": 241.0}
+    rigs = {
+        "pinhole_k5": [dict(pin, dist_coeffs=[0.08, -0.03, 0.001, -0.002, 0.004], **_rot(0.0)),
+                       dict(pin, dist_coeffs=[0.08, -0.03, 0.001, -0.002, 0.004], **_rot(2.0, 0.2))],
+        "pinhole_k14_tilt": [dict(pin, dist_coeffs=[0.05, -0.01, 0.0005, 0.0003, 0.001, 0.01, -0.002, 0.0004,
+                                                    0.001, -0.0004, 0.0006, 0.0002, 0.012, -0.018], **_rot(-1.0, -0.3))],
+        "pinhole_nodist": [dict(pin, **_rot(0.5))],
+        "normal": [dict(OUTPUT_MODELS["normal"], **_rot(0.3, 0.1)), dict(OUTPUT_MODELS["normal"], **_rot(-2.5))],
+        "perspective": [dict(OUTPUT_MODELS["perspective"], **_rot(1.2, -0.4))],
+        "ocam_fisheye": [dict(OCAM, **_rot(0.0, 0.3)), dict(OCAM, **_rot(math.pi, -0.2, 0.1))],
+        "stupidoval": [dict(_rot(0.7, 0.2))],
+        "cubic": [dict(_rot(0.4, 0.3, 0.2))],
+        "eqarea": [dict(_rot(0.2, 0.1)), dict(antarctic_circle=-0.8, **_rot(-0.3))],
+        "fullframe_selection": [dict(ff, selection=[180, 470, 20, 330], **_rot(0.0)),
+                                dict(ff, selection=[0, 640, 40, 300], **_rot(math.pi))],
+    }
+    types = {"pinhole_k5": "pinhole", "pinhole_k14_tilt": "pinhole", "pinhole_nodist": "pinhole",
+             "eqarea": ["eqareanorthpole", "eqareasouthpole"], "fullframe_selection": "fullframe_fisheye"}
+    out = {}
+    for name, opts in rigs.items():
+        t = types.get(name, name)
+        ts = t if isinstance(t, list) else [t] * len(opts)
+        out[name] = {"output": eq, "inputs": [{"type": tt, "options": o} for tt, o in zip(ts, opts)]}
+    return out
+
+
+def output_rigs():
+    """name -> rig with the model under test as the output camera and two fisheye + one equirect input."""
+    ff = {"width": 640, "height": 360, "hfov": 3.4906585, "center_dx": 0.0, "center_dy": 0.0,
+          "radial": [0.0, 0.0, 0.0], "crop": {"rect": [140, 500, 0, 360], "is_circular": True}}
+    inputs = [{"type": "fullframe_fisheye", "options": dict(ff, **_rot(0.0))},
+              {"type": "fullframe_fisheye", "options": dict(ff, **_rot(0.9, 0.1))},
+              {"type": "equirectangular", "options": _rot(0.5, 0.2)}]
+    return {t: {"output": {"type": t, "options": dict(o, **_rot(0.2, -0.1))}, "inputs": inputs}
+            for t, o in OUTPUT_MODELS.items()}

@@ -29,6 +29,13 @@ class OrcCamera(C.Structure):
         ("rad", C.c_double * 6),
         ("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double),
         ("k", C.c_double * 4),
+        ("sel", C.c_int), ("sel_l", C.c_int), ("sel_r", C.c_int), ("sel_t", C.c_int), ("sel_b", C.c_int),
+        ("dist", C.c_double * 14), ("tilt", C.c_double * 9),
+        ("aspect", C.c_double), ("cam_x", C.c_double), ("cam_y", C.c_double), ("cam_z", C.c_double),
+        ("sf", C.c_double), ("circle", C.c_double),
+        ("len_pol", C.c_int), ("len_invpol", C.c_int),
+        ("xc", C.c_double), ("yc", C.c_double), ("oc", C.c_double), ("od", C.c_double), ("oe", C.c_double),
+        ("pol", C.c_double * 64), ("invpol", C.c_double * 64),
     ]
 
 
@@ -112,8 +119,29 @@ def camera_from_json(cam):
         k = (C.c_double * 4)(*o["dist_coeffs"][:4])
         L.orc_camera_fisheye(C.byref(c), o["width"], o["height"], C.c_double(o["fx"]), C.c_double(o["fy"]),
                              C.c_double(o["cx"]), C.c_double(o["cy"]), k)
+    elif t == "pinhole":
+        d = o.get("dist_coeffs", [])
+        L.orc_camera_pinhole(C.byref(c), o["width"], o["height"], C.c_double(o["fx"]), C.c_double(o["fy"]),
+                             C.c_double(o["cx"]), C.c_double(o["cy"]), (C.c_double * max(1, len(d)))(*d), len(d))
+    elif t == "normal":
+        L.orc_camera_normal(C.byref(c), C.c_double(o["aspect_ratio"]), C.c_double(o["cam_opt"]))
+    elif t == "perspective":
+        L.orc_camera_perspective(C.byref(c), C.c_double(o["aspect_ratio"]), C.c_double(o["sf"]))
+    elif t == "ocam_fisheye":
+        pol, inv = o["pol"], o["invpol"]
+        L.orc_camera_ocam(C.byref(c), (C.c_double * len(pol))(*pol), len(pol), (C.c_double * len(inv))(*inv), len(inv),
+                          C.c_double(o["xc"]), C.c_double(o["yc"]), C.c_double(o["c"]), C.c_double(o["d"]),
+                          C.c_double(o["e"]), o["width"], o["height"])
+    elif t in ("stupidoval", "cubic", "eqareanorthpole", "eqareasouthpole"):
+        import math
+        typ = {"stupidoval": 7, "cubic": 8, "eqareanorthpole": 9, "eqareasouthpole": 10}[t]
+        circle = o.get("arctic_circle", math.pi / 3) if t == "eqareanorthpole" else o.get("antarctic_circle", -math.pi / 3)
+        L.orc_camera_simple(C.byref(c), typ, C.c_double(circle))
     else:
         raise ValueError("camera type not in the oracle: " + t)
+    if "selection" in o:
+        l, r, tt, b = o["selection"]
+        L.orc_camera_set_selection(C.byref(c), o["width"], o["height"], l, r, tt, b)
     if "rotation" in o:
         r = o["rotation"]
         R = rotation_rpy(r["roll"], r["yaw"], r["pitch"])

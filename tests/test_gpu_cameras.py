@@ -1,0 +1,60 @@
+"""GPU LUT build (lut_build_kernel, FP64) for every camera model against the oracle restatement
+(parity unpinned: no reference fixture exists for these models).  Same bar as the pinned rigs of
+test_gpu_parity.py: OCML vs glibc may differ in the last f64 ulp, so a handful of mask flips and
+1-ulp f32 map differences are allowed."""
+import json
+
+import numpy as np
+import pytest
+
+import camera_rigs as R
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+ASPECT = {"normal": 1.5, "perspective": 1.25, "stupidoval": 2.0, "cubic": 1.5, "eqareanorthpole": 1.0,
+          "eqareasouthpole": 1.0, "ocam_fisheye": 640 / 480}
+
+
+def _compare(ox, rig, W, H):
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=False)
+    W, H = mt.out_size
+    want = O.lut_build(rig, W, H, use_roi=False)
+    assert len(mt) == len(want)
+    for i, (roi, w1, w2, wm) in enumerate(want):
+        groi, g1, g2, gm, _ = mt.input(i)
+        assert groi == tuple(roi)
+        dm = gm != wm
+        assert dm.sum() <= max(2, gm.size // 20000), (i, int(dm.sum()))
+        both = (~dm) & (wm > 0)
+        u1 = np.abs(g1.view(np.int32)[both].astype(np.int64) - w1.view(np.int32)[both])
+        u2 = np.abs(g2.view(np.int32)[both].astype(np.int64) - w2.view(np.int32)[both])
+        assert u1.max(initial=0) <= 1 and u2.max(initial=0) <= 1, (i, int(u1.max(initial=0)), int(u2.max(initial=0)))
+        assert (u1 > 0).sum() + (u2 > 0).sum() <= max(4, g1.size // 2000)
+        assert (wm > 0).any()
+    return mt
+
+
+@pytest.mark.parametrize("name", sorted(R.input_rigs()))
+def test_gpu_input_camera_models_vs_oracle(product_lib, name):
+    _compare(product_lib, R.input_rigs()[name], 512, 256)
+
+
+@pytest.mark.parametrize("name", sorted(R.output_rigs()))
+def test_gpu_output_camera_models_vs_oracle(product_lib, name):
+    # out_h = 0: derived from the output camera's aspect ratio (template.cpp:32-38)
+    mt = _compare(product_lib, R.output_rigs()[name], 384, 0)
+    assert mt.out_size == (384, int(384 / ASPECT[name]))
+
+
+def test_gpu_unsupported_camera_options_fail_loudly(product_lib):
+    ox = product_lib
+    rig = R.input_rigs()["normal"]
+    bad = json.loads(json.dumps(rig))
+    bad["inputs"][0]["options"]["exclude_masks"] = [{"type": "polygonal", "args": [0, 0, 10, 0, 10, 10]}]
+    with pytest.raises(ox.OctvrError):
+        ox.MapperTemplate.from_json(json.dumps(bad), 256, 128)
+    bad = json.loads(json.dumps(rig))
+    bad["output"] = {"type": "pinhole", "options": {"width": 64, "height": 48, "fx": 1, "fy": 1, "cx": 0, "cy": 0}}
+    with pytest.raises(ox.OctvrError):
+        ox.MapperTemplate.from_json(json.dumps(bad), 256, 128)
