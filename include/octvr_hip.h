@@ -8,6 +8,8 @@
  *                                                     modules/octvr/src/template.cpp:23-322
  *   octvr_mapper_*   <- vr::Mapper                   modules/octvr/src/mapper.hpp:386-452,
  *                                                     modules/octvr/src/mapper.cpp:47-323
+ *   octvr_async_*    <- vr::AsyncMultiMapper         modules/octvr/include/octvr.hpp:103-121,
+ *                                                     modules/octvr/src/async.cpp:32-350
  *   octvr_remap_*    <- cv::remap INTER_LINEAR u8    modules/imgproc/src/imgwarp.cpp:4689-4828
  *
  * Conventions: no exceptions cross the boundary; every call returns an int status
@@ -89,9 +91,10 @@ void octvr_rig_destroy(octvr_rig* rig);
 
 /* ---- vr::Mapper ---------------------------------------------------------------------------- */
 /* Mapper(mt, in_sizes, blend, enable_gain, scale_output) (mapper.cpp:47-191).
- * blend: 0 = no blend (composite by LUT mask, later input wins; mapper.cpp:268-277).
- * (blend > 0 multi-band and blend < 0 feather return OCTVR_E_UNSUPPORTED in this ABI version.)
- * scale_w/scale_h: 0 = output at template size. */
+ * blend: 0 = no blend (composite by LUT mask, later input wins; mapper.cpp:268-277), > 0 multi-band
+ * with ceil(log2(blend)) - 1 bands (MultiBandGPUBlender), < 0 feather with border -blend
+ * (FeatherGPUBlender); blend != 0 needs seam masks (octvr_rig_create_masks or a .dat).
+ * scale_w/scale_h: 0 = output at template size, else the output is resized (mapper.cpp:290-306). */
 int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                         int enable_gain, int scale_w, int scale_h, octvr_mapper** mapper);
 /* Mapper::stitch (mapper.cpp:193-323) on device-resident YUV420P frames in the "Y over [U|V]"
