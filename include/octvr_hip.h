@@ -10,6 +10,7 @@
  *                                                     modules/octvr/src/mapper.cpp:47-323
  *   octvr_async_*    <- vr::AsyncMultiMapper         modules/octvr/include/octvr.hpp:103-121,
  *                                                     modules/octvr/src/async.cpp:32-350
+ *   octvr_fastmapper_* <- vr::FastMapper           modules/octvr/src/mapper_fast.cpp:27-195
  *   octvr_remap_*    <- cv::remap INTER_LINEAR u8    modules/imgproc/src/imgwarp.cpp:4689-4828
  *
  * Conventions: no exceptions cross the boundary; every call returns an int status
@@ -143,6 +144,20 @@ int octvr_async_pending(const octvr_async* async, int* n);
 /* Drains the frames in flight and joins the pipeline's worker threads (the reference leaves its five
  * threads running forever, async.cpp:337-349). */
 void octvr_async_destroy(octvr_async* async);
+
+/* ---- vr::FastMapper ------------------------------------------------------------------------- */
+/* FastMapper(mt, in_sizes) (modules/octvr/src/mapper_fast.cpp:27-109): feather-weighted NV12 stitch
+ * (weights 255 * max(DT_i - 5, 0) / (1e-5 + sum), half-size chroma maps); the rig's inputs must cover
+ * the whole output (no ROI, mapper_fast.cpp:50-51) and have no overlays. */
+typedef struct octvr_fastmapper octvr_fastmapper;
+int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h,
+                            octvr_fastmapper** fastmapper);
+/* FastMapper::stitch_nv12 (mapper_fast.cpp:153-195) on device NV12 frames (H rows of Y, then H/2 rows
+ * of interleaved U,V; pitch >= W).  Output: W x 3H/2, chroma rows interleaved V,U — the reference's
+ * channel order (merge of the V-then-U accumulators).  Stream-ordered. */
+int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fastmapper, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                 uint8_t* out_dev, size_t out_pitch, void* stream);
+void octvr_fastmapper_destroy(octvr_fastmapper* fastmapper);
 
 /* ---- standalone kernels --------------------------------------------------------------------- */
 /* cv::remap(src, dst, map1*sx, map2*sy, INTER_LINEAR, BORDER_CONSTANT) on u8 with cn in {1,3,4}

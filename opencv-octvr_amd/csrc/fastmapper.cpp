@@ -1,0 +1,204 @@
+// fastmapper.cpp — vr::FastMapper (modules/octvr/src/mapper_fast.cpp:27-109): per-rig setup of the NV12
+// feather stitch (fastmapper.hip).  Everything here runs once per rig on host threads:
+//   convertMaps(map * in_size, CV_16SC2) for the luma maps and for the half-size chroma maps
+//     (cv::resize of the f32 maps, 2x area fast path), imgwarp.cpp:4831-5044, 2284-2460;
+//   feather weights w_i = max(distanceTransform(mask_i) - 5, 0), u8 = sat(rne(255 * w_i / (1e-5 + sum w))),
+//     half-size weights by the u8 area fast path (mapper_fast.cpp:75-94);
+//   per 256-pixel run, the bit mask of cameras with a non-zero weight.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "host_common.hpp"
+
+using namespace octvr;
+
+namespace octvr {
+hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint32_t* runs_y,
+                                  const uint2* ent_uv, const uint32_t* runs_uv, int W, int H, uint8_t* out,
+                                  int64_t out_pitch, hipStream_t s);
+}
+
+struct octvr_fastmapper {
+    int device = 0, n = 0, W = 0, H = 0;
+    std::vector<int> in_w, in_h;
+    DevBuf<uint2> ent_y, ent_uv;
+    DevBuf<uint32_t> runs_y, runs_uv;
+};
+
+namespace {
+
+template <class F>
+void parallel_for(size_t n, F f) {
+    const size_t T = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            for (size_t k = n * t / T; k < n * (t + 1) / T; k++) f(k);
+        });
+    for (auto& x : th) x.join();
+}
+
+int sat_int_rne(float v) {  // saturate_cast<int>(float)
+    if (v != v) return INT32_MIN;
+    if (v >= 2147483648.f) return INT32_MAX;
+    if (v < -2147483648.f) return INT32_MIN;
+    return (int)lrintf(v);
+}
+uint32_t sat_s16(int v) { return (uint32_t)(uint16_t)(int16_t)std::min(32767, std::max(-32768, v)); }
+uint8_t sat_u8_rte(float v) { return !(v > 0.f) ? 0 : v >= 255.f ? 255 : (uint8_t)lrintf(v); }
+
+// convertMaps of one element (imgwarp.cpp:5039-5043) with the MatExpr scale m * s in f32, packed with
+// the weight into the kernel's entry.
+uint2 make_entry(float m1, float m2, float sx, float sy, uint8_t w) {
+    const float X = m1 * sx + 0.f, Y = m2 * sy + 0.f;
+    const int ix = sat_int_rne(X * 32), iy = sat_int_rne(Y * 32);
+    uint2 e;
+    e.x = sat_s16(ix >> 5) | (sat_s16(iy >> 5) << 16);
+    e.y = (uint32_t)((iy & 31) * 32 + (ix & 31)) | ((uint32_t)w << 16);
+    return e;
+}
+
+// cv::resize(f32 map, half size): resizeAreaFast with the SSE grouping (imgwarp.cpp:2284-2337, 2441-2454).
+float half_f32(const float* s0, const float* s1, int x, int vec) {
+    const float a = s0[2 * x], b = s0[2 * x + 1], c = s1[2 * x], d = s1[2 * x + 1];
+    const float sum = x < vec ? (a + b) + (c + d) : 0.f + (((a + b) + c) + d);
+    return sum * 0.25f;
+}
+
+}  // namespace
+
+extern "C" {
+
+int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h,
+                            octvr_fastmapper** out) {
+    try {
+        REQUIRE(rig && in_w && in_h && out, "NULL argument");
+        REQUIRE(rig->overlays.empty(), "FastMapper does not support overlays (mapper_fast.cpp:31)");
+        const int n = (int)rig->inputs.size();
+        REQUIRE(n_inputs == n && n > 0 && n <= kMaxCams && n <= 32, "in_sizes must cover the inputs (<= 32)");
+        const int W = rig->out_w, H = rig->out_h;
+        REQUIRE(W % 2 == 0 && H % 2 == 0, "NV12 output needs even width/height");
+        for (int i = 0; i < n; i++) {
+            const RigInput& in = rig->inputs[i];
+            // "does not support ROI yet" (mapper_fast.cpp:50-51): every map covers the whole output
+            REQUIRE(in.roi[0] == 0 && in.roi[1] == 0 && in.roi[2] == W && in.roi[3] == H,
+                    "FastMapper needs full-frame templates (dump without ROI)");
+            REQUIRE(in_w[i] > 0 && in_h[i] > 0 && in_w[i] % 2 == 0 && in_h[i] % 2 == 0 && in_w[i] < 32768 && in_h[i] < 32768,
+                    "input sizes must be even and < 32768");
+        }
+        auto fm = std::make_unique<octvr_fastmapper>();
+        fm->device = device;
+        fm->n = n;
+        fm->W = W;
+        fm->H = H;
+        fm->in_w.assign(in_w, in_w + n);
+        fm->in_h.assign(in_h, in_h + n);
+        const size_t npx = (size_t)W * H, hw = (size_t)W / 2, hh = (size_t)H / 2, nh = hw * hh;
+        // feather weights (mapper_fast.cpp:75-94): dst_weight_map = 1e-5 + sum_i max(DT_i - 5, 0)
+        std::vector<std::vector<float>> wt(n);
+        std::vector<float> total(npx, 1e-5f);
+        for (int i = 0; i < n; i++) {
+            wt[i].resize(npx);
+            chamfer_l2_3x3(rig->inputs[i].mask.data(), W, H, wt[i].data());
+        }
+        parallel_for(npx, [&](size_t k) {
+            float t = 1e-5f;
+            for (int i = 0; i < n; i++) {
+                const float v = wt[i][k] - 5.f;
+                wt[i][k] = v > 0.f ? v : 0.f;
+                t = wt[i][k] + t;
+            }
+            total[k] = t;
+        });
+        std::vector<uint2> ey(npx * n), euv(nh * n);
+        const size_t runs_y = (npx + 255) / 256, runs_uv = (nh + 255) / 256;
+        std::vector<uint32_t> my(runs_y, 0u), muv(runs_uv, 0u);
+        std::vector<uint8_t> fmask(npx), hmask(nh);
+        std::vector<float> h1(nh), h2(nh);
+        for (int i = 0; i < n; i++) {
+            const RigInput& in = rig->inputs[i];
+            // divide(weight_i, dst_weight_map) then convertTo(CV_8U, 255): fma(r, 255, 0), rne, saturate
+            parallel_for(npx, [&](size_t k) {
+                const float e2 = total[k];
+                const float r = e2 != 0.f ? wt[i][k] / e2 : 0.f;
+                fmask[k] = sat_u8_rte(fmaf(r, 255.f, 0.f));
+            });
+            // cv::resize(feather_mask, half): u8 area fast path (a + b + c + d + 2) >> 2
+            parallel_for(hh, [&](size_t y) {
+                for (size_t x = 0; x < hw; x++) {
+                    const uint8_t* s = fmask.data() + (2 * y) * W + 2 * x;
+                    hmask[y * hw + x] = (uint8_t)((s[0] + s[1] + s[W] + s[W + 1] + 2) >> 2);
+                }
+            });
+            const float sx = (float)in_w[i], sy = (float)in_h[i];
+            parallel_for(npx, [&](size_t k) {
+                ey[(size_t)i * npx + k] = make_entry(in.map1[k], in.map2[k], sx, sy, fmask[k]);
+            });
+            const int vec = (int)(hw / 4 * 4);
+            parallel_for(hh, [&](size_t y) {
+                const float* a0 = in.map1.data() + (2 * y) * W;
+                const float* b0 = in.map2.data() + (2 * y) * W;
+                for (size_t x = 0; x < hw; x++) {
+                    h1[y * hw + x] = half_f32(a0, a0 + W, (int)x, vec);
+                    h2[y * hw + x] = half_f32(b0, b0 + W, (int)x, vec);
+                }
+            });
+            // r_map * (in_size / 2): integer halving first (mapper_fast.cpp:62-64)
+            const float hx = (float)(in_w[i] / 2), hy = (float)(in_h[i] / 2);
+            parallel_for(nh, [&](size_t k) { euv[(size_t)i * nh + k] = make_entry(h1[k], h2[k], hx, hy, hmask[k]); });
+            for (size_t k = 0; k < npx; k++)
+                if (fmask[k]) my[k / 256] |= 1u << i;
+            for (size_t k = 0; k < nh; k++)
+                if (hmask[k]) muv[k / 256] |= 1u << i;
+        }
+        DeviceGuard dg(device);
+        fm->ent_y.upload(ey.data(), ey.size());
+        fm->ent_uv.upload(euv.data(), euv.size());
+        fm->runs_y.upload(my.data(), my.size());
+        fm->runs_uv.upload(muv.data(), muv.size());
+        *out = fm.release();
+        return OCTVR_OK;
+    } catch (const OctvrError& e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_last_error(e.what());
+        return OCTVR_E_HIP;
+    }
+}
+
+int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                 uint8_t* out_dev, size_t out_pitch, void* stream) {
+    try {
+        REQUIRE(fm && in_dev && in_pitch && out_dev, "NULL argument");
+        REQUIRE(out_pitch >= (size_t)fm->W, "output pitch smaller than width");
+        DeviceGuard dg(fm->device);
+        FrameSet fs;
+        memset(&fs, 0, sizeof fs);
+        for (int i = 0; i < fm->n; i++) {
+            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)fm->in_w[i], "bad input frame");
+            fs.f[i] = SourceFrame{in_dev[i], fm->in_w[i], fm->in_h[i], (int64_t)in_pitch[i], nullptr};
+        }
+        HIP_CHECK(launch_fastmapper_nv12(fs, fm->ent_y.p, fm->runs_y.p, fm->ent_uv.p, fm->runs_uv.p, fm->W, fm->H, out_dev,
+                                         (int64_t)out_pitch, (hipStream_t)stream));
+        return OCTVR_OK;
+    } catch (const OctvrError& e) {
+        set_last_error(e.what());
+        return e.code;
+    }
+}
+
+void octvr_fastmapper_destroy(octvr_fastmapper* fm) {
+    if (!fm) return;
+    int prev = -1;
+    if (hipGetDevice(&prev) == hipSuccess && prev != fm->device) (void)hipSetDevice(fm->device);
+    delete fm;
+    if (prev >= 0) (void)hipSetDevice(prev);
+}
+
+}  // extern "C"

@@ -76,6 +76,10 @@ _lib.octvr_async_pop.argtypes = [_VP]
 _lib.octvr_async_pending.argtypes = [_VP, C.POINTER(C.c_int)]
 _lib.octvr_async_destroy.argtypes = [_VP]
 _lib.octvr_async_destroy.restype = None
+_lib.octvr_fastmapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(_VP)]
+_lib.octvr_fastmapper_stitch_nv12.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP]
+_lib.octvr_fastmapper_destroy.argtypes = [_VP]
+_lib.octvr_fastmapper_destroy.restype = None
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
                                 C.c_float, C.c_float, _VP, C.c_size_t, _VP]
 
@@ -244,6 +248,39 @@ class Mapper:
     def close(self):
         if self._h and self._h.value:
             _lib.octvr_mapper_destroy(self._h)
+            self._h = C.c_void_p(0)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FastMapper:
+    """vr::FastMapper (modules/octvr/src/mapper_fast.cpp): feather-weighted NV12 stitch of a full-frame rig."""
+
+    def __init__(self, mt, in_sizes, device=0):
+        n = len(in_sizes)
+        w = (C.c_int * n)(*[s[0] for s in in_sizes])
+        h = (C.c_int * n)(*[s[1] for s in in_sizes])
+        hd = _VP()
+        _check(_lib.octvr_fastmapper_create(mt._h, device, n, w, h, C.byref(hd)))
+        self._h = hd
+        self.n = n
+        self.out_size = mt.out_size
+
+    def stitch_nv12(self, inputs, output, stream=None):
+        """inputs: uint8 cuda tensors (1.5H x W NV12); output: 1.5H x W (chroma rows V,U)."""
+        n = len(inputs)
+        ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
+        pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
+        _check(_lib.octvr_fastmapper_stitch_nv12(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()), output.stride(0),
+                                                 _stream_ptr(stream)))
+
+    def close(self):
+        if self._h and self._h.value:
+            _lib.octvr_fastmapper_destroy(self._h)
             self._h = C.c_void_p(0)
 
     def __del__(self):

@@ -175,6 +175,18 @@ void orc_distance_transform_l2_3x3(const uint8_t* src, int w, int h, size_t spit
  * seam_finders.cpp:97-133).  masks / seams: ROI-sized u8 (tightly packed); seams are written. */
 int orc_create_masks(int n, const int* rois, const uint8_t* const* masks, int out_w, uint8_t* const* seams);
 
+/* ---- vr::FastMapper (octvr_oracle_fast.c) --------------------------------- */
+/* convertMaps(map1 * sx, map2 * sy, CV_16SC2): s16 (x, y) pairs + u16 fraction codes (imgwarp.cpp:5039-5043). */
+void orc_convert_maps(const float* m1, const float* m2, size_t n, float sx, float sy, int16_t* xy, uint16_t* a);
+/* cv::resize of a f32 map to half size (area fast path, SSE grouping of imgwarp.cpp:2284-2337). */
+void orc_resize_half_f32(const float* src, int w, int h, float* dst);
+/* FastMapper(mt, in_sizes) + stitch_nv12 (mapper_fast.cpp:27-195): maps / masks are FULL output size
+ * (the reference asserts ROI = whole frame); inputs NV12 (Y rows, then interleaved UV rows); the output
+ * is W x 1.5H with the chroma rows interleaved V, U (the reference's channel order). */
+int orc_fastmapper_nv12(int n, const int* in_w, const int* in_h, const float* const* map1, const float* const* map2,
+                        const uint8_t* const* masks, int W, int H, const uint8_t* const* in_nv12,
+                        const size_t* in_pitch, uint8_t* out, size_t out_pitch);
+
 #ifdef __cplusplus
 }
 #endif

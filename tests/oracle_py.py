@@ -376,6 +376,23 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
     return out, gout
 
 
+def fastmapper_nv12(in_nv12, in_sizes, map1s, map2s, masks, out_w, out_h):
+    """vr::FastMapper::stitch_nv12 (full-frame maps / masks): W x 1.5H output, chroma rows V, U."""
+    n = len(in_nv12)
+    in_nv12 = [np.ascontiguousarray(a) for a in in_nv12]
+    m1 = [np.ascontiguousarray(a, np.float32) for a in map1s]
+    m2 = [np.ascontiguousarray(a, np.float32) for a in map2s]
+    mk = [np.ascontiguousarray(a, np.uint8) for a in masks]
+    out = np.zeros((out_h * 3 // 2, out_w), np.uint8)
+    P = C.c_void_p * n
+    rc = lib().orc_fastmapper_nv12(n, (C.c_int * n)(*[s[0] for s in in_sizes]), (C.c_int * n)(*[s[1] for s in in_sizes]),
+                                   P(*[a.ctypes.data for a in m1]), P(*[a.ctypes.data for a in m2]),
+                                   P(*[a.ctypes.data for a in mk]), out_w, out_h, P(*[a.ctypes.data for a in in_nv12]),
+                                   (C.c_size_t * n)(*[a.shape[1] for a in in_nv12]), _p(out), C.c_size_t(out_w))
+    assert rc == 0
+    return out
+
+
 # ---------------------------------------------------------------------------------------------
 # synthetic data (same generator as oracle/golden_gen/gen_golden.cpp)
 # ---------------------------------------------------------------------------------------------
