@@ -59,12 +59,20 @@ __device__ __forceinline__ uint32_t bilerp_ch(uint32_t a, uint32_t b, uint32_t c
     return ((32u - fy) * h0 + fy * h1 + 512u) >> 10;
 }
 
+// The same sum as one 2-D weighted sum, (w00 a + w01 b + w10 c + w11 d + 2^9) >> 10 with
+// w = {(32-fx)(32-fy), fx(32-fy), (32-fx)fy, fx fy} (<= 1024 each, exact in u32): per channel two
+// v_perm_b32 pair the taps as u16 halves and two v_dot2_u32_u16 accumulate them.
+typedef unsigned short u16x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint32_t fx,
                                             uint32_t fy, uint32_t (&rgb)[3]) {
+    const uint32_t X = fx * 0xFFFFu + 32u;  // (32 - fx) | fx << 16
+    const u16x2_t w0 = __builtin_bit_cast(u16x2_t, X * (32u - fy)), w1 = __builtin_bit_cast(u16x2_t, X * fy);
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
-        const uint32_t sh = 8u * ch;
-        rgb[ch] = bilerp_ch((c00 >> sh) & 255u, (c01 >> sh) & 255u, (c10 >> sh) & 255u, (c11 >> sh) & 255u, fx, fy);
+        const uint32_t sel = 0x0C000C00u | ((4u + ch) << 16) | (uint32_t)ch;  // {lo.ch, 0, hi.ch, 0}
+        const u16x2_t top = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c01, c00, sel));
+        const u16x2_t bot = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c11, c10, sel));
+        rgb[ch] = __builtin_amdgcn_udot2(bot, w1, __builtin_amdgcn_udot2(top, w0, 512u, false), false) >> 10;
     }
 }
 

@@ -500,8 +500,12 @@ __device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32
     // k < 2^14, rowg <= 32: (k + 0.5) / rowg is >= 1/64 away from an integer, far above f32 error
     const float inv = __builtin_amdgcn_rcpf((float)rowg);
     const uint32_t row_f = (uint32_t)(((float)k + 0.5f) * inv);
-    const uint32_t row = ok ? row_f : 0u, col = ok ? k - row_f * rowg : 0u;
+    const uint32_t row_k = ok ? row_f : 0u, col_k = ok ? k - row_f * rowg : 0u;
     const SourceFrame f = kernarg_frame(live_chunk ? cam : 0u);
+    // box groups past the image's right / bottom edge (w % 8 == 0: whole groups) stage RGBA 0:
+    // they load from the box origin and are replaced by Y = 0, U = V = 128 (-> R = G = B = 0)
+    const bool img = bx0 + col_k * 8u < (uint32_t)f.w && by0 + row_k < (uint32_t)f.h;
+    const uint32_t row = img ? row_k : 0u, col = img ? col_k : 0u;
     const uint32_t p32 = (uint32_t)f.pitch;
     const gu8* base = (const gu8*)f.yuv;
     const gu8* Yb = base + (int64_t)by0 * f.pitch + bx0;  // by0, bx0 even: chroma rows / columns exact
@@ -523,7 +527,11 @@ __device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32
         sg.uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8) | ((uint32_t)Up[2] << 16) | ((uint32_t)Up[3] << 24);
         sg.vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8) | ((uint32_t)Vp[2] << 16) | ((uint32_t)Vp[3] << 24);
     }
-    sg.dst = ok ? (int32_t)(lds + row * stride + col * 8u) : -1;
+    if (!img) {
+        sg.y0 = sg.y1 = 0u;
+        sg.uq = sg.vq = 0x80808080u;
+    }
+    sg.dst = ok ? (int32_t)(lds + row_k * stride + col_k * 8u) : -1;
     if (VIG) {  // 8 gains (32-byte aligned: w % 8 == 0); a camera without vignette reads 1.0 gains
         const float* gv = f.vig ? f.vig + (int64_t)(by0 + row) * f.w + bx0 + col * 8u : nullptr;
         sg.g0 = gv ? *reinterpret_cast<const float4*>(gv) : make_float4(1.f, 1.f, 1.f, 1.f);
@@ -744,13 +752,15 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint32_t e = ent[p];
-            const uint32_t off = e & 0x1FFFu, m = (e >> 25) & 15u;
-            const uint32_t c00 = s_rgb[(m & 1u) ? off : 0u];
-            const uint32_t c01 = s_rgb[(m & 2u) ? off + 1u : 0u];
-            const uint32_t c10 = s_rgb[(m & 4u) ? off + S : 0u];
-            const uint32_t c11 = s_rgb[(m & 8u) ? off + S + 1u : 0u];
-            bilerp_rgba(c00, c01, c10, c11, (e >> 13) & 31u, (e >> 18) & 31u, rgb[p]);
-            gain[p] = s_slot_gain[(e >> 23) & 3u];
+            // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
+            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) + (e & 0x7FFFu);
+            const uint8_t* r1 = r0 + 4u * S;
+            const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
+            const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
+            const uint32_t c10 = reinterpret_cast<const uint32_t*>(r1)[0];
+            const uint32_t c11 = reinterpret_cast<const uint32_t*>(r1)[1];
+            bilerp_rgba(c00, c01, c10, c11, (e >> 15) & 31u, (e >> 20) & 31u, rgb[p]);
+            gain[p] = s_slot_gain[(e >> 25) & 3u];
             if (MODE == 1 && (e & kEntryNoGain)) gain[p] = 1.0f;
         }
         prev = finish_any<MODE>(rgb, gain);

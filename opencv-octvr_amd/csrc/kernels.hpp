@@ -44,15 +44,13 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
 // converted once, as NPP's full-frame pass does in the reference — at a tile-uniform row stride.
 // Staging work is cut into chunks of 64 eight-pixel groups, each chunk inside one slot, so a wave's
 // chunk has wave-uniform slot parameters (scalar registers, no per-lane slot search).
-// LDS dwords 0-3 of the tile area are zero: out-of-image taps point there (BORDER_CONSTANT).
+// LDS dwords 0-3 of the tile area are zero: a black pixel's entry (0) reads its tap (x, y) there.
+// Each slot's box reaches one column / row past its taps (x0 + 1, y0 + 1), including taps outside
+// the source image: staging writes RGBA 0 for box pixels outside the image (BORDER_CONSTANT), so
+// every tap is read from LDS at off, off + 4, off + 4 S, off + 4 S + 4 (S = row stride) unmasked.
 // The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel:
-//   bits 0-12 LDS dword offset of tap (x, y); 13-17 fx; 18-22 fy; 23-24 slot;
-//   25-28 tap-valid mask (bit t: tap t in the image; taps 0 (x,y), 1 (x+1,y), 2 (x,y+1), 3 (x+1,y+1)).
-// A pixel with no camera, or with every tap outside, has mask 0 and comes out black.
-// Tiles that do not fit (> 4 cameras, a box > 256 px, or LDS need above kTileLdsBytes) are "wide":
-// their pixels use 8-byte absolute CompositeEntry records and direct global gathers, in a second
-// launch over the list of wide tiles.  The staged tiles form a compact item list (header, slots and
-// entries indexed by item), so the staged kernel has no per-tile branch between the two kinds.
+//   bits 0-14 LDS byte offset of tap (x, y); 15-19 fx; 20-24 fy; 25-26 slot; 29 "no gain".
+// A pixel with no camera, or with every tap outside, is entry 0 and comes out black.
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
 constexpr int kTileLdsBytes = 24 * 1024;

@@ -4,7 +4,7 @@
 // frame (each pixel's entry = the winning camera of the copy chain), for blend > 0 every level-0
 // tile a camera's Gaussian pyramid needs (each pixel's entry = that camera's map).  Per job the
 // builder finds the cameras (<= 4 "slots") and their even-aligned luma boxes, and encodes each
-// pixel as a 4-byte box-relative LDS offset + fractions + slot + tap-valid mask; jobs that do not
+// pixel as a 4-byte box-relative LDS byte offset + fractions + slot; jobs that do not
 // fit (> 4 cameras, a box > 256 px, or LDS above kTileLdsBytes) become "wide" with 8-byte entries.
 #include <algorithm>
 #include <thread>
@@ -50,8 +50,9 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 const int mask = ((sx < iw && sy < ih) ? 1 : 0) | ((inx && sy < ih) ? 2 : 0) |
                                  ((iny && sx < iw) ? 4 : 0) | ((inx && iny) ? 8 : 0);
                 if (!mask) continue;
-                const int x0 = std::min(sx, iw - 1), y0 = std::min(sy, ih - 1);
-                const int x1 = x0 + (((mask >> 1) | (mask >> 3)) & 1), y1 = y0 + (((mask >> 2) | (mask >> 3)) & 1);
+                // mask != 0 means sx < iw and sy < ih; the +1 taps may sit on the zero column / row
+                // just past the image, which the box then includes
+                const int x0 = sx, y0 = sy, x1 = x0 + 1, y1 = y0 + 1;
                 int sl = -1;
                 for (int j = 0; j < ns; j++)
                     if (cams[j] == cam) sl = j;
@@ -119,9 +120,8 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 if (!px[k].mask) continue;  // black
                 const TileSlot& sl = ts[px[k].slot];
                 const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
-                out[k] = off | ((uint32_t)(px[k].fxy & 31) << 13) | ((uint32_t)(px[k].fxy >> 5) << 18) |
-                         ((uint32_t)px[k].slot << 23) | ((uint32_t)px[k].mask << 25) |
-                         (px[k].nogain ? kEntryNoGain : 0u);
+                out[k] = off * 4u | ((uint32_t)(px[k].fxy & 31) << 15) | ((uint32_t)(px[k].fxy >> 5) << 20) |
+                         ((uint32_t)px[k].slot << 25) | (px[k].nogain ? kEntryNoGain : 0u);
             }
         }
     };

@@ -39,13 +39,18 @@ def test_gpu_fastmapper_nv12_bit_exact(product_lib, name):
 
 
 def test_gpu_fastmapper_needs_full_frame_templates(product_lib):
+    """mapper_fast.cpp:50-51: a template dumped with ROIs is refused (camera 0 cropped to its left half)."""
     ox = product_lib
-    rig, z = O.load_rig("rigB")
+    rig, z = O.load_rig("rigA")
     W, H = (int(v) for v in z["out_size"])
     n = len(z["rois"])
-    assert any(tuple(r) != (0, 0, W, H) for r in z["rois"].tolist())
-    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), [z[f"map1_{i}"] for i in range(n)],
-                                       [z[f"map2_{i}"] for i in range(n)], [z[f"mask_{i}"] for i in range(n)])
+    rois = z["rois"].tolist()
+    m1 = [z[f"map1_{i}"] for i in range(n)]
+    m2 = [z[f"map2_{i}"] for i in range(n)]
+    mk = [z[f"mask_{i}"] for i in range(n)]
+    rois[0] = [0, 0, W // 2, H]
+    m1[0], m2[0], mk[0] = (np.ascontiguousarray(a[:, : W // 2]) for a in (m1[0], m2[0], mk[0]))
+    mt = ox.MapperTemplate.from_arrays(W, H, rois, m1, m2, mk)
     sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
     with pytest.raises(ox.OctvrError):
         ox.FastMapper(mt, sizes)
