@@ -29,11 +29,29 @@ __device__ __forceinline__ uint32_t pack_u8(float v, uint32_t sel, uint32_t old)
 // The library's own BT.601 YUV -> RGB (stands in for NPP nppiYUV420ToRGB_8u_P3AC4R,
 // cudaimgproc/src/color.cpp:2269, whose arithmetic is closed: pinned by the oracle only).  Same
 // operation sequence as oracle/octvr_oracle.c yuv_px_to_rgb.  Returns packed R | G << 8 | B << 16.
+// R and B come from one packed fma (v_pk_fma_f32), each element rounded as the scalar fma.
 __device__ __forceinline__ uint32_t yuv_to_rgba(uint32_t y, uint32_t u, uint32_t v) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
     const float Yf = (float)y, Uf = (float)u - 128.f, Vf = (float)v - 128.f;
-    uint32_t p = pack_u8(__builtin_fmaf(1.140f, Vf, Yf), 0, 0u);
+    const f2 rb = __builtin_elementwise_fma(f2{1.140f, 2.032f}, f2{Vf, Uf}, f2{Yf, Yf});
+    uint32_t p = pack_u8(rb.x, 0, 0u);
     p = pack_u8(__builtin_fmaf(-0.581f, Vf, __builtin_fmaf(-0.394f, Uf, Yf)), 1, p);
-    return pack_u8(__builtin_fmaf(2.032f, Uf, Yf), 2, p);
+    return pack_u8(rb.y, 2, p);
+}
+
+// Two horizontally adjacent pixels sharing one (U, V) sample: the same per-element operations as
+// yuv_to_rgba, with each fma issued for both pixels as one v_pk_fma_f32.
+__device__ __forceinline__ void yuv2_to_rgba(uint32_t y0, uint32_t y1, uint32_t u, uint32_t v, uint32_t& p0,
+                                             uint32_t& p1) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 Y = {(float)y0, (float)y1};
+    const float Uf = (float)u - 128.f, Vf = (float)v - 128.f;
+    const f2 R = __builtin_elementwise_fma(f2{1.140f, 1.140f}, f2{Vf, Vf}, Y);
+    const f2 G = __builtin_elementwise_fma(f2{-0.581f, -0.581f}, f2{Vf, Vf},
+                                           __builtin_elementwise_fma(f2{-0.394f, -0.394f}, f2{Uf, Uf}, Y));
+    const f2 B = __builtin_elementwise_fma(f2{2.032f, 2.032f}, f2{Uf, Uf}, Y);
+    p0 = pack_u8(B.x, 2, pack_u8(G.x, 1, pack_u8(R.x, 0, 0u)));
+    p1 = pack_u8(B.y, 2, pack_u8(G.y, 1, pack_u8(R.y, 0, 0u)));
 }
 
 // Vignette correction of a source pixel: multiply(rgba, vignette_map) = MulOpSpecial_c4
@@ -137,26 +155,31 @@ struct QuadOut {
     uint32_t u, v;
 };
 
+// Per pixel the (B, R) pair goes through packed f32 ops (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32:
+// two lanes' worth per instruction, each element rounded exactly like the scalar op) and the chroma
+// sums accumulate as the pair (us, vs) in the same pixel order.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
     uint32_t y01 = 0, y23 = 0;
-    float us = 0.f, vs = 0.f;
+    f32x2_t uv = {0.f, 0.f};  // (us, vs)
+    const f32x2_t kuv = {0.492f, 0.877f};
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         // gain: saturate_cast<uchar>(px * g), kept as an exact float of the saturated integer
-        const float R = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][0] * gain[p]), 0.f, 255.f);
+        f32x2_t br = f32x2_t{(float)rgb[p][2], (float)rgb[p][0]} * gain[p];
+        br.x = __builtin_amdgcn_fmed3f(__builtin_rintf(br.x), 0.f, 255.f);
+        br.y = __builtin_amdgcn_fmed3f(__builtin_rintf(br.y), 0.f, 255.f);
         const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain[p]), 0.f, 255.f);
-        const float B = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][2] * gain[p]), 0.f, 255.f);
-        const float Yf = __builtin_fmaf(0.114f, B, __builtin_fmaf(0.587f, G, 0.299f * R));
+        const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
         if (p < 2) y01 = pack_u8(Yf, p, y01);
         else y23 = pack_u8(Yf, p - 2, y23);
-        us = __builtin_fmaf(0.492f, B - Yf, us);
-        vs = __builtin_fmaf(0.877f, R - Yf, vs);
+        uv = __builtin_elementwise_fma(kuv, br - Yf, uv);
     }
     QuadOut q;
     q.y01 = y01;
     q.y23 = y23;
-    q.u = pack_u8(__builtin_fmaf(us, 0.25f, 128.f), 0, 0u);
-    q.v = pack_u8(__builtin_fmaf(vs, 0.25f, 128.f), 0, 0u);
+    q.u = pack_u8(__builtin_fmaf(uv.x, 0.25f, 128.f), 0, 0u);
+    q.v = pack_u8(__builtin_fmaf(uv.y, 0.25f, 128.f), 0, 0u);
     return q;
 }
 

@@ -125,6 +125,7 @@ struct TiledLutBuild {
     std::vector<CompositeEntry> wide;
     std::vector<uint32_t> wide_tiles;
     std::vector<uint8_t> wide_cams;
+    std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
     double staged_bytes = 0;
 };
@@ -137,6 +138,7 @@ struct TiledLutDev {
     DevBuf<CompositeEntry> wide;
     DevBuf<uint32_t> wide_tiles;
     DevBuf<uint8_t> wide_cams;
+    DevBuf<int32_t> bands;
     double staged_bytes = 0;
     TiledLut view{};
     void upload(const TiledLutBuild& b);

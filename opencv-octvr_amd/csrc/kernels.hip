@@ -543,14 +543,10 @@ template <bool VIG>
 __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rgb) {
     if (sg.dst < 0) return;
     uint4 a, b;
-    a.x = yuv_to_rgba(sg.y0 & 255u, sg.uq & 255u, sg.vq & 255u);
-    a.y = yuv_to_rgba((sg.y0 >> 8) & 255u, sg.uq & 255u, sg.vq & 255u);
-    a.z = yuv_to_rgba((sg.y0 >> 16) & 255u, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
-    a.w = yuv_to_rgba(sg.y0 >> 24, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u);
-    b.x = yuv_to_rgba(sg.y1 & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u);
-    b.y = yuv_to_rgba((sg.y1 >> 8) & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u);
-    b.z = yuv_to_rgba((sg.y1 >> 16) & 255u, sg.uq >> 24, sg.vq >> 24);
-    b.w = yuv_to_rgba(sg.y1 >> 24, sg.uq >> 24, sg.vq >> 24);
+    yuv2_to_rgba(sg.y0 & 255u, (sg.y0 >> 8) & 255u, sg.uq & 255u, sg.vq & 255u, a.x, a.y);
+    yuv2_to_rgba((sg.y0 >> 16) & 255u, sg.y0 >> 24, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u, a.z, a.w);
+    yuv2_to_rgba(sg.y1 & 255u, (sg.y1 >> 8) & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u, b.x, b.y);
+    yuv2_to_rgba((sg.y1 >> 16) & 255u, sg.y1 >> 24, sg.uq >> 24, sg.vq >> 24, b.z, b.w);
     if (VIG) {
         a.x = vig_mul(a.x, sg.g0.x);
         a.y = vig_mul(a.y, sg.g0.y);
@@ -569,7 +565,16 @@ __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rg
 #define OCTVR_STITCH_BLOCKS_PER_CU 6
 #endif
 constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
-constexpr int kStageRegs = 2;  // staging groups per lane loaded one tile ahead (512 per tile)
+#ifndef OCTVR_STAGE_REGS
+#define OCTVR_STAGE_REGS 1
+#endif
+#ifndef OCTVR_STAGE_SKIP
+#define OCTVR_STAGE_SKIP 1
+#endif
+#ifndef OCTVR_INNER_PAIR
+#define OCTVR_INNER_PAIR 0
+#endif
+constexpr int kStageRegs = OCTVR_STAGE_REGS;  // staging groups per lane loaded one tile ahead (256 per reg)
 
 // Software pipeline over a block's tiles (t, t + step, ...):
 //   iteration of tile t:  stage tile t's YUV (loaded during the previous iteration) into LDS,
@@ -625,8 +630,15 @@ __device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLu
     d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? m.t : 0) * kTilePx)[tid];
     const uint32_t nchunks = live ? ((m.hd.nslots >> 8) & 0xFFu) : 0u;
 #pragma unroll
-    for (int r = 0; r < kStageRegs; r++)
+    for (int r = 0; r < kStageRegs; r++) {
+#if OCTVR_STAGE_SKIP
+        if ((uint32_t)(r * 4 + wave) >= nchunks) {  // wave-uniform: no loads for a chunk the tile lacks
+            d.sg[r].dst = -1;
+            continue;
+        }
+#endif
         stage_load<DWORD_STAGE, VIG>(m.ss, (int)(m.hd.nslots & 0xFFu), nchunks, m.hd.stride, r * 4 + wave, d.sg[r]);
+    }
 }
 
 // The composite's two sinks.  MODE 0: gain + RGB -> YUV420P into the output frame (blend = 0).
@@ -684,11 +696,11 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
     __shared__ float s_gain[kMaxCams];
     __shared__ float s_slot_gain[kTileSlots];
 
-    const int groups = 8;
+    const int groups = kStitchBands;
     const int g = blockIdx.x % groups;
     const int step = (gridDim.x - g + groups - 1) / groups;
-    const int t_begin = (int)((int64_t)lut.n_items * g / groups);
-    const int t_end = (int)((int64_t)lut.n_items * (g + 1) / groups);
+    const int t_begin = lut.bands[g];
+    const int t_end = lut.bands[g + 1];
     OutFrame of{};
     RgbaSink ro{};
     if constexpr (MODE == 0)
@@ -736,7 +748,17 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
         const uint32_t nch = (cur.hd.nslots >> 8) & 0xFFu;
         if (nch > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
             const int wave = uniform(tid >> 6);
-            for (int c = kStageRegs * 4 + wave; c < (int)nch; c += 4) {
+            int c = kStageRegs * 4 + wave;
+#if OCTVR_INNER_PAIR
+            for (; c + 4 < (int)nch; c += 8) {  // two chunks' loads in flight before their stores
+                StageGroup sa, sb;
+                stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sa);
+                stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c + 4, sb);
+                stage_store<VIG>(sa, s_rgb);
+                stage_store<VIG>(sb, s_rgb);
+            }
+#endif
+            for (; c < (int)nch; c += 4) {
                 StageGroup sg;
                 stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sg);
                 stage_store<VIG>(sg, s_rgb);

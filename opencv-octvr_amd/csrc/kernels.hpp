@@ -53,7 +53,10 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
 // A pixel with no camera, or with every tap outside, is entry 0 and comes out black.
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
-constexpr int kTileLdsBytes = 24 * 1024;
+#ifndef OCTVR_TILE_LDS_BYTES
+#define OCTVR_TILE_LDS_BYTES (24 * 1024)
+#endif
+constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
 constexpr int kTileZeroDwords = 4;
 
 struct TileSlot {
@@ -139,7 +142,17 @@ struct TiledLut {
     const CompositeEntry* wide;   // kTilePx per wide tile
     int n_wide;
     const uint8_t* wide_cams;     // RGBA mode: output camera of each wide tile
+    const int32_t* bands;         // kStitchBands + 1 staged-item boundaries (one band per XCD)
 };
+// The staged items are cut into one contiguous band per XCD (locality: neighbouring tiles share
+// source boxes in that XCD's L2), balanced by cost = base + chunk weight x staging chunks.  Measured
+// on the C2 rig (r01 v10): equal item counts (chunk weight 0) beat every chunk-weighted split tried
+// (base 16 / 8 / 4 / 2 per chunk: +2 % / +4 % / +10 % / +19 % stitch time) — the large pole boxes
+// are re-read from L2 by many tiles, so staging chunks do not predict a tile's cost.
+constexpr int kStitchBands = 8;
+#ifndef OCTVR_BAND_CHUNK_WEIGHT
+#define OCTVR_BAND_CHUNK_WEIGHT 0
+#endif
 // 4-byte tiled entries: bit 29 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
 // in-image map value; mul_scalar_with_mask, exposure_compensate.cu:15-30).  8-byte CompositeEntry
 // records carry the same flag in code bit 16.  TileHdr.nslots bits 16-20: output camera (RGBA mode).

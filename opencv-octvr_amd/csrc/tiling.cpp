@@ -150,6 +150,21 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     }
     b.n_items = n_items;
     b.n_wide = (int)b.wide_tiles.size();
+    {  // cost-balanced XCD bands over the staged items
+        std::vector<double> cum(n_items + 1, 0.0);
+        for (int t = 0; t < n_items; t++) {
+            const int ch = (int)((b.hdr[t].nslots >> 8) & 0xFFu);
+            cum[t + 1] = cum[t] + 1.0 + OCTVR_BAND_CHUNK_WEIGHT * ch;
+        }
+        b.bands.assign(kStitchBands + 1, n_items);
+        b.bands[0] = 0;
+        int t = 0;
+        for (int g = 1; g < kStitchBands; g++) {
+            const double goal = cum[n_items] * g / kStitchBands;
+            while (t < n_items && cum[t] < goal) t++;
+            b.bands[g] = std::max(t, b.bands[g - 1]);
+        }
+    }
     b.hdr.resize(std::max(n_items, 1));
     b.slots.resize((size_t)std::max(n_items, 1) * kTileSlots);
     b.entries.resize((size_t)std::max(n_items, 1) * kTilePx);
@@ -168,8 +183,9 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     wide.upload(b.wide.data(), b.wide.size());
     wide_tiles.upload(b.wide_tiles.data(), b.wide_tiles.size());
     wide_cams.upload(b.wide_cams.data(), b.wide_cams.size());
+    bands.upload(b.bands.data(), b.bands.size());
     staged_bytes = b.staged_bytes;
-    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p};
+    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p};
 }
 
 }  // namespace octvr

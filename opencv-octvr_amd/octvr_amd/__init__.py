@@ -17,7 +17,7 @@ import numpy as np
 import torch  # must be imported first: the library then binds to torch's HIP runtime (one per process)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "liboctvr_hip.so")
+LIB_PATH = os.environ.get("OCTVR_HIP_LIB") or os.path.join(os.path.dirname(_HERE), "lib", "liboctvr_hip.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

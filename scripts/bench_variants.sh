@@ -1,0 +1,14 @@
+#!/bin/bash
+# Bench the default library and every lib/variants/*.so on one config: CFG=C2 bash scripts/bench_variants.sh
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+CFG=${CFG:-C2}
+run() {
+  timeout -k 10 300 python bench.py --config $CFG --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/var_$1.log 2>&1 || { echo "$1 failed rc=$?"; tail -5 gpurun_out/var_$1.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/var_$1.log').read().strip().splitlines()[-1]); print('$1', d['value'], d['roofline']['kernel_us'])"
+}
+run default
+for f in opencv-octvr_amd/lib/variants/*.so; do
+  v=$(basename $f .so)
+  OCTVR_HIP_LIB=$PWD/$f run $v
+done
