@@ -166,6 +166,15 @@ int octvr_remap_u8(const uint8_t* src_dev, int sw, int sh, size_t spitch, int cn
                    const float* map2_dev, int mw, int mh, size_t mpitch_elems, float scale_x, float scale_y,
                    uint8_t* dst_dev, size_t dpitch, void* stream);
 
+/* ---- camera mask rasterisation (host; what octvr_rig_create_json uses for `selection`,
+ *      `exclude_masks`, `include_masks`, camera.cpp:96-187) ------------------------------------ */
+/* cv::fillPoly(img, {pts}, color), lineType 8, shift 0, on a w x h u8 image (row pitch w);
+ * pts = x0,y0,x1,y1,... (imgproc/src/drawing.cpp:1196-1405, 1894-1917). */
+int octvr_fill_poly_u8(uint8_t* img, int w, int h, const int* pts, int npts, uint8_t color);
+/* cv::imdecode(png, IMREAD_COLOR) for PNG data (imgcodecs/src/grfmt_png.cpp:240-286), written as
+ * R,G,B bytes into rgb (capacity rgb_cap bytes); *w, *h receive the size.  rgb may be NULL to query. */
+int octvr_png_decode_rgb(const uint8_t* png, size_t n, uint8_t* rgb, size_t rgb_cap, int* w, int* h);
+
 /* ---- self-test hooks (used by tests/, not by the stitching path) ---------------------------------- */
 /* Saturating float -> u8 conversion as the kernels implement it (method 0: rint + clamp in VALU,
  * method 1: v_cvt_pk_u8_f32), for a known-answer test of round-half-even and clamping on device. */

@@ -63,6 +63,10 @@ struct CameraParams {
     double circle;                              // eqarea: arctic_circle / antarctic_circle
     double xc, yc, oc, od, oe;                  // ocam: center and affine parameters c, d, e
     double pol[kOcamMaxPol], invpol[kOcamMaxPol];
+    // exclude_mask / include_mask (camera.cpp:72-123), width x height u8 in device memory, or null.
+    // `incl` is only set when both exist: get_include_mask tests exclude_mask.empty() (camera.cpp:281).
+    const uint8_t* excl;
+    const uint8_t* incl;
 };
 
 #define OCTVR_HD __host__ __device__ inline
@@ -455,10 +459,13 @@ OCTVR_HD bool selection_excludes(const CameraParams& c, double x, double y) {
     return !(W >= c.sel_l && W <= c.sel_r - 1 && H >= c.sel_t && H <= c.sel_b - 1);
 }
 
-// Output pixel (u, v) in [0,1)^2 -> input camera normalized image point (x, y) or NaN.
+// Output pixel (u, v) in [0,1)^2 -> input camera normalized image point (x, y) or NaN.  With `vis`,
+// also Camera::get_include_mask's verdict for the pixel (camera.cpp:255-294: the same projection
+// without the longitude and exclude tests, then include_mask.at(int(y*rows), int(x*cols))).
 OCTVR_HD void project_output_to_input(const CameraParams& out, const CameraParams& in, double u, double v,
-                                      double* x, double* y) {
+                                      double* x, double* y, bool* vis = nullptr) {
     double lon, lat, p[3], q[3];
+    if (vis) *vis = false;
     // out->image_to_obj (camera.cpp:296-315)
     image_to_obj_single(out, u, v, &lon, &lat);
     lonlat_to_xyz(lon, lat, p);
@@ -479,8 +486,12 @@ OCTVR_HD void project_output_to_input(const CameraParams& out, const CameraParam
     double ll, la;
     xyz_to_lonlat(q, &ll, &la);
     double px = NAN, py = NAN;
-    if (lon_ok) obj_to_image_single(in, ll, la, &px, &py);
-    if (px >= 0 && px < 1 && py >= 0 && py < 1 && selection_excludes(in, px, py)) px = py = NAN;
+    if (lon_ok || (vis && in.incl)) obj_to_image_single(in, ll, la, &px, &py);
+    const bool inside = px >= 0 && px < 1 && py >= 0 && py < 1;
+    const size_t at = inside ? (size_t)(int)(py * in.height) * in.width + (int)(px * in.width) : 0;
+    if (vis && in.incl && inside) *vis = in.incl[at] != 0;
+    if (!lon_ok) px = py = NAN;
+    else if (inside && (selection_excludes(in, px, py) || (in.excl && in.excl[at]))) px = py = NAN;
     *x = px;
     *y = py;
 }

@@ -23,7 +23,8 @@ namespace octvr {
 // bbox = {min_w, min_h, max_w, max_h} of valid pixels (int atomics, initialised by the host).
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __restrict__ cams, int W, int H,
-                                                        float* map1, float* map2, uint8_t* mask, int32_t* bbox) {
+                                                        float* map1, float* map2, uint8_t* mask, int32_t* bbox,
+                                                        uint8_t* visible) {
     const CameraParams& out = cams[0];
     const CameraParams& in = cams[1];
     __shared__ int s_bb[4];
@@ -35,9 +36,15 @@ __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __re
          idx += (int64_t)gridDim.x * blockDim.x) {
         const int h = (int)(idx / W), w = (int)(idx - (int64_t)h * W);
         double dx, dy;
-        project_output_to_input(out, in, (double)w / W, (double)h / H, &dx, &dy);
+        bool vis = false;
+        project_output_to_input(out, in, (double)w / W, (double)h / H, &dx, &dy, visible ? &vis : nullptr);
         const float x = (float)dx, y = (float)dy;
-        if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f) {
+        // visible_mask arbitration (template.cpp:86-116): a pixel an earlier camera's include mask
+        // claimed (1) is rejected; one this camera's include mask claims first is marked 2 so the host
+        // clears it from the earlier cameras' masks.
+        const bool claimed = visible && visible[idx] == 1;
+        if (visible && vis && !claimed) visible[idx] = 2;
+        if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f || claimed) {
             mask[idx] = 0;
             map1[idx] = -1.0f;
             map2[idx] = -1.0f;
@@ -67,11 +74,11 @@ __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __re
 }
 
 hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
-                            int32_t* bbox, hipStream_t s) {
+                            int32_t* bbox, uint8_t* visible, hipStream_t s) {
     const int64_t total = (int64_t)W * H;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(lut_build_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, W, H, map1, map2, mask, bbox);
+    hipLaunchKernelGGL(lut_build_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, W, H, map1, map2, mask, bbox, visible);
     return hipGetLastError();
 }
 

@@ -117,7 +117,7 @@ struct GainChunk {
 
 // cams_dev: {output camera, input camera} in device memory (CameraParams holds the ocam polynomials).
 hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
-                            int32_t* bbox, hipStream_t s);
+                            int32_t* bbox, uint8_t* visible, hipStream_t s);
 
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
                                 hipStream_t s);

@@ -24,6 +24,7 @@
 #include "host_common.hpp"
 #include "json_lite.hpp"
 #include "kernels.hpp"
+#include "masks.hpp"
 
 using namespace octvr;
 
@@ -159,11 +160,69 @@ double correction_radius(const double* coeff) {
 }
 
 void reject_unsupported_options(const JsonValue& o, const std::string& type) {
-    // polygon / PNG masks need cv::fillPoly / cv::imdecode on the host (camera.cpp:114-123,146-187)
-    for (const char* k : {"exclude_masks", "include_masks"})
-        if (o.has(k))
-            throw OctvrError(OCTVR_E_UNSUPPORTED, std::string("camera option '") + k + "' (" + type +
-                                                      ") is not implemented in this ABI version");
+    // PinholeCamera overrides obj_to_image and never consults the masks (pinhole_cam.cpp:32-50), and its
+    // get_include_mask would call the base obj_to_image_single, which throws (camera.hpp:92-94)
+    if ((type == "fisheye" || type == "pinhole") && (o.has("include_masks") || o.has("exclude_masks")))
+        throw OctvrError(OCTVR_E_UNSUPPORTED, "camera type '" + type + "' does not support include/exclude masks");
+}
+
+// The Camera constructor's mask part (camera.cpp:72-123) and draw_mask (camera.cpp:146-187): `selection`
+// fills the exclude mask with 255 and clears the rectangle; `exclude_masks` areas set exclude (polygons,
+// PNG red) and include (PNG green) bits; `include_masks` areas set include bits.  Empty vector = no mask.
+void build_camera_masks(const JsonValue& o, std::vector<uint8_t>& excl, std::vector<uint8_t>& incl) {
+    const bool any = o.has("selection") || o.has("exclude_masks") || o.has("include_masks");
+    if (!any) return;
+    REQUIRE(o.has("width") && o.has("height"), "camera masks need the camera's width and height");
+    const int w = o["width"].as_int(), h = o["height"].as_int();
+    REQUIRE(w > 0 && h > 0, "camera width/height must be positive");
+    const size_t n = (size_t)w * h;
+    auto prepare = [&](std::vector<uint8_t>& m, uint8_t init) {
+        if (m.empty()) m.assign(n, init);
+    };
+    auto draw = [&](const JsonValue& areas, bool include) {
+        for (size_t a = 0; a < areas.size(); a++) {
+            const JsonValue& area = areas[a];
+            const std::string& t = area["type"].as_string();
+            const JsonValue& args = area["args"];
+            if (t == "polygonal") {
+                std::vector<int> pts;
+                for (size_t k = 0; k + 1 < args.size(); k += 2) {
+                    pts.push_back((int)args[k].as_double());
+                    pts.push_back((int)args[k + 1].as_double());
+                }
+                fill_poly_u8(include ? incl.data() : excl.data(), w, h, pts.data(), (int)pts.size() / 2, 255);
+            } else if (t == "png") {
+                std::vector<uint8_t> bytes(args.size());
+                for (size_t k = 0; k < args.size(); k++) bytes[k] = (uint8_t)args[k].as_int();
+                int pw = 0, ph = 0;
+                std::vector<uint8_t> rgb = png_decode_rgb(bytes.data(), bytes.size(), &pw, &ph);
+                // CV_Assert(mask_img.size() == exclude_mask.size()) (camera.cpp:170)
+                REQUIRE(!excl.empty() && pw == w && ph == h, "png mask size differs from the camera's exclude mask");
+                for (size_t k = 0; k < n; k++) {
+                    if (rgb[3 * k]) excl[k] = 255;      // RED channel
+                    if (rgb[3 * k + 1]) incl[k] = 255;  // GREEN channel
+                }
+            } else {
+                throw OctvrError(OCTVR_E_INVALID, "unknown mask area type '" + t + "'");
+            }
+        }
+    };
+    if (o.has("selection")) {
+        prepare(excl, 255);
+        const JsonValue& sel = o["selection"];
+        const int l = sel[0].as_int(), r = sel[1].as_int(), t = sel[2].as_int(), b = sel[3].as_int();
+        const int rect[8] = {l, t, l, b - 1, r - 1, b - 1, r - 1, t};
+        fill_poly_u8(excl.data(), w, h, rect, 4, 0);
+    }
+    if (o.has("exclude_masks")) {
+        prepare(excl, 0);
+        prepare(incl, 0);
+        draw(o["exclude_masks"], false);
+    }
+    if (o.has("include_masks")) {
+        prepare(incl, 0);
+        draw(o["include_masks"], true);
+    }
 }
 
 // computeTiltProjectionMatrix (imgproc/detail/distortion_model.hpp:74-94), Matx products s += a*b.
@@ -414,10 +473,35 @@ std::vector<float> vignette_map(const JsonValue& o, int width, int height) {
     return m;
 }
 
+// MapperTemplate::add_input (template.cpp:46-153).  `visible` (W x H device bytes, 1 = claimed by an
+// include mask) is allocated by the caller once some camera has include masks; `priors` are the inputs
+// added before this one, whose masks lose the pixels this camera's include mask claims (:102-116).
 void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H, bool use_roi, int device,
-                 RigInput& in) {
+                 RigInput& in, DevBuf<uint8_t>* visible = nullptr, std::vector<RigInput>* priors = nullptr) {
     CameraParams c = camera_from_json(cam);
     DeviceGuard dg(device);
+    std::vector<uint8_t> excl, incl;
+    if (cam.has("options")) build_camera_masks(cam["options"], excl, incl);
+    DevBuf<uint8_t> excl_d, incl_d;
+    if (!excl.empty() || !incl.empty()) {
+        c.sel = 0;  // the selection rectangle is rasterised into the exclude mask
+        c.width = cam["options"]["width"].as_int();
+        c.height = cam["options"]["height"].as_int();
+    }
+    if (!excl.empty()) {
+        excl_d.upload(excl.data(), excl.size());
+        c.excl = excl_d.p;
+        if (!incl.empty()) {
+            incl_d.upload(incl.data(), incl.size());
+            c.incl = incl_d.p;
+        }
+    }
+    const size_t total_px = (size_t)W * H;
+    if (visible && c.incl && !visible->p) {
+        visible->alloc(total_px);
+        HIP_CHECK(hipMemset(visible->p, 0, total_px));
+    }
+    uint8_t* vis_p = visible ? visible->p : nullptr;
     const size_t total = (size_t)W * H;
     DevBuf<float> m1, m2;
     DevBuf<uint8_t> mk;
@@ -431,7 +515,7 @@ void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H
     const CameraParams both[2] = {out_cam, c};
     DevBuf<CameraParams> cams;
     cams.upload(both, 2);
-    HIP_CHECK(launch_lut_build(cams.p, W, H, m1.p, m2.p, mk.p, bb.p, nullptr));
+    HIP_CHECK(launch_lut_build(cams.p, W, H, m1.p, m2.p, mk.p, bb.p, vis_p, nullptr));
     HIP_CHECK(hipDeviceSynchronize());
     int32_t b[4];
     HIP_CHECK(hipMemcpy(b, bb.p, sizeof b, hipMemcpyDeviceToHost));
@@ -456,6 +540,18 @@ void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H
     HIP_CHECK(hipMemcpy2D(in.map2.data(), roi[2] * sizeof(float), m2.p + off, W * sizeof(float), roi[2] * sizeof(float),
                           roi[3], hipMemcpyDeviceToHost));
     HIP_CHECK(hipMemcpy2D(in.mask.data(), roi[2], mk.p + off, W, roi[2], roi[3], hipMemcpyDeviceToHost));
+    if (c.incl && priors) {  // pixels this camera claimed first (2) leave the earlier cameras' masks
+        std::vector<uint8_t> v(total_px);
+        HIP_CHECK(hipMemcpy(v.data(), vis_p, total_px, hipMemcpyDeviceToHost));
+        for (RigInput& p : *priors) {
+            if (&p == &in) break;
+            for (int y = 0; y < p.roi[3]; y++)
+                for (int x = 0; x < p.roi[2]; x++)
+                    if (v[(size_t)(y + p.roi[1]) * W + x + p.roi[0]] == 2) p.mask[(size_t)y * p.roi[2] + x] = 0;
+        }
+        for (uint8_t& b : v) b = b ? 1 : 0;
+        HIP_CHECK(hipMemcpy(vis_p, v.data(), total_px, hipMemcpyHostToDevice));
+    }
     const JsonValue& o = cam["options"];
     in.in_w = o.has("width") ? o["width"].as_int() : 0;
     in.in_h = o.has("height") ? o["height"].as_int() : 0;
@@ -837,6 +933,24 @@ int octvr_memcpy_h2d(void* dst, const void* src, size_t bytes) {
     return guarded([&] { HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice)); });
 }
 
+int octvr_fill_poly_u8(uint8_t* img, int w, int h, const int* pts, int npts, uint8_t color) {
+    return guarded([&] {
+        REQUIRE(img && w > 0 && h > 0 && (pts || npts == 0) && npts >= 0, "bad arguments");
+        fill_poly_u8(img, w, h, pts, npts, color);
+    });
+}
+
+int octvr_png_decode_rgb(const uint8_t* png, size_t n, uint8_t* rgb, size_t rgb_cap, int* w, int* h) {
+    return guarded([&] {
+        REQUIRE(png && w && h, "bad arguments");
+        std::vector<uint8_t> v = png_decode_rgb(png, n, w, h);
+        if (rgb) {
+            REQUIRE(rgb_cap >= v.size(), "rgb buffer too small");
+            memcpy(rgb, v.data(), v.size());
+        }
+    });
+}
+
 int octvr_memcpy_d2h(void* dst, const void* src, size_t bytes) {
     return guarded([&] { HIP_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost)); });
 }
@@ -865,8 +979,9 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
         rig->device = device;
         const JsonValue& ins = doc["inputs"];
         rig->inputs.resize(ins.size());
+        DevBuf<uint8_t> visible;  // template.cpp visible_mask, allocated once an include mask appears
         for (size_t i = 0; i < ins.size(); i++)
-            build_input(out_cam, ins[i], out_w, out_h, use_roi != 0, device, rig->inputs[i]);
+            build_input(out_cam, ins[i], out_w, out_h, use_roi != 0, device, rig->inputs[i], &visible, &rig->inputs);
         if (doc.has("overlays")) {
             const JsonValue& ov = doc["overlays"];
             rig->overlays.resize(ov.size());

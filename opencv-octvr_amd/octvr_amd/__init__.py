@@ -76,6 +76,8 @@ _lib.octvr_async_pop.argtypes = [_VP]
 _lib.octvr_async_pending.argtypes = [_VP, C.POINTER(C.c_int)]
 _lib.octvr_async_destroy.argtypes = [_VP]
 _lib.octvr_async_destroy.restype = None
+_lib.octvr_fill_poly_u8.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.c_int, C.c_uint8]
+_lib.octvr_png_decode_rgb.argtypes = [C.c_char_p, C.c_size_t, _VP, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
 _lib.octvr_fastmapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(_VP)]
 _lib.octvr_fastmapper_stitch_nv12.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP]
 _lib.octvr_fastmapper_destroy.argtypes = [_VP]
@@ -373,4 +375,24 @@ def remap_u8(src, map1, map2, scale_x, scale_y, out=None, stream=None):
     _check(_lib.octvr_remap_u8(C.c_void_p(src.data_ptr()), src.shape[1], src.shape[0], src.stride(0), cn,
                                C.c_void_p(map1.data_ptr()), C.c_void_p(map2.data_ptr()), mw, mh, map1.stride(0),
                                scale_x, scale_y, C.c_void_p(out.data_ptr()), out.stride(0), _stream_ptr(stream)))
+    return out
+
+
+def fill_poly(img, pts, color):
+    """cv::fillPoly(img, {pts}, color) on a 2-D uint8 numpy array, in place (octvr_fill_poly_u8)."""
+    import numpy as np
+    assert img.dtype == np.uint8 and img.ndim == 2 and img.flags.c_contiguous
+    flat = np.ascontiguousarray(np.asarray(pts, np.int32).reshape(-1))
+    _check(_lib.octvr_fill_poly_u8(img.ctypes.data, img.shape[1], img.shape[0],
+                                   flat.ctypes.data_as(C.POINTER(C.c_int)), len(flat) // 2, color))
+    return img
+
+
+def png_decode_rgb(data):
+    """cv::imdecode(png, IMREAD_COLOR) with the channels in R,G,B order (octvr_png_decode_rgb)."""
+    import numpy as np
+    w, h = C.c_int(), C.c_int()
+    _check(_lib.octvr_png_decode_rgb(data, len(data), None, 0, C.byref(w), C.byref(h)))
+    out = np.empty((h.value, w.value, 3), np.uint8)
+    _check(_lib.octvr_png_decode_rgb(data, len(data), out.ctypes.data, out.nbytes, C.byref(w), C.byref(h)))
     return out

@@ -580,7 +580,17 @@ static void obj_to_image_single(const orc_camera* c, double lon, double lat, dou
 }
 
 /* One output pixel through out->image_to_obj then in->obj_to_image (camera.cpp:212-253, 296-315). */
+/* vis (optional): Camera::get_include_mask for the pixel (camera.cpp:255-294) -- the same projection
+ * without the longitude / exclude tests, then include_mask.at(int(y*rows), int(x*cols)); it is only
+ * consulted when exclude_mask is non-empty too (camera.cpp:281). */
+static void project_pixel_vis(const orc_camera* out, const orc_camera* in, double u, double v, double* x, double* y,
+                              int* vis);
 static void project_pixel(const orc_camera* out, const orc_camera* in, double u, double v, double* x, double* y) {
+    project_pixel_vis(out, in, u, v, x, y, NULL);
+}
+static void project_pixel_vis(const orc_camera* out, const orc_camera* in, double u, double v, double* x, double* y,
+                              int* vis) {
+    if (vis) *vis = 0;
     double lon, lat, p[3], q[3];
     /* output: image_to_obj */
     image_to_obj_single(out, u, v, &lon, &lat);
@@ -602,8 +612,16 @@ static void project_pixel(const orc_camera* out, const orc_camera* in, double u,
     double ll, la;
     xyz_to_lonlat(q, &ll, &la);
     double px = NAN, py = NAN;
+    if (vis && in->excl && in->incl) {
+        double qx = NAN, qy = NAN;
+        obj_to_image_single(in, ll, la, &qx, &qy);
+        if (qx >= 0 && qx < 1 && qy >= 0 && qy < 1)
+            *vis = in->incl[(size_t)(int)(qy * in->height) * in->width + (int)(qx * in->width)] != 0;
+    }
     if (lon_ok) obj_to_image_single(in, ll, la, &px, &py);
-    if (px >= 0 && px < 1 && py >= 0 && py < 1 && in->sel) {
+    if (px >= 0 && px < 1 && py >= 0 && py < 1 && in->excl) {  /* camera.cpp:239-246 */
+        if (in->excl[(size_t)(int)(py * in->height) * in->width + (int)(px * in->width)]) px = py = NAN;
+    } else if (px >= 0 && px < 1 && py >= 0 && py < 1 && in->sel) {
         /* exclude_mask.at(int(p.y * rows), int(p.x * cols)) (camera.cpp:239-246): 255 outside the
          * fillPoly'd selection rectangle [l, r-1] x [t, b-1] (camera.cpp:96-112) */
         int W = (int)(px * in->width), H = (int)(py * in->height);
@@ -634,14 +652,24 @@ void orc_lut_rows(const orc_camera* out, const orc_camera* in, int W, int H, int
 
 int orc_lut_build(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
                   uint8_t* mask, int use_roi, int roi[4]) {
+    return orc_lut_build_vis(out, in, W, H, map1, map2, mask, use_roi, roi, NULL);
+}
+
+int orc_lut_build_vis(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
+                      uint8_t* mask, int use_roi, int roi[4], uint8_t* visible) {
     int min_h = H, max_h = 0, min_w = W, max_w = 0;
     for (int h = 0; h < H; h++)
         for (int w = 0; w < W; w++) {
             double dx, dy;
-            project_pixel(out, in, (double)w / W, (double)h / H, &dx, &dy);
+            int vis = 0;
+            project_pixel_vis(out, in, (double)w / W, (double)h / H, &dx, &dy, visible ? &vis : NULL);
             float x = (float)dx, y = (float)dy;
             size_t idx = (size_t)h * W + w;
-            if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f) {
+            /* template.cpp:86-116: visible_mask[index] before this camera's update rejects the pixel;
+             * a first claim is marked 2 for the caller to clear from the earlier cameras' masks */
+            int claimed = visible && visible[idx] == 1;
+            if (visible && vis && !claimed) visible[idx] = 2;
+            if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f || claimed) {
                 mask[idx] = 0;
                 map1[idx] = map2[idx] = -1.0f;
             } else {

@@ -48,6 +48,9 @@ typedef struct {
     int len_pol, len_invpol;            /* ocam_fisheye.hpp:23-35 */
     double xc, yc, oc, od, oe;
     double pol[64], invpol[64];
+    /* exclude_mask / include_mask (camera.cpp:72-123), width x height, or NULL */
+    const uint8_t* excl;
+    const uint8_t* incl;
 } orc_camera;
 
 /* Type initialisers reset rotation to identity and longitude range to [-pi, pi]; call
@@ -80,6 +83,12 @@ void orc_camera_set_selection(orc_camera* c, int width, int height, int l, int r
  * map1/map2/mask are FULL output-size buffers (W*H); roi[4] = x,y,w,h (±8 pad, or full if !use_roi). */
 int orc_lut_build(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
                   uint8_t* mask, int use_roi, int roi[4]);
+/* The same with the include-mask arbitration (template.cpp:86-116): visible is W*H, 1 = claimed by an
+ * earlier camera (rejected here); pixels this camera claims first are set to 2. */
+int orc_lut_build_vis(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
+                      uint8_t* mask, int use_roi, int roi[4], uint8_t* visible);
+/* cv::fillPoly(img, {pts}, color), lineType 8, shift 0 (octvr_oracle_masks.c) */
+void orc_fill_poly(uint8_t* img, int w, int h, const int* pts, int count, uint8_t color);
 
 /* The same per-pixel LUT rule for output rows [y0, y1) only (no ROI); buffers are (y1-y0) x W. */
 void orc_lut_rows(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, float* map1,

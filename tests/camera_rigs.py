@@ -62,3 +62,47 @@ def output_rigs():
               {"type": "equirectangular", "options": _rot(0.5, 0.2)}]
     return {t: {"output": {"type": t, "options": dict(o, **_rot(0.2, -0.1))}, "inputs": inputs}
             for t, o in OUTPUT_MODELS.items()}
+
+
+def mask_rigs():
+    """name -> rig exercising the camera masks of camera.cpp:96-187 on 640x360 fullframe fisheyes, and
+    the include-mask visibility arbitration of template.cpp:86-116.  PNG areas register their decoded
+    ground truth with the oracle (oracle_py.PNG_TRUTH)."""
+    import numpy as np
+
+    import oracle_py
+    import png_fixture
+
+    ff = {"width": 640, "height": 360, "hfov": 3.4906585, "center_dx": 0.0, "center_dy": 0.0,
+          "radial": [0.0, 0.0, 0.0], "crop": {"rect": [140, 500, 0, 360], "is_circular": True}}
+
+    def poly(*pts):
+        return {"type": "polygonal", "args": [float(v) + 0.25 for v in pts]}  # int() truncation of args
+
+    concave = poly(200, 50, 400, 80, 300, 180, 420, 300, 180, 320, 250, 180)
+    outside = poly(600, -20, 700, 100, 560, 200)
+    # PNG: red block (exclude) and a green band (include), blocky so it compresses
+    img = np.zeros((360, 640, 3), np.int64)
+    img[40:140, 150:260, 0] = 255
+    img[200:330, 300:480, 1] = 200
+    img[100:220, 380:420, :] = 90
+    png, rgb = png_fixture.encode(img, 2, 8, seed=3)
+    oracle_py.PNG_TRUTH[png] = rgb
+    rigs = {
+        "exclude_poly": [dict(ff, exclude_masks=[concave, outside], **_rot(0.0)),
+                         dict(ff, selection=[150, 500, 10, 350], exclude_masks=[poly(300, 100, 340, 250, 260, 250)],
+                              **_rot(2.0, 0.1))],
+        "include_arbitration": [dict(ff, **_rot(0.0)),
+                                dict(ff, exclude_masks=[], include_masks=[poly(150, 20, 480, 20, 480, 340, 150, 340)],
+                                     **_rot(1.2)),
+                                dict(ff, exclude_masks=[poly(10, 10, 60, 10, 35, 80)],
+                                     include_masks=[poly(140, 60, 500, 100, 320, 330)], **_rot(2.4, -0.1)),
+                                dict(ff, **_rot(-1.5))],
+        "include_without_exclude": [dict(ff, include_masks=[poly(150, 20, 480, 20, 480, 340)], **_rot(0.5)),
+                                    dict(ff, **_rot(1.5))],
+        "png": [dict(ff, exclude_masks=[{"type": "png", "args": list(png)}], **_rot(0.3)),
+                dict(ff, exclude_masks=[], include_masks=[concave], **_rot(-0.9))],
+    }
+    return {name: {"output": {"type": "equirectangular", "options": _rot(0.1, 0.05)},
+                   "inputs": [{"type": "fullframe_fisheye", "options": o} for o in opts]}
+            for name, opts in rigs.items()}

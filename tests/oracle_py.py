@@ -36,6 +36,7 @@ class OrcCamera(C.Structure):
         ("len_pol", C.c_int), ("len_invpol", C.c_int),
         ("xc", C.c_double), ("yc", C.c_double), ("oc", C.c_double), ("od", C.c_double), ("oe", C.c_double),
         ("pol", C.c_double * 64), ("invpol", C.c_double * 64),
+        ("excl", C.c_void_p), ("incl", C.c_void_p),
     ]
 
 
@@ -153,21 +154,88 @@ def camera_from_json(cam):
     L.orc_camera_set_rotation(C.byref(c), Rc)
     if "longitude_selection" in o:
         c.min_lon, c.max_lon = o["longitude_selection"]
+    excl, incl = camera_masks(o)
+    c._masks = (excl, incl)  # keep the arrays alive while the struct points at them
+    if excl is not None:
+        c.sel = 0
+        c.width, c.height = o["width"], o["height"]
+        c.excl = excl.ctypes.data
+        if incl is not None:
+            c.incl = incl.ctypes.data
     return c
 
 
+# PNG mask areas: tests register the RGB image each PNG byte string encodes (tests/png_fixture.py); the
+# oracle takes that ground truth instead of decoding (libpng is a third-party dependency).
+PNG_TRUTH = {}
+
+
+def fill_poly(img, pts, color):
+    """cv::fillPoly(img, {pts}, color) restatement (oracle/octvr_oracle_masks.c)."""
+    flat = np.ascontiguousarray(np.asarray(pts, np.int32).reshape(-1))
+    lib().orc_fill_poly(_p(img), img.shape[1], img.shape[0], _p(flat), len(flat) // 2, C.c_uint8(color))
+
+
+def camera_masks(o):
+    """Camera ctor mask part (camera.cpp:72-123) + draw_mask (:146-187) -> (exclude, include) or None."""
+    if not any(k in o for k in ("selection", "exclude_masks", "include_masks")):
+        return None, None
+    w, h = o["width"], o["height"]
+    m = {"excl": None, "incl": None}
+
+    def prepare(k, v):
+        if m[k] is None:
+            m[k] = np.full((h, w), v, np.uint8)
+
+    def draw(areas, include):
+        for a in areas:
+            if a["type"] == "polygonal":
+                pts = [int(v) for v in a["args"]]
+                fill_poly(m["incl" if include else "excl"], pts, 255)
+            elif a["type"] == "png":
+                rgb = PNG_TRUTH[bytes(a["args"])]
+                if m["excl"] is None or rgb.shape[:2] != (h, w):
+                    raise ValueError("png mask size differs from the exclude mask (camera.cpp:170)")
+                m["excl"][rgb[..., 0] != 0] = 255
+                m["incl"][rgb[..., 1] != 0] = 255
+            else:
+                raise ValueError(a["type"])
+    if "selection" in o:
+        prepare("excl", 255)
+        l, r, t, b = o["selection"]
+        fill_poly(m["excl"], [l, t, l, b - 1, r - 1, b - 1, r - 1, t], 0)
+    if "exclude_masks" in o:
+        prepare("excl", 0)
+        prepare("incl", 0)
+        draw(o["exclude_masks"], False)
+    if "include_masks" in o:
+        prepare("incl", 0)
+        draw(o["include_masks"], True)
+    return m["excl"], m["incl"]
+
+
 def lut_build(rig, out_w, out_h, use_roi=True):
-    """Per input: (roi, map1, map2, mask) cropped to the ROI, as MapperTemplate::add_input."""
+    """Per input: (roi, map1, map2, mask) cropped to the ROI, as MapperTemplate::add_input, including the
+    include-mask visible_mask arbitration across inputs (template.cpp:86-116)."""
     out = camera_from_json(rig["output"])
     res = []
+    visible = None
     for cam in rig["inputs"]:
         c = camera_from_json(cam)
         m1 = np.empty((out_h, out_w), np.float32)
         m2 = np.empty((out_h, out_w), np.float32)
         mk = np.empty((out_h, out_w), np.uint8)
         roi = (C.c_int * 4)()
-        rc = lib().orc_lut_build(C.byref(out), C.byref(c), out_w, out_h, _p(m1), _p(m2), _p(mk), int(use_roi), roi)
+        if visible is None and c.incl:
+            visible = np.zeros((out_h, out_w), np.uint8)
+        vp = _p(visible) if visible is not None else None
+        rc = lib().orc_lut_build_vis(C.byref(out), C.byref(c), out_w, out_h, _p(m1), _p(m2), _p(mk), int(use_roi),
+                                     roi, vp)
         assert rc == 0
+        if visible is not None and c.incl:
+            for (px, py, pw, ph), _, _, pm in res:
+                pm[visible[py:py + ph, px:px + pw] == 2] = 0
+            visible[visible == 2] = 1
         x, y, w, h = roi[:]
         res.append(((x, y, w, h), m1[y:y + h, x:x + w].copy(), m2[y:y + h, x:x + w].copy(), mk[y:y + h, x:x + w].copy()))
     return res

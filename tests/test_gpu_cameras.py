@@ -16,10 +16,10 @@ ASPECT = {"normal": 1.5, "perspective": 1.25, "stupidoval": 2.0, "cubic": 1.5, "
           "eqareasouthpole": 1.0, "ocam_fisheye": 640 / 480}
 
 
-def _compare(ox, rig, W, H):
-    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=False)
+def _compare(ox, rig, W, H, use_roi=False):
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=use_roi)
     W, H = mt.out_size
-    want = O.lut_build(rig, W, H, use_roi=False)
+    want = O.lut_build(rig, W, H, use_roi=use_roi)
     assert len(mt) == len(want)
     for i, (roi, w1, w2, wm) in enumerate(want):
         groi, g1, g2, gm, _ = mt.input(i)
@@ -52,9 +52,50 @@ def test_gpu_unsupported_camera_options_fail_loudly(product_lib):
     rig = R.input_rigs()["normal"]
     bad = json.loads(json.dumps(rig))
     bad["inputs"][0]["options"]["exclude_masks"] = [{"type": "polygonal", "args": [0, 0, 10, 0, 10, 10]}]
-    with pytest.raises(ox.OctvrError):
+    with pytest.raises(ox.OctvrError):  # masks need the camera's width / height (camera.cpp:73-74)
+        ox.MapperTemplate.from_json(json.dumps(bad), 256, 128)
+    bad = json.loads(json.dumps(R.input_rigs()["pinhole_nodist"]))
+    bad["inputs"][0]["options"]["exclude_masks"] = [{"type": "polygonal", "args": [0, 0, 10, 0, 10, 10]}]
+    with pytest.raises(ox.OctvrError):  # PinholeCamera never consults the masks (pinhole_cam.cpp:32-50)
+        ox.MapperTemplate.from_json(json.dumps(bad), 256, 128)
+    bad = json.loads(json.dumps(R.mask_rigs()["png"]))
+    bad["inputs"][0]["options"]["include_masks"] = bad["inputs"][0]["options"].pop("exclude_masks")
+    with pytest.raises(ox.OctvrError):  # PNG area without an exclude mask (camera.cpp:170)
         ox.MapperTemplate.from_json(json.dumps(bad), 256, 128)
     bad = json.loads(json.dumps(rig))
     bad["output"] = {"type": "pinhole", "options": {"width": 64, "height": 48, "fx": 1, "fy": 1, "cx": 0, "cy": 0}}
     with pytest.raises(ox.OctvrError):
         ox.MapperTemplate.from_json(json.dumps(bad), 256, 128)
+
+
+@pytest.mark.parametrize("name", sorted(R.mask_rigs()))
+@pytest.mark.parametrize("use_roi", [False, True])
+def test_gpu_camera_masks_vs_oracle(product_lib, name, use_roi):
+    """selection / exclude_masks / include_masks (polygons and PNG) and the include-mask visibility
+    arbitration across inputs (camera.cpp:96-187, 212-294; template.cpp:86-116)."""
+    _compare(product_lib, R.mask_rigs()[name], 512, 256, use_roi=use_roi)
+
+
+def test_gpu_selection_equals_its_polygon(product_lib):
+    """`selection` = exclude everything, then clear the rectangle polygon: the same LUT as an
+    exclude_masks polygon ring around it (independent of the oracle)."""
+    import copy
+    ox = product_lib
+    rig = R.input_rigs()["fullframe_selection"]
+    alt = copy.deepcopy(rig)
+    for cam in alt["inputs"]:
+        o = cam["options"]
+        l, r, t, b = o.pop("selection")
+        w, h = o["width"], o["height"]
+        o["exclude_masks"] = [{"type": "polygonal", "args": a} for a in (
+            [0, 0, w - 1, 0, w - 1, t - 1, 0, t - 1] if t > 0 else None,
+            [0, b, w - 1, b, w - 1, h - 1, 0, h - 1] if b < h else None,
+            [0, 0, l - 1, 0, l - 1, h - 1, 0, h - 1] if l > 0 else None,
+            [r, 0, w - 1, 0, w - 1, h - 1, r, h - 1] if r < w else None) if a]
+    a = ox.MapperTemplate.from_json(json.dumps(rig), 512, 256, use_roi=False)
+    b = ox.MapperTemplate.from_json(json.dumps(alt), 512, 256, use_roi=False)
+    for i in range(len(a)):
+        ia, ib = a.input(i), b.input(i)
+        assert ia[0] == ib[0]
+        for k in (1, 2, 3):
+            assert np.array_equal(ia[k], ib[k])
