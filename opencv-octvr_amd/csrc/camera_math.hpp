@@ -157,8 +157,92 @@ OCTVR_HD void ocam_world2cam(const CameraParams& c, const double* p3, double* p2
 }
 
 // Output camera: (x, y) in [0,1)^2 -> lonlat before the output rotation; NaN when undefined.
+// cv::solvePoly (core/src/mathfuncs.cpp:2063-2182, maxIters 300) on a real polynomial a[0] + a[1] x +
+// ... + a[n0] x^n0: trailing zero coefficients trimmed, Durand-Kerner (Weierstrass) iteration from the
+// powers of (1 + i), each root updated in place, until no update moves.  Complex ops as cv::Complex
+// (core/types.hpp:960-1029).  Returns the trimmed degree n; only re/im[0..n) are defined (the reference
+// fills rows n..n0-1 from uninitialised memory).  The coincident-iterate branch (num_same_root > 1,
+// :2119-2157) needs two iterates to be bit-identical and is not taken by this restatement.
+OCTVR_HD int solve_poly_real(const double* a, int n0, double* re, double* im) {
+    int n = n0;
+    for (; n > 1; n--)
+        if (fabs(a[n]) + 0.0 > 2.220446049250313e-16) break;
+    double pr = 1, pi = 0;
+    for (int i = 0; i < n; i++) {
+        re[i] = pr;
+        im[i] = pi;
+        const double tr = pr * 1.0 - pi * 1.0, ti = pr * 1.0 + pi * 1.0;
+        pr = tr;
+        pi = ti;
+    }
+    for (int iter = 0; iter < 300; iter++) {
+        double max_diff = 0;
+        for (int i = 0; i < n; i++) {
+            const double xr = re[i], xi = im[i];
+            double nr = a[n], ni = 0, dr = a[n], di = 0;
+            for (int j = 0; j < n; j++) {
+                double tr = nr * xr - ni * xi, ti = nr * xi + ni * xr;
+                nr = tr + a[n - j - 1];
+                ni = ti + 0.0;
+                if (j != i) {
+                    const double er = xr - re[j], ei = xi - im[j];
+                    if (er != 0 || ei != 0) {
+                        tr = dr * er - di * ei;
+                        ti = dr * ei + di * er;
+                        dr = tr;
+                        di = ti;
+                    }
+                }
+            }
+            const double t = 1. / (dr * dr + di * di);
+            const double qr = (nr * dr + ni * di) * t, qi = (-nr * di + ni * dr) * t;
+            re[i] = xr - qr;
+            im[i] = xi - qi;
+            max_diff = fmax(max_diff, sqrt(qr * qr + qi * qi));
+        }
+        if (max_diff <= 0) break;
+    }
+    for (int i = 0; i < n; i++)
+        if (fabs(im[i]) < 1e-100) im[i] = 0;
+    return n;
+}
+
+// FullFrameFisheyeCamera::image_to_obj_single (fullframe_fisheye_cam.cpp:223-253) with
+// do_reverse_radial_distort (:160-185); the crop must be the whole image (checked at rig creation).
+OCTVR_HD void fullframe_fisheye_image_to_obj(const CameraParams& c, double x, double y, double* lon, double* lat) {
+    x -= 0.5;
+    y -= 0.5;
+    x *= (double)c.crop_w;
+    y *= (double)c.crop_h;
+    x -= c.center_dx;
+    y -= c.center_dy;
+    if (fabs(x) < 1e-5 && fabs(y) < 1e-5) {
+        *lon = 0;
+        *lat = 0;
+        return;
+    }
+    const double s = sqrt(x * x + y * y);
+    const double coeffs[5] = {-s / c.rad[4], c.rad[0], c.rad[1], c.rad[2], c.rad[3]};
+    double rre[4], rim[4], r = -1;
+    const int n = solve_poly_real(coeffs, 4, rre, rim);
+    for (int i = 0; i < n; i++)
+        if (fabs(rim[i]) < 1e-3 && rre[i] > 0 && (rre[i] < r || r < 0)) r = rre[i];
+    const double scale = (r < c.rad[5] && r > 0) ? s / c.rad[4] / r : 1000.0;
+    x = x / scale;
+    y = y / scale;
+    const double distance = double(c.crop_w) / c.hfov;
+    const double alpha = atan2(-y, x);
+    double theta = -y / distance / sin(alpha);
+    if (fabs(sin(alpha)) < 1e-3) theta = -x / distance / cos(alpha);
+    *lon = atan2(sin(theta) * cos(alpha), cos(theta));
+    *lat = atan(tan(alpha) * sin(*lon));
+}
+
 OCTVR_HD void image_to_obj_single(const CameraParams& c, double x, double y, double* lon, double* lat) {
     switch (c.type) {
+        case CAM_FULLFRAME_FISHEYE:
+            fullframe_fisheye_image_to_obj(c, x, y, lon, lat);
+            return;
         case CAM_NORMAL: {
             double xx = c.cam_x;
             double yy = c.cam_y - y * 2.0 * c.cam_y;

@@ -969,10 +969,14 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
         double ar = aspect_ratio(oc);
         if (out_h <= 0) out_h = int(double(out_w) / ar);
         if (out_w <= 0) out_w = int(double(out_h) * ar);
-        // the output camera needs image_to_obj_single: fisheye / pinhole throw NotImplemented (camera.hpp:101-103);
-        // fullframe_fisheye's needs cv::solvePoly (fullframe_fisheye_cam.cpp:160-184), not provided here
-        if (out_cam.type == CAM_FULLFRAME_FISHEYE || out_cam.type == CAM_FISHEYE || out_cam.type == CAM_PINHOLE)
+        // the output camera needs image_to_obj_single: fisheye / pinhole throw NotImplemented (camera.hpp:101-103)
+        if (out_cam.type == CAM_FISHEYE || out_cam.type == CAM_PINHOLE)
             throw OctvrError(OCTVR_E_UNSUPPORTED, "output camera type '" + oc["type"].as_string() + "' is not supported");
+        // CV_Assert(crop.size() == size && crop.tl() == Point(0, 0)) (fullframe_fisheye_cam.cpp:224)
+        if (out_cam.type == CAM_FULLFRAME_FISHEYE)
+            REQUIRE(out_cam.crop_x == 0 && out_cam.crop_y == 0 && out_cam.crop_w == out_cam.width &&
+                        out_cam.crop_h == out_cam.height,
+                    "fullframe_fisheye output camera: crop must cover the whole image");
         auto rig = std::make_unique<octvr_rig>();
         rig->out_w = out_w;
         rig->out_h = out_h;

@@ -426,8 +426,78 @@ static void lonlat_of(double x, double y, double z, double* lon, double* lat) {
 }
 
 /* image_to_obj_single of the output camera types (the cameras/ files cited in octvr_oracle.h). */
+/* cv::solvePoly (core/src/mathfuncs.cpp:2063-2182, maxIters 300) for real coefficients, written with
+ * cv::Complex<double> semantics (core/types.hpp:960-1029).  Returns the trimmed degree; only roots
+ * [0, n) are defined (the reference copies uninitialised memory into rows n..n0-1).  The
+ * num_same_root > 1 branch (:2119-2157) needs bit-identical iterates and is not restated. */
+typedef struct { double re, im; } cplx;
+static cplx c_mul(cplx a, cplx b) { cplx r = {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; return r; }
+static cplx c_add(cplx a, cplx b) { cplx r = {a.re + b.re, a.im + b.im}; return r; }
+static cplx c_sub(cplx a, cplx b) { cplx r = {a.re - b.re, a.im - b.im}; return r; }
+static cplx c_div(cplx a, cplx b) {
+    double t = 1. / ((double)b.re * b.re + (double)b.im * b.im);
+    cplx r = {(a.re * b.re + a.im * b.im) * t, (-a.re * b.im + a.im * b.re) * t};
+    return r;
+}
+static int solve_poly(const double* a, int n0, cplx* roots) {
+    cplx coeffs[16];
+    int n = n0;
+    for (int i = 0; i <= n0; i++) { coeffs[i].re = a[i]; coeffs[i].im = 0; }
+    for (; n > 1; n--)
+        if (fabs(coeffs[n].re) + fabs(coeffs[n].im) > DBL_EPSILON) break;
+    cplx p = {1, 0}, r = {1, 1};
+    for (int i = 0; i < n; i++) { roots[i] = p; p = c_mul(p, r); }
+    for (int iter = 0; iter < 300; iter++) {
+        double maxDiff = 0;
+        for (int i = 0; i < n; i++) {
+            p = roots[i];
+            cplx num = coeffs[n], denom = coeffs[n];
+            for (int j = 0; j < n; j++) {
+                num = c_add(c_mul(num, p), coeffs[n - j - 1]);
+                if (j != i) {
+                    cplx d = c_sub(p, roots[j]);
+                    if (d.re != 0 || d.im != 0) denom = c_mul(denom, d);
+                }
+            }
+            num = c_div(num, denom);
+            roots[i] = c_sub(p, num);
+            double ad = sqrt((double)num.re * num.re + (double)num.im * num.im);
+            if (ad > maxDiff) maxDiff = ad;
+        }
+        if (maxDiff <= 0) break;
+    }
+    for (int i = 0; i < n; i++)
+        if (fabs(roots[i].im) < 1e-100) roots[i].im = 0;
+    return n;
+}
+
+/* FullFrameFisheyeCamera::image_to_obj_single + do_reverse_radial_distort
+ * (cameras/fullframe_fisheye_cam.cpp:160-185, 223-253) */
+static void fullframe_image_to_obj(const orc_camera* c, double x, double y, double* lon, double* lat) {
+    x = (x - 0.5) * (double)c->crop_w - c->center_dx;
+    y = (y - 0.5) * (double)c->crop_h - c->center_dy;
+    if (fabs(x) < 1e-5 && fabs(y) < 1e-5) { *lon = 0; *lat = 0; return; }
+    double sq = sqrt(x * x + y * y);
+    double coeffs[5] = {-sq / c->rad[4], c->rad[0], c->rad[1], c->rad[2], c->rad[3]};
+    cplx roots[4];
+    double r = -1;
+    int n = solve_poly(coeffs, 4, roots);
+    for (int i = 0; i < n; i++)
+        if (fabs(roots[i].im) < 1e-3 && roots[i].re > 0 && (roots[i].re < r || r < 0)) r = roots[i].re;
+    double scale = (r < c->rad[5] && r > 0) ? sq / c->rad[4] / r : 1000.0;
+    x /= scale;
+    y /= scale;
+    double distance = (double)c->crop_w / c->hfov;
+    double alpha = atan2(-y, x);
+    double theta = -y / distance / sin(alpha);
+    if (fabs(sin(alpha)) < 1e-3) theta = -x / distance / cos(alpha);
+    *lon = atan2(sin(theta) * cos(alpha), cos(theta));
+    *lat = atan(tan(alpha) * sin(*lon));
+}
+
 static void image_to_obj_single(const orc_camera* c, double x, double y, double* lon, double* lat) {
     switch (c->type) {
+    case ORC_FULLFRAME_FISHEYE: fullframe_image_to_obj(c, x, y, lon, lat); return;
     case ORC_NORMAL: /* normal.cpp:24-30 */
         lonlat_of(c->cam_x, c->cam_y - y * 2.0 * c->cam_y, c->cam_z - x * 2.0 * c->cam_z, lon, lat);
         return;

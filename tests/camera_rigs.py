@@ -15,6 +15,9 @@ OUTPUT_MODELS = {
     "eqareanorthpole": {},
     "eqareasouthpole": {"antarctic_circle": -0.9},
     "ocam_fisheye": OCAM,
+    # no crop: the output fisheye's crop must be the whole image (fullframe_fisheye_cam.cpp:224)
+    "fullframe_fisheye": {"width": 480, "height": 320, "hfov": 3.0, "center_dx": 2.0, "center_dy": -1.5,
+                          "radial": [0.02, -0.05, 0.01]},
 }
 
 

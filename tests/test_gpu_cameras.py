@@ -13,7 +13,8 @@ import oracle_py as O
 pytestmark = pytest.mark.gpu
 
 ASPECT = {"normal": 1.5, "perspective": 1.25, "stupidoval": 2.0, "cubic": 1.5, "eqareanorthpole": 1.0,
-          "eqareasouthpole": 1.0, "ocam_fisheye": 640 / 480}
+          "eqareasouthpole": 1.0, "ocam_fisheye": 640 / 480,
+          "fullframe_fisheye": 1.5}
 
 
 def _compare(ox, rig, W, H, use_roi=False):

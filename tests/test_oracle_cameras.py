@@ -10,7 +10,8 @@ import camera_rigs as R
 import oracle_py as O
 
 
-@pytest.mark.parametrize("t", ["normal", "perspective", "stupidoval", "eqareanorthpole", "eqareasouthpole", "cubic"])
+@pytest.mark.parametrize("t", ["normal", "perspective", "stupidoval", "eqareanorthpole", "eqareasouthpole", "cubic",
+                               "fullframe_fisheye"])
 def test_oracle_camera_round_trip(t):
     o = R.OUTPUT_MODELS[t]
     rig = {"output": {"type": t, "options": o}, "inputs": [{"type": t, "options": o}]}
@@ -60,3 +61,16 @@ def test_oracle_selection_excludes_outside_rectangle():
         px, py = (m1 * c["options"]["width"]).astype(int), (m2 * c["options"]["height"]).astype(int)
         inside = (mk > 0) & (px >= l) & (px <= r - 1) & (py >= t) & (py <= btm - 1)
         assert np.array_equal(a[3] > 0, inside)
+
+
+def test_oracle_fullframe_output_without_distortion_round_trip():
+    """radial [0,0,0]: solvePoly trims the quartic to degree 1 (mathfuncs.cpp:2091-2095)."""
+    o = dict(R.OUTPUT_MODELS["fullframe_fisheye"], radial=[0.0, 0.0, 0.0], center_dx=0.0, center_dy=0.0)
+    rig = {"output": {"type": "fullframe_fisheye", "options": o}, "inputs": [{"type": "fullframe_fisheye", "options": o}]}
+    W, H = 96, 64
+    _, m1, m2, mk = O.lut_build(rig, W, H, use_roi=False)[0]
+    xs = (np.arange(W) / W)[None, :]
+    ys = (np.arange(H) / H)[:, None]
+    v = mk > 0
+    assert v.mean() > 0.9
+    assert ((np.abs(m1 - xs) < 1e-6) & (np.abs(m2 - ys) < 1e-6))[v].all()
