@@ -73,10 +73,12 @@ def test_oracle_fullframe_output_without_distortion_round_trip():
     ys = (np.arange(H) / H)[:, None]
     v = mk > 0
     assert v.mean() > 0.9
-    # the centre row's left half is mirrored by the reference itself: y == 0 gives alpha = atan2(-0., x<0)
-    # = -pi, |sin(alpha)| < 1e-3 selects theta = -x/distance/cos(alpha) > 0 ... < 0 (cam.cpp:242-248)
+    # the centre row is mirrored by the reference itself: y == 0 gives alpha = atan2(-0., x) = -pi or -0,
+    # |sin(alpha)| < 1e-3 selects theta = -x / distance / cos(alpha), whose sign is flipped against the
+    # forward model (fullframe_fisheye_cam.cpp:242-248)
     quirk = np.zeros_like(v)
-    quirk[H // 2, 1:W // 2] = True
+    quirk[H // 2, 1:] = True
+    quirk[H // 2, W // 2] = False
     ok = (np.abs(m1 - xs) < 1e-6) & (np.abs(m2 - ys) < 1e-6)
     assert ok[v & ~quirk].all()
-    assert np.allclose(m1[quirk], 1.0 - xs[0, 1:W // 2], atol=1e-6)
+    assert np.allclose(m1[quirk], 1.0 - xs[0][quirk[H // 2]], atol=1e-6)
