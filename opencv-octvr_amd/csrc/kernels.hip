@@ -12,6 +12,9 @@
 
 #include "device_common.hpp"
 #include "kernels.hpp"
+#ifndef OCTVR_LU_BLOCK_MIN  // smallest n solved by the workgroup-parallel LU (below: one lane, registers)
+#define OCTVR_LU_BLOCK_MIN 9
+#endif
 #ifndef OCTVR_FEED_VARIANT
 #define OCTVR_FEED_VARIANT 0
 #endif
@@ -402,7 +405,7 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
     // cv::solve (lapack.cpp:1050-1275): one lane with the matrix in registers for n <= 8 (closed forms
     // n <= 3); the LU across the workgroup for 9..16
     bool ok;
-    if (n <= 8) {
+    if (n < OCTVR_LU_BLOCK_MIN || n <= 3) {
         if (tid == 0) s_last = solve_dispatch(s_A, s_b, n, s_x) ? 1 : 0;
         __syncthreads();
         ok = s_last != 0;
