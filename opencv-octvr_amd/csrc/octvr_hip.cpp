@@ -990,7 +990,10 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
             const JsonValue& ov = doc["overlays"];
             rig->overlays.resize(ov.size());
             for (size_t i = 0; i < ov.size(); i++)
-                build_input(out_cam, ov[i], out_w, out_h, use_roi != 0, device, rig->overlays[i]);
+                // overlays go through the same add_input: they share visible_mask and their include
+                // masks clear the (non-overlay) inputs' masks (template.cpp:102-116, 147-150)
+                build_input(out_cam, ov[i], out_w, out_h, use_roi != 0, device, rig->overlays[i], &visible,
+                            &rig->inputs);
         }
         *out = rig.release();
     });

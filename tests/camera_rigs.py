@@ -106,6 +106,12 @@ def mask_rigs():
         "png": [dict(ff, exclude_masks=[{"type": "png", "args": list(png)}], **_rot(0.3)),
                 dict(ff, exclude_masks=[], include_masks=[concave], **_rot(-0.9))],
     }
-    return {name: {"output": {"type": "equirectangular", "options": _rot(0.1, 0.05)},
-                   "inputs": [{"type": "fullframe_fisheye", "options": o} for o in opts]}
-            for name, opts in rigs.items()}
+    out = {name: {"output": {"type": "equirectangular", "options": _rot(0.1, 0.05)},
+                  "inputs": [{"type": "fullframe_fisheye", "options": o} for o in opts]}
+           for name, opts in rigs.items()}
+    # an overlay whose include mask claims pixels: the inputs' masks lose them (template.cpp:102-116)
+    ov = dict(out["exclude_poly"])
+    ov["overlays"] = [{"type": "fullframe_fisheye", "options": dict(
+        ff, exclude_masks=[], include_masks=[poly(200, 40, 440, 40, 440, 320, 200, 320)], **_rot(1.0))}]
+    out["overlay_include"] = ov
+    return out

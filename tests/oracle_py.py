@@ -215,12 +215,14 @@ def camera_masks(o):
 
 
 def lut_build(rig, out_w, out_h, use_roi=True):
-    """Per input: (roi, map1, map2, mask) cropped to the ROI, as MapperTemplate::add_input, including the
-    include-mask visible_mask arbitration across inputs (template.cpp:86-116)."""
+    """Per input, then per overlay: (roi, map1, map2, mask) cropped to the ROI, as
+    MapperTemplate::add_input, including the include-mask visible_mask arbitration across inputs and
+    overlays (template.cpp:86-116)."""
     out = camera_from_json(rig["output"])
     res = []
     visible = None
-    for cam in rig["inputs"]:
+    n_inputs = len(rig["inputs"])
+    for k, cam in enumerate(rig["inputs"] + rig.get("overlays", [])):
         c = camera_from_json(cam)
         m1 = np.empty((out_h, out_w), np.float32)
         m2 = np.empty((out_h, out_w), np.float32)
@@ -233,7 +235,7 @@ def lut_build(rig, out_w, out_h, use_roi=True):
                                      roi, vp)
         assert rc == 0
         if visible is not None and c.incl:
-            for (px, py, pw, ph), _, _, pm in res:
+            for (px, py, pw, ph), _, _, pm in res[:n_inputs]:  # only this->inputs (template.cpp:106)
                 pm[visible[py:py + ph, px:px + pw] == 2] = 0
             visible[visible == 2] = 1
         x, y, w, h = roi[:]
