@@ -159,17 +159,20 @@ struct QuadOut {
 // two lanes' worth per instruction, each element rounded exactly like the scalar op) and the chroma
 // sums accumulate as the pair (us, vs) in the same pixel order.
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
+// gain2[p] = {g, g}: the pair the packed multiply reads, held in two defined registers (a scalar
+// gain broadcast by op_sel would make the multiply read the register after it, and the compiler
+// then waits for whatever load is in flight into that one).
+__device__ __forceinline__ QuadOut finish_quad2(const uint32_t (&rgb)[4][3], const f32x2_t (&gain2)[4]) {
     uint32_t y01 = 0, y23 = 0;
     f32x2_t uv = {0.f, 0.f};  // (us, vs)
     const f32x2_t kuv = {0.492f, 0.877f};
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         // gain: saturate_cast<uchar>(px * g), kept as an exact float of the saturated integer
-        f32x2_t br = f32x2_t{(float)rgb[p][2], (float)rgb[p][0]} * gain[p];
+        f32x2_t br = f32x2_t{(float)rgb[p][2], (float)rgb[p][0]} * gain2[p];
         br.x = __builtin_amdgcn_fmed3f(__builtin_rintf(br.x), 0.f, 255.f);
         br.y = __builtin_amdgcn_fmed3f(__builtin_rintf(br.y), 0.f, 255.f);
-        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain[p]), 0.f, 255.f);
+        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain2[p].x), 0.f, 255.f);
         const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
         if (p < 2) y01 = pack_u8(Yf, p, y01);
         else y23 = pack_u8(Yf, p - 2, y23);
@@ -181,6 +184,11 @@ __device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], cons
     q.u = pack_u8(__builtin_fmaf(uv.x, 0.25f, 128.f), 0, 0u);
     q.v = pack_u8(__builtin_fmaf(uv.y, 0.25f, 128.f), 0, 0u);
     return q;
+}
+
+__device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
+    const f32x2_t g2[4] = {{gain[0], gain[0]}, {gain[1], gain[1]}, {gain[2], gain[2]}, {gain[3], gain[3]}};
+    return finish_quad2(rgb, g2);
 }
 
 // The output frame as a buffer resource: stores of a quad outside W x H get an offset past the

@@ -128,6 +128,7 @@ struct TiledLutBuild {
     std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
     double staged_bytes = 0;
+    std::string stats;  // JSON fragment: staged items by staging chunks / LDS bytes, per-band chunk sums
 };
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
                               const std::vector<int>& in_h);
@@ -139,7 +140,9 @@ struct TiledLutDev {
     DevBuf<uint32_t> wide_tiles;
     DevBuf<uint8_t> wide_cams;
     DevBuf<int32_t> bands;
+    DevBuf<uint32_t> queue;
     double staged_bytes = 0;
+    std::string stats;
     TiledLut view{};
     void upload(const TiledLutBuild& b);
 };

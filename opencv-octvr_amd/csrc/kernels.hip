@@ -21,6 +21,17 @@
 
 namespace octvr {
 
+#if OCTVR_PHASES && !OCTVR_STAMPS
+#define OCTVR_STAMPS 2  // the phase rows share the stamp buffer (no per-workgroup stamps then)
+#endif
+#if OCTVR_STAMPS
+// Diagnostic builds only (scripts/build_variant.sh NAME -DOCTVR_STAMPS=1): per-workgroup start / end
+// wall-clock stamps (s_memrealtime, 100 MHz) of the stitch and gain-feed kernels, read back with
+// octvr_debug_stamps().  Rows of 4 u64: start, end, items processed, staging chunks processed.
+constexpr int kStampRows = 8192;
+__device__ unsigned long long g_octvr_stamps[2 * kStampRows * 4];
+#endif
+
 // ---------------------------------------------------------------------------------------------
 // LUT build: MapperTemplate::add_input (template.cpp:46-133), one thread per output pixel, FP64.
 // bbox = {min_w, min_h, max_w, max_h} of valid pixels (int atomics, initialised by the host).
@@ -311,6 +322,9 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
     __shared__ double s_b[kGainMaxCams];
     __shared__ double s_x[kGainMaxCams];
     const int tid = threadIdx.x, lane = tid & 63;
+#if OCTVR_STAMPS == 1
+    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+#endif
     const GainChunk ch = chunks[blockIdx.x];
     double acc[kGainMaxCams];
 #pragma unroll
@@ -367,6 +381,15 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
             last = __hip_atomic_fetch_add(&tickets[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
         }
         s_last = last;
+#if OCTVR_STAMPS == 1
+        if (blockIdx.x < kStampRows) {
+            unsigned long long* r = g_octvr_stamps + (size_t)(kStampRows + blockIdx.x) * 4;
+            r[0] = st0;
+            r[1] = __builtin_amdgcn_s_memrealtime();
+            r[2] = (unsigned long long)last;
+            r[3] = (unsigned long long)(ch.end - ch.begin);
+        }
+#endif
     }
     __syncthreads();
     if (!s_last) return;
@@ -413,6 +436,10 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
         ok = lu_solve_block(s_A, s_b, n, s_x);
     }
     if (tid < n) gains[tid] = ok ? s_x[tid] : 1.0;  // cv::solve failure leaves gains_ unspecified; 1 as the oracle
+#if OCTVR_STAMPS == 1
+    if (tid == 0 && blockIdx.x < kStampRows)
+        g_octvr_stamps[(size_t)(kStampRows + blockIdx.x) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
@@ -448,17 +475,7 @@ hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, 
 // walked grid-stride; blocks b, b+8, ... (one XCD under round-robin dispatch) take a contiguous
 // band of tiles so their source boxes share that XCD's L2.
 // ---------------------------------------------------------------------------------------------
-// The tile's slot descriptors as 16 raw dwords in scalar registers (the tile index is wave-uniform).
-// Slot q: dword 4q = cam | bw << 16, 4q+1 = bh | lds << 16, 4q+2 = bx0 | by0 << 16, 4q+3 = chunk0.
-// Only static indices and explicit selects touch it, so it never lands in scratch memory.
-struct SlotSet {
-    uint32_t w[4 * kTileSlots];
-};
 static_assert(sizeof(TileSlot) == 16, "TileSlot layout");
-
-__device__ __forceinline__ uint32_t sel4(int q, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
-    return q == 0 ? a0 : q == 1 ? a1 : q == 2 ? a2 : a3;
-}
 
 // The per-call FrameSet is the FIRST argument of the stitch kernels: index it in the kernarg
 // segment directly (a wave-uniform index gives scalar loads; indexing the by-value parameter would
@@ -481,47 +498,86 @@ struct StageGroup {
     uint32_t y0, y1;  // 8 Y bytes
     uint32_t uq, vq;  // 4 U bytes, 4 V bytes
     int32_t dst;      // dword index of the group's first RGBA pixel; -1 = none
+    uint32_t flags;   // kStageBlack: box group outside the image; kStageNoVig: camera without vignette
     float4 g0, g1;    // VIG: vignette gains of the 8 pixels
 };
+// The loaded bytes are only touched in stage_store (an iteration later): a select on them right
+// after the load would make the compiler wait for the load in the iteration that issues it.
+constexpr uint32_t kStageBlack = 1u, kStageNoVig = 2u;
 
-// Loads of staging chunk c (wave-uniform) of a tile: 64 groups of 8 luma pixels inside one slot.
-// The slot is found with scalar compares on the slots' first chunks; a lane's group k within the
-// slot is row k / (bw/8), column k % (bw/8) of the slot's box.  Lanes past the slot's groups (and
-// chunks past the tile's) read the box origin / frame start and are marked dst = -1.  With box
-// columns 8-aligned, the Y load is 8-byte and the U / V loads 4-byte aligned (DWORD_STAGE).
-template <bool DWORD_STAGE, bool VIG>
-__device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32_t nchunks, uint32_t stride, int c,
-                                           StageGroup& sg) {
-    const int lane = threadIdx.x & 63;
-    const bool live_chunk = (uint32_t)c < nchunks;
+// Metadata of a staged item as the waves hold it: one 16-byte load by 5 lanes (lane 0 the TileHdr,
+// lane 1 + q slot q's TileSlot), decoded with v_readlane on demand (a uniform lane index), so the
+// slot descriptors never occupy scalar registers.
+// Slot q, component j of lane 1 + q: 0 = cam | bw << 16, 1 = bh | lds << 16, 2 = bx0 | by0 << 16,
+// 3 = chunk0.
+struct TileMeta {
+    int t;
+    uint4 v;
+    uint32_t tile, nslots, stride;
+};
+
+// dword j (0-3) of slot q (wave-uniform)
+__device__ __forceinline__ uint32_t slot_word(const TileMeta& m, int q, int j) {
+    const uint32_t c = j == 0 ? m.v.x : j == 1 ? m.v.y : j == 2 ? m.v.z : m.v.w;
+    return (uint32_t)__builtin_amdgcn_readlane((int)c, 1 + q);
+}
+
+// The slot of staging chunk c (wave-uniform) and the frame it reads, resolved with scalar work and
+// scalar kernarg loads; done one phase before the vector loads that use it, so their latency hides.
+struct StageSlot {
+    uint32_t live;             // c is a chunk of a live item
+    uint32_t cam, bw, bh, lds, bx0, by0, chunk0;
+    SourceFrame f;
+};
+
+__device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, int c) {
+    StageSlot s;
+    const uint32_t nchunks = m.t < t_end ? ((m.nslots >> 8) & 0xFFu) : 0u;
+    const int nslots = (int)(m.nslots & 0xFFu);
+    s.live = (uint32_t)c < nchunks ? 1u : 0u;
     int q = 0;
 #pragma unroll
-    for (int j = 1; j < kTileSlots; j++) q += (j < nslots && c >= (int)(ss.w[4 * j + 3] & 0xFFFFu)) ? 1 : 0;
-    const uint32_t d0 = sel4(q, ss.w[0], ss.w[4], ss.w[8], ss.w[12]);
-    const uint32_t d1 = sel4(q, ss.w[1], ss.w[5], ss.w[9], ss.w[13]);
-    const uint32_t d2 = sel4(q, ss.w[2], ss.w[6], ss.w[10], ss.w[14]);
-    const uint32_t d3 = sel4(q, ss.w[3], ss.w[7], ss.w[11], ss.w[15]);
-    const uint32_t cam = d0 & 31u, bw = d0 >> 16, bh = d1 & 0xFFFFu, lds = d1 >> 16;
-    const uint32_t bx0 = d2 & 0xFFFFu, by0 = d2 >> 16, chunk0 = d3 & 0xFFFFu;
-    const uint32_t rowg = max(1u, bw >> 3);
-    const uint32_t groups = bw * bh >> 3;
-    const uint32_t k = (uint32_t)(c - (int)chunk0) * 64u + (uint32_t)lane;
-    const bool ok = live_chunk && k < groups;
+    for (int j = 1; j < kTileSlots; j++) q += (j < nslots && c >= (int)(slot_word(m, j, 3) & 0xFFFFu)) ? 1 : 0;
+    const uint32_t d0 = slot_word(m, q, 0), d1 = slot_word(m, q, 1);
+    const uint32_t d2 = slot_word(m, q, 2), d3 = slot_word(m, q, 3);
+    s.cam = s.live ? (d0 & 31u) : 0u;
+    s.bw = d0 >> 16;
+    s.bh = d1 & 0xFFFFu;
+    s.lds = d1 >> 16;
+    s.bx0 = d2 & 0xFFFFu;
+    s.by0 = d2 >> 16;
+    s.chunk0 = d3 & 0xFFFFu;
+    s.f = kernarg_frame(s.cam);
+    return s;
+}
+
+// Loads of staging chunk c of a tile: 64 groups of 8 luma pixels inside one slot.  A lane's group k
+// within the slot is row k / (bw/8), column k % (bw/8) of the slot's box.  Lanes past the slot's
+// groups (and chunks past the item's) read the box origin and are marked dst = -1.  With box columns
+// 8-aligned, the Y load is 8-byte and the U / V loads 4-byte aligned (DWORD_STAGE).
+// Offsets use 24-bit multiplies: rows < 256, pitch < 2^24 (checked on the host).
+template <bool DWORD_STAGE, bool VIG>
+__device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, int c, StageGroup& sg) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t rowg = max(1u, s.bw >> 3);
+    const uint32_t groups = s.bw * s.bh >> 3;
+    const uint32_t k = (uint32_t)(c - (int)s.chunk0) * 64u + (uint32_t)lane;
+    const bool ok = s.live && k < groups;
     // k < 2^14, rowg <= 32: (k + 0.5) / rowg is >= 1/64 away from an integer, far above f32 error
     const float inv = __builtin_amdgcn_rcpf((float)rowg);
     const uint32_t row_f = (uint32_t)(((float)k + 0.5f) * inv);
-    const uint32_t row_k = ok ? row_f : 0u, col_k = ok ? k - row_f * rowg : 0u;
-    const SourceFrame f = kernarg_frame(live_chunk ? cam : 0u);
+    const uint32_t row_k = ok ? row_f : 0u, col_k = ok ? k - __umul24(row_f, rowg) : 0u;
+    const SourceFrame& f = s.f;
     // box groups past the image's right / bottom edge (w % 8 == 0: whole groups) stage RGBA 0:
     // they load from the box origin and are replaced by Y = 0, U = V = 128 (-> R = G = B = 0)
-    const bool img = bx0 + col_k * 8u < (uint32_t)f.w && by0 + row_k < (uint32_t)f.h;
+    const bool img = s.bx0 + col_k * 8u < (uint32_t)f.w && s.by0 + row_k < (uint32_t)f.h;
     const uint32_t row = img ? row_k : 0u, col = img ? col_k : 0u;
     const uint32_t p32 = (uint32_t)f.pitch;
     const gu8* base = (const gu8*)f.yuv;
-    const gu8* Yb = base + (int64_t)by0 * f.pitch + bx0;  // by0, bx0 even: chroma rows / columns exact
-    const gu8* Ub = base + (int64_t)(f.h + (int)(by0 >> 1)) * f.pitch + (bx0 >> 1);
+    const gu8* Yb = base + (int64_t)s.by0 * f.pitch + s.bx0;  // by0, bx0 even: chroma rows / columns exact
+    const gu8* Ub = base + (int64_t)(f.h + (int)(s.by0 >> 1)) * f.pitch + (s.bx0 >> 1);
     const gu8* Vb = Ub + (f.w >> 1);
-    const uint32_t oy = row * p32 + col * 8u, oc = (row >> 1) * p32 + col * 4u;
+    const uint32_t oy = __umul24(row, p32) + col * 8u, oc = __umul24(row >> 1, p32) + col * 4u;
     if (DWORD_STAGE) {
         const uint64_t yy = *(const gu64*)(Yb + oy);
         sg.y0 = (uint32_t)yy;
@@ -537,27 +593,29 @@ __device__ __forceinline__ void stage_load(const SlotSet& ss, int nslots, uint32
         sg.uq = (uint32_t)Up[0] | ((uint32_t)Up[1] << 8) | ((uint32_t)Up[2] << 16) | ((uint32_t)Up[3] << 24);
         sg.vq = (uint32_t)Vp[0] | ((uint32_t)Vp[1] << 8) | ((uint32_t)Vp[2] << 16) | ((uint32_t)Vp[3] << 24);
     }
-    if (!img) {
-        sg.y0 = sg.y1 = 0u;
-        sg.uq = sg.vq = 0x80808080u;
-    }
-    sg.dst = ok ? (int32_t)(lds + row_k * stride + col_k * 8u) : -1;
-    if (VIG) {  // 8 gains (32-byte aligned: w % 8 == 0); a camera without vignette reads 1.0 gains
-        const float* gv = f.vig ? f.vig + (int64_t)(by0 + row) * f.w + bx0 + col * 8u : nullptr;
-        sg.g0 = gv ? *reinterpret_cast<const float4*>(gv) : make_float4(1.f, 1.f, 1.f, 1.f);
-        sg.g1 = gv ? *reinterpret_cast<const float4*>(gv + 4) : make_float4(1.f, 1.f, 1.f, 1.f);
+    sg.flags = img ? 0u : kStageBlack;
+    sg.dst = ok ? (int32_t)(s.lds + __umul24(row_k, stride) + col_k * 8u) : -1;
+    if (VIG) {  // 8 gains (32-byte aligned: w % 8 == 0); a camera without vignette uses 1.0 gains
+        const float* gv = f.vig ? f.vig + (int64_t)(s.by0 + row) * f.w + s.bx0 + col * 8u
+                                : reinterpret_cast<const float*>(f.yuv);  // any readable 32 B, unused
+        sg.g0 = *reinterpret_cast<const float4*>(gv);
+        sg.g1 = *reinterpret_cast<const float4*>(gv + 4);
+        if (!f.vig) sg.flags |= kStageNoVig;
     }
 }
 
 template <bool VIG>
 __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rgb) {
     if (sg.dst < 0) return;
+    const bool black = (sg.flags & kStageBlack) != 0;  // Y = 0, U = V = 128 -> RGBA 0
+    const uint32_t y0 = black ? 0u : sg.y0, y1 = black ? 0u : sg.y1;
+    const uint32_t uq = black ? 0x80808080u : sg.uq, vq = black ? 0x80808080u : sg.vq;
     uint4 a, b;
-    yuv2_to_rgba(sg.y0 & 255u, (sg.y0 >> 8) & 255u, sg.uq & 255u, sg.vq & 255u, a.x, a.y);
-    yuv2_to_rgba((sg.y0 >> 16) & 255u, sg.y0 >> 24, (sg.uq >> 8) & 255u, (sg.vq >> 8) & 255u, a.z, a.w);
-    yuv2_to_rgba(sg.y1 & 255u, (sg.y1 >> 8) & 255u, (sg.uq >> 16) & 255u, (sg.vq >> 16) & 255u, b.x, b.y);
-    yuv2_to_rgba((sg.y1 >> 16) & 255u, sg.y1 >> 24, sg.uq >> 24, sg.vq >> 24, b.z, b.w);
-    if (VIG) {
+    yuv2_to_rgba(y0 & 255u, (y0 >> 8) & 255u, uq & 255u, vq & 255u, a.x, a.y);
+    yuv2_to_rgba((y0 >> 16) & 255u, y0 >> 24, (uq >> 8) & 255u, (vq >> 8) & 255u, a.z, a.w);
+    yuv2_to_rgba(y1 & 255u, (y1 >> 8) & 255u, (uq >> 16) & 255u, (vq >> 16) & 255u, b.x, b.y);
+    yuv2_to_rgba((y1 >> 16) & 255u, y1 >> 24, uq >> 24, vq >> 24, b.z, b.w);
+    if (VIG && !(sg.flags & kStageNoVig)) {
         a.x = vig_mul(a.x, sg.g0.x);
         a.y = vig_mul(a.y, sg.g0.y);
         a.z = vig_mul(a.z, sg.g0.z);
@@ -575,14 +633,23 @@ __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rg
 #define OCTVR_STITCH_BLOCKS_PER_CU 6
 #endif
 constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
+// Residency of 256-thread workgroups is also capped by scalar registers: min(8, 800 / (sgpr16 + 16))
+// (MI355X_MICROARCH.md, Residency), i.e. <= 80 SGPRs for 8 per CU, <= 96 for 7 (the compiler's own
+// occupancy model allows more, so the budget is set explicitly).
+#ifndef OCTVR_STITCH_SGPRS
+#define OCTVR_STITCH_SGPRS (kStitchBlocksPerCU >= 8 ? 80 : kStitchBlocksPerCU == 7 ? 96 : 102)
+#endif
 #ifndef OCTVR_STAGE_REGS
 #define OCTVR_STAGE_REGS 1
 #endif
 #ifndef OCTVR_STAGE_SKIP
 #define OCTVR_STAGE_SKIP 1
 #endif
-#ifndef OCTVR_INNER_PAIR
-#define OCTVR_INNER_PAIR 0
+#ifndef OCTVR_DYN  // 0: static round-robin dealing of a band's items (no work counters)
+#define OCTVR_DYN 1
+#endif
+#ifndef OCTVR_WIDE_OUT  // 0: always the per-quad 1-2-byte output stores
+#define OCTVR_WIDE_OUT 1
 #endif
 constexpr int kStageRegs = OCTVR_STAGE_REGS;  // staging groups per lane loaded one tile ahead (256 per reg)
 
@@ -595,34 +662,23 @@ constexpr int kStageRegs = OCTVR_STAGE_REGS;  // staging groups per lane loaded 
 // same vector-memory operations in the same order (clamped addresses instead of branches), so the
 // compiler's wait counts stay exact across the loop.
 //
-// Metadata in flight is one VGPR: lanes 0-3 hold the header's dwords, lanes 4-19 the 4 slots'.
-struct TileMeta {
-    int t;
-    TileHdr hd;
-    SlotSet ss;
-};
-
-__device__ __forceinline__ uint32_t meta_issue(const TiledLut& lut, int t, int t_end) {  // t: staged item
+__device__ __forceinline__ uint4 meta_issue(const TiledLut& lut, int t, int t_end) {  // t: staged item
     const int lane = threadIdx.x & 63;
     const int tt = t < t_end ? t : 0;
-    const uint32_t* p = lane < 4 ? reinterpret_cast<const uint32_t*>(lut.hdr + tt) + lane
-                                 : reinterpret_cast<const uint32_t*>(lut.slots + (int64_t)tt * kTileSlots) +
-                                       (lane < 20 ? lane - 4 : 0);
-    return *p;
+    uint4 v;
+    if (lane < 1 + kTileSlots)  // exec-masked: the instruction (and its vmcnt) is the same for every wave
+        v = lane == 0 ? *reinterpret_cast<const uint4*>(lut.hdr + tt)
+                      : *reinterpret_cast<const uint4*>(lut.slots + (int64_t)tt * kTileSlots + (lane - 1));
+    return v;
 }
 
-__device__ __forceinline__ TileMeta meta_read(uint32_t v, int t) {
+__device__ __forceinline__ TileMeta meta_read(const uint4& v, int t) {
     TileMeta m;
     m.t = t;
-    m.hd.tile = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
-    m.hd.nslots = (uint32_t)__builtin_amdgcn_readlane((int)v, 1);
-    m.hd.stage_groups = (uint32_t)__builtin_amdgcn_readlane((int)v, 2);
-    m.hd.stride = (uint32_t)__builtin_amdgcn_readlane((int)v, 3);
-    uint32_t w[4 * kTileSlots];
-#pragma unroll
-    for (int q = 0; q < 4 * kTileSlots; q++) w[q] = (uint32_t)__builtin_amdgcn_readlane((int)v, 4 + q);
-#pragma unroll
-    for (int q = 0; q < 4 * kTileSlots; q++) m.ss.w[q] = w[q];
+    m.v = v;
+    m.tile = (uint32_t)__builtin_amdgcn_readlane((int)v.x, 0);
+    m.nslots = (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0);
+    m.stride = (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0);
     return m;
 }
 
@@ -631,23 +687,28 @@ struct TileData {
     StageGroup sg[kStageRegs];
 };
 
+// Issue an item's entry load and the staging loads of its first kStageRegs chunks per wave
+// (sl[r]: the slots of chunks r * 4 + wave, from stage_slot).
 template <bool DWORD_STAGE, bool VIG>
-__device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLut& lut, const TileMeta& m, int t_end,
-                                           TileData& d) {
+__device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& m, int t_end,
+                                           const StageSlot (&sl)[kStageRegs], TileData& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
+#if OCTVR_DIAG_HOTENT  // diagnostic: every item reads item 0's entries (L2-resident)
+    d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? 0 : 0) * kTilePx)[tid];
+#else
     d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? m.t : 0) * kTilePx)[tid];
-    const uint32_t nchunks = live ? ((m.hd.nslots >> 8) & 0xFFu) : 0u;
+#endif
 #pragma unroll
     for (int r = 0; r < kStageRegs; r++) {
 #if OCTVR_STAGE_SKIP
-        if ((uint32_t)(r * 4 + wave) >= nchunks) {  // wave-uniform: no loads for a chunk the tile lacks
+        if (!sl[r].live) {  // wave-uniform: no loads for a chunk the item lacks
             d.sg[r].dst = -1;
             continue;
         }
 #endif
-        stage_load<DWORD_STAGE, VIG>(m.ss, (int)(m.hd.nslots & 0xFFu), nchunks, m.hd.stride, r * 4 + wave, d.sg[r]);
+        stage_load<DWORD_STAGE, VIG>(sl[r], m.stride, r * 4 + wave, d.sg[r]);
     }
 }
 
@@ -656,16 +717,16 @@ __device__ __forceinline__ void data_issue(const FrameSet& frames, const TiledLu
 // Mapper::stitch hands to the blender, mapper.cpp:233-262); pixels outside the camera's aligned ROI
 // are dropped.  Either way a quad's result is 4 dwords.
 template <int MODE>
-__device__ __forceinline__ QuadOut finish_any(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
+__device__ __forceinline__ QuadOut finish_any(const uint32_t (&rgb)[4][3], const f32x2_t (&gain)[4]) {
     if constexpr (MODE == 0) {
-        return finish_quad(rgb, gain);
+        return finish_quad2(rgb, gain);
     } else {
         uint32_t px[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            uint32_t v = pack_u8((float)rgb[p][0] * gain[p], 0, 0u);
-            v = pack_u8((float)rgb[p][1] * gain[p], 1, v);
-            px[p] = pack_u8((float)rgb[p][2] * gain[p], 2, v);
+            uint32_t v = pack_u8((float)rgb[p][0] * gain[p].x, 0, 0u);
+            v = pack_u8((float)rgb[p][1] * gain[p].x, 1, v);
+            px[p] = pack_u8((float)rgb[p][2] * gain[p].x, 2, v);
         }
         return QuadOut{px[0], px[1], px[2], px[3]};
     }
@@ -696,15 +757,59 @@ __device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro
         store_rgba(ro, q, cam, x, y, in);
 }
 
+// MODE 2 output staging (kernels.hpp kTileOutBytes): Y rows 0-7 (128 B each), then U rows 0-3 and
+// V rows 0-3 (64 B each) of one tile.  Each lane writes its quad's 2 + 2 Y bytes and U, V bytes.
+__device__ __forceinline__ void stage_out_quad(uint32_t* s_out, const QuadOut& q, int qx, int qy) {
+    uint8_t* b = reinterpret_cast<uint8_t*>(s_out);
+    *reinterpret_cast<uint16_t*>(b + (2 * qy) * kTileW + 2 * qx) = (uint16_t)q.y01;
+    *reinterpret_cast<uint16_t*>(b + (2 * qy + 1) * kTileW + 2 * qx) = (uint16_t)q.y23;
+    b[kTileW * kTileH + qy * (kTileW / 2) + qx] = (uint8_t)q.u;
+    b[kTileW * kTileH + (kTileH / 2) * (kTileW / 2) + qy * (kTileW / 2) + qx] = (uint8_t)q.v;
+}
+
+// Wave w stores Y rows 2w, 2w+1 and U, V row w of the staged tile whose top-left pixel is
+// (px - 2 qx, py - 2 qy) of the calling lane (px, py: the lane's quad).  Needs W % 32 == 0 and a
+// 16-byte aligned frame and pitch (checked on the host); rows at or past H are dropped.
+__device__ __forceinline__ void store_tile_wide(const OutFrame& o, const uint32_t* s_out, int px, int py, bool in, int H) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int x0 = px - 2 * (threadIdx.x & 63), y0 = py - 2 * (threadIdx.x >> 6);  // tile origin
+    int lds, row, col;  // byte offset in s_out, output row in its plane, byte column in the row
+    uint32_t plane;
+    if (lane < 16) {
+        row = y0 + 2 * w + (lane >> 3);
+        col = x0 + 16 * (lane & 7);
+        lds = (2 * w + (lane >> 3)) * kTileW + 16 * (lane & 7);
+        plane = 0u;
+    } else {
+        const int k = lane < 20 ? lane - 16 : lane - 20;
+        row = (y0 >> 1) + w;
+        col = (x0 >> 1) + 16 * (k & 3);
+        lds = kTileW * kTileH + (lane < 20 ? 0 : (kTileH / 2) * (kTileW / 2)) + w * (kTileW / 2) + 16 * (k & 3);
+        plane = lane < 20 ? o.u_off : o.v_off;
+    }
+    const bool ok = in && lane < 24 && (lane < 16 ? row < H : row < (H >> 1));
+    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + (lane < 24 ? lds : 0));
+    const uint32_t off = ok ? plane + (uint32_t)row * o.pitch + (uint32_t)col : kDropOffset;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, o.rsrc, off, 0, 0);
+}
+
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
 template <bool DWORD_STAGE, int MODE, bool VIG>
-__global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
+__global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
                                                               int64_t out_pitch, RgbaOut rgba) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
     __shared__ float s_gain[kMaxCams];
-    __shared__ float s_slot_gain[kTileSlots];
+    __shared__ f32x2_t s_slot_gain[kTileSlots];  // {g, g} per slot (finish_quad2)
+    __shared__ uint32_t s_claim;
+    // MODE 2: the previous item's YUV420P output, staged so every wave writes it with one 16-byte
+    // store per lane (Y rows 2w, 2w+1: lanes 0-15; U / V row w: lanes 16-19 / 20-23) instead of
+    // four 1-2-byte stores per quad
+    constexpr bool kWideOut = MODE == 2;
+    constexpr int SM = MODE == 1 ? 1 : 0;  // sink: YUV (finish_quad) or RGBA
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[kWideOut ? kTileOutBytes / 4 : 1];
 
     const int groups = kStitchBands;
     const int g = blockIdx.x % groups;
@@ -713,24 +818,47 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
     const int t_end = lut.bands[g + 1];
     OutFrame of{};
     RgbaSink ro{};
-    if constexpr (MODE == 0)
+    if constexpr (SM == 0)
         of = make_out_frame(out, W, H, out_pitch);
     else
         ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
+#if OCTVR_STAMPS == 1
+    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long st_items = 0, st_chunks = 0;
+#endif
 
     if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
     if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
+    // Item sequence of this workgroup: its first three items are static (t0, t0 + step, t0 + 2 step,
+    // i.e. the band's first 3 * step items dealt round-robin), every later one is claimed from the
+    // band's work counter (one returning atomic per item, issued one iteration before the item's
+    // metadata load and handed to the other waves through LDS), so workgroups that drew cheap items
+    // keep pulling work while expensive ones finish (static dealing left the band's workgroups
+    // finishing between 31 and 80 us on C2, scripts/stamps.py).
     const int t0 = t_begin + (int)(blockIdx.x / groups);
+    const int dyn0 = t_begin + 3 * step;  // item of claim value 0
+    uint32_t* const q = lut.queue + g * kQueueStride;
+    const int wave = uniform(tid >> 6);
     TileMeta cur = meta_read(meta_issue(lut, t0, t_end), t0);
     __syncthreads();
     TileData d;
-    data_issue<DWORD_STAGE, VIG>(frames, lut, cur, t_end, d);
-    uint32_t mv = meta_issue(lut, t0 + step, t_end);
+    {
+        StageSlot sl[kStageRegs];
+#pragma unroll
+        for (int r = 0; r < kStageRegs; r++) sl[r] = stage_slot(cur, t_end, r * 4 + wave);
+        data_issue<DWORD_STAGE, VIG>(lut, cur, t_end, sl, d);
+    }
+    int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
+    int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
+    uint4 mv = meta_issue(lut, t_mv, t_end);
+    uint32_t claim = 0u;  // lane 0 of wave 0: returned value of the claim in flight
+    bool claimed = false; // a claim for the item after t_n2 is in flight (uniform)
+    bool first = true;
     // opaque copies of the prologue loads: the loop-header phis then merge a load with a non-load,
     // so the compiler cannot fold them into one load at the header (waited on right there)
-    asm volatile("" : "+v"(mv));
+    asm volatile("" : "+v"(mv.x), "+v"(mv.y), "+v"(mv.z), "+v"(mv.w));
     asm volatile("" : "+v"(d.e4.x), "+v"(d.e4.y), "+v"(d.e4.z), "+v"(d.e4.w));
 #pragma unroll
     for (int r = 0; r < kStageRegs; r++)
@@ -743,44 +871,94 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
     int px = 0, py = 0;
     uint32_t pcam = 0;
     bool pin = false;
+#if OCTVR_PHASES
+    // diagnostic: per-wave shader cycles spent in each phase of the item loop (s_memtime)
+    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long pt = __builtin_amdgcn_s_memtime();
+#define OCTVR_PHASE(k)                                             \
+    do {                                                           \
+        const unsigned long long tn_ = __builtin_amdgcn_s_memtime(); \
+        ph[k] += tn_ - pt;                                         \
+        pt = tn_;                                                  \
+    } while (0)
+#else
+#define OCTVR_PHASE(k) \
+    do {               \
+    } while (0)
+#endif
     while (cur.t < t_end) {
-        const int x = (int)(cur.hd.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.hd.tile >> 16) * kTileH + qy * 2;
-        const uint32_t S = cur.hd.stride;
+        const int x = (int)(cur.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.tile >> 16) * kTileH + qy * 2;
+        const uint32_t S = cur.stride;
         const uint4 e4 = d.e4;
+        OCTVR_PHASE(5);   // back edge: waits for the loads of this item
+#if !OCTVR_DIAG_NOBAR  // diagnostic ablations (wrong output, timing only): scripts/ablate.sh
         __syncthreads();  // the previous tile's LDS readers are done
-        const TileMeta nxt = meta_read(mv, cur.t + step);
-        if (tid < kTileSlots) {
-            const uint32_t cam = sel4(tid, cur.ss.w[0], cur.ss.w[4], cur.ss.w[8], cur.ss.w[12]) & 31u;
-            s_slot_gain[tid] = s_gain[cam];
+#endif
+        OCTVR_PHASE(0);
+        const TileMeta nxt = meta_read(mv, t_mv);
+        // the next item's staging slots (+ their frames' kernarg loads), used after the barrier below
+        StageSlot sln[kStageRegs];
+#pragma unroll
+        for (int r = 0; r < kStageRegs; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
+        {  // slot q's camera word sits in lane 1 + q of the metadata's first component
+            const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
+            if (tid < kTileSlots) s_slot_gain[tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
         }
+        if (claimed && tid == 0) s_claim = claim;  // issued one iteration ago
+#if !OCTVR_DIAG_NOSTAGE
 #pragma unroll
         for (int r = 0; r < kStageRegs; r++) stage_store<VIG>(d.sg[r], s_rgb);
-        const uint32_t nch = (cur.hd.nslots >> 8) & 0xFFu;
-        if (nch > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
-            const int wave = uniform(tid >> 6);
-            int c = kStageRegs * 4 + wave;
-#if OCTVR_INNER_PAIR
-            for (; c + 4 < (int)nch; c += 8) {  // two chunks' loads in flight before their stores
-                StageGroup sa, sb;
-                stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sa);
-                stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c + 4, sb);
-                stage_store<VIG>(sa, s_rgb);
-                stage_store<VIG>(sb, s_rgb);
-            }
+        const uint32_t nch = (cur.nslots >> 8) & 0xFFu;
+#else
+        const uint32_t nch = 0;
 #endif
-            for (; c < (int)nch; c += 4) {
+#if OCTVR_STAMPS == 1
+        st_items++;
+        st_chunks += nch;
+#endif
+        if (nch > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
+            for (int c = kStageRegs * 4 + wave; c < (int)nch; c += 4) {
                 StageGroup sg;
-                stage_load<DWORD_STAGE, VIG>(cur.ss, (int)(cur.hd.nslots & 0xFFu), nch, S, c, sg);
+                stage_load<DWORD_STAGE, VIG>(stage_slot(cur, t_end, c), S, c, sg);
                 stage_store<VIG>(sg, s_rgb);
             }
         }
+        OCTVR_PHASE(1);
+#if !OCTVR_DIAG_NOBAR
         __syncthreads();
-        store_any<MODE>(of, ro, prev, pcam, px, py, pin);
-        data_issue<DWORD_STAGE, VIG>(frames, lut, nxt, t_end, d);
-        mv = meta_issue(lut, cur.t + 2 * step, t_end);
+#endif
+        OCTVR_PHASE(2);
+        // the item two ahead: static on the first iteration, else the claim handed over above
+        if (!first) {
+#if OCTVR_DYN
+            const int v = claimed ? dyn0 + (int)uniform((int)s_claim) : t_end;
+#else  // static dealing (round-robin over the band's workgroups)
+            const int v = t_n2 < t_end ? t_n2 + step : t_end;
+#endif
+            t_n2 = v < t_end ? v : t_end;
+        }
+        first = false;
+#if !OCTVR_DIAG_NOSTORE
+        if constexpr (kWideOut)
+            store_tile_wide(of, s_out, px, py, pin, H);
+        else
+            store_any<SM>(of, ro, prev, pcam, px, py, pin);
+#endif
+        data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
+        mv = meta_issue(lut, t_n2, t_end);
+        t_mv = t_n2;
+        claimed = OCTVR_DYN && t_n2 < t_end;  // claim the item after it (only while the sequence is live)
+        if (claimed && tid == 0) {
+            // an opaque (per-lane looking) address: the atomic optimizer would otherwise rewrite the
+            // single-lane claim into a wave-level one whose result it broadcasts (and waits for) at once
+            int zero = tid;
+            asm volatile("" : "+v"(zero));
+            claim = __hip_atomic_fetch_add(q + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        OCTVR_PHASE(3);
         const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
         uint32_t rgb[4][3];
-        float gain[4];
+        f32x2_t gain[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint32_t e = ent[p];
@@ -791,18 +969,66 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) stitch_tiled_kernel(F
             const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
             const uint32_t c10 = reinterpret_cast<const uint32_t*>(r1)[0];
             const uint32_t c11 = reinterpret_cast<const uint32_t*>(r1)[1];
+#if OCTVR_DIAG_NOTAPS
+            (void)c00; (void)c01; (void)c10; (void)c11;
+            rgb[p][0] = e & 255u; rgb[p][1] = (e >> 8) & 255u; rgb[p][2] = (e >> 16) & 255u;
+#else
             bilerp_rgba(c00, c01, c10, c11, (e >> 15) & 31u, (e >> 20) & 31u, rgb[p]);
+#endif
             gain[p] = s_slot_gain[(e >> 25) & 3u];
-            if (MODE == 1 && (e & kEntryNoGain)) gain[p] = 1.0f;
+            if (SM == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
         }
-        prev = finish_any<MODE>(rgb, gain);
+#if OCTVR_DIAG_NOCOMPUTE
+        prev = QuadOut{rgb[0][0] ^ rgb[1][1], rgb[2][2] ^ rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
+#else
+        prev = finish_any<SM>(rgb, gain);
+#endif
+        if constexpr (kWideOut) stage_out_quad(s_out, prev, qx, qy);  // read after the next barrier
+#if OCTVR_PHASES
+        asm volatile("" : "+v"(prev.y01), "+v"(prev.y23), "+v"(prev.u), "+v"(prev.v));
+#endif
+        OCTVR_PHASE(4);
         px = x;
         py = y;
-        pcam = (cur.hd.nslots >> 16) & 31u;
+        pcam = (cur.nslots >> 16) & 31u;
         pin = x < W && y < H;
         cur = nxt;
     }
-    store_any<MODE>(of, ro, prev, pcam, px, py, pin);
+    // the last workgroup to finish resets the work counters for the next launch (stream order makes
+    // the reset visible to it); every claim of this workgroup has returned before its ticket
+#if OCTVR_PHASES
+    if ((tid & 63) == 0 && MODE != 1 && blockIdx.x * 4 + (tid >> 6) < 2 * kStampRows * 4 / 8) {
+        unsigned long long* r = g_octvr_stamps + (size_t)(blockIdx.x * 4 + (tid >> 6)) * 8;
+        for (int k = 0; k < 6; k++) r[k] = ph[k];
+        r[6] = (unsigned long long)g;
+        r[7] = 1;
+    }
+#endif
+#undef OCTVR_PHASE
+    if (tid == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        (void)claim;
+        if (__hip_atomic_fetch_add(lut.queue + kStitchBands * kQueueStride, 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+            for (int k = 0; k <= kStitchBands; k++)
+                __hip_atomic_exchange(lut.queue + k * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if constexpr (kWideOut) {
+        __syncthreads();
+        store_tile_wide(of, s_out, px, py, pin, H);
+    } else {
+        store_any<SM>(of, ro, prev, pcam, px, py, pin);
+    }
+#if OCTVR_STAMPS == 1
+    if (MODE != 1 && tid == 0 && blockIdx.x < kStampRows) {
+        unsigned long long* r = g_octvr_stamps + (size_t)blockIdx.x * 4;
+        r[0] = st0;
+        r[1] = __builtin_amdgcn_s_memrealtime();
+        r[2] = st_items;
+        r[3] = st_chunks;
+    }
+#endif
 }
 
 // Wide tiles: one workgroup per tile, 8-byte absolute entries, direct global gathers.
@@ -830,11 +1056,12 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 #pragma unroll
     for (int p = 0; p < 4; p++) gather_taps(frames, xy[p], cd[p], tp[p]);
     uint32_t rgb[4][3];
-    float gain[4];
+    f32x2_t gain[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
-        gain[p] = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
+        const float gp = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
+        gain[p] = f32x2_t{gp, gp};
     }
     const uint32_t cam = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;
     store_any<MODE>(of, ro, finish_any<MODE>(rgb, gain), cam, x, y, x < W && y < H);
@@ -856,9 +1083,18 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
             if ((reinterpret_cast<uintptr_t>(f.yuv) & 7u) || (f.pitch & 7) || (f.w & 7)) dw = false;
             vig |= f.vig != nullptr;
         }
-#define OCTVR_LAUNCH_TILED(DW, V)                                                                          \
-    hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H, \
-                       gains, use_gain, out, out_pitch, rgba)
+        // YUV output with 16-byte row segments: the LDS-staged wide stores (MODE 2)
+        const bool wide_out = MODE == 0 && OCTVR_WIDE_OUT && W % 32 == 0 && out_pitch % 16 == 0 &&
+                              (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+#define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
+    do {                                                                                                       \
+        if (wide_out)                                                                                          \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H, \
+                               gains, use_gain, out, out_pitch, rgba);                                         \
+        else                                                                                                   \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), 0, s, frames, lut, W, \
+                               H, gains, use_gain, out, out_pitch, rgba);                                      \
+    } while (0)
         if (dw && !vig)
             OCTVR_LAUNCH_TILED(true, false);
         else if (dw)
@@ -876,6 +1112,15 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
                            use_gain, out, out_pitch, rgba);
     return hipGetLastError();
 }
+
+#if OCTVR_STAMPS
+extern "C" int octvr_debug_stamps(unsigned long long* out, int rows) {
+    if (rows > 2 * kStampRows) rows = 2 * kStampRows;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_octvr_stamps), (size_t)rows * 4 * 8, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess ? rows : -1;
+}
+#endif
 
 hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                          int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {

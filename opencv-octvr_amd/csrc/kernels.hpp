@@ -58,6 +58,7 @@ constexpr int kTileSlots = 4;
 #endif
 constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
 constexpr int kTileZeroDwords = 4;
+constexpr int kTileOutBytes = kTileW * kTileH * 3 / 2;  // one tile's YUV420P output (LDS-staged stores)
 
 struct TileSlot {
     uint16_t cam;
@@ -143,7 +144,10 @@ struct TiledLut {
     int n_wide;
     const uint8_t* wide_cams;     // RGBA mode: output camera of each wide tile
     const int32_t* bands;         // kStitchBands + 1 staged-item boundaries (one band per XCD)
+    uint32_t* queue;              // per band a work counter, then a done ticket, kQueueStride apart;
+                                  // zero before a launch, left zero by its last workgroup
 };
+constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter
 // The staged items are cut into one contiguous band per XCD (locality: neighbouring tiles share
 // source boxes in that XCD's L2), balanced by cost = base + chunk weight x staging chunks.  Measured
 // on the C2 rig (r01 v10): equal item counts (chunk weight 0) beat every chunk-weighted split tried

@@ -668,9 +668,11 @@ struct octvr_mapper {
     DevBuf<uint8_t> result;
     DevBuf<MbCamLevel> result_view;  // the result frame as a one-entry RGBA sink of the composite
     hipStream_t last_stream = nullptr;
+    hipEvent_t order_ev = nullptr;  // orders a stitch on a new stream after the previous one
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
     ~octvr_mapper() {
+        if (order_ev) (void)hipEventDestroy(order_ev);
         for (auto& e : events) {
             (void)hipEventDestroy(e.first);
             (void)hipEventDestroy(e.second);
@@ -849,8 +851,14 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         memset(&fs, 0, sizeof fs);
         for (int i = 0; i < m->n; i++) {
             REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
+            // the staging loads form row offsets with 24-bit multiplies (kernels.hip stage_load)
+            REQUIRE(in_pitch[i] < ((size_t)1 << 24), "input pitch must be below 16 MiB");
             fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
         }
+        // consecutive stitches share the mapper's device state (gains, feed totals, work counters):
+        // a stitch on another stream waits for the previous one (vr::Mapper is not re-entrant either)
+        // (order_ev is recorded after every stitch, so the previous stream may since have been destroyed)
+        if (m->order_ev && m->last_stream != s) HIP_CHECK(hipStreamWaitEvent(s, m->order_ev, 0));
         if (m->use_gain) {
             if (gains_dev) {
                 HIP_CHECK(hipMemcpyAsync(m->gains.p, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
@@ -889,6 +897,8 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
         }
+        if (!m->order_ev) HIP_CHECK(hipEventCreateWithFlags(&m->order_ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(m->order_ev, s));
         m->last_stream = s;
     }
 }
@@ -1308,6 +1318,7 @@ int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
                  m->mb ? 0.0 : m->tiles.staged_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks, m->SW, m->SH);
         std::string js = tmp;
         if (m->mb) js += ", " + multiband_info(*m->mb);
+        else if (!m->tiles.stats.empty()) js += ", " + m->tiles.stats;
         js += "}";
         REQUIRE(js.size() < len, "buffer too small");
         memcpy(buf, js.c_str(), js.size() + 1);

@@ -165,6 +165,34 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             b.bands[g] = std::max(t, b.bands[g - 1]);
         }
     }
+    {  // build statistics (mapper info): how the staging work is distributed over items and bands
+        const int edges[] = {0, 1, 2, 3, 4, 6, 8, 12, 16, 32, 256};
+        const int n_bins = (int)(sizeof(edges) / sizeof(edges[0])) - 1;
+        std::vector<long> hist(n_bins, 0), lds_hist(7, 0);
+        std::vector<long> band_chunks(kStitchBands, 0);
+        for (int t = 0; t < n_items; t++) {
+            const int ch = (int)((b.hdr[t].nslots >> 8) & 0xFFu);
+            int k = 0;
+            while (k + 1 < n_bins && ch >= edges[k + 1]) k++;
+            hist[k]++;
+            uint32_t lds = kTileZeroDwords;
+            for (int j = 0; j < (int)(b.hdr[t].nslots & 0xFFu); j++)
+                lds += b.hdr[t].stride * b.slots[(size_t)t * kTileSlots + j].bh;
+            const uint32_t kb = lds * 4u / 1024u;  // 0-1, 1-2, 2-4, 4-8, 8-16, 16-24, >24 KiB
+            lds_hist[kb < 1 ? 0 : kb < 2 ? 1 : kb < 4 ? 2 : kb < 8 ? 3 : kb < 16 ? 4 : kb < 24 ? 5 : 6]++;
+            for (int g = 0; g < kStitchBands; g++)
+                if (t >= b.bands[g] && t < b.bands[g + 1]) band_chunks[g] += ch;
+        }
+        std::string s = "\"items_by_chunks\": {";
+        for (int k = 0; k < n_bins; k++)
+            s += (k ? ", \"" : "\"") + std::to_string(edges[k]) + "\": " + std::to_string(hist[k]);
+        s += "}, \"items_by_lds_kib\": [";
+        for (int k = 0; k < 7; k++) s += (k ? ", " : "") + std::to_string(lds_hist[k]);
+        s += "], \"band_chunks\": [";
+        for (int g = 0; g < kStitchBands; g++) s += (g ? ", " : "") + std::to_string(band_chunks[g]);
+        s += "]";
+        b.stats = s;
+    }
     b.hdr.resize(std::max(n_items, 1));
     b.slots.resize((size_t)std::max(n_items, 1) * kTileSlots);
     b.entries.resize((size_t)std::max(n_items, 1) * kTilePx);
@@ -184,8 +212,11 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     wide_tiles.upload(b.wide_tiles.data(), b.wide_tiles.size());
     wide_cams.upload(b.wide_cams.data(), b.wide_cams.size());
     bands.upload(b.bands.data(), b.bands.size());
+    queue.alloc((size_t)(kStitchBands + 1) * kQueueStride);
+    HIP_CHECK(hipMemset(queue.p, 0, queue.n * sizeof(uint32_t)));
     staged_bytes = b.staged_bytes;
-    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p};
+    stats = b.stats;
+    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p};
 }
 
 }  // namespace octvr

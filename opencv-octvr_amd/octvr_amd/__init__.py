@@ -234,8 +234,8 @@ class Mapper:
         return b.value
 
     def info(self):
-        buf = C.create_string_buffer(1024)
-        _check(_lib.octvr_mapper_info(self._h, buf, 1024))
+        buf = C.create_string_buffer(8192)
+        _check(_lib.octvr_mapper_info(self._h, buf, 8192))
         return _json.loads(buf.value.decode())
 
     def set_timing(self, enable=True):
