@@ -113,7 +113,7 @@ void mapper_out_size(const octvr_mapper* m, int* w, int* h);
 
 // ---- tiled composite LUT builder (tiling.cpp) ----------------------------------------------------
 struct TileJob {
-    int tx, ty;  // 128x8 tile of the output (or level-0) grid
+    int tx, ty;  // 128 x (8 qpl) item of the output (or level-0) grid
     int cam;     // RGBA mode: the camera whose pyramid image the tile is written to
 };
 // entry(job, x, y): the 8-byte CompositeEntry of grid pixel (x, y) for that job ({0,0} = black)
@@ -127,11 +127,12 @@ struct TiledLutBuild {
     std::vector<uint8_t> wide_cams;
     std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
+    int qpl = 1;  // 128x8 halves per item (kernels.hpp TiledLut::qpl)
     double staged_bytes = 0;
     std::string stats;  // JSON fragment: staged items by staging chunks / LDS bytes, per-band chunk sums
 };
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
-                              const std::vector<int>& in_h);
+                              const std::vector<int>& in_h, int qpl = 1);
 struct TiledLutDev {
     DevBuf<TileHdr> hdr;
     DevBuf<TileSlot> slots;

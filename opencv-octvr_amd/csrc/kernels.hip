@@ -648,10 +648,17 @@ constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
 #ifndef OCTVR_DYN  // 0: static round-robin dealing of a band's items (no work counters)
 #define OCTVR_DYN 1
 #endif
-#ifndef OCTVR_WIDE_OUT  // 0: always the per-quad 1-2-byte output stores
-#define OCTVR_WIDE_OUT 1
+#ifndef OCTVR_WIDE_OUT  // 1: LDS-staged 16-byte output stores (measured no faster on C2; off)
+#define OCTVR_WIDE_OUT 0
 #endif
-constexpr int kStageRegs = OCTVR_STAGE_REGS;  // staging groups per lane loaded one tile ahead (256 per reg)
+// staging groups per lane loaded one item ahead (256 per reg) for items of 1 / 2 halves
+constexpr int kStageRegs = OCTVR_STAGE_REGS;
+#ifndef OCTVR_STAGE_REGS2
+#define OCTVR_STAGE_REGS2 1
+#endif
+#ifndef OCTVR_QPL  // quads per lane (128 x 8 halves per item) of the blend = 0 composite
+#define OCTVR_QPL 2
+#endif
 
 // Software pipeline over a block's tiles (t, t + step, ...):
 //   iteration of tile t:  stage tile t's YUV (loaded during the previous iteration) into LDS,
@@ -682,26 +689,32 @@ __device__ __forceinline__ TileMeta meta_read(const uint4& v, int t) {
     return m;
 }
 
+// An item's in-flight loads: its entries (one uint4 = one quad per lane and half) and the staging
+// groups of R chunks per wave.
+template <int Q, int R>
 struct TileData {
-    uint4 e4;
-    StageGroup sg[kStageRegs];
+    uint4 e4[Q];
+    StageGroup sg[R];
 };
 
-// Issue an item's entry load and the staging loads of its first kStageRegs chunks per wave
-// (sl[r]: the slots of chunks r * 4 + wave, from stage_slot).
-template <bool DWORD_STAGE, bool VIG>
+// Issue an item's entry loads and the staging loads of its first R chunks per wave (sl[r]: the
+// slots of chunks r * 4 + wave, from stage_slot).
+template <bool DWORD_STAGE, bool VIG, int Q, int R>
 __device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& m, int t_end,
-                                           const StageSlot (&sl)[kStageRegs], TileData& d) {
+                                           const StageSlot (&sl)[R], TileData<Q, R>& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
-#if OCTVR_DIAG_HOTENT  // diagnostic: every item reads item 0's entries (L2-resident)
-    d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? 0 : 0) * kTilePx)[tid];
-#else
-    d.e4 = reinterpret_cast<const uint4*>(lut.entries + (int64_t)(live ? m.t : 0) * kTilePx)[tid];
-#endif
 #pragma unroll
-    for (int r = 0; r < kStageRegs; r++) {
+    for (int h = 0; h < Q; h++) {
+#if OCTVR_DIAG_HOTENT  // diagnostic: every item reads item 0's entries (L2-resident)
+        d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + (int64_t)h * kTilePx)[tid];
+#else
+        d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + ((int64_t)(live ? m.t : 0) * Q + h) * kTilePx)[tid];
+#endif
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
 #if OCTVR_STAGE_SKIP
         if (!sl[r].live) {  // wave-uniform: no loads for a chunk the item lacks
             d.sg[r].dst = -1;
@@ -796,7 +809,7 @@ __device__ __forceinline__ void store_tile_wide(const OutFrame& o, const uint32_
 
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
-template <bool DWORD_STAGE, int MODE, bool VIG>
+template <bool DWORD_STAGE, int MODE, bool VIG, int QPL>
 __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
                                                               int64_t out_pitch, RgbaOut rgba) {
@@ -809,7 +822,10 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
     // four 1-2-byte stores per quad
     constexpr bool kWideOut = MODE == 2;
     constexpr int SM = MODE == 1 ? 1 : 0;  // sink: YUV (finish_quad) or RGBA
-    __shared__ __attribute__((aligned(16))) uint32_t s_out[kWideOut ? kTileOutBytes / 4 : 1];
+    __shared__ __attribute__((aligned(16))) uint32_t s_out[kWideOut ? QPL * kTileOutBytes / 4 : 1];
+    constexpr int R = QPL == 1 ? kStageRegs : OCTVR_STAGE_REGS2;  // staging chunks prefetched per wave
+    static_assert(QPL == 1 || QPL == 2 || QPL == 4, "items of 1, 2 or 4 halves");
+    constexpr int kItemH = kTileH * QPL;
 
     const int groups = kStitchBands;
     const int g = blockIdx.x % groups;
@@ -843,11 +859,11 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
     const int wave = uniform(tid >> 6);
     TileMeta cur = meta_read(meta_issue(lut, t0, t_end), t0);
     __syncthreads();
-    TileData d;
+    TileData<QPL, R> d;
     {
-        StageSlot sl[kStageRegs];
+        StageSlot sl[R];
 #pragma unroll
-        for (int r = 0; r < kStageRegs; r++) sl[r] = stage_slot(cur, t_end, r * 4 + wave);
+        for (int r = 0; r < R; r++) sl[r] = stage_slot(cur, t_end, r * 4 + wave);
         data_issue<DWORD_STAGE, VIG>(lut, cur, t_end, sl, d);
     }
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
@@ -859,16 +875,19 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
     // opaque copies of the prologue loads: the loop-header phis then merge a load with a non-load,
     // so the compiler cannot fold them into one load at the header (waited on right there)
     asm volatile("" : "+v"(mv.x), "+v"(mv.y), "+v"(mv.z), "+v"(mv.w));
-    asm volatile("" : "+v"(d.e4.x), "+v"(d.e4.y), "+v"(d.e4.z), "+v"(d.e4.w));
 #pragma unroll
-    for (int r = 0; r < kStageRegs; r++)
+    for (int h = 0; h < QPL; h++) asm volatile("" : "+v"(d.e4[h].x), "+v"(d.e4[h].y), "+v"(d.e4[h].z), "+v"(d.e4[h].w));
+#pragma unroll
+    for (int r = 0; r < R; r++)
         asm volatile("" : "+v"(d.sg[r].y0), "+v"(d.sg[r].y1), "+v"(d.sg[r].uq), "+v"(d.sg[r].vq));
 
     // the previous tile's output, stored at the top of the next iteration: every store is then
     // older than the loads it shares the iteration with (vmcnt waits on a load that is older than
     // a store must drain everything, as loads and stores complete out of order)
-    QuadOut prev{0u, 0u, 0u, 0u};
-    int px = 0, py = 0;
+    QuadOut prev[QPL];
+#pragma unroll
+    for (int h = 0; h < QPL; h++) prev[h] = QuadOut{0u, 0u, 0u, 0u};
+    int px = 0, py = 0;  // the previous item's quad of this lane in its first half
     uint32_t pcam = 0;
     bool pin = false;
 #if OCTVR_PHASES
@@ -887,9 +906,11 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
     } while (0)
 #endif
     while (cur.t < t_end) {
-        const int x = (int)(cur.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.tile >> 16) * kTileH + qy * 2;
+        const int x = (int)(cur.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.tile >> 16) * kItemH + qy * 2;
         const uint32_t S = cur.stride;
-        const uint4 e4 = d.e4;
+        uint4 e4[QPL];
+#pragma unroll
+        for (int h = 0; h < QPL; h++) e4[h] = d.e4[h];
         OCTVR_PHASE(5);   // back edge: waits for the loads of this item
 #if !OCTVR_DIAG_NOBAR  // diagnostic ablations (wrong output, timing only): scripts/ablate.sh
         __syncthreads();  // the previous tile's LDS readers are done
@@ -897,9 +918,9 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         OCTVR_PHASE(0);
         const TileMeta nxt = meta_read(mv, t_mv);
         // the next item's staging slots (+ their frames' kernarg loads), used after the barrier below
-        StageSlot sln[kStageRegs];
+        StageSlot sln[R];
 #pragma unroll
-        for (int r = 0; r < kStageRegs; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
+        for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
             if (tid < kTileSlots) s_slot_gain[tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
@@ -907,7 +928,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         if (claimed && tid == 0) s_claim = claim;  // issued one iteration ago
 #if !OCTVR_DIAG_NOSTAGE
 #pragma unroll
-        for (int r = 0; r < kStageRegs; r++) stage_store<VIG>(d.sg[r], s_rgb);
+        for (int r = 0; r < R; r++) stage_store<VIG>(d.sg[r], s_rgb);
         const uint32_t nch = (cur.nslots >> 8) & 0xFFu;
 #else
         const uint32_t nch = 0;
@@ -916,8 +937,8 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         st_items++;
         st_chunks += nch;
 #endif
-        if (nch > (uint32_t)(kStageRegs * 4)) {  // large boxes only: the other chunks now
-            for (int c = kStageRegs * 4 + wave; c < (int)nch; c += 4) {
+        if (nch > (uint32_t)(R * 4)) {  // large boxes only: the other chunks now
+            for (int c = R * 4 + wave; c < (int)nch; c += 4) {
                 StageGroup sg;
                 stage_load<DWORD_STAGE, VIG>(stage_slot(cur, t_end, c), S, c, sg);
                 stage_store<VIG>(sg, s_rgb);
@@ -939,10 +960,13 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         }
         first = false;
 #if !OCTVR_DIAG_NOSTORE
-        if constexpr (kWideOut)
-            store_tile_wide(of, s_out, px, py, pin, H);
-        else
-            store_any<SM>(of, ro, prev, pcam, px, py, pin);
+#pragma unroll
+        for (int h = 0; h < QPL; h++) {
+            if constexpr (kWideOut)
+                store_tile_wide(of, s_out + h * (kTileOutBytes / 4), px, py + h * kTileH, pin, H);
+            else
+                store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+        }
 #endif
         data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
         mv = meta_issue(lut, t_n2, t_end);
@@ -956,7 +980,9 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
             claim = __hip_atomic_fetch_add(q + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         OCTVR_PHASE(3);
-        const uint32_t ent[4] = {e4.x, e4.y, e4.z, e4.w};
+#pragma unroll
+        for (int h = 0; h < QPL; h++) {
+        const uint32_t ent[4] = {e4[h].x, e4[h].y, e4[h].z, e4[h].w};
         uint32_t rgb[4][3];
         f32x2_t gain[4];
 #pragma unroll
@@ -979,14 +1005,16 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
             if (SM == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
         }
 #if OCTVR_DIAG_NOCOMPUTE
-        prev = QuadOut{rgb[0][0] ^ rgb[1][1], rgb[2][2] ^ rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
+        prev[h] = QuadOut{rgb[0][0] ^ rgb[1][1], rgb[2][2] ^ rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
 #else
-        prev = finish_any<SM>(rgb, gain);
+        prev[h] = finish_any<SM>(rgb, gain);
 #endif
-        if constexpr (kWideOut) stage_out_quad(s_out, prev, qx, qy);  // read after the next barrier
+        // MODE 2: staged for the wide stores after the next barrier
+        if constexpr (kWideOut) stage_out_quad(s_out + h * (kTileOutBytes / 4), prev[h], qx, qy);
 #if OCTVR_PHASES
-        asm volatile("" : "+v"(prev.y01), "+v"(prev.y23), "+v"(prev.u), "+v"(prev.v));
+        asm volatile("" : "+v"(prev[h].y01), "+v"(prev[h].y23), "+v"(prev[h].u), "+v"(prev[h].v));
 #endif
+        }
         OCTVR_PHASE(4);
         px = x;
         py = y;
@@ -1014,11 +1042,13 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
                 __hip_atomic_exchange(lut.queue + k * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if constexpr (kWideOut) {
-        __syncthreads();
-        store_tile_wide(of, s_out, px, py, pin, H);
-    } else {
-        store_any<SM>(of, ro, prev, pcam, px, py, pin);
+    if constexpr (kWideOut) __syncthreads();
+#pragma unroll
+    for (int h = 0; h < QPL; h++) {
+        if constexpr (kWideOut)
+            store_tile_wide(of, s_out + h * (kTileOutBytes / 4), px, py + h * kTileH, pin, H);
+        else
+            store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
     }
 #if OCTVR_STAMPS == 1
     if (MODE != 1 && tid == 0 && blockIdx.x < kStampRows) {
@@ -1086,15 +1116,37 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
         // YUV output with 16-byte row segments: the LDS-staged wide stores (MODE 2)
         const bool wide_out = MODE == 0 && OCTVR_WIDE_OUT && W % 32 == 0 && out_pitch % 16 == 0 &&
                               (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
+#if OCTVR_WIDE_OUT
 #define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
     do {                                                                                                       \
-        if (wide_out)                                                                                          \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V>), dim3(blocks), dim3(256), 0, s, frames, lut, W, H, \
-                               gains, use_gain, out, out_pitch, rgba);                                         \
-        else                                                                                                   \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), 0, s, frames, lut, W, \
+        if (lut.qpl == 2 && wide_out)                                                                          \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, W, \
                                H, gains, use_gain, out, out_pitch, rgba);                                      \
+        else if (lut.qpl == 2)                                                                                 \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+        else if (wide_out)                                                                                     \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 1>), dim3(blocks), dim3(256), 0, s, frames, lut, W, \
+                               H, gains, use_gain, out, out_pitch, rgba);                                      \
+        else                                                                                                   \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), 0, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
     } while (0)
+#else
+#define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
+    do {                                                                                                       \
+        (void)wide_out;                                                                                        \
+        if (OCTVR_QPL == 4 && lut.qpl == 4)                                                                    \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, OCTVR_QPL == 4 ? 4 : 1>), dim3(blocks), dim3(256), \
+                               0, s, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);                \
+        else if (lut.qpl == 2)                                                                                 \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+        else                                                                                                   \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), 0, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+    } while (0)
+#endif
         if (dw && !vig)
             OCTVR_LAUNCH_TILED(true, false);
         else if (dw)
@@ -1121,6 +1173,8 @@ extern "C" int octvr_debug_stamps(unsigned long long* out, int rows) {
                    hipSuccess ? rows : -1;
 }
 #endif
+
+int composite_qpl() { return OCTVR_QPL; }
 
 hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                          int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {

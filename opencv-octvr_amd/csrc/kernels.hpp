@@ -70,7 +70,7 @@ struct TileSlot {
 };
 
 struct TileHdr {           // one staged item
-    uint32_t tile;          // tile column | tile row << 16
+    uint32_t tile;          // item column | item row << 16 (items of 128 x 8 qpl pixels)
     uint32_t nslots;        // bits 0-7: slots used (0..4); bits 8-15: 64-group staging chunks
     uint32_t stage_groups;  // 4-pixel groups to convert into LDS
     uint32_t stride;        // LDS row stride in dwords (max box width of the tile)
@@ -146,6 +146,7 @@ struct TiledLut {
     const int32_t* bands;         // kStitchBands + 1 staged-item boundaries (one band per XCD)
     uint32_t* queue;              // per band a work counter, then a done ticket, kQueueStride apart;
                                   // zero before a launch, left zero by its last workgroup
+    int qpl;                      // quads per lane: an item is 128 x (8 qpl) pixels, qpl * kTilePx entries
 };
 constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter
 // The staged items are cut into one contiguous band per XCD (locality: neighbouring tiles share
@@ -162,6 +163,9 @@ constexpr int kStitchBands = 8;
 // records carry the same flag in code bit 16.  TileHdr.nslots bits 16-20: output camera (RGBA mode).
 constexpr uint32_t kEntryNoGain = 1u << 29;
 constexpr uint32_t kCodeNoGain = 1u << 16;
+
+// Quads per lane of the blend = 0 composite's items (OCTVR_QPL, default 2: 128 x 16 items).
+int composite_qpl();
 
 hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W, int H,
                          const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s);

@@ -1210,7 +1210,9 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
                 m2[i].reset();
                 mk[i].reset();
             }
-            const int tx_n = (m->W + kTileW - 1) / kTileW, ty_n = (m->H + kTileH - 1) / kTileH;
+            // items of 128 x 16 (two quads per lane, OCTVR_QPL) for the per-frame composite
+            const int qpl = composite_qpl();
+            const int tx_n = (m->W + kTileW - 1) / kTileW, ty_n = (m->H + kTileH * qpl - 1) / (kTileH * qpl);
             std::vector<TileJob> jobs;
             jobs.reserve((size_t)tx_n * ty_n);
             for (int ty = 0; ty < ty_n; ty++)
@@ -1218,7 +1220,7 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             const int W = m->W, H = m->H;
             m->tiles.upload(build_tiled_lut(jobs, [&](int, int x, int y) {
                 return (x < W && y < H) ? lut8[(size_t)y * W + x] : CompositeEntry{0u, 0u};
-            }, m->in_w, m->in_h));
+            }, m->in_w, m->in_h, qpl));
             m->n_tiles = tx_n * ty_n;
         }
         if (m->scaled) {
@@ -1273,7 +1275,7 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
             return;
         }
         const TiledLut& t = m->tiles.view;
-        double b = 4.0 * t.n_items * kTilePx + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
+        double b = 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
                    (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide;
         for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
         *bytes = b;

@@ -1,6 +1,7 @@
 // tiling.cpp — the tiled composite LUT (kernels.hpp "tiled composite"), built once per rig.
 //
-// A job is one 128x8 output tile written by one launch item: for blend = 0 every tile of the output
+// A job is one 128 x (8 qpl) output tile written by one launch item (qpl = 2 for the blend = 0
+// composite: each lane of the workgroup takes two quads, halving the per-item costs per pixel): for blend = 0 every tile of the output
 // frame (each pixel's entry = the winning camera of the copy chain), for blend > 0 every level-0
 // tile a camera's Gaussian pyramid needs (each pixel's entry = that camera's map).  Per job the
 // builder finds the cameras (<= 4 "slots") and their even-aligned luma boxes, and encodes each
@@ -16,12 +17,14 @@
 namespace octvr {
 
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
-                              const std::vector<int>& in_h) {
+                              const std::vector<int>& in_h, int qpl) {
     const int n_jobs = (int)jobs.size();
+    const int item_px = kTilePx * qpl;  // qpl 128x8 halves stacked vertically
     TiledLutBuild b;
+    b.qpl = qpl;
     b.hdr.resize(n_jobs);
     b.slots.resize((size_t)n_jobs * kTileSlots);
-    b.entries.assign((size_t)n_jobs * kTilePx, 0u);
+    b.entries.assign((size_t)n_jobs * item_px, 0u);
     std::vector<uint8_t> is_wide(n_jobs, 0);
     std::vector<std::vector<CompositeEntry>> wide_raw(n_jobs);
     const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -29,16 +32,18 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
         struct Px {
             int slot, x0, y0, fxy, mask, nogain;
         };
-        std::vector<Px> px(kTilePx);
-        std::vector<CompositeEntry> raw(kTilePx);
+        std::vector<Px> px(item_px);
+        std::vector<CompositeEntry> raw(item_px);
         for (int t = tid; t < n_jobs; t += T) {
             const TileJob& J = jobs[t];
             int cams[8], ns = 0;
             int minx[8], maxx[8], miny[8], maxy[8];
             bool wide = false;
-            for (int k = 0; k < kTilePx; k++) {
-                const int q = k >> 2, p = k & 3;
-                const int x = J.tx * kTileW + (q & 63) * 2 + (p & 1), y = J.ty * kTileH + (q >> 6) * 2 + (p >> 1);
+            for (int k = 0; k < item_px; k++) {
+                // half h = k / kTilePx holds rows 8 h .. 8 h + 7; inside it quad-major (lane = quad)
+                const int h = k / kTilePx, q = (k % kTilePx) >> 2, p = k & 3;
+                const int x = J.tx * kTileW + (q & 63) * 2 + (p & 1);
+                const int y = J.ty * kTileH * qpl + h * kTileH + (q >> 6) * 2 + (p >> 1);
                 const CompositeEntry e = entry(t, x, y);
                 raw[k] = e;
                 px[k].mask = 0;
@@ -115,8 +120,8 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             b.hdr[t] = TileHdr{(uint32_t)J.tx | ((uint32_t)J.ty << 16),
                                (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16), groups, stride};
             for (int j = 0; j < kTileSlots; j++) b.slots[(size_t)t * kTileSlots + j] = ts[j];
-            uint32_t* out = b.entries.data() + (size_t)t * kTilePx;
-            for (int k = 0; k < kTilePx; k++) {
+            uint32_t* out = b.entries.data() + (size_t)t * item_px;
+            for (int k = 0; k < item_px; k++) {
                 if (!px[k].mask) continue;  // black
                 const TileSlot& sl = ts[px[k].slot];
                 const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
@@ -131,19 +136,22 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     // staged items: the non-wide jobs in job order, compacted in place; wide jobs in job order
     int n_items = 0;
     for (int t = 0; t < n_jobs; t++) {
-        if (is_wide[t]) {
+        if (is_wide[t]) {  // one 128x8 wide tile per half
             const TileJob& J = jobs[t];
-            b.wide_tiles.push_back((uint32_t)J.tx | ((uint32_t)J.ty << 16));
-            b.wide_cams.push_back((uint8_t)J.cam);
-            b.wide.insert(b.wide.end(), wide_raw[t].begin(), wide_raw[t].end());
+            for (int h = 0; h < qpl; h++) {
+                b.wide_tiles.push_back((uint32_t)J.tx | ((uint32_t)(J.ty * qpl + h) << 16));
+                b.wide_cams.push_back((uint8_t)J.cam);
+                b.wide.insert(b.wide.end(), wide_raw[t].begin() + (size_t)h * kTilePx,
+                              wide_raw[t].begin() + (size_t)(h + 1) * kTilePx);
+            }
             continue;
         }
         if (n_items != t) {
             b.hdr[n_items] = b.hdr[t];
             std::copy(b.slots.begin() + (size_t)t * kTileSlots, b.slots.begin() + (size_t)(t + 1) * kTileSlots,
                       b.slots.begin() + (size_t)n_items * kTileSlots);
-            std::copy(b.entries.begin() + (size_t)t * kTilePx, b.entries.begin() + (size_t)(t + 1) * kTilePx,
-                      b.entries.begin() + (size_t)n_items * kTilePx);
+            std::copy(b.entries.begin() + (size_t)t * item_px, b.entries.begin() + (size_t)(t + 1) * item_px,
+                      b.entries.begin() + (size_t)n_items * item_px);
         }
         b.staged_bytes += 8.0 * b.hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes per 4-pixel group
         n_items++;
@@ -195,7 +203,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     }
     b.hdr.resize(std::max(n_items, 1));
     b.slots.resize((size_t)std::max(n_items, 1) * kTileSlots);
-    b.entries.resize((size_t)std::max(n_items, 1) * kTilePx);
+    b.entries.resize((size_t)std::max(n_items, 1) * item_px);
     if (b.wide.empty()) {
         b.wide.push_back(CompositeEntry{0, 0});
         b.wide_tiles.push_back(0u);
@@ -216,7 +224,8 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     HIP_CHECK(hipMemset(queue.p, 0, queue.n * sizeof(uint32_t)));
     staged_bytes = b.staged_bytes;
     stats = b.stats;
-    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p};
+    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
+                    b.qpl};
 }
 
 }  // namespace octvr
