@@ -200,14 +200,19 @@ struct OutFrame {
     uint32_t u_off, v_off;  // byte offsets of the U and V planes
 };
 constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host: frame < 2^31 - 64 B)
+// Cache-policy bits of the output-frame stores (gfx950: 1 sc0, 2 nt, 16 sc1).  sc1 writes the frame
+// through (nothing of it left dirty in the XCD L2s when the kernel ends): C2 stitch -1.5 %.
+#ifndef OCTVR_OUT_POLICY
+#define OCTVR_OUT_POLICY 16
+#endif
 
 __device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
     const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
     const uint32_t oc = in ? (uint32_t)(y >> 1) * o.pitch + (uint32_t)(x >> 1) : kDropOffset;
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, OCTVR_OUT_POLICY);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, OCTVR_OUT_POLICY);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, OCTVR_OUT_POLICY);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, OCTVR_OUT_POLICY);
 }
 
 

@@ -29,6 +29,7 @@ namespace octvr {
 // wall-clock stamps (s_memrealtime, 100 MHz) of the stitch and gain-feed kernels, read back with
 // octvr_debug_stamps().  Rows of 4 u64: start, end, items processed, staging chunks processed.
 constexpr int kStampRows = 8192;
+constexpr size_t kFeedStampBase = 4 * (size_t)kStampRows;  // gain-feed rows of 8 u64 after the stitch rows
 __device__ unsigned long long g_octvr_stamps[2 * kStampRows * 4];
 #endif
 
@@ -149,18 +150,20 @@ __device__ bool lu_solve(double (&A)[N * N], double (&b)[N]) {
             }
         }
         if (best < eps) return false;
+        if (k != i) {  // rare (A is diagonally dominant here): the select-based swap only when needed
 #pragma unroll
-        for (int j = i + 1; j < N; j++) {  // row swap i <-> k as selects (static indices only)
-            const bool sw = (j == k);
+            for (int j = i + 1; j < N; j++) {  // row swap i <-> k as selects (static indices only)
+                const bool sw = (j == k);
 #pragma unroll
-            for (int c = i; c < N; c++) {
-                const double ai = A[i * N + c], aj = A[j * N + c];
-                A[i * N + c] = sw ? aj : ai;
-                A[j * N + c] = sw ? ai : aj;
+                for (int c = i; c < N; c++) {
+                    const double ai = A[i * N + c], aj = A[j * N + c];
+                    A[i * N + c] = sw ? aj : ai;
+                    A[j * N + c] = sw ? ai : aj;
+                }
+                const double bi = b[i], bj = b[j];
+                b[i] = sw ? bj : bi;
+                b[j] = sw ? bi : bj;
             }
-            const double bi = b[i], bj = b[j];
-            b[i] = sw ? bj : bi;
-            b[j] = sw ? bi : bj;
         }
         const double d = -1 / A[i * N + i];
 #pragma unroll
@@ -305,15 +308,108 @@ __device__ bool solve_dispatch(double* A, double* b, int n, double* x) {
 // totals with returning atomics (executed at the memory side, so no L2 staleness across XCDs),
 // resets them, assembles A, b and solves.
 // ---------------------------------------------------------------------------------------------
+// Wave sum of an f64 through DPP moves (quad perms, row rotations, row broadcasts 15 / 31; the
+// total lands in lane 63) instead of LDS-routed shuffles.  The gain-feed sums are exact (see below),
+// so the summation order does not change the result.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    return __hiloint2double(__builtin_amdgcn_update_dpp(0, hi, CTRL, 0xf, 0xf, false),
+                            __builtin_amdgcn_update_dpp(0, lo, CTRL, 0xf, 0xf, false));
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+    v += dpp_f64<0xb1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4e>(v);   // quad_perm [2,3,0,1]
+    v += dpp_f64<0x124>(v);  // row_ror 4
+    v += dpp_f64<0x128>(v);  // row_ror 8
+    v += dpp_f64<0x142>(v);  // row_bcast 15
+    v += dpp_f64<0x143>(v);  // row_bcast 31
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), 63),
+                            __builtin_amdgcn_readlane(__double2loint(v), 63));
+}
+
+// Row i of GainCompensatorGPU::feed's system (exposure_compensate.cpp:279-296) from I(i,j) and
+// N(i,j) (both n x n), in the reference's j order: A(i,i) = sum_j beta N + (j != i) 2 alpha I^2 N,
+// A(i,j) = -2 alpha I(i,j) I(j,i) N, b(i) = sum_j beta N.  A has row stride n.
+__device__ __forceinline__ void gain_system_row(const double* I, const int32_t* Nm, int n, int i, double* A, double* b) {
+    const double alpha = 0.01, beta = 100;
+    double bi = 0.0, aii = 0.0;
+    for (int j = 0; j < n; j++) {
+        const int Nij = Nm[i * n + j];
+        bi += beta * Nij;
+        aii += beta * Nij;
+        if (j == i) continue;
+        aii += 2 * alpha * I[i * n + j] * I[i * n + j] * Nij;
+        A[i * n + j] = 0.0 - 2 * alpha * I[i * n + j] * I[j * n + i] * Nij;
+    }
+    A[i * n + i] = aii;
+    b[i] = bi;
+}
+
+// Gain-feed gathers: per sample the 2 luma and 2 chroma rows of its 2x2 taps as 8-byte buffer loads
+// from 4-byte aligned starts (6 loads instead of 12 byte loads); a frame-sized buffer resource
+// returns 0 past the frame end.  The taps are extracted and converted in feed_taps_finish, after
+// every sample's loads are in flight.
+struct FeedRaw {
+    uint2 y0, y1, u0, u1, v0, v1;
+    uint32_t xy, code;
+};
+
+__device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
+                                                uint32_t code, FeedRaw& r) {
+    const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
+    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);
+    const int y1 = sy + 1 < f.h ? sy + 1 : y0;
+    const uint32_t p = (uint32_t)f.pitch;
+    const uint32_t uo = (uint32_t)f.h * p, vo = uo + (uint32_t)(f.w >> 1);
+    const uint32_t xa = (uint32_t)x0 & ~3u, ca = ((uint32_t)x0 >> 1) & ~3u;
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 t;
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)y0 * p + xa, 0, 0);
+    r.y0 = make_uint2(t.x, t.y);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)y1 * p + xa, 0, 0);
+    r.y1 = make_uint2(t.x, t.y);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + (uint32_t)(y0 >> 1) * p + ca, 0, 0);
+    r.u0 = make_uint2(t.x, t.y);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + (uint32_t)(y1 >> 1) * p + ca, 0, 0);
+    r.u1 = make_uint2(t.x, t.y);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + (uint32_t)(y0 >> 1) * p + ca, 0, 0);
+    r.v0 = make_uint2(t.x, t.y);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + (uint32_t)(y1 >> 1) * p + ca, 0, 0);
+    r.v1 = make_uint2(t.x, t.y);
+    r.xy = xy;
+    r.code = code;
+}
+
+// byte k (0-7) of an 8-byte row segment
+__device__ __forceinline__ uint32_t seg_byte(const uint2& v, uint32_t k) {
+    return (uint32_t)(((((uint64_t)v.y) << 32) | v.x) >> (8u * k)) & 255u;
+}
+
+// Same taps, validity and conversions as gather_taps_frame (device_common.hpp), without vignette.
+__device__ __forceinline__ void feed_taps_finish(const SourceFrame& f, const FeedRaw& r, Taps& t) {
+    const bool valid = (r.code & 0x8000u) != 0;
+    const int sx = (int)(r.xy & 0xFFFFu), sy = (int)(r.xy >> 16);
+    const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
+    const bool in0 = valid && sx < f.w && sy < f.h;
+    const int x0 = min(sx, f.w - 1);
+    const int x1 = inx ? sx + 1 : x0;
+    const uint32_t ky0 = (uint32_t)x0 & 3u, ky1 = ky0 + (uint32_t)(x1 - x0);
+    const uint32_t kc0 = ((uint32_t)x0 >> 1) & 3u, kc1 = kc0 + (uint32_t)((x1 >> 1) - (x0 >> 1));
+    const uint32_t ca = yuv_to_rgba(seg_byte(r.y0, ky0), seg_byte(r.u0, kc0), seg_byte(r.v0, kc0));
+    const uint32_t cb = yuv_to_rgba(seg_byte(r.y0, ky1), seg_byte(r.u0, kc1), seg_byte(r.v0, kc1));
+    const uint32_t cc = yuv_to_rgba(seg_byte(r.y1, ky0), seg_byte(r.u1, kc0), seg_byte(r.v1, kc0));
+    const uint32_t cd = yuv_to_rgba(seg_byte(r.y1, ky1), seg_byte(r.u1, kc1), seg_byte(r.v1, kc1));
+    t.c[0] = in0 ? ca : 0u;
+    t.c[1] = (valid && inx && sy < f.h) ? cb : 0u;
+    t.c[2] = (valid && iny && sx < f.w) ? cc : 0u;
+    t.c[3] = (valid && inx && iny) ? cd : 0u;
+    t.fx = r.code & 31u;
+    t.fy = (r.code >> 5) & 31u;
 }
 
 __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
-                                                        const uint16_t* partners, const GainChunk* chunks,
-                                                        int n_chunks, const int32_t* N, int n,
+                                                        const uint16_t* partners, int n_chunks, const int32_t* N, int n,
                                                         unsigned long long* totals, uint32_t* tickets,
                                                         double* gains) {
     __shared__ int s_last;
@@ -325,23 +421,36 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
 #if OCTVR_STAMPS == 1
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    const GainChunk ch = chunks[blockIdx.x];
     double acc[kGainMaxCams];
 #pragma unroll
     for (int j = 0; j < kGainMaxCams; j++) acc[j] = 0.0;
-    // kGainChunk / 256 samples per thread, all gathers issued before any arithmetic
-    constexpr int kPer = kGainChunk / 256;
+    // kGainPer samples per lane, all gathers issued before any arithmetic.  Wave w of workgroup b
+    // takes the kGainWaveRun contiguous samples from (4 b + w) kGainWaveRun: one camera's (runs padded
+    // on the host with invalid samples, partner mask 0), named in every entry's code.
+    constexpr int kPer = kGainPer;
     uint32_t pm[kPer];
     Taps t[kPer];
-    const int cam = uniform(ch.cam);  // a chunk holds one camera's samples: its frame is wave-uniform
-    const SourceFrame fr = frames.f[cam];
+    CompositeEntry es[kPer];
+    const int wave = tid >> 6;
 #pragma unroll
     for (int u = 0; u < kPer; u++) {
-        const int k = ch.begin + u * 256 + tid;
-        const bool in = k < ch.end;
-        const CompositeEntry e = in ? samples[k] : CompositeEntry{0u, 0u};
-        pm[u] = in ? partners[k] : 0u;
-        gather_taps_frame(fr, e.xy, e.code, t[u]);
+        const int k = (blockIdx.x * 4 + wave) * kGainWaveRun + u * 64 + lane;
+        es[u] = samples[k];
+        pm[u] = partners[k];
+    }
+    const int cam = uniform((int)((es[0].code >> 10) & 31u));  // one camera per wave: uniform frame
+    const SourceFrame fr = frames.f[cam];
+    if (fr.vig) {  // vignette: per-tap byte gathers with the vignette multiply
+#pragma unroll
+        for (int u = 0; u < kPer; u++) gather_taps_frame(fr, es[u].xy, es[u].code, t[u]);
+    } else {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(fr.yuv), 0, (int)((uint32_t)fr.pitch * (uint32_t)(fr.h + fr.h / 2)), 0x00020000);
+        FeedRaw raw[kPer];
+#pragma unroll
+        for (int u = 0; u < kPer; u++) feed_taps_issue(rs, fr, es[u].xy, es[u].code, raw[u]);
+#pragma unroll
+        for (int u = 0; u < kPer; u++) feed_taps_finish(fr, raw[u], t[u]);
     }
 #pragma unroll
     for (int u = 0; u < kPer; u++) {
@@ -352,26 +461,48 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
         for (int j = 0; j < kGainMaxCams; j++)
             if (pm[u] & (1u << j)) acc[j] += nv;
     }
-    // exact sums: per wave, then per workgroup, then one u64 atomic per partner
-    __shared__ double s_wsum[4][kGainMaxCams];
-    for (int j = 0; j < n; j++) {
-        double v = 0.0;
-#pragma unroll
-        for (int q = 0; q < kGainMaxCams; q++)
-            if (q == j) v = acc[q];
-        v = wave_sum(v);
-        if (lane == 0) s_wsum[tid >> 6][j] = v;
+#if OCTVR_STAMPS == 1
+    unsigned long long st1 = 0, st2 = 0, st3 = 0;
+    if (tid == 0) {  // after the gathers and the f32 norms (the loop above consumed every load)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        st1 = __builtin_amdgcn_s_memrealtime();
     }
+#endif
+    // exact sums: per wave (DPP), then per (camera, partner) over the workgroup's waves, then one u64
+    // atomic per pair
+    __shared__ double s_wsum[4][kGainMaxCams];
+    __shared__ int s_wcam[4];
+#pragma unroll
+    for (int j = 0; j < kGainMaxCams; j++) {  // unrolled: the n reductions' DPP chains interleave
+        if (j < n) {
+            const double v = wave_sum(acc[j]);
+            if (lane == 0) s_wsum[wave][j] = v;
+        }
+    }
+    if (lane == 0) s_wcam[wave] = cam;
     __syncthreads();
-    if (tid < n) {
-        const double v = (s_wsum[0][tid] + s_wsum[1][tid]) + (s_wsum[2][tid] + s_wsum[3][tid]);
-        if (v != 0.0)
-            __hip_atomic_fetch_add(&totals[(cam * kGainMaxCams + tid) * kGainTotalStride],
-                                   (unsigned long long)(v * 8388608.0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if OCTVR_STAMPS == 1
+    if (tid == 0) st2 = __builtin_amdgcn_s_memrealtime();
+#endif
+    if (tid < 4 * n) {  // (wave w, partner j); the first wave of each camera adds for all its waves
+        const int w = tid / n, j = tid - w * n, c = s_wcam[w];
+        bool first = true;
+        for (int x = 0; x < w; x++) first &= s_wcam[x] != c;
+        if (first) {
+            double v = 0.0;
+            for (int x = w; x < 4; x++)
+                if (s_wcam[x] == c) v += s_wsum[x][j];
+            if (v != 0.0)
+                __hip_atomic_fetch_add(&totals[(c * kGainMaxCams + j) * kGainTotalStride],
+                                       (unsigned long long)(v * 8388608.0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     // every wave's adds have completed before the workgroup takes its ticket
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#if OCTVR_STAMPS == 1
+    if (tid == 0) st3 = __builtin_amdgcn_s_memrealtime();
+#endif
     if (tid == 0) {
         const int xcd = blockIdx.x & 7;
         const uint32_t in_xcd = (uint32_t)((n_chunks - xcd + 7) >> 3);
@@ -382,12 +513,17 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
         }
         s_last = last;
 #if OCTVR_STAMPS == 1
-        if (blockIdx.x < kStampRows) {
-            unsigned long long* r = g_octvr_stamps + (size_t)(kStampRows + blockIdx.x) * 4;
+        if (blockIdx.x < 2048) {  // rows of 8: start, gathered, reduced, adds done, ticket, last, ...
+            unsigned long long* r = g_octvr_stamps + kFeedStampBase + (size_t)blockIdx.x * 8;
             r[0] = st0;
-            r[1] = __builtin_amdgcn_s_memrealtime();
-            r[2] = (unsigned long long)last;
-            r[3] = (unsigned long long)(ch.end - ch.begin);
+            r[1] = st1;
+            r[2] = st2;
+            r[3] = st3;
+            r[4] = __builtin_amdgcn_s_memrealtime();
+            r[5] = (unsigned long long)last;
+            r[6] = 0;
+            r[7] = 0;
+            (void)cam;
         }
 #endif
     }
@@ -405,26 +541,18 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
     }
     if (tid < 9) __hip_atomic_exchange(&tickets[tid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+#if OCTVR_STAMPS == 1
+    if (tid == 0) g_octvr_stamps[kFeedStampBase + (size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
+#endif
 #if OCTVR_FEED_VARIANT == 1
     if (tid < n) gains[tid] = s_I[tid];
     return;
 #endif
-    const double alpha = 0.01, beta = 100;
-    if (tid < n) {  // row i of A and b, in the reference's j order (exposure_compensate.cpp:282-294)
-        const int i = tid;
-        double bi = 0.0, aii = 0.0;
-        for (int j = 0; j < n; j++) {
-            const int Nij = s_N[i * n + j];
-            bi += beta * Nij;
-            aii += beta * Nij;
-            if (j == i) continue;
-            aii += 2 * alpha * s_I[i * n + j] * s_I[i * n + j] * Nij;
-            s_A[i * n + j] = 0.0 - 2 * alpha * s_I[i * n + j] * s_I[j * n + i] * Nij;
-        }
-        s_A[i * n + i] = aii;
-        s_b[i] = bi;
-    }
+    if (tid < n) gain_system_row(s_I, s_N, n, tid, s_A, s_b);
     __syncthreads();
+#if OCTVR_STAMPS == 1
+    if (tid == 0) g_octvr_stamps[kFeedStampBase + 2048 * 8] = __builtin_amdgcn_s_memrealtime();
+#endif
     // cv::solve (lapack.cpp:1050-1275): one lane with the matrix in registers for n <= 8 (closed forms
     // n <= 3); the LU across the workgroup for 9..16
     bool ok;
@@ -435,18 +563,20 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
     } else {
         ok = lu_solve_block(s_A, s_b, n, s_x);
     }
+#if OCTVR_STAMPS == 1
+    if (tid == 0) g_octvr_stamps[kFeedStampBase + 2048 * 8 + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
     if (tid < n) gains[tid] = ok ? s_x[tid] : 1.0;  // cv::solve failure leaves gains_ unspecified; 1 as the oracle
 #if OCTVR_STAMPS == 1
-    if (tid == 0 && blockIdx.x < kStampRows)
-        g_octvr_stamps[(size_t)(kStampRows + blockIdx.x) * 4 + 2] = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) g_octvr_stamps[kFeedStampBase + (size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
-                            const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
+                            int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s) {
     if (n_chunks <= 0 || n > kGainMaxCams) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, chunks, n_chunks,
+    hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, n_chunks,
                        N, n, totals, tickets, gains);
     return hipGetLastError();
 }
@@ -804,7 +934,7 @@ __device__ __forceinline__ void store_tile_wide(const OutFrame& o, const uint32_
     const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + (lane < 24 ? lds : 0));
     const uint32_t off = ok ? plane + (uint32_t)row * o.pitch + (uint32_t)col : kDropOffset;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, o.rsrc, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, o.rsrc, off, 0, OCTVR_OUT_POLICY);
 }
 
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin

@@ -101,20 +101,18 @@ struct CamTemplate {
 // Gain-feed work description (built on the host once per rig, GainCompensatorGPU ctor
 // exposure_compensate.cpp:174-221 + Mapper ctor mapper.cpp:94-114).  Every working-scale pixel of
 // camera i that lies in the bitwise-AND intersection with some camera j becomes one sample: its
-// 8-byte entry plus a partner mask (bit j).  Samples are sorted by (camera, source row, column) and
-// cut into single-camera chunks of up to kGainChunk samples, one workgroup each.
+// 8-byte entry plus a partner mask (bit j).  Samples are sorted by (camera, source row, column); each
+// camera's run is padded with invalid samples (partner mask 0) to whole runs of kGainWaveRun (one
+// wave each, so a wave's frame is uniform), the whole array to chunks of kGainChunk (one workgroup,
+// 386 workgroups on C2).
 constexpr int kGainMaxCams = 16;
-#ifndef OCTVR_GAIN_CHUNK
-#define OCTVR_GAIN_CHUNK 1024
+#ifndef OCTVR_GAIN_PER  // samples per lane of the gain feed
+#define OCTVR_GAIN_PER 6
 #endif
-constexpr int kGainChunk = OCTVR_GAIN_CHUNK;
+constexpr int kGainPer = OCTVR_GAIN_PER;
+constexpr int kGainWaveRun = 64 * kGainPer;  // one wave's samples: contiguous, one camera
+constexpr int kGainChunk = 4 * kGainWaveRun;  // one workgroup's samples (4 waves)
 constexpr int kGainTotalStride = 32;  // u64 words between pair totals: one 256-B line each
-struct GainChunk {
-    int32_t cam;
-    int32_t begin;  // [begin, end) into the sample arrays
-    int32_t end;
-    int32_t pad_;
-};
 
 // cams_dev: {output camera, input camera} in device memory (CameraParams holds the ocam polynomials).
 hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
@@ -129,7 +127,7 @@ hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H
 // resets the totals, assembles I(i,j), A, b and solves.  `totals` (kGainMaxCams^2) and `tickets`
 // (9) must be zero before the first launch; the last workgroup leaves them zero.
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
-                            const GainChunk* chunks, int n_chunks, const int32_t* N, int n,
+                            int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s);
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);

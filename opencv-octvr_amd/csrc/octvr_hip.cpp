@@ -653,7 +653,6 @@ struct octvr_mapper {
     // gain feed
     DevBuf<CompositeEntry> samples;  // working-scale samples that lie in some pair intersection
     DevBuf<uint16_t> partners;       // per sample: bit j = the sample is in the (camera, j) intersection
-    DevBuf<GainChunk> chunks;        // single-camera runs of <= kGainChunk samples, one workgroup each
     DevBuf<unsigned long long> totals;  // [kGainMaxCams][kGainMaxCams] exact pair sums, units of 2^-23
     DevBuf<int32_t> N;
     DevBuf<uint32_t> tickets;        // 8 per-XCD + 1 global last-workgroup-done counters
@@ -792,7 +791,7 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
     // a wave gather from a few neighbouring source lines; invalid (mask 0) samples read as 0 and go last
     std::vector<CompositeEntry> uniq;
     std::vector<uint16_t> pmask;
-    std::vector<GainChunk> chunks;
+    int n_chunks = 0;  // workgroups of kGainChunk samples (4 single-camera wave runs each)
     for (int i = 0; i < n; i++) {
         std::vector<uint32_t> ks;
         for (size_t k = 0; k < samp[i].size(); k++)
@@ -810,12 +809,18 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
             uniq.push_back(e);
             pmask.push_back(partner[i][k]);
         }
-        for (int s0 = begin; s0 < (int)uniq.size(); s0 += kGainChunk)
-            chunks.push_back(GainChunk{i, s0, std::min((int)uniq.size(), s0 + kGainChunk), 0});
+        while ((uniq.size() - begin) % kGainWaveRun) {  // pad: invalid samples of camera i, no partners
+            uniq.push_back(CompositeEntry{0u, (uint32_t)(i << 10)});
+            pmask.push_back(0);
+        }
     }
+    while (uniq.size() % kGainChunk) {  // whole workgroups
+        uniq.push_back(CompositeEntry{0u, 0u});
+        pmask.push_back(0);
+    }
+    n_chunks = (int)(uniq.size() / kGainChunk);
     m.samples.upload(uniq.data(), uniq.size());
     m.partners.upload(pmask.data(), pmask.size());
-    m.chunks.upload(chunks.data(), chunks.size());
     // exactness bound of the fixed-point totals (kernels.hip, gain feed): < 2^21 samples per camera
     for (int i = 0; i < n; i++) REQUIRE(samp[i].size() < (1u << 21), "working-scale ROI too large for exact gain sums");
     m.totals.alloc((size_t)kGainMaxCams * kGainMaxCams * kGainTotalStride);
@@ -823,7 +828,7 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
     m.N.upload(N.data(), N.size());
     m.tickets.alloc(9);
     HIP_CHECK(hipMemset(m.tickets.p, 0, sizeof(uint32_t) * 9));
-    m.n_chunks = (int)chunks.size();
+    m.n_chunks = n_chunks;
     m.n_samples = (int)uniq.size();
     size_t pairs_px = 0;
     for (uint16_t pm : pmask) pairs_px += (size_t)__builtin_popcount(pm);
@@ -853,6 +858,9 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
             // the staging loads form row offsets with 24-bit multiplies (kernels.hip stage_load)
             REQUIRE(in_pitch[i] < ((size_t)1 << 24), "input pitch must be below 16 MiB");
+            // the gain feed reads frames through 32-bit buffer resources
+            REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) < 0x7FFFFFFFull,
+                    "input frame larger than 2 GiB");
             fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
         }
         // consecutive stitches share the mapper's device state (gains, feed totals, work counters):
@@ -869,7 +877,7 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                 const std::vector<double> ones(m->n, 1.0);
                 HIP_CHECK(launch_set_gains(ones.data(), m->n, m->gains.p, s));
             } else {
-                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->chunks.p, m->n_chunks, m->N.p, m->n,
+                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n,
                                            m->totals.p, m->tickets.p, m->gains.p, s));
             }
         }

@@ -38,7 +38,8 @@ def main():
     rows = 2 * 8192
     buf = np.zeros((rows, 4), np.uint64)
     for rep in range(args.reps):
-        m.stitch(frames, out)
+        for _ in range(3):  # back to back, as in bench.py: the stamps are the last launch's
+            m.stitch(frames, out)
         torch.cuda.synchronize()
         assert lib.octvr_debug_stamps(buf.ctypes.data, rows) == rows
         st = buf[:8192].astype(np.int64)
@@ -55,16 +56,23 @@ def main():
             e = (st[sel, 1] - t0) / 100.0
             print("  band %d: end min %.1f med %.1f max %.1f us; items %d chunks %d (per wg max %d / %d)" % (
                 g, e.min(), np.median(e), e.max(), st[sel, 2].sum(), st[sel, 3].sum(), st[sel, 2].max(), st[sel, 3].max()))
-        glive = gf[:, 1] > 0
-        g2 = gf[glive]
-        if len(g2):
-            gt0 = g2[:, 0].min()
-            last = g2[g2[:, 2] > 1]
-            print("  gain feed: %d wgs, start spread %.2f us, end min %.2f med %.2f max %.2f us, solve done %.2f us; "
-                  "stitch starts %.2f us after feed start" % (
-                      len(g2), (g2[:, 0].max() - gt0) / 100.0, (g2[:, 1].min() - gt0) / 100.0,
-                      np.median(g2[:, 1] - gt0) / 100.0, (g2[:, 1].max() - gt0) / 100.0,
-                      ((last[:, 2].max() - gt0) / 100.0) if len(last) else -1, (t0 - gt0) / 100.0))
+        f = buf.reshape(-1)[4 * 8192:4 * 8192 + 2048 * 8].reshape(-1, 8).astype(np.int64)
+        f = f[f[:, 4] > 0]
+        if len(f):
+            ft0 = f[:, 0].min()
+            rel = (f - ft0) / 100.0
+            print("  gain feed: %d wgs; start spread %.2f; per-wg (median) gathered %.2f, reduced %.2f, adds done %.2f, "
+                  "ticket %.2f us after its start; last ticket at %.2f" % (
+                      len(f), rel[:, 0].max(), np.median(rel[:, 1] - rel[:, 0]), np.median(rel[:, 2] - rel[:, 0]),
+                      np.median(rel[:, 3] - rel[:, 0]), np.median(rel[:, 4] - rel[:, 0]), rel[:, 4].max()))
+            last = f[f[:, 5] == 1]
+            if len(last):
+                L = (last[0] - ft0) / 100.0
+                X = (buf.reshape(-1)[4 * 8192 + 2048 * 8:4 * 8192 + 2048 * 8 + 2].astype(np.int64) - ft0) / 100.0
+                print("  last workgroup: totals read %.2f, A/b built %.2f, solved %.2f, written %.2f; stitch starts %.2f us "
+                      "after feed start; start times by 8-quantile %s" % (
+                          L[6], X[0], X[1], L[7], (t0 - ft0) / 100.0,
+                          np.round(np.quantile(rel[:, 0], np.linspace(0, 1, 9)), 2).tolist()))
         buf[:] = 0
         # clear the device copy too: the next rep overwrites every live row anyway
 
