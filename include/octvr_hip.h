@@ -88,6 +88,12 @@ int octvr_rig_create_from_arrays(int out_w, int out_h, int n_inputs, const int* 
 int octvr_rig_num_inputs(const octvr_rig* rig, int* n);
 int octvr_rig_out_size(const octvr_rig* rig, int* w, int* h);
 int octvr_rig_get_input(const octvr_rig* rig, int i, octvr_input_view* view);
+
+/* Overlay inputs of the rig (MapperTemplate::overlay_inputs, octvr.hpp:62; built like the inputs by
+ * add_input(..., overlay = true), template.cpp:46-153, written to .dat at template.cpp:248-255). */
+int octvr_rig_num_overlays(const octvr_rig* rig, int* n);
+/* ROI, maps, mask (and vignette) of overlay i; seam_mask is NULL (overlays have none). */
+int octvr_rig_get_overlay(const octvr_rig* rig, int i, octvr_input_view* view);
 void octvr_rig_destroy(octvr_rig* rig);
 
 /* ---- vr::Mapper ---------------------------------------------------------------------------- */

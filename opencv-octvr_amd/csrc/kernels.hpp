@@ -104,7 +104,7 @@ struct CamTemplate {
 // 8-byte entry plus a partner mask (bit j).  Samples are sorted by (camera, source row, column); each
 // camera's run is padded with invalid samples (partner mask 0) to whole runs of kGainWaveRun (one
 // wave each, so a wave's frame is uniform), the whole array to chunks of kGainChunk (one workgroup,
-// 386 workgroups on C2).
+// about one workgroup per CU on C2).
 constexpr int kGainMaxCams = 16;
 #ifndef OCTVR_GAIN_PER  // samples per lane of the gain feed
 #define OCTVR_GAIN_PER 6

@@ -266,7 +266,7 @@ size_t unfilter(uint8_t* d, size_t avail, int w, int h, int bits_pp, std::vector
 
 }  // namespace
 
-std::vector<uint8_t> png_decode_rgb(const uint8_t* buf, size_t n, int* out_w, int* out_h) {
+std::vector<uint8_t> png_decode_rgb(const uint8_t* buf, size_t n, int* out_w, int* out_h, int expect_w, int expect_h) {
     static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
     REQUIRE(n >= 8 && memcmp(buf, sig, 8) == 0, "png: bad signature (only PNG masks are supported)");
     int w = 0, h = 0, depth = 0, ctype = 0, interlace = 0;
@@ -295,7 +295,16 @@ std::vector<uint8_t> png_decode_rgb(const uint8_t* buf, size_t n, int* out_w, in
     REQUIRE(w > 0 && h > 0, "png: missing IHDR");
     const int chans = ctype == 0 ? 1 : ctype == 2 ? 3 : ctype == 3 ? 1 : ctype == 4 ? 2 : ctype == 6 ? 4 : 0;
     REQUIRE(chans > 0, "png: bad colour type");
-    REQUIRE(depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16, "png: bad bit depth");
+    // the colour type / bit depth pairs the PNG spec allows (libpng rejects the others, so
+    // cv::imdecode fails and camera.cpp:175-176 asserts): gray 1/2/4/8/16, palette 1/2/4/8,
+    // RGB / gray+alpha / RGBA 8/16
+    const bool legal = ctype == 0   ? (depth == 1 || depth == 2 || depth == 4 || depth == 8 || depth == 16)
+                       : ctype == 3 ? (depth == 1 || depth == 2 || depth == 4 || depth == 8)
+                                    : (depth == 8 || depth == 16);
+    REQUIRE(legal, "png: bit depth not allowed for this colour type");
+    // size check against the camera before anything is inflated or allocated
+    if (expect_w > 0) REQUIRE(w == expect_w && h == expect_h, "png mask size differs from the camera's exclude mask");
+    REQUIRE((uint64_t)w * (uint64_t)h <= ((uint64_t)1 << 28), "png: image too large for a mask");
     REQUIRE(ctype != 3 || !plte.empty(), "png: palette image without PLTE");
     const int bits_pp = chans * depth;
     // inflate the whole stream (its size is bounded by the passes' (stride + 1) * rows)

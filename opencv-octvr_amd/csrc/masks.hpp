@@ -10,6 +10,7 @@ namespace octvr {
 void fill_poly_u8(uint8_t* img, int w, int h, const int* pts, int npts, uint8_t color);
 
 // cv::imdecode(png, IMREAD_COLOR) restricted to PNG; returns w*h*3 bytes in R,G,B order.
-std::vector<uint8_t> png_decode_rgb(const uint8_t* buf, size_t n, int* w, int* h);
+// expect_w > 0: the image must be expect_w x expect_h (checked on the IHDR, before inflating)
+std::vector<uint8_t> png_decode_rgb(const uint8_t* buf, size_t n, int* w, int* h, int expect_w = 0, int expect_h = 0);
 
 }  // namespace octvr

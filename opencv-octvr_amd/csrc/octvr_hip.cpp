@@ -195,9 +195,9 @@ void build_camera_masks(const JsonValue& o, std::vector<uint8_t>& excl, std::vec
                 std::vector<uint8_t> bytes(args.size());
                 for (size_t k = 0; k < args.size(); k++) bytes[k] = (uint8_t)args[k].as_int();
                 int pw = 0, ph = 0;
-                std::vector<uint8_t> rgb = png_decode_rgb(bytes.data(), bytes.size(), &pw, &ph);
-                // CV_Assert(mask_img.size() == exclude_mask.size()) (camera.cpp:170)
-                REQUIRE(!excl.empty() && pw == w && ph == h, "png mask size differs from the camera's exclude mask");
+                // CV_Assert(mask_img.size() == exclude_mask.size()) (camera.cpp:170), checked on the IHDR
+                REQUIRE(!excl.empty() && w > 0 && h > 0, "png mask without a camera size");
+                std::vector<uint8_t> rgb = png_decode_rgb(bytes.data(), bytes.size(), &pw, &ph, w, h);
                 for (size_t k = 0; k < n; k++) {
                     if (rgb[3 * k]) excl[k] = 255;      // RED channel
                     if (rgb[3 * k + 1]) incl[k] = 255;  // GREEN channel
@@ -595,14 +595,19 @@ struct DatReader {
     }
     // Rmat: returns rows, cols, type; data appended to `out` (bytes)
     void mat(int want_type, int& rows, int& cols, std::vector<uint8_t>& out) {
-        int type = (int)i64();
-        rows = (int)i64();
-        cols = (int)i64();
+        const int64_t type = i64(), r64 = i64(), c64 = i64();
         out.clear();
+        // cv::Mat dimensions are non-negative ints; bound the element count before allocating
+        if (r64 < 0 || c64 < 0 || r64 > INT32_MAX || c64 > INT32_MAX)
+            throw OctvrError(OCTVR_E_PARSE, ".dat: bad Mat dimensions");
+        rows = (int)r64;
+        cols = (int)c64;
         if ((int64_t)rows * cols == 0) {
             rows = cols = 0;
             return;
         }
+        if ((uint64_t)rows * (uint64_t)cols > ((uint64_t)1 << 34))
+            throw OctvrError(OCTVR_E_PARSE, ".dat: Mat too large");
         if (want_type >= 0 && type != want_type) throw OctvrError(OCTVR_E_PARSE, "unexpected Mat type in .dat");
         size_t elem = type == CV_32FC1 ? 4 : type == CV_8UC1 ? 1 : 0;
         if (!elem) throw OctvrError(OCTVR_E_PARSE, "unsupported Mat type in .dat");
@@ -610,8 +615,13 @@ struct DatReader {
         f.read(reinterpret_cast<char*>(out.data()), (std::streamsize)out.size());
         if (!f) throw OctvrError(OCTVR_E_PARSE, "truncated .dat file");
     }
-    void input(RigInput& in) {
-        for (int k = 0; k < 4; k++) in.roi[k] = (int)i64();
+    // ROI x, y >= 0, w, h > 0 and inside the out_w x out_h frame (as octvr_rig_create_from_arrays)
+    void input(RigInput& in, int out_w, int out_h) {
+        int64_t roi[4];
+        for (int k = 0; k < 4; k++) roi[k] = i64();
+        if (roi[0] < 0 || roi[1] < 0 || roi[2] <= 0 || roi[3] <= 0 || roi[0] + roi[2] > out_w || roi[1] + roi[3] > out_h)
+            throw OctvrError(OCTVR_E_PARSE, ".dat: ROI outside the output frame");
+        for (int k = 0; k < 4; k++) in.roi[k] = (int)roi[k];
         std::vector<uint8_t> b;
         int r, c;
         mat(CV_32FC1, r, c, b);
@@ -622,8 +632,9 @@ struct DatReader {
         memcpy(in.map2.data(), b.data(), b.size());
         mat(CV_8UC1, r, c, b);
         in.mask = b;
-        if ((int)in.map1.size() != in.roi[2] * in.roi[3] || (int)in.mask.size() != in.roi[2] * in.roi[3])
-            throw OctvrError(OCTVR_E_PARSE, ".dat: map size does not match ROI");
+        const size_t roi_px = (size_t)in.roi[2] * (size_t)in.roi[3];
+        if (in.map1.size() != roi_px || in.map2.size() != roi_px || in.mask.size() != roi_px)
+            throw OctvrError(OCTVR_E_PARSE, ".dat: map / mask size does not match ROI");
         mat(-1, r, c, b);
         in.vignette.resize(b.size() / 4);
         if (!b.empty()) memcpy(in.vignette.data(), b.data(), b.size());
@@ -1059,21 +1070,26 @@ int octvr_rig_load_dat(const char* path, octvr_rig** out) {
         if (!r.f || strncmp(magic, kDatMagic, 5) != 0)
             throw OctvrError(OCTVR_E_PARSE, "Invalid data file (version does not match)");
         auto rig = std::make_unique<octvr_rig>();
-        rig->out_w = (int)r.i64();
-        rig->out_h = (int)r.i64();
+        const int64_t ow = r.i64(), oh = r.i64();
+        if (ow <= 0 || oh <= 0 || ow > 65535 || oh > 65535) throw OctvrError(OCTVR_E_PARSE, ".dat: bad output size");
+        rig->out_w = (int)ow;
+        rig->out_h = (int)oh;
         int64_t n = r.i64();
-        REQUIRE(n >= 0 && n <= kMaxCams, ".dat: bad input count");
+        if (n < 0 || n > kMaxCams) throw OctvrError(OCTVR_E_PARSE, ".dat: bad input count");
         rig->inputs.resize(n);
-        for (auto& in : rig->inputs) r.input(in);
+        for (auto& in : rig->inputs) r.input(in, rig->out_w, rig->out_h);
         rig->seam_masks.resize(n);
         for (int64_t i = 0; i < n; i++) {
             int rr, cc;
             r.mat(CV_8UC1, rr, cc, rig->seam_masks[i]);
+            // MapperTemplate::dump writes one ROI-sized seam mask per input (template.cpp:245-246)
+            if (rig->seam_masks[i].size() != (size_t)rig->inputs[i].roi[2] * (size_t)rig->inputs[i].roi[3])
+                throw OctvrError(OCTVR_E_PARSE, ".dat: seam mask size does not match ROI");
         }
         int64_t no = r.i64();
-        REQUIRE(no >= 0 && no <= kMaxCams, ".dat: bad overlay count");
+        if (no < 0 || no > kMaxCams) throw OctvrError(OCTVR_E_PARSE, ".dat: bad overlay count");
         rig->overlays.resize(no);
-        for (auto& in : rig->overlays) r.input(in);
+        for (auto& in : rig->overlays) r.input(in, rig->out_w, rig->out_h);
         *out = rig.release();
     });
 }
@@ -1142,14 +1158,40 @@ int octvr_rig_get_input(const octvr_rig* rig, int i, octvr_input_view* v) {
     });
 }
 
+int octvr_rig_num_overlays(const octvr_rig* rig, int* n) {
+    return guarded([&] {
+        REQUIRE(rig && n, "NULL argument");
+        *n = (int)rig->overlays.size();
+    });
+}
+
+int octvr_rig_get_overlay(const octvr_rig* rig, int i, octvr_input_view* v) {
+    return guarded([&] {
+        REQUIRE(rig && v && i >= 0 && i < (int)rig->overlays.size(), "bad overlay index");
+        const RigInput& in = rig->overlays[i];
+        v->roi_x = in.roi[0];
+        v->roi_y = in.roi[1];
+        v->roi_w = in.roi[2];
+        v->roi_h = in.roi[3];
+        v->map1 = in.map1.data();
+        v->map2 = in.map2.data();
+        v->mask = in.mask.data();
+        v->seam_mask = nullptr;
+        v->vignette = in.vignette.empty() ? nullptr : in.vignette.data();
+        v->vignette_w = in.vig_w;
+        v->vignette_h = in.vig_h;
+    });
+}
+
 void octvr_rig_destroy(octvr_rig* rig) { delete rig; }
 
 int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                         int enable_gain, int scale_w, int scale_h, octvr_mapper** out) {
     return guarded([&] {
         REQUIRE(rig && out && in_w && in_h, "NULL argument");
-        REQUIRE(n_inputs == (int)(rig->inputs.size() + rig->overlays.size()), "in_sizes must cover inputs + overlays");
-        REQUIRE(rig->overlays.empty(), "overlay inputs are not implemented in this ABI version");
+        if (!rig->overlays.empty())  // checked first: the real reason, whatever n_inputs says
+            throw OctvrError(OCTVR_E_UNSUPPORTED, "overlay inputs are not implemented in this ABI version");
+        REQUIRE(n_inputs == (int)rig->inputs.size(), "in_sizes must cover every input");
         REQUIRE((int)rig->inputs.size() <= kMaxCams, "too many inputs");
         REQUIRE(scale_w >= 0 && scale_h >= 0 && (scale_w == 0) == (scale_h == 0), "bad scaled output size");
         REQUIRE(rig->out_w % 2 == 0 && rig->out_h % 2 == 0, "YUV420 output needs even width/height");

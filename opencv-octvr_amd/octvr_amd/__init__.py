@@ -55,6 +55,8 @@ _lib.octvr_rig_create_from_arrays.argtypes = [C.c_int, C.c_int, C.c_int, C.POINT
 _lib.octvr_rig_num_inputs.argtypes = [_VP, C.POINTER(C.c_int)]
 _lib.octvr_rig_out_size.argtypes = [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]
 _lib.octvr_rig_get_input.argtypes = [_VP, C.c_int, C.POINTER(InputView)]
+_lib.octvr_rig_num_overlays.argtypes = [_VP, C.POINTER(C.c_int)]
+_lib.octvr_rig_get_overlay.argtypes = [_VP, C.c_int, C.POINTER(InputView)]
 _lib.octvr_rig_destroy.argtypes = [_VP]
 _lib.octvr_rig_destroy.restype = None
 _lib.octvr_mapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
@@ -156,10 +158,20 @@ class MapperTemplate:
         _check(_lib.octvr_rig_num_inputs(self._h, C.byref(n)))
         return n.value
 
-    def input(self, i):
+    @property
+    def num_overlays(self):
+        n = C.c_int()
+        _check(_lib.octvr_rig_num_overlays(self._h, C.byref(n)))
+        return n.value
+
+    def overlay(self, i):
+        """Overlay input i (MapperTemplate::overlay_inputs): (roi, map1, map2, mask, None)."""
+        return self.input(i, _overlay=True)
+
+    def input(self, i, _overlay=False):
         """(roi, map1, map2, mask, seam_mask) as numpy copies."""
         v = InputView()
-        _check(_lib.octvr_rig_get_input(self._h, i, C.byref(v)))
+        _check((_lib.octvr_rig_get_overlay if _overlay else _lib.octvr_rig_get_input)(self._h, i, C.byref(v)))
         k = v.roi_w * v.roi_h
         shape = (v.roi_h, v.roi_w)
 

@@ -79,3 +79,65 @@ def test_dump_without_seams_is_an_error(product_lib, tmp_path):
                                                [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]])
     with pytest.raises(product_lib.OctvrError):
         mt.dump(str(tmp_path / "x.dat"))
+
+
+def _dat(out=(8, 4), rois=((0, 0, 4, 2),), mats=None, seams=None, n_ov=0, raw_inputs=None):
+    """A small VRv11 file (template.cpp:206-256 layout): W, H, n, per input ROI + map1 + map2 + mask +
+    vignette (empty), seam masks, overlay count.  `mats` / `seams` override the (type, rows, cols,
+    payload) of each Mat."""
+    i64 = lambda *v: np.array(v, np.int64).tobytes()
+    b = b"VRv11" + i64(out[0], out[1], len(rois))
+    for k, roi in enumerate(rois):
+        w, h = roi[2], roi[3]
+        b += i64(*roi)
+        ms = (mats or {}).get(k) or [(5, h, w, np.zeros(w * h, np.float32).tobytes()),
+                                      (5, h, w, np.zeros(w * h, np.float32).tobytes()),
+                                      (0, h, w, np.zeros(w * h, np.uint8).tobytes()),
+                                      (0, 0, 0, b"")]
+        for t, r, c, payload in ms:
+            b += i64(t, r, c) + payload
+    for k, roi in enumerate(rois):
+        t, r, c, payload = (seams or {}).get(k) or (0, roi[3], roi[2], np.zeros(roi[2] * roi[3], np.uint8).tobytes())
+        b += i64(t, r, c) + payload
+    return b + i64(n_ov)
+
+
+def test_dat_reader_accepts_minimal_file(product_lib, tmp_path):
+    p = tmp_path / "ok.dat"
+    p.write_bytes(_dat())
+    mt = product_lib.MapperTemplate.load(str(p))
+    assert mt.out_size == (8, 4) and len(mt) == 1
+
+
+@pytest.mark.parametrize("case", ["rows_cols_minus1", "map2_short", "seam_mismatch", "roi_outside", "roi_negative",
+                                  "roi_empty", "out_zero", "negative_count", "truncated_map", "truncated_seam"])
+def test_dat_reader_rejects_malformed(product_lib, tmp_path, case):
+    """every Mat must match its input's ROI and every ROI must lie inside the output frame,
+    so a malformed .dat fails in the reader instead of reaching the mapper's ROI indexing."""
+    z4 = lambda n, dt: np.zeros(n, dt).tobytes()
+    if case == "rows_cols_minus1":  # (size_t)-1 * (size_t)-1 == 1 == 1 x 1 ROI
+        data = _dat(rois=((0, 0, 1, 1),), mats={0: [(5, -1, -1, z4(1, np.float32)), (5, 1, 1, z4(1, np.float32)),
+                                                    (0, 1, 1, z4(1, np.uint8)), (0, 0, 0, b"")]})
+    elif case == "map2_short":
+        data = _dat(mats={0: [(5, 2, 4, z4(8, np.float32)), (5, 1, 4, z4(4, np.float32)),
+                              (0, 2, 4, z4(8, np.uint8)), (0, 0, 0, b"")]})
+    elif case == "seam_mismatch":
+        data = _dat(seams={0: (0, 1, 4, z4(4, np.uint8))})
+    elif case == "roi_outside":
+        data = _dat(rois=((6, 0, 4, 2),))
+    elif case == "roi_negative":
+        data = _dat(rois=((-1, 0, 4, 2),))
+    elif case == "roi_empty":
+        data = _dat(rois=((0, 0, 0, 2),))
+    elif case == "out_zero":
+        data = _dat(out=(0, 4))
+    elif case == "negative_count":
+        data = b"VRv11" + np.array([8, 4, -1], np.int64).tobytes()
+    elif case == "truncated_map":
+        data = _dat()[:5 + 24 + 32 + 24 + 10]
+    else:
+        data = _dat()[:-20]
+    p = tmp_path / ("bad_%s.dat" % case)
+    p.write_bytes(data)
+    with pytest.raises(product_lib.OctvrError):
+        product_lib.MapperTemplate.load(str(p))

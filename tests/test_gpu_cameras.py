@@ -100,3 +100,35 @@ def test_gpu_selection_equals_its_polygon(product_lib):
         assert ia[0] == ib[0]
         for k in (1, 2, 3):
             assert np.array_equal(ia[k], ib[k])
+
+
+@pytest.mark.parametrize("use_roi", [False, True])
+def test_gpu_overlay_luts_vs_oracle(product_lib, tmp_path, use_roi):
+    """The overlays' own LUTs (maps, mask, ROI) against the oracle's add_input(overlay = true)
+    restatement (template.cpp:46-153), and their .dat round trip (template.cpp:248-255, 306-311)."""
+    ox = product_lib
+    rig = R.mask_rigs()["overlay_include"]
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), 512, 256, use_roi=use_roi)
+    n_in = len(rig["inputs"])
+    want = O.lut_build(rig, 512, 256, use_roi=use_roi)[n_in:]
+    assert mt.num_overlays == len(want) == len(rig["overlays"])
+    for i, (roi, w1, w2, wm) in enumerate(want):
+        groi, g1, g2, gm, gs = mt.overlay(i)
+        assert groi == tuple(roi) and gs is None
+        dm = gm != wm
+        assert dm.sum() <= max(2, gm.size // 20000), (i, int(dm.sum()))
+        both = (~dm) & (wm > 0)
+        u1 = np.abs(g1.view(np.int32)[both].astype(np.int64) - w1.view(np.int32)[both])
+        u2 = np.abs(g2.view(np.int32)[both].astype(np.int64) - w2.view(np.int32)[both])
+        assert u1.max(initial=0) <= 1 and u2.max(initial=0) <= 1
+        assert (wm > 0).any()
+    p = tmp_path / "ov.dat"
+    mt.dump(str(p))
+    back = ox.MapperTemplate.load(str(p))
+    assert back.num_overlays == mt.num_overlays
+    for i in range(mt.num_overlays):
+        a, b = mt.overlay(i), back.overlay(i)
+        assert a[0] == b[0] and all(np.array_equal(a[k], b[k]) for k in (1, 2, 3))
+    with pytest.raises(ox.OctvrError) as e:  # overlays reach the mapper: unsupported, with the real reason
+        ox.Mapper(back, [(256, 256)] * len(back), blend=0, enable_gain=False)
+    assert "overlay" in str(e.value)

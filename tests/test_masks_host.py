@@ -90,3 +90,16 @@ def test_png_decode_rejects_garbage(product_lib):
     png, _ = P.encode(np.zeros((4, 4, 3), np.int64), 2)
     with pytest.raises(product_lib.OctvrError):
         product_lib.png_decode_rgb(png[:-30])
+
+
+@pytest.mark.parametrize("ctype,depth", [(2, 4), (2, 1), (6, 2), (4, 4), (3, 16)])
+def test_png_decode_rejects_illegal_depth(product_lib, ctype, depth):
+    """ADVICE r01: colour type / bit depth pairs the PNG spec forbids (libpng, hence cv::imdecode at
+    camera.cpp:175-176, rejects them) fail instead of decoding to garbage."""
+    chans = {0: 1, 2: 3, 3: 1, 4: 2, 6: 4}[ctype]
+    samples = np.zeros((3, 5, chans), np.int64)
+    palette = np.zeros((256, 3), np.int64) if ctype == 3 else None
+    png, _ = P.encode(samples, ctype, depth, palette, False, seed=1)
+    with pytest.raises(product_lib.OctvrError) as e:
+        product_lib.png_decode_rgb(png)
+    assert "depth" in str(e.value)
