@@ -112,12 +112,14 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* mapper, const uint8_t* const* in_d
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream);
 /* Mapper::gains() (mapper.hpp:445-447): gains used by the last stitch (synchronizes the stream). */
 int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
-/* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 8 B LUT +
- * 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each source frame read once). */
+/* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 4 B tiled
+ * LUT entry (8 B in wide tiles) + 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each
+ * source frame read once) + the per-item headers (multi-band / feather: the whole blend sequence). */
 int octvr_mapper_traffic(const octvr_mapper* mapper, double* bytes_per_frame);
-/* Live per-kernel timing for roofline accounting: while enabled, every stitch brackets its main
- * (composite) kernel with HIP events on the caller's stream.  kernel_time synchronizes on the
- * recorded events, returns the summed device time and launch count, and resets the log. */
+/* Live per-kernel timing for roofline accounting: with enable = k > 0, every k-th stitch brackets
+ * its main (composite) kernel with HIP events on the caller's stream (0 = off).  kernel_time
+ * synchronizes on the recorded events, returns the summed device time and launch count, and resets
+ * the log. */
 int octvr_mapper_set_timing(octvr_mapper* mapper, int enable);
 int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launches);
 /* Build-time statistics of a mapper as a JSON object (tiles, wide tiles, staged bytes, gain samples). */

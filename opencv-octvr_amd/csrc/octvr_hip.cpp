@@ -679,14 +679,16 @@ struct octvr_mapper {
     DevBuf<MbCamLevel> result_view;  // the result frame as a one-entry RGBA sink of the composite
     hipStream_t last_stream = nullptr;
     hipEvent_t order_ev = nullptr;  // orders a stitch on a new stream after the previous one
-    bool timing = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+    int timing = 0;             // event-timing period in stitches (0 = off)
+    uint64_t timed_calls = 0;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events, free_events;  // recorded / reusable
     ~octvr_mapper() {
         if (order_ev) (void)hipEventDestroy(order_ev);
-        for (auto& e : events) {
-            (void)hipEventDestroy(e.first);
-            (void)hipEventDestroy(e.second);
-        }
+        for (auto* v : {&events, &free_events})
+            for (auto& e : *v) {
+                (void)hipEventDestroy(e.first);
+                (void)hipEventDestroy(e.second);
+            }
     }
 };
 
@@ -893,9 +895,16 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             }
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (m->timing) {
-            HIP_CHECK(hipEventCreate(&e0));
-            HIP_CHECK(hipEventCreate(&e1));
+        const bool timed = m->timing > 0 && (m->timed_calls++ % (uint64_t)m->timing) == 0;
+        if (timed) {
+            if (m->free_events.empty()) {
+                HIP_CHECK(hipEventCreate(&e0));
+                HIP_CHECK(hipEventCreate(&e1));
+            } else {
+                e0 = m->free_events.back().first;
+                e1 = m->free_events.back().second;
+                m->free_events.pop_back();
+            }
             HIP_CHECK(hipEventRecord(e0, s));
         }
         if (m->scaled) {
@@ -912,7 +921,7 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         } else {
             HIP_CHECK(launch_stitch(fs, m->tiles.view, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
         }
-        if (m->timing) {
+        if (timed) {
             HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
         }
@@ -1334,8 +1343,9 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
 
 int octvr_mapper_set_timing(octvr_mapper* m, int enable) {
     return guarded([&] {
-        REQUIRE(m, "NULL mapper");
-        m->timing = enable != 0;
+        REQUIRE(m && enable >= 0, "bad arguments");
+        m->timing = enable;
+        m->timed_calls = 0;
     });
 }
 
@@ -1349,8 +1359,7 @@ int octvr_mapper_kernel_time(octvr_mapper* m, double* total_ms, int* launches) {
             float ms = 0;
             HIP_CHECK(hipEventElapsedTime(&ms, e.first, e.second));
             t += ms;
-            (void)hipEventDestroy(e.first);
-            (void)hipEventDestroy(e.second);
+            m->free_events.push_back(e);
         }
         *launches = (int)m->events.size();
         *total_ms = t;
