@@ -207,6 +207,9 @@ constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host:
 #endif
 
 __device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
+#if OCTVR_DIAG_HOTOUT  // diagnostic: every tile row writes rows 0-7 (the same 64 KB): no DRAM writes
+    y &= 7;
+#endif
     const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
     const uint32_t oc = in ? (uint32_t)(y >> 1) * o.pitch + (uint32_t)(x >> 1) : kDropOffset;
     __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, OCTVR_OUT_POLICY);

@@ -775,6 +775,9 @@ constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
 #ifndef OCTVR_STAGE_SKIP
 #define OCTVR_STAGE_SKIP 1
 #endif
+#ifndef OCTVR_STORE_LATE
+#define OCTVR_STORE_LATE 0
+#endif
 #ifndef OCTVR_DYN  // 0: static round-robin dealing of a band's items (no work counters)
 #define OCTVR_DYN 1
 #endif
@@ -900,38 +903,47 @@ __device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro
         store_rgba(ro, q, cam, x, y, in);
 }
 
-// MODE 2 output staging (kernels.hpp kTileOutBytes): Y rows 0-7 (128 B each), then U rows 0-3 and
-// V rows 0-3 (64 B each) of one tile.  Each lane writes its quad's 2 + 2 Y bytes and U, V bytes.
-__device__ __forceinline__ void stage_out_quad(uint32_t* s_out, const QuadOut& q, int qx, int qy) {
+// MODE 2 output staging: one item's YUV420P output (Q halves of 128 x 8) in LDS as Y rows 0..8Q-1
+// (128 B each), then U rows 0..4Q-1 and V rows 0..4Q-1 (64 B each).  Each lane writes its quad's
+// 2 + 2 Y bytes and U, V bytes; after the next barrier lanes 0..96Q-1 store it with one 16-byte
+// store each (Y: 8 lanes per row, U / V: 4) instead of four 1-2-byte stores per quad.
+template <int Q>
+__device__ __forceinline__ void stage_out_quad(uint32_t* s_out, const QuadOut& q, int h, int qx, int qy) {
     uint8_t* b = reinterpret_cast<uint8_t*>(s_out);
-    *reinterpret_cast<uint16_t*>(b + (2 * qy) * kTileW + 2 * qx) = (uint16_t)q.y01;
-    *reinterpret_cast<uint16_t*>(b + (2 * qy + 1) * kTileW + 2 * qx) = (uint16_t)q.y23;
-    b[kTileW * kTileH + qy * (kTileW / 2) + qx] = (uint8_t)q.u;
-    b[kTileW * kTileH + (kTileH / 2) * (kTileW / 2) + qy * (kTileW / 2) + qx] = (uint8_t)q.v;
+    constexpr int kU = kTileW * kTileH * Q, kV = kU + (kTileH / 2) * (kTileW / 2) * Q;
+    const int yr = h * kTileH + 2 * qy, cr = h * (kTileH / 2) + qy;
+    *reinterpret_cast<uint16_t*>(b + yr * kTileW + 2 * qx) = (uint16_t)q.y01;
+    *reinterpret_cast<uint16_t*>(b + (yr + 1) * kTileW + 2 * qx) = (uint16_t)q.y23;
+    b[kU + cr * (kTileW / 2) + qx] = (uint8_t)q.u;
+    b[kV + cr * (kTileW / 2) + qx] = (uint8_t)q.v;
 }
 
-// Wave w stores Y rows 2w, 2w+1 and U, V row w of the staged tile whose top-left pixel is
-// (px - 2 qx, py - 2 qy) of the calling lane (px, py: the lane's quad).  Needs W % 32 == 0 and a
-// 16-byte aligned frame and pitch (checked on the host); rows at or past H are dropped.
-__device__ __forceinline__ void store_tile_wide(const OutFrame& o, const uint32_t* s_out, int px, int py, bool in, int H) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int x0 = px - 2 * (threadIdx.x & 63), y0 = py - 2 * (threadIdx.x >> 6);  // tile origin
-    int lds, row, col;  // byte offset in s_out, output row in its plane, byte column in the row
+// Needs W % 32 == 0 and a 16-byte aligned frame and pitch (checked on the host); rows at or past H
+// (luma) / H/2 (chroma) are dropped.  (x0, y0): the item's top-left output pixel.
+template <int Q>
+__device__ __forceinline__ void store_item_wide(const OutFrame& o, const uint32_t* s_out, int x0, int y0, bool in, int H) {
+    const int l = threadIdx.x;
+    constexpr int kYl = 8 * kTileH * Q, kCl = 4 * (kTileH / 2) * Q;  // lanes of Y / of U (and V)
+    constexpr int kU = kTileW * kTileH * Q, kV = kU + (kTileH / 2) * (kTileW / 2) * Q;
+    int lds, row, col;
     uint32_t plane;
-    if (lane < 16) {
-        row = y0 + 2 * w + (lane >> 3);
-        col = x0 + 16 * (lane & 7);
-        lds = (2 * w + (lane >> 3)) * kTileW + 16 * (lane & 7);
+    bool ok;
+    if (l < kYl) {
+        row = y0 + (l >> 3);
+        col = x0 + 16 * (l & 7);
+        lds = (l >> 3) * kTileW + 16 * (l & 7);
         plane = 0u;
+        ok = row < H;
     } else {
-        const int k = lane < 20 ? lane - 16 : lane - 20;
-        row = (y0 >> 1) + w;
-        col = (x0 >> 1) + 16 * (k & 3);
-        lds = kTileW * kTileH + (lane < 20 ? 0 : (kTileH / 2) * (kTileW / 2)) + w * (kTileW / 2) + 16 * (k & 3);
-        plane = lane < 20 ? o.u_off : o.v_off;
+        const int k = l - kYl, isv = k >= kCl ? 1 : 0, kk = k - isv * kCl;
+        row = (y0 >> 1) + (kk >> 2);
+        col = (x0 >> 1) + 16 * (kk & 3);
+        lds = (isv ? kV : kU) + (kk >> 2) * (kTileW / 2) + 16 * (kk & 3);
+        plane = isv ? o.v_off : o.u_off;
+        ok = k < 2 * kCl && row < (H >> 1);
     }
-    const bool ok = in && lane < 24 && (lane < 16 ? row < H : row < (H >> 1));
-    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + (lane < 24 ? lds : 0));
+    ok = ok && in;
+    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + (ok ? lds : 0));
     const uint32_t off = ok ? plane + (uint32_t)row * o.pitch + (uint32_t)col : kDropOffset;
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, o.rsrc, off, 0, OCTVR_OUT_POLICY);
@@ -947,10 +959,12 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
     __shared__ float s_gain[kMaxCams];
     __shared__ f32x2_t s_slot_gain[kTileSlots];  // {g, g} per slot (finish_quad2)
     __shared__ uint32_t s_claim;
-    // MODE 2: the previous item's YUV420P output, staged so every wave writes it with one 16-byte
-    // store per lane (Y rows 2w, 2w+1: lanes 0-15; U / V row w: lanes 16-19 / 20-23) instead of
-    // four 1-2-byte stores per quad
+    // MODE 2: the previous item's YUV420P output, staged in LDS and written with one 16-byte store
+    // per lane (store_item_wide) instead of four 1-2-byte stores per quad
     constexpr bool kWideOut = MODE == 2;
+    // kStoreLate: an item's output is stored right after its computation, behind the next item's
+    // loads (so waiting for those loads need not drain the stores); else at the next iteration's top
+    constexpr bool kStoreLate = OCTVR_STORE_LATE != 0;
     constexpr int SM = MODE == 1 ? 1 : 0;  // sink: YUV (finish_quad) or RGBA
     __shared__ __attribute__((aligned(16))) uint32_t s_out[kWideOut ? QPL * kTileOutBytes / 4 : 1];
     constexpr int R = QPL == 1 ? kStageRegs : OCTVR_STAGE_REGS2;  // staging chunks prefetched per wave
@@ -1090,11 +1104,11 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         }
         first = false;
 #if !OCTVR_DIAG_NOSTORE
+        if constexpr (kWideOut) {
+            store_item_wide<QPL>(of, s_out, px - 2 * qx, py - 2 * qy, pin, H);
+        } else if constexpr (!kStoreLate) {
 #pragma unroll
-        for (int h = 0; h < QPL; h++) {
-            if constexpr (kWideOut)
-                store_tile_wide(of, s_out + h * (kTileOutBytes / 4), px, py + h * kTileH, pin, H);
-            else
+            for (int h = 0; h < QPL; h++)
                 store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
 #endif
@@ -1140,7 +1154,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         prev[h] = finish_any<SM>(rgb, gain);
 #endif
         // MODE 2: staged for the wide stores after the next barrier
-        if constexpr (kWideOut) stage_out_quad(s_out + h * (kTileOutBytes / 4), prev[h], qx, qy);
+        if constexpr (kWideOut) stage_out_quad<QPL>(s_out, prev[h], h, qx, qy);
 #if OCTVR_PHASES
         asm volatile("" : "+v"(prev[h].y01), "+v"(prev[h].y23), "+v"(prev[h].u), "+v"(prev[h].v));
 #endif
@@ -1150,6 +1164,13 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         py = y;
         pcam = (cur.nslots >> 16) & 31u;
         pin = x < W && y < H;
+#if !OCTVR_DIAG_NOSTORE
+        if constexpr (kStoreLate && !kWideOut) {  // youngest ops of the iteration (see kStoreLate)
+#pragma unroll
+            for (int h = 0; h < QPL; h++)
+                store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+        }
+#endif
         cur = nxt;
     }
     // the last workgroup to finish resets the work counters for the next launch (stream order makes
@@ -1172,12 +1193,12 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
                 __hip_atomic_exchange(lut.queue + k * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if constexpr (kWideOut) __syncthreads();
+    if constexpr (kWideOut) {
+        __syncthreads();
+        store_item_wide<QPL>(of, s_out, px - 2 * qx, py - 2 * qy, pin, H);
+    } else if constexpr (!kStoreLate) {
 #pragma unroll
-    for (int h = 0; h < QPL; h++) {
-        if constexpr (kWideOut)
-            store_tile_wide(of, s_out + h * (kTileOutBytes / 4), px, py + h * kTileH, pin, H);
-        else
+        for (int h = 0; h < QPL; h++)
             store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
     }
 #if OCTVR_STAMPS == 1
