@@ -94,6 +94,19 @@ int octvr_rig_get_input(const octvr_rig* rig, int i, octvr_input_view* view);
 int octvr_rig_num_overlays(const octvr_rig* rig, int* n);
 /* ROI, maps, mask (and vignette) of overlay i; seam_mask is NULL (overlays have none). */
 int octvr_rig_get_overlay(const octvr_rig* rig, int i, octvr_input_view* view);
+/* MapperTemplate::morph_controlpoints(control_points) (modules/octvr/src/template_morph.cpp:69-237,
+ * called by octvr_dump -c, apps/octvr/dump.cpp:98-99): control_points_json is the rig JSON's
+ * "control_points" array, [[n0, n1, x0, y0, x1, y1], ...] (n0 < n1, normalized input coordinates).
+ * Warps every input's map1 / map2 / mask piecewise-affinely (Delaunay triangles of the control
+ * points' output positions -> their distance-weighted midpoints); seam masks are left as they are.
+ * Needs a rig built by octvr_rig_create_json (camera models): OCTVR_E_UNSUPPORTED otherwise, and for
+ * fisheye / pinhole control-point cameras (no image_to_obj in the reference).  Points that the
+ * reference would index out of bounds (NaN projection, outside the camera's ROI) give
+ * OCTVR_E_INVALID.  n_used (optional): control points kept after the 0.1 distance filter. */
+int octvr_rig_morph_controlpoints(octvr_rig* rig, const char* control_points_json, int* n_used);
+/* inputs[i].src_triangles / dst_triangles (octvr.hpp:60) of the last morph: 6 floats (x0 y0 x1 y1 x2
+ * y2, normalized output coordinates) per triangle.  *n = count; src / dst may be NULL (count only). */
+int octvr_rig_get_triangles(const octvr_rig* rig, int i, float* src, float* dst, int cap, int* n);
 void octvr_rig_destroy(octvr_rig* rig);
 
 /* ---- vr::Mapper ---------------------------------------------------------------------------- */

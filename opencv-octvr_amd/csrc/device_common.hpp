@@ -113,11 +113,8 @@ struct Taps {
 
 __device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t xy, uint32_t code, Taps& t) {
     const bool valid = (code & 0x8000u) != 0;
-    const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
-    const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
-    const bool in0 = valid && sx < f.w && sy < f.h;
-    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);
-    const int x1 = inx ? sx + 1 : x0, y1 = iny ? sy + 1 : y0;
+    const TapCell tc = tap_cell(xy, f.w, f.h);
+    const int x0 = tc.x0, x1 = tc.x1, y0 = tc.y0, y1 = tc.y1;
     const int64_t p = f.pitch;
     const uint8_t* Y = f.yuv;
     const uint8_t* U = Y + (int64_t)f.h * p;
@@ -137,10 +134,10 @@ __device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t
         cc = vig_mul(cc, g1[x0]);
         cd = vig_mul(cd, g1[x1]);
     }
-    t.c[0] = in0 ? ca : 0u;
-    t.c[1] = (valid && inx && sy < f.h) ? cb : 0u;
-    t.c[2] = (valid && iny && sx < f.w) ? cc : 0u;
-    t.c[3] = (valid && inx && iny) ? cd : 0u;
+    t.c[0] = (valid && tc.ix0 && tc.iy0) ? ca : 0u;
+    t.c[1] = (valid && tc.ix1 && tc.iy0) ? cb : 0u;
+    t.c[2] = (valid && tc.ix0 && tc.iy1) ? cc : 0u;
+    t.c[3] = (valid && tc.ix1 && tc.iy1) ? cd : 0u;
     t.fx = code & 31u;
     t.fy = (code >> 5) & 31u;
 }

@@ -87,6 +87,8 @@ struct RigInput {
     std::vector<uint8_t> mask;
     std::vector<float> vignette;
     int vig_w = 0, vig_h = 0;
+    // morph_controlpoints' triangles (octvr.hpp:60 src_triangles / dst_triangles), 6 floats each
+    std::vector<float> src_tris, dst_tris;
 };
 
 struct octvr_rig {
@@ -95,11 +97,21 @@ struct octvr_rig {
     std::vector<RigInput> inputs;
     std::vector<RigInput> overlays;
     std::vector<std::vector<uint8_t>> seam_masks;
+    // camera models of a JSON-built rig (MapperTemplate::output_cam / input_cams, octvr.hpp:69-70);
+    // a rig loaded from .dat has none, like the reference's
+    bool has_cameras = false;
+    bool out_cam_masks = false;  // the output camera has exclude / include masks (not kept)
+    octvr::CameraParams out_cam{};
+    std::vector<octvr::CameraParams> cams;
 };
 
 namespace octvr {
 // MapperTemplate::create_masks() (template.cpp:155-204) — seams.cpp
 void rig_create_masks(octvr_rig& rig);
+// MapperTemplate::morph_controlpoints (template_morph.cpp:69-237) — morph.cpp; returns the number of
+// control points kept
+struct JsonValue;
+int rig_morph_controlpoints(octvr_rig& rig, const JsonValue& control_points);
 // cv::distanceTransform(src, dst, DIST_L2, 3) on the host (distransform.cpp:48-139); w x h, packed
 void chamfer_l2_3x3(const uint8_t* src, int w, int h, float* dist);
 

@@ -357,9 +357,8 @@ struct FeedRaw {
 
 __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
                                                 uint32_t code, FeedRaw& r) {
-    const int sx = (int)(xy & 0xFFFFu), sy = (int)(xy >> 16);
-    const int x0 = min(sx, f.w - 1), y0 = min(sy, f.h - 1);
-    const int y1 = sy + 1 < f.h ? sy + 1 : y0;
+    const TapCell tc = tap_cell(xy, f.w, f.h);
+    const int x0 = tc.x0, y0 = tc.y0, y1 = tc.y1;
     const uint32_t p = (uint32_t)f.pitch;
     const uint32_t uo = (uint32_t)f.h * p, vo = uo + (uint32_t)(f.w >> 1);
     const uint32_t xa = (uint32_t)x0 & ~3u, ca = ((uint32_t)x0 >> 1) & ~3u;
@@ -389,21 +388,18 @@ __device__ __forceinline__ uint32_t seg_byte(const uint2& v, uint32_t k) {
 // Same taps, validity and conversions as gather_taps_frame (device_common.hpp), without vignette.
 __device__ __forceinline__ void feed_taps_finish(const SourceFrame& f, const FeedRaw& r, Taps& t) {
     const bool valid = (r.code & 0x8000u) != 0;
-    const int sx = (int)(r.xy & 0xFFFFu), sy = (int)(r.xy >> 16);
-    const bool inx = sx + 1 < f.w, iny = sy + 1 < f.h;
-    const bool in0 = valid && sx < f.w && sy < f.h;
-    const int x0 = min(sx, f.w - 1);
-    const int x1 = inx ? sx + 1 : x0;
+    const TapCell tc = tap_cell(r.xy, f.w, f.h);
+    const int x0 = tc.x0, x1 = tc.x1;
     const uint32_t ky0 = (uint32_t)x0 & 3u, ky1 = ky0 + (uint32_t)(x1 - x0);
     const uint32_t kc0 = ((uint32_t)x0 >> 1) & 3u, kc1 = kc0 + (uint32_t)((x1 >> 1) - (x0 >> 1));
     const uint32_t ca = yuv_to_rgba(seg_byte(r.y0, ky0), seg_byte(r.u0, kc0), seg_byte(r.v0, kc0));
     const uint32_t cb = yuv_to_rgba(seg_byte(r.y0, ky1), seg_byte(r.u0, kc1), seg_byte(r.v0, kc1));
     const uint32_t cc = yuv_to_rgba(seg_byte(r.y1, ky0), seg_byte(r.u1, kc0), seg_byte(r.v1, kc0));
     const uint32_t cd = yuv_to_rgba(seg_byte(r.y1, ky1), seg_byte(r.u1, kc1), seg_byte(r.v1, kc1));
-    t.c[0] = in0 ? ca : 0u;
-    t.c[1] = (valid && inx && sy < f.h) ? cb : 0u;
-    t.c[2] = (valid && iny && sx < f.w) ? cc : 0u;
-    t.c[3] = (valid && inx && iny) ? cd : 0u;
+    t.c[0] = (valid && tc.ix0 && tc.iy0) ? ca : 0u;
+    t.c[1] = (valid && tc.ix1 && tc.iy0) ? cb : 0u;
+    t.c[2] = (valid && tc.ix0 && tc.iy1) ? cc : 0u;
+    t.c[3] = (valid && tc.ix1 && tc.iy1) ? cd : 0u;
     t.fx = r.code & 31u;
     t.fy = (r.code >> 5) & 31u;
 }
@@ -1371,6 +1367,71 @@ __global__ void __launch_bounds__(256) remap_u8_kernel(const uint8_t* src, int s
 #pragma unroll
         for (int k = 0; k < CN; k++) d[k] = (uint8_t)bilerp_ch(v[0][k], v[1][k], v[2][k], v[3][k], fx, fy);
     }
+}
+
+// ---------------------------------------------------------------------------------------------
+// morph_controlpoints' piecewise-affine LUT warp (template_morph.cpp:207-231).  The reference warps
+// the whole ROI three times per triangle and copies the triangle's fillPoly'd pixels; here each
+// pixel is computed once, by the last triangle that covers it (owner, rasterised on the host).
+// cv::warpAffine (imgwarp.cpp:5627-5745, WarpAffineInvoker :5282-5470): AB_BITS = 10 fixed-point
+// source coordinates, X = (round((M1 y + M2) 1024) + 16 + round(M0 x 1024)) >> 5, then remap's
+// INTER_LINEAR (remapBilinear :3812-4030): f32 planes with the float table ((1-fy)(1-fx), (1-fy)fx,
+// fy(1-fx), fy fx in 1/32 steps, exact), u8 with the 15-bit table; taps outside the ROI read 0.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int cv_round_sse2(double v) {  // _mm_cvtsd_si32: ties to even, out of range -> INT_MIN
+    const double r = __builtin_rint(v);
+    return (r >= -2147483648.0 && r <= 2147483647.0) ? (int)r : INT32_MIN;
+}
+
+__global__ void __launch_bounds__(256) morph_warp_kernel(const float* __restrict__ map1, const float* __restrict__ map2,
+                                                         const uint8_t* __restrict__ mask, int w, int h,
+                                                         const int16_t* __restrict__ owner, const double* __restrict__ M,
+                                                         float* out1, float* out2, uint8_t* out_mask) {
+    const int64_t total = (int64_t)w * h;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int k = owner[idx];
+        if (k < 0) {
+            out1[idx] = map1[idx];
+            out2[idx] = map2[idx];
+            out_mask[idx] = mask[idx];
+            continue;
+        }
+        const int y = (int)(idx / w), x = (int)(idx - (int64_t)y * w);
+        const double* m = M + 6 * k;
+        const int X0 = cv_round_sse2((m[1] * (double)y + m[2]) * 1024.0) + 16;  // round_delta = 1024 / 32 / 2
+        const int Y0 = cv_round_sse2((m[4] * (double)y + m[5]) * 1024.0) + 16;
+        const int ad = cv_round_sse2(m[0] * (double)x * 1024.0), bd = cv_round_sse2(m[3] * (double)x * 1024.0);
+        const int X = (int)((uint32_t)X0 + (uint32_t)ad) >> 5, Y = (int)((uint32_t)Y0 + (uint32_t)bd) >> 5;
+        const int sx = min(max(X >> 5, -32768), 32767), sy = min(max(Y >> 5, -32768), 32767);
+        const uint32_t fx = (uint32_t)(X & 31), fy = (uint32_t)(Y & 31);
+        float a1[4], a2[4];
+        uint32_t am[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            const int tx = sx + (t & 1), ty = sy + (t >> 1);
+            const bool in = tx >= 0 && tx < w && ty >= 0 && ty < h;
+            const int64_t o = in ? (int64_t)ty * w + tx : 0;
+            a1[t] = in ? map1[o] : 0.f;
+            a2[t] = in ? map2[o] : 0.f;
+            am[t] = in ? mask[o] : 0u;
+        }
+        const float vy1 = (float)fy * (1.f / 32), vy0 = 1.f - vy1, vx1 = (float)fx * (1.f / 32), vx0 = 1.f - vx1;
+        const float w0 = vy0 * vx0, w1 = vy0 * vx1, w2 = vy1 * vx0, w3 = vy1 * vx1;
+        out1[idx] = a1[0] * w0 + a1[1] * w1 + a1[2] * w2 + a1[3] * w3;
+        out2[idx] = a2[0] * w0 + a2[1] * w1 + a2[2] * w2 + a2[3] * w3;
+        out_mask[idx] = (uint8_t)bilerp_ch(am[0], am[1], am[2], am[3], fx, fy);
+    }
+}
+
+hipError_t launch_morph_warp(const float* map1, const float* map2, const uint8_t* mask, int w, int h,
+                             const int16_t* owner, const double* M, float* out1, float* out2, uint8_t* out_mask,
+                             hipStream_t s) {
+    const int64_t total = (int64_t)w * h;
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 256 * 16));
+    hipLaunchKernelGGL(morph_warp_kernel, dim3(blocks), dim3(256), 0, s, map1, map2, mask, w, h, owner, M, out1, out2,
+                       out_mask);
+    return hipGetLastError();
 }
 
 hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, int cn,

@@ -12,7 +12,7 @@ namespace octvr {
 constexpr int kMaxCams = 32;
 
 // Composite-LUT entry (8 bytes per output pixel), built once per rig by composite_lut:
-//   x = sx | sy << 16                      integer source pixel of the top-left tap
+//   x = sx | sy << 16                      integer source pixel of the top-left tap, s16 each
 //   y = fx | fy << 5 | cam << 10 | 1 << 15  5-bit fractions, winning camera, valid flag
 // An entry with the valid bit clear produces black (no camera covers the pixel).
 struct CompositeEntry {
@@ -21,19 +21,44 @@ struct CompositeEntry {
 };
 
 // Fixed-point source coordinate of a normalized map value, as RemapInvoker derives it from the
-// caller's `map * W` (template.cpp:174-176): X = fl32(m * W); ix = round_half_even(X * 32).
+// caller's `map * W` (template.cpp:174-176): X = fl32(m * W); ix = round_half_even(X * 32), NaN and
+// out-of-int-range values INT_MIN (_mm_cvtps_epi32, imgwarp.cpp:4385-4420).
 __host__ __device__ inline int quantize_coord(float m, float scale) {
     float X = m * scale;
-    return (int)rintf(X * 32.0f);
+    float f = X * 32.0f;
+    if (!(f >= -2147483648.f && f < 2147483648.f)) return INT32_MIN;
+    return (int)rintf(f);
 }
 
-// Entry for a valid map value (mask != 0 guarantees 0 <= m < 1, so 0 <= sx <= W).
+// Entry for a claimed pixel.  Template-built LUTs keep 0 <= m < 1 where the mask is set, but
+// morphed or externally made ones (.dat, from_arrays) need not: the tap cell saturates to s16 like
+// remap's (short) conversion and every tap outside the image reads 0 (BORDER_CONSTANT).
 __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w, float h, int cam) {
     int ix = quantize_coord(m1, w), iy = quantize_coord(m2, h);
+    const int sx = min(max(ix >> 5, -32768), 32767), sy = min(max(iy >> 5, -32768), 32767);
     CompositeEntry e;
-    e.xy = (uint32_t)(ix >> 5) | ((uint32_t)(iy >> 5) << 16);
+    e.xy = (uint32_t)(uint16_t)sx | ((uint32_t)(uint16_t)sy << 16);
     e.code = (uint32_t)(ix & 31) | ((uint32_t)(iy & 31) << 5) | ((uint32_t)cam << 10) | (1u << 15);
     return e;
+}
+
+// The 2 x 2 taps of an entry's cell (sx, sy) in a w x h image: clamped addresses and in-image flags.
+struct TapCell {
+    int x0, x1, y0, y1;
+    bool ix0, ix1, iy0, iy1;
+};
+__host__ __device__ inline TapCell tap_cell(uint32_t xy, int w, int h) {
+    const int sx = (int)(int16_t)(xy & 0xFFFFu), sy = (int)(int16_t)(xy >> 16);
+    TapCell c;
+    c.ix0 = (unsigned)sx < (unsigned)w;
+    c.ix1 = (unsigned)(sx + 1) < (unsigned)w;
+    c.iy0 = (unsigned)sy < (unsigned)h;
+    c.iy1 = (unsigned)(sy + 1) < (unsigned)h;
+    c.x0 = min(max(sx, 0), w - 1);
+    c.x1 = min(max(sx + 1, 0), w - 1);
+    c.y0 = min(max(sy, 0), h - 1);
+    c.y1 = min(max(sy + 1, 0), h - 1);
+    return c;
 }
 
 // ---- tiled composite (the per-frame hot path) -------------------------------------------------
@@ -244,6 +269,13 @@ hipError_t launch_block_activity(const void* weight, int is_u8, int w, int h, in
 hipError_t launch_remap_u8(const uint8_t* src, int sw, int sh, int64_t spitch, int cn, const float* map1,
                            const float* map2, int mw, int mh, int64_t mpitch, float scale_x, float scale_y,
                            uint8_t* dst, int64_t dpitch, hipStream_t s);
+
+// morph_controlpoints' warps (template_morph.cpp:207-231): pixel i of the w x h ROI takes the
+// cv::warpAffine (INTER_LINEAR, BORDER_CONSTANT 0) of map1 / map2 / mask by triangle owner[i]'s
+// matrix M[6 owner[i] ..] (already inverted as warpAffine inverts it), or is copied (owner < 0).
+hipError_t launch_morph_warp(const float* map1, const float* map2, const uint8_t* mask, int w, int h,
+                             const int16_t* owner, const double* M, float* out1, float* out2, uint8_t* out_mask,
+                             hipStream_t s);
 
 // cv::resize INTER_LINEAR, u8, one channel, with the CPU path's fixed-point rule
 // (imgwarp.cpp:1391-1500): per output column the source column and 11-bit weights, per output row

@@ -489,7 +489,6 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             for (int ty = 0; ty < L0.ty_n; ty++)
                 for (int tx = 0; tx < L0.tx_n; tx++)
                     if (req[0][i].b[(size_t)ty * L0.tx_n + tx]) jobs.push_back(TileJob{tx, ty, i});
-        std::atomic<bool> bad{false};
         const Rect arr = M.arr;
         auto entry = [&](int job, int x, int y) -> CompositeEntry {
             const int i = jobs[job].cam;
@@ -500,21 +499,13 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             const size_t k = (size_t)ry * in.roi[2] + rx;
             const float m1 = in.map1[k], m2 = in.map2[k];
             if (in.mask[k]) return make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
-            // LUT mask 0: the remap still runs there, without gain (mul_scalar_with_mask)
-            if (m1 >= 0.f && m1 < 1.f && m2 >= 0.f && m2 < 1.f) {
-                CompositeEntry e = make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
-                e.code |= kCodeNoGain;
-                return e;
-            }
-            const float X32 = m1 * (float)in_w[i] * 32.f, Y32 = m2 * (float)in_h[i] * 32.f;
-            if (X32 == X32 && Y32 == Y32 && std::fabs(X32) < 1e9f && std::fabs(Y32) < 1e9f) {
-                const int sx = (int)std::lrint(X32) >> 5, sy = (int)std::lrint(Y32) >> 5;
-                if (sx >= -1 && sx < in_w[i] && sy >= -1 && sy < in_h[i]) bad = true;
-            }
-            return CompositeEntry{0u, 0u};
+            // LUT mask 0: the remap still runs there, without gain (mul_scalar_with_mask); a template's
+            // -1 maps put every tap outside the image (black), other values follow remap's rule
+            CompositeEntry e = make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
+            e.code |= kCodeNoGain;
+            return e;
         };
         TiledLutBuild tb = build_tiled_lut(jobs, entry, in_w, in_h);
-        REQUIRE(!bad, "multi-band: a LUT-mask-0 pixel maps into the image just outside [0,1) (unsupported)");
         M.remap.upload(tb);
     }
     return mb.release();

@@ -1021,6 +1021,11 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
         rig->device = device;
         const JsonValue& ins = doc["inputs"];
         rig->inputs.resize(ins.size());
+        // the camera models stay with the rig for morph_controlpoints (its masks are not needed there)
+        rig->has_cameras = true;
+        rig->out_cam = out_cam;
+        rig->out_cam_masks = oc.has("options") && (oc["options"].has("exclude_masks") || oc["options"].has("include_masks"));
+        for (size_t i = 0; i < ins.size(); i++) rig->cams.push_back(camera_from_json(ins[i]));
         DevBuf<uint8_t> visible;  // template.cpp visible_mask, allocated once an include mask appears
         for (size_t i = 0; i < ins.size(); i++)
             build_input(out_cam, ins[i], out_w, out_h, use_roi != 0, device, rig->inputs[i], &visible, &rig->inputs);
@@ -1189,6 +1194,31 @@ int octvr_rig_get_overlay(const octvr_rig* rig, int i, octvr_input_view* v) {
         v->vignette = in.vignette.empty() ? nullptr : in.vignette.data();
         v->vignette_w = in.vig_w;
         v->vignette_h = in.vig_h;
+    });
+}
+
+int octvr_rig_morph_controlpoints(octvr_rig* rig, const char* control_points_json, int* n_used) {
+    return guarded([&] {
+        REQUIRE(rig && control_points_json, "NULL argument");
+        if (rig->has_cameras && rig->out_cam_masks)
+            throw OctvrError(OCTVR_E_UNSUPPORTED, "morph_controlpoints with output-camera masks is not implemented");
+        const JsonValue cps = json_parse(control_points_json);
+        const int k = rig_morph_controlpoints(*rig, cps);
+        if (n_used) *n_used = k;
+    });
+}
+
+int octvr_rig_get_triangles(const octvr_rig* rig, int i, float* src, float* dst, int cap, int* n) {
+    return guarded([&] {
+        REQUIRE(rig && n && i >= 0 && i < (int)rig->inputs.size(), "bad input index");
+        const RigInput& in = rig->inputs[i];
+        const int nt = (int)in.src_tris.size() / 6;
+        *n = nt;
+        if (src && dst) {
+            REQUIRE(cap >= nt, "triangle buffer too small");
+            std::copy(in.src_tris.begin(), in.src_tris.end(), src);
+            std::copy(in.dst_tris.begin(), in.dst_tris.end(), dst);
+        }
     });
 }
 

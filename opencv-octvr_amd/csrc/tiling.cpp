@@ -49,14 +49,20 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 px[k].mask = 0;
                 if (!(e.code & 0x8000u)) continue;
                 const int cam = (int)((e.code >> 10) & 31u);
-                const int sx = (int)(e.xy & 0xFFFFu), sy = (int)(e.xy >> 16);
+                const int sx = (int)(int16_t)(e.xy & 0xFFFFu), sy = (int)(int16_t)(e.xy >> 16);
                 const int iw = in_w[cam], ih = in_h[cam];
-                const bool inx = sx + 1 < iw, iny = sy + 1 < ih;
-                const int mask = ((sx < iw && sy < ih) ? 1 : 0) | ((inx && sy < ih) ? 2 : 0) |
-                                 ((iny && sx < iw) ? 4 : 0) | ((inx && iny) ? 8 : 0);
-                if (!mask) continue;
-                // mask != 0 means sx < iw and sy < ih; the +1 taps may sit on the zero column / row
-                // just past the image, which the box then includes
+                const TapCell tc = tap_cell(e.xy, iw, ih);
+                const int mask = ((tc.ix0 && tc.iy0) ? 1 : 0) | ((tc.ix1 && tc.iy0) ? 2 : 0) |
+                                 ((tc.ix0 && tc.iy1) ? 4 : 0) | ((tc.ix1 && tc.iy1) ? 8 : 0);
+                if (!mask) continue;  // every tap outside: black
+                // a cell straddling the image's left or top edge (only in morphed / external LUTs):
+                // the staged boxes start inside the image, so the tile takes the gather path
+                if (sx < 0 || sy < 0) {
+                    wide = true;
+                    continue;
+                }
+                // here sx < iw and sy < ih; the +1 taps may sit on the zero column / row just past
+                // the image, which the box then includes
                 const int x0 = sx, y0 = sy, x1 = x0 + 1, y1 = y0 + 1;
                 int sl = -1;
                 for (int j = 0; j < ns; j++)

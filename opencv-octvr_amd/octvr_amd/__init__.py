@@ -27,6 +27,10 @@ if not os.path.exists(LIB_PATH):
 _lib = C.CDLL(LIB_PATH)
 
 
+# status codes of include/octvr_hip.h
+E_INVALID, E_PARSE, E_HIP, E_UNSUPPORTED, E_IO = -1, -2, -3, -4, -5
+
+
 class OctvrError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__("octvr error %d: %s" % (code, msg))
@@ -57,6 +61,8 @@ _lib.octvr_rig_out_size.argtypes = [_VP, C.POINTER(C.c_int), C.POINTER(C.c_int)]
 _lib.octvr_rig_get_input.argtypes = [_VP, C.c_int, C.POINTER(InputView)]
 _lib.octvr_rig_num_overlays.argtypes = [_VP, C.POINTER(C.c_int)]
 _lib.octvr_rig_get_overlay.argtypes = [_VP, C.c_int, C.POINTER(InputView)]
+_lib.octvr_rig_morph_controlpoints.argtypes = [_VP, C.c_char_p, C.POINTER(C.c_int)]
+_lib.octvr_rig_get_triangles.argtypes = [_VP, C.c_int, _VP, _VP, C.c_int, C.POINTER(C.c_int)]
 _lib.octvr_rig_destroy.argtypes = [_VP]
 _lib.octvr_rig_destroy.restype = None
 _lib.octvr_mapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
@@ -146,6 +152,23 @@ class MapperTemplate:
     def create_masks(self, device=0):
         """MapperTemplate::create_masks(): L2 distance seams (resizes on `device`)."""
         _check(_lib.octvr_rig_create_masks(self._h, device))
+
+    def morph_controlpoints(self, control_points):
+        """MapperTemplate::morph_controlpoints (template_morph.cpp:69-237): control_points is the rig
+        JSON's "control_points" list of [n0, n1, x0, y0, x1, y1].  Returns the number kept."""
+        text = control_points if isinstance(control_points, str) else _json.dumps(control_points)
+        k = C.c_int()
+        _check(_lib.octvr_rig_morph_controlpoints(self._h, text.encode(), C.byref(k)))
+        return k.value
+
+    def triangles(self, i):
+        """inputs[i].src_triangles, dst_triangles of the last morph: two (n, 6) float32 arrays."""
+        n = C.c_int()
+        _check(_lib.octvr_rig_get_triangles(self._h, i, None, None, 0, C.byref(n)))
+        src = np.zeros((n.value, 6), np.float32)
+        dst = np.zeros((n.value, 6), np.float32)
+        _check(_lib.octvr_rig_get_triangles(self._h, i, src.ctypes.data, dst.ctypes.data, n.value, C.byref(n)))
+        return src, dst
 
     @property
     def out_size(self):

@@ -701,6 +701,19 @@ static void project_pixel_vis(const orc_camera* out, const orc_camera* in, doubl
     *y = py;
 }
 
+/* Camera::image_to_obj of `from` then Camera::obj_to_image of `to` (camera.cpp:212-253, 296-315), as
+ * morph_controlpoints' _translate uses it (template_morph.cpp:86-90).  Returns nonzero where the
+ * reference throws: fisheye / pinhole have no image_to_obj_single (camera.hpp:101-103), and
+ * fullframe_fisheye's asserts a crop covering the image (fullframe_fisheye_cam.cpp:224). */
+int orc_project(const orc_camera* from, const orc_camera* to, double u, double v, double* x, double* y) {
+    if (from->type == ORC_FISHEYE || from->type == ORC_PINHOLE) return 1;
+    if (from->type == ORC_FULLFRAME_FISHEYE &&
+        !(from->crop_x == 0 && from->crop_y == 0 && from->crop_w == from->width && from->crop_h == from->height))
+        return 1;
+    project_pixel(from, to, u, v, x, y);
+    return 0;
+}
+
 void orc_lut_rows(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, float* map1,
                   float* map2, uint8_t* mask) {
     for (int h = y0; h < y1; h++)

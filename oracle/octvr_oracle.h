@@ -90,6 +90,21 @@ int orc_lut_build_vis(const orc_camera* out, const orc_camera* in, int W, int H,
 /* cv::fillPoly(img, {pts}, color), lineType 8, shift 0 (octvr_oracle_masks.c) */
 void orc_fill_poly(uint8_t* img, int w, int h, const int* pts, int count, uint8_t color);
 
+/* Camera::image_to_obj of `from`, then obj_to_image of `to`; nonzero where the reference throws. */
+int orc_project(const orc_camera* from, const orc_camera* to, double u, double v, double* x, double* y);
+/* MapperTemplate::morph_controlpoints (template_morph.cpp:69-237) on ROI-sized LUT planes, in place
+ * (octvr_oracle_morph.c).  cps: n_cps x {n0, n1, x0, y0, x1, y1}; src_tris[i] / dst_tris[i] receive
+ * camera i's triangles (6 floats each, at most tri_cap), n_tris[i] their count.  Returns the number
+ * of control points kept, or < 0: -1 bad / out-of-bounds point, -2 camera without image_to_obj,
+ * -3 frame loop does not advance, -4 triangulation failure. */
+int orc_morph_controlpoints(const orc_camera* out, const orc_camera* const* cams, int n, int W, int H,
+                            const int* rois, float* const* map1, float* const* map2, uint8_t* const* masks,
+                            const double* cps, int n_cps, float* const* src_tris, float* const* dst_tris,
+                            int tri_cap, int* n_tris);
+
+/* cv::Subdiv2D(Rect(0,0,1,1)) + insert + getTriangleList, triangles with all corners in [0,1]^2. */
+int orc_delaunay_triangles(const float* pts, int n, float* out, int cap);
+
 /* The same per-pixel LUT rule for output rows [y0, y1) only (no ROI); buffers are (y1-y0) x W. */
 void orc_lut_rows(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, float* map1,
                   float* map2, uint8_t* mask);

@@ -7,7 +7,7 @@ NAME=$1; shift
 B=/tmp/octvr_variant_$NAME; mkdir -p $B "$ROOT/opencv-octvr_amd/lib/variants"
 FLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I$ROOT/include -I$ROOT/opencv-octvr_amd/csrc $*"
 OBJS=
-for f in octvr_hip.cpp async.cpp fastmapper.cpp seams.cpp tiling.cpp multiband_host.cpp masks.cpp kernels.hip multiband.hip fastmapper.hip; do
+for f in octvr_hip.cpp async.cpp fastmapper.cpp seams.cpp tiling.cpp multiband_host.cpp masks.cpp morph.cpp kernels.hip multiband.hip fastmapper.hip; do
   o=$B/${f%.*}_${f##*.}.o
   X=; [[ $f == *.hip ]] && X="-x hip"
   /opt/rocm/bin/hipcc $FLAGS $X -c "$ROOT/opencv-octvr_amd/csrc/$f" -o $o &

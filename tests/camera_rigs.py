@@ -115,3 +115,43 @@ def mask_rigs():
         ff, exclude_masks=[], include_masks=[poly(200, 40, 440, 40, 440, 320, 200, 320)], **_rot(1.0))}]
     out["overlay_include"] = ov
     return out
+
+
+# ---- morph_controlpoints (template_morph.cpp:69-237) --------------------------------------------
+def morph_rig(with_equirect=False):
+    """Three full-frame fisheyes 120 degrees apart (crop = whole image, as image_to_obj requires,
+    fullframe_fisheye_cam.cpp:224), optionally a fourth, equirectangular input."""
+    ff = {"width": 480, "height": 320, "hfov": 3.4906585, "center_dx": 1.5, "center_dy": -1.0,
+          "radial": [0.01, -0.02, 0.005]}
+    ins = [{"type": "fullframe_fisheye", "options": dict(ff, **_rot(k * 2.0943951, 0.05 * k, 0.02 * k))}
+           for k in range(3)]
+    if with_equirect:
+        ins.append({"type": "equirectangular", "options": _rot(0.7, 0.1)})
+    return {"output": {"type": "equirectangular", "options": {}}, "inputs": ins}
+
+
+def morph_points(luts, per_pair=5, seed=0, jitter=0.003):
+    """Control points [n0, n1, x0, y0, x1, y1]: output pixels seen by both cameras of a pair, camera
+    n0's point read from its map, camera n1's jittered by up to `jitter` (normalized input units)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    n = len(luts)
+    cps = []
+    for a in range(n):
+        for b in range(a + 1, n):
+            (ax, ay, aw, ah), a1, a2, am = luts[a]
+            (bx, by, bw, bh), b1, b2, bm = luts[b]
+            x0, y0 = max(ax, bx), max(ay, by)
+            x1, y1 = min(ax + aw, bx + bw), min(ay + ah, by + bh)
+            if x0 >= x1 or y0 >= y1:
+                continue
+            both = (am[y0 - ay:y1 - ay, x0 - ax:x1 - ax] > 0) & (bm[y0 - by:y1 - by, x0 - bx:x1 - bx] > 0)
+            ys, xs = np.nonzero(both)
+            if len(ys) < per_pair:
+                continue
+            for k in rng.choice(len(ys), per_pair, replace=False):
+                X, Y = xs[k] + x0, ys[k] + y0
+                j = rng.uniform(-jitter, jitter, 2)
+                cps.append([a, b, float(a1[Y - ay, X - ax]), float(a2[Y - ay, X - ax]),
+                            float(b1[Y - by, X - bx] + j[0]), float(b2[Y - by, X - bx] + j[1])])
+    return cps

@@ -243,6 +243,51 @@ def lut_build(rig, out_w, out_h, use_roi=True):
     return res
 
 
+def project(cam_from, cam_to, u, v):
+    """Camera::image_to_obj of cam_from, then obj_to_image of cam_to (JSON cameras); None where the
+    reference throws (no image_to_obj)."""
+    a, b = camera_from_json(cam_from), camera_from_json(cam_to)
+    x, y = C.c_double(), C.c_double()
+    if lib().orc_project(C.byref(a), C.byref(b), C.c_double(u), C.c_double(v), C.byref(x), C.byref(y)):
+        return None
+    return x.value, y.value
+
+
+def morph_controlpoints(rig, luts, out_w, out_h, control_points, tri_cap=4096):
+    """MapperTemplate::morph_controlpoints on lut_build()'s per-input (roi, map1, map2, mask) (inputs
+    only).  Returns (kept or negative error, new luts, [(src_tris, dst_tris)] per input)."""
+    out = camera_from_json(rig["output"])
+    cams = [camera_from_json(c) for c in rig["inputs"]]
+    n = len(cams)
+    cam_arr = (C.c_void_p * n)(*[C.addressof(c) for c in cams])
+    rois = (C.c_int * (4 * n))(*[v for (roi, _, _, _) in luts[:n] for v in roi])
+    m1 = [np.ascontiguousarray(l[1], np.float32).copy() for l in luts[:n]]
+    m2 = [np.ascontiguousarray(l[2], np.float32).copy() for l in luts[:n]]
+    mk = [np.ascontiguousarray(l[3], np.uint8).copy() for l in luts[:n]]
+    cps = np.ascontiguousarray(np.asarray(control_points, np.float64).reshape(-1, 6))
+    st = [np.zeros((tri_cap, 6), np.float32) for _ in range(n)]
+    dt = [np.zeros((tri_cap, 6), np.float32) for _ in range(n)]
+    nt = (C.c_int * n)()
+    P = lambda arrs: (C.c_void_p * n)(*[a.ctypes.data for a in arrs])
+    L = lib()
+    L.orc_morph_controlpoints.restype = C.c_int
+    rc = L.orc_morph_controlpoints(C.byref(out), cam_arr, n, out_w, out_h, rois, P(m1), P(m2), P(mk), _p(cps),
+                                   len(cps), P(st), P(dt), tri_cap, nt)
+    new = [(luts[i][0], m1[i], m2[i], mk[i]) for i in range(n)]
+    return rc, new, [(st[i][:nt[i]].copy(), dt[i][:nt[i]].copy()) for i in range(n)]
+
+
+def delaunay(points, cap=8192):
+    """cv::Subdiv2D(Rect(0,0,1,1)) + insert + getTriangleList, triangles inside [0,1]^2 kept."""
+    pts = np.ascontiguousarray(np.asarray(points, np.float32).reshape(-1))
+    out = np.zeros((cap, 6), np.float32)
+    L = lib()
+    L.orc_delaunay_triangles.restype = C.c_int
+    k = L.orc_delaunay_triangles(_p(pts), len(pts) // 2, _p(out), cap)
+    assert k >= 0, k
+    return out[:k].copy()
+
+
 def lut_rows(rig_cam_out, rig_cam_in, W, H, y0, y1):
     """Oracle LUT for output rows [y0, y1) of one input camera (full width, no ROI crop)."""
     out = camera_from_json(rig_cam_out)
