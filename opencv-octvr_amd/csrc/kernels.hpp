@@ -203,11 +203,13 @@ constexpr int kMbMaxBands = 10;
 // pyrUp source patch of one 128x8 tile: <= 8 rows (4 quad rows, the row quirk, any block phase)
 // by <= 72 columns (64 quad columns + borders), staged in LDS
 constexpr int kUpPatchRows = 8, kUpPatchCols = 72;
-struct UpQuad {          // one quad row (or column) of a pyrUp output
+struct alignas(16) UpQuad {  // one quad row (or column) of a pyrUp output; 16 B: one load per lane
     uint16_t idx[3];      // source rows (cols) of the 3 union taps, clamped, local to the coarser level
+    uint16_t pad0;
     uint8_t w0[3], w1[3]; // integer weights of the quad's first / second row (col) over them
+    uint8_t pad1[2];
 };
-static_assert(sizeof(UpQuad) == 12, "UpQuad layout");
+static_assert(sizeof(UpQuad) == 16, "UpQuad layout");
 
 struct MbCamLevel {       // one camera at one level
     uint32_t g_off;        // byte offset of the camera's G in the level's pyramid allocation

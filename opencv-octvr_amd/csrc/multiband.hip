@@ -137,7 +137,31 @@ struct Up9 {
 };
 
 // pyrUp sums of a quad from a staged LDS patch (rows r0.., cols c0.. of the coarser level):
-// 3 x 3 union taps, per-pixel integer weights over them (UpQuad).
+// 3 x 3 union taps, per-pixel integer weights over them (UpQuad).  The 1-D weights of a quad row /
+// column sum to 8 (1 6 1 or 4 4), so with s16 sources every product and partial sum fits 24 bits:
+// 24-bit multiplies (full rate; a 32-bit v_mul_lo is quarter rate).
+__device__ __forceinline__ void up_weigh(const UpQuad& ur, const UpQuad& uc, const int (&v)[3][3][3], Up9& o) {
+#pragma unroll
+    for (int pc = 0; pc < 2; pc++) {
+        const uint8_t* wx = pc ? uc.w1 : uc.w0;
+        int h[3][3];  // [row][ch]
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++)
+                h[j][ch] = __mul24((int)wx[0], v[j][0][ch]) + __mul24((int)wx[1], v[j][1][ch]) +
+                           __mul24((int)wx[2], v[j][2][ch]);
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++) {
+            const uint8_t* wy = pr ? ur.w1 : ur.w0;
+#pragma unroll
+            for (int ch = 0; ch < 3; ch++)
+                o.s[pr * 2 + pc][ch] = __mul24((int)wy[0], h[0][ch]) + __mul24((int)wy[1], h[1][ch]) +
+                                       __mul24((int)wy[2], h[2][ch]);
+        }
+    }
+}
+
 template <class T, class UNPACK>
 __device__ __forceinline__ void up_quad_lds(const UpQuad& ur, const UpQuad& uc, int r0, int c0, const T* patch,
                                             UNPACK unpack, Up9& o) {
@@ -151,21 +175,38 @@ __device__ __forceinline__ void up_quad_lds(const UpQuad& ur, const UpQuad& uc, 
             unpack(patch[pr * kUpPatchCols + pc], v[j][k]);
         }
     }
+    up_weigh(ur, uc, v, o);
+}
+
+// The 3 x 3 taps of a quad straight from global memory (the table's indices are clamped into the
+// source; neighbouring lanes share the lines, so these are mostly L1 / L2 hits): no LDS staging and
+// no barriers.
+__device__ __forceinline__ UpQuad load_up(const UpQuad* t, int i) {
+    return __builtin_bit_cast(UpQuad, *reinterpret_cast<const uint4*>(t + i));
+}
+template <class T>
+struct Taps9 {
+    T t[3][3];
+};
+template <class T>
+__device__ __forceinline__ void up_taps_issue(const UpQuad& ur, const UpQuad& uc, const uint8_t* base, int64_t pitch,
+                                              Taps9<T>& o) {
 #pragma unroll
-    for (int pc = 0; pc < 2; pc++) {
-        const uint8_t* wx = pc ? uc.w1 : uc.w0;
-        int h[3][3];  // [row][ch]
+    for (int j = 0; j < 3; j++) {
+        const uint8_t* row = base + (int64_t)ur.idx[j] * pitch;
 #pragma unroll
-        for (int j = 0; j < 3; j++)
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) h[j][ch] = wx[0] * v[j][0][ch] + wx[1] * v[j][1][ch] + wx[2] * v[j][2][ch];
-#pragma unroll
-        for (int pr = 0; pr < 2; pr++) {
-            const uint8_t* wy = pr ? ur.w1 : ur.w0;
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) o.s[pr * 2 + pc][ch] = wy[0] * h[0][ch] + wy[1] * h[1][ch] + wy[2] * h[2][ch];
-        }
+        for (int k = 0; k < 3; k++) o.t[j][k] = *reinterpret_cast<const T*>(row + (int64_t)uc.idx[k] * sizeof(T));
     }
+}
+template <class T, class UNPACK>
+__device__ __forceinline__ void up_quad_taps(const UpQuad& ur, const UpQuad& uc, const Taps9<T>& tp, UNPACK unpack,
+                                             Up9& o) {
+    int v[3][3][3];
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int k = 0; k < 3; k++) unpack(tp.t[j][k], v[j][k]);
+    up_weigh(ur, uc, v, o);
 }
 
 // Cooperative load of an 8 x 72 patch (rows r0.., cols c0.., clamped to the source) into registers:
@@ -194,17 +235,28 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
     }
 }
 
+#ifndef MB_PAIR_LOADS  // one 8-byte load per quad row for G and the weights
+#define MB_PAIR_LOADS 1
+#endif
+#ifndef MB_DIRECT_TAPS  // pyrUp taps read per lane from global memory instead of LDS-staged patches
+#define MB_DIRECT_TAPS 1
+#endif
+
 __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
+#if !MB_DIRECT_TAPS
     __shared__ uint2 s_r[kPatchN];     // collapsed coarser level (s16x4)
     __shared__ uint32_t s_g[kPatchN];  // the current camera's coarser Gaussian level (u8x4)
+#endif
     const int tid = threadIdx.x;
     const int tile = blockIdx.x;
     const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-    const int x = tx * kTileW + 2 * (tid & 63), y = ty * kTileH + 2 * (tid >> 6);  // quad origin (even)
+    const int wv = uniform(tid >> 6);                                         // quad row of the wave
+    const int x = tx * kTileW + 2 * (tid & 63), y = ty * kTileH + 2 * wv;  // quad origin (even)
     const bool top = a.level == a.bands;
     bool valid[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) valid[p] = (x + (p & 1)) < a.W && (y + (p >> 1)) < a.H;
+#if !MB_DIRECT_TAPS
     // the collapse patch first: its loads overlap the camera loop
     PatchRegs<uint2> rp;
     int rr0 = 0, rc0 = 0;
@@ -214,6 +266,7 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
         patch_issue<uint2>(reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, a.H_next, a.W_next, rr0,
                            rc0, rp);
     }
+#endif
     int D[4][3];
     float wsum[4];
 #pragma unroll
@@ -228,9 +281,52 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
         m &= m - 1;
         const MbCamLevel c = a.cams[n];
         const int xl = x - c.ox, yl = y - c.oy;  // camera-local quad origin (any parity)
-        // all of this camera's loads at once: weights, G, and the coarser-level patch
+        // all of this camera's loads at once: weights, G, and the coarser level's taps
         float w[4];
         uint32_t gv[4];
+#if MB_PAIR_LOADS
+        if (c.w >= 2) {
+            // per quad row one 8-byte load of G and of the weights at the clamped pair start x0:
+            // pixel px is element px - x0 (0 or 1 whenever it lies inside the camera)
+            const int x0 = min(max(xl, 0), c.w - 2);
+            // u8 level-0 weights: an 8-byte buffer load from the dword at or below the pair (dword loads
+            // ignore the low address bits, so the resource starts at the dword below the weights and
+            // reads past the end return 0)
+            const uint32_t dlt = (uint32_t)(reinterpret_cast<uintptr_t>(c.weight) & 3u);
+            const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t*>(static_cast<const uint8_t*>(c.weight) - dlt), 0,
+                (int)(c.w * c.h + dlt), 0x00020000);
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const int py = yl + r, cy = min(max(py, 0), c.h - 1);
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                const uint2 gp = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + x0 * 4);
+                float wp[2];
+                if (a.w_u8) {
+                    const uint32_t at = dlt + (uint32_t)(cy * c.w + x0), a4 = at & ~3u;
+                    const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(wr, a4, 0, 0);
+                    const uint64_t q = ((uint64_t)t.y << 32) | t.x;
+                    const uint32_t sh = 8u * (at - a4);
+                    // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
+                    wp[0] = (float)(1. / 255) * (float)(uint32_t)((q >> sh) & 255u);
+                    wp[1] = (float)(1. / 255) * (float)(uint32_t)((q >> (sh + 8u)) & 255u);
+                } else {  // f32 levels: in-bounds 8-byte load at the pair start
+                    const float2 t = *reinterpret_cast<const float2*>(static_cast<const float*>(c.weight) +
+                                                                      (int64_t)cy * c.w + x0);
+                    wp[0] = t.x;
+                    wp[1] = t.y;
+                }
+#pragma unroll
+                for (int pc = 0; pc < 2; pc++) {
+                    const int p = 2 * r + pc, px = xl + pc;
+                    const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
+                    const bool hi = ((px - x0) & 1) != 0;
+                    w[p] = in ? (hi ? wp[1] : wp[0]) : 0.f;
+                    gv[p] = hi ? gp.y : gp.x;
+                }
+            }
+        } else
+#endif
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const int px = xl + (p & 1), py = yl + (p >> 1);
@@ -238,39 +334,43 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
             const int cx = min(max(px, 0), c.w - 1), cy = min(max(py, 0), c.h - 1);
             const int64_t k = (int64_t)cy * c.w + cx;
             // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
-            const float wv = a.w_u8 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
-                                    : static_cast<const float*>(c.weight)[k];
-            w[p] = in ? wv : 0.f;
+            const float wv_ = a.w_u8 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
+                                     : static_cast<const float*>(c.weight)[k];
+            w[p] = in ? wv_ : 0.f;
             gv[p] = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + cx * 4);
         }
-        PatchRegs<uint32_t> gp;
-        int gr0 = 0, gc0 = 0;
+        int g[4][3];
         if (!top) {
             const MbCamLevel cn = a.cams_next[n];
-            gr0 = c.up_r0[ty];
-            gc0 = c.up_c0[tx];
+            Up9 u;
+            auto unpack = [](uint32_t v, int (&o)[3]) {
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
+            };
+#if MB_DIRECT_TAPS
+            const UpQuad ur = c.up_rows[y >> 1], uc = load_up(c.up_cols, x >> 1);
+            Taps9<uint32_t> tp;
+            up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
+            up_quad_taps(ur, uc, tp, unpack, u);
+#else
+            PatchRegs<uint32_t> gp;
+            const int gr0 = c.up_r0[ty], gc0 = c.up_c0[tx];
             patch_issue<uint32_t>(a.g_next + cn.g_off, cn.g_pitch, cn.h, cn.w, gr0, gc0, gp);
             __syncthreads();  // the previous camera's patch readers are done
             patch_store(gp, s_g);
             __syncthreads();
-        }
-        int g[4][3];
-#pragma unroll
-        for (int p = 0; p < 4; p++)
-#pragma unroll
-            for (int ch = 0; ch < 3; ch++) g[p][ch] = (int)ch_of(gv[p], ch);
-        if (!top) {
-            Up9 u;
-            up_quad_lds(c.up_rows[y >> 1], c.up_cols[x >> 1], gr0, gc0, s_g,
-                        [](uint32_t v, int (&o)[3]) {
-#pragma unroll
-                            for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
-                        },
-                        u);
+            up_quad_lds(c.up_rows[y >> 1], c.up_cols[x >> 1], gr0, gc0, s_g, unpack, u);
+#endif
 #pragma unroll
             for (int p = 0; p < 4; p++)
 #pragma unroll
-                for (int ch = 0; ch < 3; ch++) g[p][ch] -= min(max(rne_shr<6>(u.s[p][ch]), 0), 255);  // sat u8
+                for (int ch = 0; ch < 3; ch++)
+                    g[p][ch] = (int)ch_of(gv[p], ch) - min(max(rne_shr<6>(u.s[p][ch]), 0), 255);  // sat u8
+        } else {
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) g[p][ch] = (int)ch_of(gv[p], ch);
         }
 #pragma unroll
         for (int p = 0; p < 4; p++) {
@@ -294,16 +394,22 @@ __global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
             R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf((float)D[p][ch] * rcp), -32768.f, 32767.f);
     }
     if (!top) {
+        Up9 u;
+        auto unpack = [](uint2 v, int (&o)[3]) {
+            o[0] = (int)(int16_t)(v.x & 0xFFFFu);
+            o[1] = (int)(int16_t)(v.x >> 16);
+            o[2] = (int)(int16_t)(v.y & 0xFFFFu);
+        };
+#if MB_DIRECT_TAPS
+        const UpQuad ur = a.rup_rows[y >> 1], uc = load_up(a.rup_cols, x >> 1);
+        Taps9<uint2> tp;
+        up_taps_issue<uint2>(ur, uc, reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, tp);
+        up_quad_taps(ur, uc, tp, unpack, u);
+#else
         patch_store(rp, s_r);
         __syncthreads();
-        Up9 u;
-        up_quad_lds(a.rup_rows[y >> 1], a.rup_cols[x >> 1], rr0, rc0, s_r,
-                    [](uint2 v, int (&o)[3]) {
-                        o[0] = (int)(int16_t)(v.x & 0xFFFFu);
-                        o[1] = (int)(int16_t)(v.x >> 16);
-                        o[2] = (int)(int16_t)(v.y & 0xFFFFu);
-                    },
-                    u);
+        up_quad_lds(a.rup_rows[y >> 1], a.rup_cols[x >> 1], rr0, rc0, s_r, unpack, u);
+#endif
 #pragma unroll
         for (int p = 0; p < 4; p++)
 #pragma unroll

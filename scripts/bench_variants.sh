@@ -8,7 +8,7 @@ run() {
   python3 -c "import json; d=json.loads(open('gpurun_out/var_$1.log').read().strip().splitlines()[-1]); print('$1', d['value'], d['roofline']['kernel_us'])"
 }
 run default
-for f in opencv-octvr_amd/lib/variants/*.so; do
+for f in $(ls opencv-octvr_amd/lib/variants/*.so 2>/dev/null); do
   v=$(basename $f .so)
   OCTVR_HIP_LIB=$PWD/$f run $v
 done
