@@ -484,11 +484,17 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     // ---- level-0 remap jobs (camera, required tile) -------------------------------------------
     {
         auto& L0 = M.lv[0];
+        // items of qpl vertically adjacent tiles (128 x 8 qpl), kept when any of them is required
+        const int qpl = composite_qpl();
         std::vector<TileJob> jobs;
         for (int i = 0; i < n; i++)
-            for (int ty = 0; ty < L0.ty_n; ty++)
-                for (int tx = 0; tx < L0.tx_n; tx++)
-                    if (req[0][i].b[(size_t)ty * L0.tx_n + tx]) jobs.push_back(TileJob{tx, ty, i});
+            for (int ty = 0; ty < (L0.ty_n + qpl - 1) / qpl; ty++)
+                for (int tx = 0; tx < L0.tx_n; tx++) {
+                    bool any = false;
+                    for (int h = 0; h < qpl && ty * qpl + h < L0.ty_n; h++)
+                        any |= req[0][i].b[(size_t)(ty * qpl + h) * L0.tx_n + tx] != 0;
+                    if (any) jobs.push_back(TileJob{tx, ty, i});
+                }
         const Rect arr = M.arr;
         auto entry = [&](int job, int x, int y) -> CompositeEntry {
             const int i = jobs[job].cam;
@@ -505,7 +511,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             e.code |= kCodeNoGain;
             return e;
         };
-        TiledLutBuild tb = build_tiled_lut(jobs, entry, in_w, in_h);
+        TiledLutBuild tb = build_tiled_lut(jobs, entry, in_w, in_h, qpl);
         M.remap.upload(tb);
     }
     return mb.release();
@@ -578,7 +584,7 @@ double multiband_traffic(const MultiBand& M) {
     // (camera, pixel) of every weight tile G + weight + 9/4 coarser taps, R reads/writes, output
     const auto& L0 = M.lv[0];
     const TiledLut& t = M.remap.view;
-    double b = (4.0 + 4.0) * t.n_items * kTilePx + (8.0 + 4.0) * t.n_wide * kTilePx;
+    double b = (4.0 + 4.0) * t.n_items * kTilePx * t.qpl + (8.0 + 4.0) * t.n_wide * kTilePx;
     for (int l = 1; l <= M.B; l++) b += (double)M.lv[l].n_down * kTilePx * (16.0 + 4.0);
     for (int l = 0; l <= M.B; l++) {
         const auto& L = M.lv[l];
