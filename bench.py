@@ -34,6 +34,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: independent frame sets stitched round-robin on this many streams "
+                         "(octvr_mapper_set_frames_in_flight; blend 0 at template size only, else 1)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -103,20 +106,31 @@ def main():
     if blend > 0:
         mt.create_masks(dev)  # MapperTemplate::create_masks (DistanceSeamFinder), as octvr_dump does
     m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, device=dev)
-    # each rank stitches an independent rig instance: frames seeded by (rank, camera)
+    # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
+    # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
+    inflight = max(1, args.inflight) if blend == 0 else 1
+    m.set_frames_in_flight(inflight)
+    # each rank stitches an independent rig instance: frames seeded by (rank, in-flight slot, camera)
     frames_np = [synthetic.yuv_frame(w, h, 1000 * (rank + 1) + i) for i, (w, h) in enumerate(sizes)]
-    frames = [torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]
-    out = torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}")
-    stream = torch.cuda.current_stream(dev)
+    frame_sets = [[torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]]
+    for j in range(1, inflight):
+        frame_sets.append([torch.from_numpy(synthetic.yuv_frame(w, h, 1000 * (rank + 1) + 100 * j + i)).to(f"cuda:{dev}")
+                           for i, (w, h) in enumerate(sizes)])
+    outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+
+    def step(k):
+        j = k % inflight
+        m.stitch(frame_sets[j], outs[j], stream=streams[j])
 
     if args.pmc_child:  # a few launches for rocprofv3 --pmc passes
-        for _ in range(max(args.steps, 1)):
-            m.stitch(frames, out, stream=stream)
+        for k in range(max(args.steps, 1)):
+            step(k)
         torch.cuda.synchronize(dev)
         return
 
-    for _ in range(args.warmup):
-        m.stitch(frames, out, stream=stream)
+    for k in range(args.warmup):
+        step(k)
     torch.cuda.synchronize(dev)
     m.kernel_time()  # drop anything recorded before the timed region
     # HIP events around the stitch kernel of every 4th step (each event pair costs ~5 us of GPU
@@ -126,8 +140,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m.stitch(frames, out, stream=stream)
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize(dev)
     if dist:
         dist.barrier()
@@ -182,7 +196,7 @@ def main():
                                    args.config, len(sizes), sizes[0][0], sizes[0][1], W, H,
                                    "multi-band blend=%d (%d bands)" % (blend, int(math.ceil(math.log(blend) / math.log(2.)) - 1))
                                    if blend > 0 else "no-blend composite"),
-                   "rigs_per_gpu": 1, "parallelism": "independent rig per GPU"},
+                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
                      "kernel": "multiband sequence (remap, pyrDown, blend levels)" if blend > 0 else "stitch_kernel",

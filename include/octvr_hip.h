@@ -125,6 +125,14 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* mapper, const uint8_t* const* in_d
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream);
 /* Mapper::gains() (mapper.hpp:445-447): gains used by the last stitch (synchronizes the stream). */
 int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
+/* Frames in flight (no reference counterpart: vr::Mapper is not re-entrant, and AsyncMultiMapper
+ * serialises its stitches on one compute stream, async.cpp:78-92).  k slots of per-frame device state
+ * (gains, gain-feed totals, composite work queue); consecutive stitches take the slots in turn, so
+ * stitches issued on different streams overlap (frame k+1's gain feed under frame k's composite).
+ * A stitch waits only for its slot's previous stitch when that one was issued on another stream.
+ * k > 1 needs blend == 0 and no scaled output (OCTVR_E_UNSUPPORTED otherwise).  Synchronizes. */
+#define OCTVR_MAX_FRAMES_IN_FLIGHT 4
+int octvr_mapper_set_frames_in_flight(octvr_mapper* mapper, int k);
 /* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 4 B tiled
  * LUT entry (8 B in wide tiles) + 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each
  * source frame read once) + the per-item headers (multi-band / feather: the whole blend sequence). */

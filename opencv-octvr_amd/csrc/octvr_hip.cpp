@@ -677,13 +677,33 @@ struct octvr_mapper {
     bool scaled = false;
     DevBuf<uint8_t> result;
     DevBuf<MbCamLevel> result_view;  // the result frame as a one-entry RGBA sink of the composite
-    hipStream_t last_stream = nullptr;
-    hipEvent_t order_ev = nullptr;  // orders a stitch on a new stream after the previous one
+    // Per-frame device state that consecutive stitches would otherwise share: the gains, the feed's
+    // pair totals and tickets, the composite's work queue.  Slot 0 is the buffers above;
+    // octvr_mapper_set_frames_in_flight adds slots so that stitches issued on different streams overlap
+    // (frame k+1's gain feed runs under frame k's composite).  A stitch takes the next slot in turn and
+    // waits only for that slot's previous stitch when it was issued on another stream.
+    struct FrameSlot {
+        double* gains = nullptr;
+        unsigned long long* totals = nullptr;
+        uint32_t* tickets = nullptr;
+        uint32_t* queue = nullptr;
+        hipStream_t stream = nullptr;
+        hipEvent_t done = nullptr;  // recorded after the slot's last stitch (the stream may since be gone)
+    };
+    struct SlotBufs {
+        DevBuf<double> gains;
+        DevBuf<unsigned long long> totals;
+        DevBuf<uint32_t> tickets, queue;
+    };
+    std::vector<FrameSlot> slots;
+    std::vector<std::unique_ptr<SlotBufs>> slot_bufs;  // owners of slots 1..k-1
+    int cur_slot = 0;                                  // slot of the last stitch
     int timing = 0;             // event-timing period in stitches (0 = off)
     uint64_t timed_calls = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events, free_events;  // recorded / reusable
     ~octvr_mapper() {
-        if (order_ev) (void)hipEventDestroy(order_ev);
+        for (auto& sl : slots)
+            if (sl.done) (void)hipEventDestroy(sl.done);
         for (auto* v : {&events, &free_events})
             for (auto& e : *v) {
                 (void)hipEventDestroy(e.first);
@@ -876,22 +896,24 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                     "input frame larger than 2 GiB");
             fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
         }
-        // consecutive stitches share the mapper's device state (gains, feed totals, work counters):
-        // a stitch on another stream waits for the previous one (vr::Mapper is not re-entrant either)
-        // (order_ev is recorded after every stitch, so the previous stream may since have been destroyed)
-        if (m->order_ev && m->last_stream != s) HIP_CHECK(hipStreamWaitEvent(s, m->order_ev, 0));
+        // stitches sharing a frame slot (gains, feed totals, work counters) are ordered: one on another
+        // stream waits for the slot's previous stitch (with one slot: for the previous stitch, as
+        // vr::Mapper is not re-entrant either)
+        const int k = (m->cur_slot + 1) % (int)m->slots.size();
+        octvr_mapper::FrameSlot& sl = m->slots[k];
+        if (sl.done && sl.stream != s) HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
         if (m->use_gain) {
             if (gains_dev) {
-                HIP_CHECK(hipMemcpyAsync(m->gains.p, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
+                HIP_CHECK(hipMemcpyAsync(sl.gains, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
             } else if (gains) {
                 REQUIRE(n_gains == m->n, "gains must have one entry per input");
-                HIP_CHECK(launch_set_gains(gains, m->n, m->gains.p, s));
+                HIP_CHECK(launch_set_gains(gains, m->n, sl.gains, s));
             } else if (m->n_chunks == 0) {  // no intersections: A = diag(b), every gain is 1
                 const std::vector<double> ones(m->n, 1.0);
-                HIP_CHECK(launch_set_gains(ones.data(), m->n, m->gains.p, s));
+                HIP_CHECK(launch_set_gains(ones.data(), m->n, sl.gains, s));
             } else {
                 HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n,
-                                           m->totals.p, m->tickets.p, m->gains.p, s));
+                                           sl.totals, sl.tickets, sl.gains, s));
             }
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -909,31 +931,35 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         }
         if (m->scaled) {
             // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
+            // (one frame slot only: the result frame and the multi-band state are shared)
             if (m->mb)
-                multiband_run(*m->mb, fs, m->gains.p, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
+                multiband_run(*m->mb, fs, sl.gains, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
             else
-                HIP_CHECK(launch_mb_remap(fs, m->tiles.view, m->gains.p, m->use_gain,
+                HIP_CHECK(launch_mb_remap(fs, m->tiles.view, sl.gains, m->use_gain,
                                           RgbaOut{m->result.p, (uint32_t)m->result.n, m->result_view.p}, s));
             HIP_CHECK(launch_resize_rgba_yuv420(m->result.p, m->W, m->H, (int64_t)m->W * 4, out_dev, m->SW, m->SH,
                                                 (int64_t)out_pitch, s));
         } else if (m->mb) {
-            multiband_run(*m->mb, fs, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s);
+            multiband_run(*m->mb, fs, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s);
         } else {
-            HIP_CHECK(launch_stitch(fs, m->tiles.view, m->W, m->H, m->gains.p, m->use_gain, out_dev, (int64_t)out_pitch, s));
+            TiledLut view = m->tiles.view;
+            view.queue = sl.queue;
+            HIP_CHECK(launch_stitch(fs, view, m->W, m->H, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s));
         }
         if (timed) {
             HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
         }
-        if (!m->order_ev) HIP_CHECK(hipEventCreateWithFlags(&m->order_ev, hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(m->order_ev, s));
-        m->last_stream = s;
+        if (!sl.done) HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(sl.done, s));
+        sl.stream = s;
+        m->cur_slot = k;
     }
 }
 
 int mapper_num_inputs(const octvr_mapper* m) { return m->n; }
 bool mapper_has_gain(const octvr_mapper* m) { return m->use_gain != 0; }
-const double* mapper_gains_dev(const octvr_mapper* m) { return m->gains.p; }
+const double* mapper_gains_dev(const octvr_mapper* m) { return m->slots[m->cur_slot].gains; }
 void mapper_out_size(const octvr_mapper* m, int* w, int* h) {
     *w = m->SW;
     *h = m->SH;
@@ -1328,6 +1354,12 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         HIP_CHECK(hipMemcpy(m->gains.p, ones.data(), kMaxCams * sizeof(double), hipMemcpyHostToDevice));
         m->last_gains.assign(m->n, 1.0);
         if (m->use_gain) setup_gain(*m, *rig);
+        octvr_mapper::FrameSlot s0;
+        s0.gains = m->gains.p;
+        s0.totals = m->totals.p;
+        s0.tickets = m->tickets.p;
+        s0.queue = m->tiles.view.queue;
+        m->slots.push_back(s0);
         *out = m.release();
     });
 }
@@ -1347,8 +1379,53 @@ int octvr_mapper_gains(octvr_mapper* m, double* g, int n) {
             for (int i = 0; i < n; i++) g[i] = 1.0;
             return;
         }
-        HIP_CHECK(hipStreamSynchronize(m->last_stream));
-        HIP_CHECK(hipMemcpy(g, m->gains.p, m->n * sizeof(double), hipMemcpyDeviceToHost));
+        const octvr_mapper::FrameSlot& sl = m->slots[m->cur_slot];
+        if (sl.done) HIP_CHECK(hipEventSynchronize(sl.done));
+        HIP_CHECK(hipMemcpy(g, sl.gains, m->n * sizeof(double), hipMemcpyDeviceToHost));
+    });
+}
+
+int octvr_mapper_set_frames_in_flight(octvr_mapper* m, int k) {
+    return guarded([&] {
+        REQUIRE(m && k >= 1 && k <= OCTVR_MAX_FRAMES_IN_FLIGHT, "frames in flight must be 1..OCTVR_MAX_FRAMES_IN_FLIGHT");
+        if (k > 1 && (m->mb || m->scaled))
+            throw OctvrError(OCTVR_E_UNSUPPORTED,
+                             "frames in flight > 1 need the no-blend composite at template size (blend = 0, no scaled output)");
+        DeviceGuard dg(m->device);
+        for (auto& sl : m->slots)
+            if (sl.done) HIP_CHECK(hipEventSynchronize(sl.done));
+        if (m->cur_slot != 0) {  // keep the last frame's gains for gains() / chaining
+            HIP_CHECK(hipMemcpy(m->slots[0].gains, m->slots[m->cur_slot].gains, sizeof(double) * m->n,
+                                hipMemcpyDeviceToDevice));
+            m->cur_slot = 0;
+        }
+        for (size_t i = 1; i < m->slots.size(); i++)
+            if (m->slots[i].done) (void)hipEventDestroy(m->slots[i].done);
+        m->slots.resize(1);
+        m->slot_bufs.clear();
+        std::vector<double> ones(kMaxCams, 1.0);
+        for (int i = 1; i < k; i++) {
+            auto b = std::make_unique<octvr_mapper::SlotBufs>();
+            b->gains.upload(ones.data(), ones.size());
+            if (m->totals.p) {
+                b->totals.alloc(m->totals.n);
+                HIP_CHECK(hipMemset(b->totals.p, 0, b->totals.n * sizeof(unsigned long long)));
+            }
+            if (m->tickets.p) {
+                b->tickets.alloc(m->tickets.n);
+                HIP_CHECK(hipMemset(b->tickets.p, 0, b->tickets.n * sizeof(uint32_t)));
+            }
+            b->queue.alloc(m->tiles.queue.n);
+            HIP_CHECK(hipMemset(b->queue.p, 0, b->queue.n * sizeof(uint32_t)));
+            octvr_mapper::FrameSlot sl;
+            sl.gains = b->gains.p;
+            sl.totals = b->totals.p;
+            sl.tickets = b->tickets.p;
+            sl.queue = b->queue.p;
+            m->slots.push_back(sl);
+            m->slot_bufs.push_back(std::move(b));
+        }
+        HIP_CHECK(hipDeviceSynchronize());  // the memsets complete before any stream uses the slots
     });
 }
 

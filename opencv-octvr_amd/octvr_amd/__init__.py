@@ -70,6 +70,7 @@ _lib.octvr_mapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), 
 _lib.octvr_mapper_stitch_yuv420p.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t,
                                              C.POINTER(C.c_double), C.c_int, _VP]
 _lib.octvr_mapper_gains.argtypes = [_VP, C.POINTER(C.c_double), C.c_int]
+_lib.octvr_mapper_set_frames_in_flight.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
 _lib.octvr_mapper_set_timing.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int)]
@@ -262,6 +263,11 @@ class Mapper:
         g = (C.c_double * self.n)()
         _check(_lib.octvr_mapper_gains(self._h, g, self.n))
         return list(g)
+
+    def set_frames_in_flight(self, k):
+        """k slots of per-frame device state: stitches issued on different streams overlap
+        (octvr_mapper_set_frames_in_flight; blend == 0 at template size only)."""
+        _check(_lib.octvr_mapper_set_frames_in_flight(self._h, int(k)))
 
     def traffic_bytes(self):
         b = C.c_double()
