@@ -838,6 +838,11 @@ __device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& 
     for (int h = 0; h < Q; h++) {
 #if OCTVR_DIAG_HOTENT  // diagnostic: every item reads item 0's entries (L2-resident)
         d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + (int64_t)h * kTilePx)[tid];
+#elif OCTVR_ENT_NT  // entries stream once: non-temporal loads (keep the source boxes in L2)
+        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+        const u32x4_t v = __builtin_nontemporal_load(
+            reinterpret_cast<const u32x4_t*>(lut.entries + ((int64_t)(live ? m.t : 0) * Q + h) * kTilePx) + tid);
+        d.e4[h] = uint4{v.x, v.y, v.z, v.w};
 #else
         d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + ((int64_t)(live ? m.t : 0) * Q + h) * kTilePx)[tid];
 #endif
