@@ -242,7 +242,10 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
 #define MB_DIRECT_TAPS 1
 #endif
 
-__global__ void __launch_bounds__(256) mb_blend_kernel(MbBlendArgs a) {
+#ifndef MB_BLEND_WAVES  // waves per SIMD the blend is compiled for (register budget)
+#define MB_BLEND_WAVES 7
+#endif
+__global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendArgs a) {
 #if !MB_DIRECT_TAPS
     __shared__ uint2 s_r[kPatchN];     // collapsed coarser level (s16x4)
     __shared__ uint32_t s_g[kPatchN];  // the current camera's coarser Gaussian level (u8x4)
