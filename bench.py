@@ -36,7 +36,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight: independent frame sets stitched round-robin on this many streams "
-                         "(octvr_mapper_set_frames_in_flight; blend 0 at template size only, else 1)")
+                         "(octvr_mapper_set_frames_in_flight)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -108,7 +108,7 @@ def main():
     m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, device=dev)
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
-    inflight = max(1, args.inflight) if blend == 0 else 1
+    inflight = max(1, args.inflight)
     m.set_frames_in_flight(inflight)
     # each rank stitches an independent rig instance: frames seeded by (rank, in-flight slot, camera)
     frames_np = [synthetic.yuv_frame(w, h, 1000 * (rank + 1) + i) for i, (w, h) in enumerate(sizes)]
@@ -148,6 +148,17 @@ def main():
     elapsed = time.perf_counter() - t0
     m.set_timing(False)
     kern_ms, launches = m.kernel_time()
+    serial = None
+    if inflight > 1 and not dist:
+        # supplementary, after the timed region: the composite kernel's duration with one frame in
+        # flight (with two, the events on a stream also span the other stream's kernels)
+        m.set_timing(1)
+        for k in range(8):
+            m.stitch(frame_sets[0], outs[0], stream=streams[0])
+        torch.cuda.synchronize(dev)
+        s_ms, s_n = m.kernel_time()
+        m.set_timing(False)
+        serial = s_ms / 1e3 / max(s_n, 1)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -203,8 +214,14 @@ def main():
                      "kernel_us": round(avg_kernel_s * 1e6, 2),
                      "bytes_per_launch": bytes_per_launch,
                      "survey_b_alg_bytes": survey_b_alg,
-                     "survey_b_alg_frac_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
+                     "survey_b_alg_frac_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "frac_at_step_time": round(bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
         "gains": [round(g, 6) for g in gains],
+        **({"roofline_one_in_flight": {"kernel_us": round(serial * 1e6, 2),
+                                        "achieved": round(bytes_per_launch / serial / 1e9, 1),
+                                        "frac": round(bytes_per_launch / serial / 1e9 / HBM_PEAK_GBPS, 4),
+                                        "note": "8 stitches after the timed region, one frame in flight"}}
+           if serial else {}),
         "mapper": m.info(),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

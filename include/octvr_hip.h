@@ -130,7 +130,8 @@ int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
  * (gains, gain-feed totals, composite work queue); consecutive stitches take the slots in turn, so
  * stitches issued on different streams overlap (frame k+1's gain feed under frame k's composite).
  * A stitch waits only for its slot's previous stitch when that one was issued on another stream.
- * k > 1 needs blend == 0 and no scaled output (OCTVR_E_UNSUPPORTED otherwise).  Synchronizes. */
+ * k > 1 needs the output at template size (no scaled output; OCTVR_E_UNSUPPORTED otherwise);
+ * multi-band / feather mappers get per-slot pyramids.  Synchronizes. */
 #define OCTVR_MAX_FRAMES_IN_FLIGHT 4
 int octvr_mapper_set_frames_in_flight(octvr_mapper* mapper, int k);
 /* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 4 B tiled

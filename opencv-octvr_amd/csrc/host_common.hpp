@@ -173,8 +173,11 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                             const std::vector<int>& in_h, int feather_border = 0);
 // One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P
 // (or, with `rgba`, the RGB result as RGBA for a scaled output).
-void multiband_run(MultiBand& mb, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
+// slot: frame slot (0 = the buffers built with the rig, 1..k-1 after multiband_set_slots(k)).
+void multiband_run(MultiBand& mb, int slot, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
                    int64_t out_pitch, hipStream_t s, uint8_t* rgba = nullptr, int64_t rgba_pitch = 0);
+// Per-frame buffers (pyramid levels, collapsed levels, remap work queue) for k frames in flight.
+void multiband_set_slots(MultiBand& mb, int k);
 // Algorithmic bytes of one frame and a JSON fragment of build statistics.
 double multiband_traffic(const MultiBand& mb);
 std::string multiband_info(const MultiBand& mb);

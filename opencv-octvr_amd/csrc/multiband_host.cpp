@@ -65,6 +65,14 @@ class MultiBand {
     };
     std::vector<Level> lv;
     TiledLutDev remap;
+    // frames in flight (octvr_mapper_set_frames_in_flight): slot k > 0 has its own Gaussian levels,
+    // collapsed levels and remap work queue; everything else above is per rig and read-only per frame
+    struct FrameBufs {
+        std::vector<DevBuf<uint8_t>> g;
+        std::vector<DevBuf<int16_t>> R;
+        DevBuf<uint32_t> queue;
+    };
+    std::vector<std::unique_ptr<FrameBufs>> extra;
     bool feather = false;  // FeatherGPUBlender instead of MultiBandGPUBlender
     bool full_cover = true;
     int crop_w = 0, crop_h = 0;
@@ -517,14 +525,35 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     return mb.release();
 }
 
-void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
+void multiband_set_slots(MultiBand& M, int k) {
+    M.extra.clear();
+    for (int i = 1; i < k; i++) {
+        auto f = std::make_unique<MultiBand::FrameBufs>();
+        f->g.resize(M.lv.size());
+        f->R.resize(M.lv.size());
+        for (size_t l = 0; l < M.lv.size(); l++) {
+            f->g[l].alloc(M.lv[l].g.n);
+            f->R[l].alloc(M.lv[l].R.n);
+        }
+        f->queue.alloc(M.remap.queue.n);
+        HIP_CHECK(hipMemset(f->queue.p, 0, f->queue.n * sizeof(uint32_t)));
+        M.extra.push_back(std::move(f));
+    }
+}
+
+void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double* gains_dev, int use_gain, uint8_t* out,
                    int64_t out_pitch, hipStream_t s, uint8_t* rgba, int64_t rgba_pitch) {
+    REQUIRE(slot >= 0 && slot <= (int)M.extra.size(), "bad frame slot");
+    MultiBand::FrameBufs* fb = slot ? M.extra[slot - 1].get() : nullptr;
+    auto G = [&](int l) { return fb ? fb->g[l].p : M.lv[l].g.p; };
+    auto Rl = [&](int l) { return fb ? fb->R[l].p : M.lv[l].R.p; };
     auto& L0 = M.lv[0];
-    HIP_CHECK(launch_mb_remap(frames, M.remap.view, gains_dev, use_gain,
-                              RgbaOut{L0.g.p, (uint32_t)L0.g_bytes, L0.cams.p}, s));
+    TiledLut view = M.remap.view;
+    if (fb) view.queue = fb->queue.p;
+    HIP_CHECK(launch_mb_remap(frames, view, gains_dev, use_gain, RgbaOut{G(0), (uint32_t)L0.g_bytes, L0.cams.p}, s));
     for (int l = 1; l <= M.B; l++) {
         auto& L = M.lv[l];
-        HIP_CHECK(launch_mb_down(L.down_items.p, L.n_down, L.cams.p, M.lv[l - 1].cams.p, M.lv[l - 1].g.p, L.g.p, s));
+        HIP_CHECK(launch_mb_down(L.down_items.p, L.n_down, L.cams.p, M.lv[l - 1].cams.p, G(l - 1), G(l), s));
     }
     if (!M.full_cover) {  // result pixels outside the blended ROI stay 0 (mapper.cpp:155): Y 0, U = V = 128
         if (rgba) {
@@ -548,12 +577,12 @@ void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev
         a.tiles_x = L.tx_n;
         a.tile_cams = L.tile_cams.p;
         a.cams = L.cams.p;
-        a.g = L.g.p;
+        a.g = G(l);
         if (l < M.B) {
             auto& Ln = M.lv[l + 1];
             a.cams_next = Ln.cams.p;
-            a.g_next = Ln.g.p;
-            a.r_next = Ln.R.p;
+            a.g_next = G(l + 1);
+            a.r_next = Rl(l + 1);
             a.W_next = Ln.W;
             a.H_next = Ln.H;
             a.rup_rows = L.rup.p;
@@ -562,7 +591,7 @@ void multiband_run(MultiBand& M, const FrameSet& frames, const double* gains_dev
             a.rup_c0 = L.rup_org.p + L.ty_n;
         }
         if (l > 0) {
-            a.r_out = L.R.p;
+            a.r_out = Rl(l);
         } else {
             a.out = out;
             a.out_pitch = out_pitch;

@@ -931,16 +931,16 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         }
         if (m->scaled) {
             // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
-            // (one frame slot only: the result frame and the multi-band state are shared)
+            // (one frame slot only: the result frame is shared)
             if (m->mb)
-                multiband_run(*m->mb, fs, sl.gains, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
+                multiband_run(*m->mb, 0, fs, sl.gains, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
             else
                 HIP_CHECK(launch_mb_remap(fs, m->tiles.view, sl.gains, m->use_gain,
                                           RgbaOut{m->result.p, (uint32_t)m->result.n, m->result_view.p}, s));
             HIP_CHECK(launch_resize_rgba_yuv420(m->result.p, m->W, m->H, (int64_t)m->W * 4, out_dev, m->SW, m->SH,
                                                 (int64_t)out_pitch, s));
         } else if (m->mb) {
-            multiband_run(*m->mb, fs, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s);
+            multiband_run(*m->mb, k, fs, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s);
         } else {
             TiledLut view = m->tiles.view;
             view.queue = sl.queue;
@@ -1388,9 +1388,8 @@ int octvr_mapper_gains(octvr_mapper* m, double* g, int n) {
 int octvr_mapper_set_frames_in_flight(octvr_mapper* m, int k) {
     return guarded([&] {
         REQUIRE(m && k >= 1 && k <= OCTVR_MAX_FRAMES_IN_FLIGHT, "frames in flight must be 1..OCTVR_MAX_FRAMES_IN_FLIGHT");
-        if (k > 1 && (m->mb || m->scaled))
-            throw OctvrError(OCTVR_E_UNSUPPORTED,
-                             "frames in flight > 1 need the no-blend composite at template size (blend = 0, no scaled output)");
+        if (k > 1 && m->scaled)
+            throw OctvrError(OCTVR_E_UNSUPPORTED, "frames in flight > 1 need the output at template size (no scaled output)");
         DeviceGuard dg(m->device);
         for (auto& sl : m->slots)
             if (sl.done) HIP_CHECK(hipEventSynchronize(sl.done));
@@ -1415,8 +1414,10 @@ int octvr_mapper_set_frames_in_flight(octvr_mapper* m, int k) {
                 b->tickets.alloc(m->tickets.n);
                 HIP_CHECK(hipMemset(b->tickets.p, 0, b->tickets.n * sizeof(uint32_t)));
             }
-            b->queue.alloc(m->tiles.queue.n);
-            HIP_CHECK(hipMemset(b->queue.p, 0, b->queue.n * sizeof(uint32_t)));
+            if (m->tiles.queue.n) {
+                b->queue.alloc(m->tiles.queue.n);
+                HIP_CHECK(hipMemset(b->queue.p, 0, b->queue.n * sizeof(uint32_t)));
+            }
             octvr_mapper::FrameSlot sl;
             sl.gains = b->gains.p;
             sl.totals = b->totals.p;
@@ -1425,6 +1426,7 @@ int octvr_mapper_set_frames_in_flight(octvr_mapper* m, int k) {
             m->slots.push_back(sl);
             m->slot_bufs.push_back(std::move(b));
         }
+        if (m->mb) multiband_set_slots(*m->mb, k);
         HIP_CHECK(hipDeviceSynchronize());  // the memsets complete before any stream uses the slots
     });
 }

@@ -185,23 +185,26 @@ def test_gpu_stitch_is_deterministic_and_stream_ordered(ox):
     assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
-@pytest.mark.parametrize("k", [2, 3])
-def test_gpu_frames_in_flight_vs_oracle(ox, k):
+@pytest.mark.parametrize("k,blend", [(2, 0), (3, 0), (2, 16), (3, -10)])
+def test_gpu_frames_in_flight_vs_oracle(ox, k, blend):
     """octvr_mapper_set_frames_in_flight(k): 2k frames with their own inputs and outputs issued
     round-robin on k streams (no host sync in between) -> every output and the last frame's gains
-    equal the oracle's for that frame, as if stitched one after another."""
+    equal the oracle's for that frame, as if stitched one after another (no-blend composite,
+    multi-band and feather: each slot has its own pyramids)."""
     import torch
     from octvr_amd import synthetic
     n = 6
     rig = _ring_rig(n)
     W, H = 512, 256
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
+    if blend:
+        mt.create_masks(0)
     sizes = [(320, 240)] * n
-    rois, maps1, maps2, masks = [], [], [], []
+    rois, maps1, maps2, masks, seams = [], [], [], [], []
     for i in range(n):
-        roi, m1, m2, mk, _ = mt.input(i)
-        rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk)
-    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True)
+        roi, m1, m2, mk, sm = mt.input(i)
+        rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk); seams.append(sm)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True)
     m.set_frames_in_flight(k)
     streams = [torch.cuda.Stream() for _ in range(k)]
     frames = [[synthetic.smooth_yuv_frame(w, h, 500 + 10 * f + i) for i, (w, h) in enumerate(sizes)]
@@ -214,7 +217,8 @@ def test_gpu_frames_in_flight_vs_oracle(ox, k):
     g_last = np.array(m.gains())
     torch.cuda.synchronize()
     for f in range(2 * k):
-        want, g_orc = O.stitch_frame(frames[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None)
+        want, g_orc = O.stitch_frame(frames[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None,
+                                     blend=blend, seams=seams if blend else None, threads=8)
         assert np.array_equal(outs[f].cpu().numpy(), want), f
         if f == 2 * k - 1:
             np.testing.assert_array_equal(g_last, np.array(g_orc))
@@ -227,16 +231,17 @@ def test_gpu_frames_in_flight_vs_oracle(ox, k):
     assert torch.equal(o, outs[0])
 
 
-def test_gpu_frames_in_flight_rejected_for_blends(ox):
+def test_gpu_frames_in_flight_rejected_for_scaled_output(ox):
     rig, z = O.load_rig("rigA")
     seams = [z["seam_0"], z["seam_1"]]
     mt = ox.MapperTemplate.from_arrays(512, 256, z["rois"].tolist(), [z["map1_0"], z["map1_1"]],
                                        [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]], seams)
-    m = ox.Mapper(mt, [(256, 144)] * 2, blend=16)
-    with pytest.raises(ox.OctvrError) as e:
-        m.set_frames_in_flight(2)
-    assert e.value.code == -4
-    m.set_frames_in_flight(1)
+    for blend in (0, 16):
+        m = ox.Mapper(mt, [(256, 144)] * 2, blend=blend, scale_output=(256, 128))
+        with pytest.raises(ox.OctvrError) as e:
+            m.set_frames_in_flight(2)
+        assert e.value.code == -4
+        m.set_frames_in_flight(1)
     m0 = ox.Mapper(mt, [(256, 144)] * 2, blend=0)
     for bad in (0, 5):
         with pytest.raises(ox.OctvrError):
