@@ -1057,9 +1057,9 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
 #pragma unroll
         for (int h = 0; h < QPL; h++) e4[h] = d.e4[h];
         OCTVR_PHASE(5);   // back edge: waits for the loads of this item
-#if !OCTVR_DIAG_NOBAR  // diagnostic ablations (wrong output, timing only): scripts/ablate.sh
+        // (diagnostic ablations below: wrong output, timing only.  The barriers are never ablated: the
+        // claim hand-over through LDS then desynchronises the waves, and a barrier-free build faulted)
         __syncthreads();  // the previous tile's LDS readers are done
-#endif
         OCTVR_PHASE(0);
         const TileMeta nxt = meta_read(mv, t_mv);
         // the next item's staging slots (+ their frames' kernarg loads), used after the barrier below
@@ -1090,9 +1090,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
             }
         }
         OCTVR_PHASE(1);
-#if !OCTVR_DIAG_NOBAR
         __syncthreads();
-#endif
         OCTVR_PHASE(2);
         // the item two ahead: static on the first iteration, else the claim handed over above
         if (!first) {
