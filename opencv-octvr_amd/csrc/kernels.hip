@@ -777,6 +777,10 @@ constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
 #ifndef OCTVR_DYN  // 0: static round-robin dealing of a band's items (no work counters)
 #define OCTVR_DYN 1
 #endif
+#ifndef OCTVR_LDS_DB  // 1: small items alternate between two LDS halves (one barrier per item; C2 measured
+                      // 65.5 vs 63.7 us: the barrier is not what the item loop waits on), 0: off
+#define OCTVR_LDS_DB 0
+#endif
 #ifndef OCTVR_WIDE_OUT  // 1: LDS-staged 16-byte output stores (measured no faster on C2; off)
 #define OCTVR_WIDE_OUT 0
 #endif
@@ -958,8 +962,10 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
                                                               int64_t out_pitch, RgbaOut rgba) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
     __shared__ float s_gain[kMaxCams];
-    __shared__ f32x2_t s_slot_gain[kTileSlots];  // {g, g} per slot (finish_quad2)
-    __shared__ uint32_t s_claim;
+    // per iteration parity: written before an item's staging barrier, read after it (the next write
+    // to the same entry is two items later, behind the next barrier)
+    __shared__ f32x2_t s_slot_gain[2][kTileSlots];  // {g, g} per slot (finish_quad2)
+    __shared__ uint32_t s_claim[2];
     // MODE 2: the previous item's YUV420P output, staged in LDS and written with one 16-byte store
     // per lane (store_item_wide) instead of four 1-2-byte stores per quad
     constexpr bool kWideOut = MODE == 2;
@@ -1035,6 +1041,8 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
     int px = 0, py = 0;  // the previous item's quad of this lane in its first half
     uint32_t pcam = 0;
     bool pin = false;
+    uint32_t par = 0, half = 0;  // iteration parity; LDS half of the next small item
+    bool prev_big = true;
 #if OCTVR_PHASES
     // diagnostic: per-wave shader cycles spent in each phase of the item loop (s_memtime)
     unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
@@ -1059,7 +1067,12 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         OCTVR_PHASE(5);   // back edge: waits for the loads of this item
         // (diagnostic ablations below: wrong output, timing only.  The barriers are never ablated: the
         // claim hand-over through LDS then desynchronises the waves, and a barrier-free build faulted)
-        __syncthreads();  // the previous tile's LDS readers are done
+        // Staging region: a small item takes the LDS half the previous item does not read; a big item
+        // (or one after a big item) overlaps it and first waits for its readers.
+        const bool big = !OCTVR_LDS_DB || (cur.nslots & kHdrBigItem) != 0u;
+        if (big || prev_big) __syncthreads();
+        uint32_t* const s_stage = s_rgb + (big ? 0u : half * (uint32_t)(kTileHalfBytes / 4));
+        if (tid < kTileZeroDwords) s_stage[tid] = 0u;  // black pixels read offset 0 of the region
         OCTVR_PHASE(0);
         const TileMeta nxt = meta_read(mv, t_mv);
         // the next item's staging slots (+ their frames' kernarg loads), used after the barrier below
@@ -1068,12 +1081,12 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
-            if (tid < kTileSlots) s_slot_gain[tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
+            if (tid < kTileSlots) s_slot_gain[par][tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
         }
-        if (claimed && tid == 0) s_claim = claim;  // issued one iteration ago
+        if (claimed && tid == 0) s_claim[par] = claim;  // issued one iteration ago
 #if !OCTVR_DIAG_NOSTAGE
 #pragma unroll
-        for (int r = 0; r < R; r++) stage_store<VIG>(d.sg[r], s_rgb);
+        for (int r = 0; r < R; r++) stage_store<VIG>(d.sg[r], s_stage);
         const uint32_t nch = (cur.nslots >> 8) & 0xFFu;
 #else
         const uint32_t nch = 0;
@@ -1086,7 +1099,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
             for (int c = R * 4 + wave; c < (int)nch; c += 4) {
                 StageGroup sg;
                 stage_load<DWORD_STAGE, VIG>(stage_slot(cur, t_end, c), S, c, sg);
-                stage_store<VIG>(sg, s_rgb);
+                stage_store<VIG>(sg, s_stage);
             }
         }
         OCTVR_PHASE(1);
@@ -1095,7 +1108,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         // the item two ahead: static on the first iteration, else the claim handed over above
         if (!first) {
 #if OCTVR_DYN
-            const int v = claimed ? dyn0 + (int)uniform((int)s_claim) : t_end;
+            const int v = claimed ? dyn0 + (int)uniform((int)s_claim[par]) : t_end;
 #else  // static dealing (round-robin over the band's workgroups)
             const int v = t_n2 < t_end ? t_n2 + step : t_end;
 #endif
@@ -1132,7 +1145,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
         for (int p = 0; p < 4; p++) {
             const uint32_t e = ent[p];
             // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
-            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) + (e & 0x7FFFu);
+            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + (e & 0x7FFFu);
             const uint8_t* r1 = r0 + 4u * S;
             const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
             const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
@@ -1144,7 +1157,7 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
 #else
             bilerp_rgba(c00, c01, c10, c11, (e >> 15) & 31u, (e >> 20) & 31u, rgb[p]);
 #endif
-            gain[p] = s_slot_gain[(e >> 25) & 3u];
+            gain[p] = s_slot_gain[par][(e >> 25) & 3u];
             if (SM == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
         }
 #if OCTVR_DIAG_NOCOMPUTE
@@ -1170,6 +1183,9 @@ __global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu
                 store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
 #endif
+        prev_big = big;
+        half ^= big ? 0u : 1u;
+        par ^= 1u;
         cur = nxt;
     }
     // the last workgroup to finish resets the work counters for the next launch (stream order makes

@@ -83,6 +83,11 @@ constexpr int kTileSlots = 4;
 #endif
 constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
 constexpr int kTileZeroDwords = 4;
+// Items whose staged boxes fit half the staging LDS alternate between the two halves, so an item is
+// staged while the previous one is still being read (one barrier per item); larger items carry
+// kHdrBigItem in TileHdr::nslots and take the whole buffer behind an extra barrier.
+constexpr int kTileHalfBytes = kTileLdsBytes / 2;
+constexpr uint32_t kHdrBigItem = 1u << 24;
 constexpr int kTileOutBytes = kTileW * kTileH * 3 / 2;  // one tile's YUV420P output (LDS-staged stores)
 
 struct TileSlot {

@@ -124,7 +124,9 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 continue;
             }
             b.hdr[t] = TileHdr{(uint32_t)J.tx | ((uint32_t)J.ty << 16),
-                               (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16), groups, stride};
+                               (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16) |
+                                   (lds * 4 > (uint32_t)kTileHalfBytes ? kHdrBigItem : 0u),
+                               groups, stride};
             for (int j = 0; j < kTileSlots; j++) b.slots[(size_t)t * kTileSlots + j] = ts[j];
             uint32_t* out = b.entries.data() + (size_t)t * item_px;
             for (int k = 0; k < item_px; k++) {
