@@ -31,15 +31,14 @@ __device__ __forceinline__ uint32_t ch_of(uint32_t v, int c) { return (v >> (8 *
 // ---------------------------------------------------------------------------------------------
 // fastPyrDown<uchar4> (fast_pyr_down.cu:17-76): out = sat(rne(sum_{j,k} w_j w_k src / 256)),
 // w = [1 4 6 4 1], texture clamp border (camera-local).  One workgroup per (camera, 128x8 tile of
-// level l): the 20 x 260 source patch of level l-1 is staged in LDS, then a vertical pass into 8
-// rows of u16 channel sums, then the horizontal pass per 2x2 output quad.
+// level l): each lane loads one column of the 20 x 260 source patch of level l-1 into registers and
+// sums it vertically into 8 rows of u16 channel sums in LDS; then the horizontal pass per 2x2 quad.
 // ---------------------------------------------------------------------------------------------
 constexpr int kDnRows = 2 * kTileH + 4, kDnCols = 2 * kTileW + 4;
 
 __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ items, const MbCamLevel* cams_l,
                                                       const MbCamLevel* cams_prev, const uint8_t* __restrict__ g_prev,
                                                       uint8_t* __restrict__ g_l) {
-    __shared__ uint32_t s_src[kDnRows * kDnCols];      // 20.3 KiB
     __shared__ uint2 s_v[kTileH * kDnCols];             // 16.3 KiB: (c0 | c1 << 16, c2)
     const uint2 it = items[blockIdx.x];
     const int cam = uniform((int)it.x);
@@ -51,8 +50,9 @@ __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ 
     const int xo = tx * kTileW - c.ox, yo = ty * kTileH - c.oy;
     const int sx0 = 2 * xo - 2, sy0 = 2 * yo - 2;
     const uint8_t* src = g_prev + p.g_off;
-    // staging: lane t loads column t of each of the 20 rows (lanes 0-3 also columns 256-259), all
-    // loads in flight before the first LDS write
+    // lane t holds column t of the 20 source rows in registers (lanes 0-3 also columns 256-259), all
+    // loads in flight before the first use; the vertical pass runs on them directly
+    const uint32_t w5[5] = {1u, 4u, 6u, 4u, 1u};
     {
         const int sxa = min(max(sx0 + tid, 0), p.w - 1), sxb = min(max(sx0 + kDnCols - 4 + (tid & 3), 0), p.w - 1);
         uint32_t va[kDnRows], vb[kDnRows];
@@ -63,28 +63,18 @@ __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ 
             vb[r] = *reinterpret_cast<const uint32_t*>(row + (int64_t)sxb * 4);
         }
 #pragma unroll
-        for (int r = 0; r < kDnRows; r++) {
-            s_src[r * kDnCols + tid] = va[r];
-            if (tid < 4) s_src[r * kDnCols + kDnCols - 4 + tid] = vb[r];
-        }
-    }
-    __syncthreads();
-    const uint32_t w5[5] = {1u, 4u, 6u, 4u, 1u};
+        for (int r = 0; r < kTileH; r++) {
 #pragma unroll
-    for (int r = 0; r < kTileH; r++) {
+            for (int half = 0; half < 2; half++) {
+                if (half && tid >= 4) continue;
+                const uint32_t* col = half ? vb : va;
+                uint32_t acc[3] = {0u, 0u, 0u};
 #pragma unroll
-        for (int half = 0; half < 2; half++) {
-            const int q = half ? kDnCols - 4 + (tid & 3) : tid;
-            if (half && tid >= 4) continue;
-            const uint32_t* col = s_src + (2 * r) * kDnCols + q;
-            uint32_t acc[3] = {0u, 0u, 0u};
+                for (int j = 0; j < 5; j++)
 #pragma unroll
-            for (int j = 0; j < 5; j++) {
-                const uint32_t v = col[j * kDnCols];
-#pragma unroll
-                for (int ch = 0; ch < 3; ch++) acc[ch] += w5[j] * ch_of(v, ch);
+                    for (int ch = 0; ch < 3; ch++) acc[ch] += w5[j] * ch_of(col[2 * r + j], ch);
+                s_v[r * kDnCols + (half ? kDnCols - 4 + tid : tid)] = make_uint2(acc[0] | (acc[1] << 16), acc[2]);
             }
-            s_v[r * kDnCols + q] = make_uint2(acc[0] | (acc[1] << 16), acc[2]);
         }
     }
     __syncthreads();
