@@ -61,6 +61,38 @@ def host_threads():
     return max(1, min(int(n) if n else avail, avail, 64))
 
 
+def frame_seed(rank, slot, cam):
+    """Seed of camera `cam`'s synthetic frame for in-flight slot `slot` on rank `rank`: every rank
+    stitches its own independent rig instance."""
+    return 1000 * (rank + 1) + 100 * slot + cam
+
+
+def timed_region(step, steps, sync, dist=None):
+    """Exactly `steps` calls of step(k), bracketed by a barrier + device sync on both sides; returns
+    the MAX over ranks of the elapsed wall time (the job is as slow as its slowest rank)."""
+    if dist:
+        dist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    sync()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+    return elapsed
+
+
+def aggregate_mps(world, steps, frame_px, elapsed):
+    """Whole-job throughput: every rank stitched `steps` frames of `frame_px` output pixels."""
+    return world * steps * frame_px / 1e6 / elapsed
+
+
 def cpu_baseline(mt, frames_np, sizes, W, H, blend=0):
     """The reference CPU path restated by the oracle (YUV->RGBA, fixed-point cv::remap of every
     camera over its full ROI, gain feed + apply, copyTo(mask) or the multi-band blender,
@@ -111,10 +143,10 @@ def main():
     inflight = max(1, args.inflight)
     m.set_frames_in_flight(inflight)
     # each rank stitches an independent rig instance: frames seeded by (rank, in-flight slot, camera)
-    frames_np = [synthetic.yuv_frame(w, h, 1000 * (rank + 1) + i) for i, (w, h) in enumerate(sizes)]
+    frames_np = [synthetic.yuv_frame(w, h, frame_seed(rank, 0, i)) for i, (w, h) in enumerate(sizes)]
     frame_sets = [[torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]]
     for j in range(1, inflight):
-        frame_sets.append([torch.from_numpy(synthetic.yuv_frame(w, h, 1000 * (rank + 1) + 100 * j + i)).to(f"cuda:{dev}")
+        frame_sets.append([torch.from_numpy(synthetic.yuv_frame(w, h, frame_seed(rank, j, i))).to(f"cuda:{dev}")
                            for i, (w, h) in enumerate(sizes)])
     outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
@@ -136,16 +168,7 @@ def main():
     # HIP events around the stitch kernel of every 4th step (each event pair costs ~5 us of GPU
     # timeline per step: timing every step would slow the very loop it measures)
     m.set_timing(4)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
     m.set_timing(False)
     kern_ms, launches = m.kernel_time()
     serial = None
@@ -159,14 +182,10 @@ def main():
         s_ms, s_n = m.kernel_time()
         m.set_timing(False)
         serial = s_ms / 1e3 / max(s_n, 1)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
 
     gains = m.gains()
     frame_px = W * H
-    value = world * args.steps * frame_px / 1e6 / elapsed
+    value = aggregate_mps(world, args.steps, frame_px, elapsed)
     bytes_per_launch = m.traffic_bytes()
     avg_kernel_s = kern_ms / 1e3 / max(launches, 1)
     achieved = bytes_per_launch / avg_kernel_s / 1e9
