@@ -34,7 +34,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: independent frame sets stitched round-robin on this many streams "
                          "(octvr_mapper_set_frames_in_flight)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)

@@ -291,6 +291,16 @@ __device__ bool solve_dispatch(double* A, double* b, int n, double* x) {
     }
 }
 
+// n <= 3 only: the closed forms (few registers)
+__device__ bool solve_small(double* A, double* b, int n, double* x) {
+    switch (n) {
+        case 1: return solve_fixed<1>(A, b, x);
+        case 2: return solve_fixed<2>(A, b, x);
+        case 3: return solve_fixed<3>(A, b, x);
+        default: return false;
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Gain feed (GainCompensatorGPU::feed, exposure_compensate.cpp:223-297) — one launch.
 // Sample s of camera i (a working-scale pixel, nearest resize of the warped ROI, mapper.cpp:234-237)
@@ -404,10 +414,19 @@ __device__ __forceinline__ void feed_taps_finish(const SourceFrame& f, const Fee
     t.fy = (r.code >> 5) & 31u;
 }
 
-__global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
-                                                        const uint16_t* partners, int n_chunks, const int32_t* N, int n,
-                                                        unsigned long long* totals, uint32_t* tickets,
-                                                        double* gains) {
+// LEAN = false: every sample's gathers in flight at once (kGainPer samples per lane) and the register
+// LU (163 VGPRs: the shortest feed on an idle GPU).  LEAN = true: kLeanBatch samples per lane per
+// round, partner sums in LDS, the workgroup LU above n = 3 (<= 80 VGPRs), so the feed of frame k+1
+// fits beside frame k's composite (6 workgroups per CU at 72 VGPRs / 96 SGPRs / 20.7 KiB LDS) and runs
+// under it.  Both sum the same exact values: identical gains.
+#ifndef OCTVR_LEAN_BATCH  // lean feed: samples per lane in flight per round
+#define OCTVR_LEAN_BATCH 3
+#endif
+constexpr int kLeanBatch = OCTVR_LEAN_BATCH;
+template <bool LEAN>
+__device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const CompositeEntry* samples,
+                                               const uint16_t* partners, int n_chunks, const int32_t* N, int n,
+                                               unsigned long long* totals, uint32_t* tickets, double* gains) {
     __shared__ int s_last;
     __shared__ double s_I[kGainMaxCams * kGainMaxCams];
     __shared__ double s_A[kGainMaxCams * kGainMaxCams];
@@ -417,45 +436,106 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
 #if OCTVR_STAMPS == 1
     const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
 #endif
-    double acc[kGainMaxCams];
-#pragma unroll
-    for (int j = 0; j < kGainMaxCams; j++) acc[j] = 0.0;
-    // kGainPer samples per lane, all gathers issued before any arithmetic.  Wave w of workgroup b
-    // takes the kGainWaveRun contiguous samples from (4 b + w) kGainWaveRun: one camera's (runs padded
-    // on the host with invalid samples, partner mask 0), named in every entry's code.
+    // Wave w of workgroup b takes the kGainWaveRun contiguous samples from (4 b + w) kGainWaveRun: one
+    // camera's (runs padded on the host with invalid samples, partner mask 0), named in every entry's
+    // code.  Every norm is 0 or a multiple of 2^-23 in [1, 2^9), so the f64 sums below are exact in any order.
     constexpr int kPer = kGainPer;
-    uint32_t pm[kPer];
-    Taps t[kPer];
-    CompositeEntry es[kPer];
     const int wave = tid >> 6;
+    __shared__ double s_wsum[4][kGainMaxCams];
+    __shared__ int s_wcam[4];
+    const int k0 = (blockIdx.x * 4 + wave) * kGainWaveRun + lane;
+    const int cam = uniform((int)((samples[(blockIdx.x * 4 + wave) * kGainWaveRun].code >> 10) & 31u));
+    const SourceFrame fr = frames.f[cam];  // one camera per wave: uniform frame
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(fr.yuv), 0, (int)((uint32_t)fr.pitch * (uint32_t)(fr.h + fr.h / 2)), 0x00020000);
+    if constexpr (LEAN) {
+        // one sample per lane at a time; per partner a wave sum added into the wave's LDS row
+        // (kLeanBatch samples per lane in flight per round)
+        if (lane < kGainMaxCams) s_wsum[wave][lane] = 0.0;
+        static_assert(kPer % kLeanBatch == 0, "lean feed batches");
+#pragma unroll 1
+        for (int u0 = 0; u0 < kPer; u0 += kLeanBatch) {
+            CompositeEntry e[kLeanBatch];
+            uint32_t pm[kLeanBatch];
 #pragma unroll
-    for (int u = 0; u < kPer; u++) {
-        const int k = (blockIdx.x * 4 + wave) * kGainWaveRun + u * 64 + lane;
-        es[u] = samples[k];
-        pm[u] = partners[k];
-    }
-    const int cam = uniform((int)((es[0].code >> 10) & 31u));  // one camera per wave: uniform frame
-    const SourceFrame fr = frames.f[cam];
-    if (fr.vig) {  // vignette: per-tap byte gathers with the vignette multiply
+            for (int u = 0; u < kLeanBatch; u++) {
+                e[u] = samples[k0 + (u0 + u) * 64];
+                pm[u] = partners[k0 + (u0 + u) * 64];
+            }
+            Taps t[kLeanBatch];
+            if (fr.vig) {  // vignette: per-tap byte gathers with the vignette multiply
 #pragma unroll
-        for (int u = 0; u < kPer; u++) gather_taps_frame(fr, es[u].xy, es[u].code, t[u]);
+                for (int u = 0; u < kLeanBatch; u++) gather_taps_frame(fr, e[u].xy, e[u].code, t[u]);
+            } else {
+                FeedRaw raw[kLeanBatch];
+#pragma unroll
+                for (int u = 0; u < kLeanBatch; u++) feed_taps_issue(rs, fr, e[u].xy, e[u].code, raw[u]);
+#pragma unroll
+                for (int u = 0; u < kLeanBatch; u++) feed_taps_finish(fr, raw[u], t[u]);
+            }
+            double nv[kLeanBatch];
+            uint32_t pm_any = 0u;
+#pragma unroll
+            for (int u = 0; u < kLeanBatch; u++) {
+                uint32_t rgb[3];
+                bilerp_rgba(t[u].c[0], t[u].c[1], t[u].c[2], t[u].c[3], t[u].fx, t[u].fy, rgb);
+                nv[u] = (double)sqrtf((float)(rgb[0] * rgb[0] + rgb[1] * rgb[1] + rgb[2] * rgb[2]));
+                pm_any |= pm[u];
+            }
+            // partners present in this wave's batch (wave-uniform): one wave sum each
+            uint32_t jm = 0u;
+            for (int j = 0; j < n; j++) jm |= __ballot((pm_any >> j) & 1u) ? 1u << j : 0u;
+#pragma unroll 1
+            while (jm) {
+                const int j = __builtin_ctz(jm);
+                jm &= jm - 1;
+                double v = 0.0;
+#pragma unroll
+                for (int u = 0; u < kLeanBatch; u++) v += ((pm[u] >> j) & 1u) ? nv[u] : 0.0;
+                v = wave_sum(v);
+                if (lane == 0) s_wsum[wave][j] += v;
+            }
+        }
     } else {
-        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(fr.yuv), 0, (int)((uint32_t)fr.pitch * (uint32_t)(fr.h + fr.h / 2)), 0x00020000);
-        FeedRaw raw[kPer];
+        // kGainPer samples per lane, all gathers issued before any arithmetic
+        double acc[kGainMaxCams];
 #pragma unroll
-        for (int u = 0; u < kPer; u++) feed_taps_issue(rs, fr, es[u].xy, es[u].code, raw[u]);
+        for (int j = 0; j < kGainMaxCams; j++) acc[j] = 0.0;
+        uint32_t pm[kPer];
+        Taps t[kPer];
+        CompositeEntry es[kPer];
 #pragma unroll
-        for (int u = 0; u < kPer; u++) feed_taps_finish(fr, raw[u], t[u]);
-    }
+        for (int u = 0; u < kPer; u++) {
+            es[u] = samples[k0 + u * 64];
+            pm[u] = partners[k0 + u * 64];
+        }
+        if (fr.vig) {  // vignette: per-tap byte gathers with the vignette multiply
 #pragma unroll
-    for (int u = 0; u < kPer; u++) {
-        uint32_t rgb[3];
-        bilerp_rgba(t[u].c[0], t[u].c[1], t[u].c[2], t[u].c[3], t[u].fx, t[u].fy, rgb);
-        const double nv = (double)sqrtf((float)(rgb[0] * rgb[0] + rgb[1] * rgb[1] + rgb[2] * rgb[2]));
+            for (int u = 0; u < kPer; u++) gather_taps_frame(fr, es[u].xy, es[u].code, t[u]);
+        } else {
+            FeedRaw raw[kPer];
 #pragma unroll
-        for (int j = 0; j < kGainMaxCams; j++)
-            if (pm[u] & (1u << j)) acc[j] += nv;
+            for (int u = 0; u < kPer; u++) feed_taps_issue(rs, fr, es[u].xy, es[u].code, raw[u]);
+#pragma unroll
+            for (int u = 0; u < kPer; u++) feed_taps_finish(fr, raw[u], t[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < kPer; u++) {
+            uint32_t rgb[3];
+            bilerp_rgba(t[u].c[0], t[u].c[1], t[u].c[2], t[u].c[3], t[u].fx, t[u].fy, rgb);
+            const double nv = (double)sqrtf((float)(rgb[0] * rgb[0] + rgb[1] * rgb[1] + rgb[2] * rgb[2]));
+#pragma unroll
+            for (int j = 0; j < kGainMaxCams; j++)
+                if (pm[u] & (1u << j)) acc[j] += nv;
+        }
+        // exact sums: per wave (DPP)
+#pragma unroll
+        for (int j = 0; j < kGainMaxCams; j++) {  // unrolled: the n reductions' DPP chains interleave
+            if (j < n) {
+                const double v = wave_sum(acc[j]);
+                if (lane == 0) s_wsum[wave][j] = v;
+            }
+        }
     }
 #if OCTVR_STAMPS == 1
     unsigned long long st1 = 0, st2 = 0, st3 = 0;
@@ -464,17 +544,7 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
         st1 = __builtin_amdgcn_s_memrealtime();
     }
 #endif
-    // exact sums: per wave (DPP), then per (camera, partner) over the workgroup's waves, then one u64
-    // atomic per pair
-    __shared__ double s_wsum[4][kGainMaxCams];
-    __shared__ int s_wcam[4];
-#pragma unroll
-    for (int j = 0; j < kGainMaxCams; j++) {  // unrolled: the n reductions' DPP chains interleave
-        if (j < n) {
-            const double v = wave_sum(acc[j]);
-            if (lane == 0) s_wsum[wave][j] = v;
-        }
-    }
+    // then per (camera, partner) over the workgroup's waves, then one u64 atomic per pair
     if (lane == 0) s_wcam[wave] = cam;
     __syncthreads();
 #if OCTVR_STAMPS == 1
@@ -552,8 +622,10 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
     // cv::solve (lapack.cpp:1050-1275): one lane with the matrix in registers for n <= 8 (closed forms
     // n <= 3); the LU across the workgroup for 9..16
     bool ok;
-    if (n < OCTVR_LU_BLOCK_MIN || n <= 3) {
-        if (tid == 0) s_last = solve_dispatch(s_A, s_b, n, s_x) ? 1 : 0;
+    if (LEAN && n > 3) {  // the register LU would set the lean kernel's VGPR budget
+        ok = lu_solve_block(s_A, s_b, n, s_x);
+    } else if (LEAN || n < OCTVR_LU_BLOCK_MIN || n <= 3) {
+        if (tid == 0) s_last = (LEAN ? solve_small(s_A, s_b, n, s_x) : solve_dispatch(s_A, s_b, n, s_x)) ? 1 : 0;
         __syncthreads();
         ok = s_last != 0;
     } else {
@@ -568,12 +640,27 @@ __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const C
 #endif
 }
 
+__global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
+                                                        const uint16_t* partners, int n_chunks, const int32_t* N, int n,
+                                                        unsigned long long* totals, uint32_t* tickets, double* gains) {
+    gain_feed_body<false>(frames, samples, partners, n_chunks, N, n, totals, tickets, gains);
+}
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(80)))
+gain_feed_lean_kernel(FrameSet frames, const CompositeEntry* samples, const uint16_t* partners, int n_chunks,
+                      const int32_t* N, int n, unsigned long long* totals, uint32_t* tickets, double* gains) {
+    gain_feed_body<true>(frames, samples, partners, n_chunks, N, n, totals, tickets, gains);
+}
+
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
                             int n_chunks, const int32_t* N, int n,
-                            unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s) {
+                            unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s, bool lean) {
     if (n_chunks <= 0 || n > kGainMaxCams) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, n_chunks,
-                       N, n, totals, tickets, gains);
+    if (lean)
+        hipLaunchKernelGGL(gain_feed_lean_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners,
+                           n_chunks, N, n, totals, tickets, gains);
+    else
+        hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners,
+                           n_chunks, N, n, totals, tickets, gains);
     return hipGetLastError();
 }
 
@@ -762,8 +849,15 @@ constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
 // Residency of 256-thread workgroups is also capped by scalar registers: min(8, 800 / (sgpr16 + 16))
 // (MI355X_MICROARCH.md, Residency), i.e. <= 80 SGPRs for 8 per CU, <= 96 for 7 (the compiler's own
 // occupancy model allows more, so the budget is set explicitly).
+// The register budget is that of one workgroup more than the grid places per CU: the VGPRs / SGPRs
+// left on each SIMD (80 / 96 with 6 composite waves at <= 72 / 96) hold one wave of the lean gain
+// feed, so the next frame's feed runs beside this frame's composite (frames in flight).
+#ifndef OCTVR_STITCH_REG_BLOCKS
+#define OCTVR_STITCH_REG_BLOCKS (kStitchBlocksPerCU + 1)
+#endif
+constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_REG_BLOCKS;
 #ifndef OCTVR_STITCH_SGPRS
-#define OCTVR_STITCH_SGPRS (kStitchBlocksPerCU >= 8 ? 80 : kStitchBlocksPerCU == 7 ? 96 : 102)
+#define OCTVR_STITCH_SGPRS (kStitchRegBlocks >= 8 ? 80 : kStitchRegBlocks == 7 ? 96 : 102)
 #endif
 #ifndef OCTVR_STAGE_REGS
 #define OCTVR_STAGE_REGS 1
@@ -957,7 +1051,7 @@ __device__ __forceinline__ void store_item_wide(const OutFrame& o, const uint32_
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
 template <bool DWORD_STAGE, int MODE, bool VIG, int QPL>
-__global__ void __launch_bounds__(256, kStitchBlocksPerCU) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
+__global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
                                                               int64_t out_pitch, RgbaOut rgba) {
     __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];

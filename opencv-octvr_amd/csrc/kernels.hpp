@@ -79,7 +79,7 @@ __host__ __device__ inline TapCell tap_cell(uint32_t xy, int w, int h) {
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
 #ifndef OCTVR_TILE_LDS_BYTES
-#define OCTVR_TILE_LDS_BYTES (24 * 1024)
+#define OCTVR_TILE_LDS_BYTES (20 * 1024)  // 20 KiB: 7 workgroups fit by LDS, so the composite can take a 7-wave register budget
 #endif
 constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
 constexpr int kTileZeroDwords = 4;
@@ -158,7 +158,8 @@ hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H
 // (9) must be zero before the first launch; the last workgroup leaves them zero.
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
                             int n_chunks, const int32_t* N, int n,
-                            unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s);
+                            unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s,
+                            bool lean = false);  // lean: <= 32 VGPRs, runs beside a composite (kernels.hip)
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 

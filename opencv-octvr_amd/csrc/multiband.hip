@@ -232,6 +232,9 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
 #define MB_DIRECT_TAPS 1
 #endif
 
+#ifndef MB_RUP_EARLY
+#define MB_RUP_EARLY 0
+#endif
 #ifndef MB_BLEND_WAVES  // waves per SIMD the blend is compiled for (register budget)
 #define MB_BLEND_WAVES 7
 #endif
@@ -268,6 +271,10 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) D[p][ch] = 0;
     }
+#if MB_RUP_EARLY  // the collapse's per-column tap table loaded before the camera loop, kept raw
+    uint4 ucR_raw = make_uint4(0u, 0u, 0u, 0u);
+    if (!top) ucR_raw = *reinterpret_cast<const uint4*>(a.rup_cols + (x >> 1));
+#endif
     uint32_t m = (uint32_t)uniform((int)a.tile_cams[tile]);
     while (m) {
         const int n = __builtin_ctz(m);
@@ -394,7 +401,12 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             o[2] = (int)(int16_t)(v.y & 0xFFFFu);
         };
 #if MB_DIRECT_TAPS
+#if MB_RUP_EARLY
+        asm volatile("" : "+v"(ucR_raw.x), "+v"(ucR_raw.y), "+v"(ucR_raw.z), "+v"(ucR_raw.w));
+        const UpQuad ur = a.rup_rows[y >> 1], uc = __builtin_bit_cast(UpQuad, ucR_raw);
+#else
         const UpQuad ur = a.rup_rows[y >> 1], uc = load_up(a.rup_cols, x >> 1);
+#endif
         Taps9<uint2> tp;
         up_taps_issue<uint2>(ur, uc, reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, tp);
         up_quad_taps(ur, uc, tp, unpack, u);

@@ -875,6 +875,15 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
 // =================================================================================================
 namespace octvr {
 
+// OCTVR_LEAN_FEED=0 keeps the wide-prefetch gain feed with frames in flight (measurement knob)
+static bool lean_feed() {
+    static const bool v = [] {
+        const char* e = getenv("OCTVR_LEAN_FEED");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // Mapper::stitch (mapper.cpp:193-323).  gains_dev (device, n doubles): gains of another mapper of the
 // same inputs, copied stream-ordered (AsyncMultiMapper's gain_modes chaining, async.cpp:78-86).
 void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch, uint8_t* out_dev,
@@ -912,8 +921,10 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                 const std::vector<double> ones(m->n, 1.0);
                 HIP_CHECK(launch_set_gains(ones.data(), m->n, sl.gains, s));
             } else {
+                // with frames in flight the feed runs beside the previous frame's composite: the lean
+                // variant fits next to it (the wide-prefetch one waits for its workgroups to drain)
                 HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n,
-                                           sl.totals, sl.tickets, sl.gains, s));
+                                           sl.totals, sl.tickets, sl.gains, s, m->slots.size() > 1 && lean_feed()));
             }
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;

@@ -185,15 +185,15 @@ def test_gpu_stitch_is_deterministic_and_stream_ordered(ox):
     assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
-@pytest.mark.parametrize("k,blend", [(2, 0), (3, 0), (2, 16), (3, -10)])
-def test_gpu_frames_in_flight_vs_oracle(ox, k, blend):
+@pytest.mark.parametrize("k,blend,n", [(2, 0, 6), (3, 0, 6), (2, 0, 3), (2, 0, 12), (2, 16, 6), (3, -10, 6)])
+def test_gpu_frames_in_flight_vs_oracle(ox, k, blend, n):
     """octvr_mapper_set_frames_in_flight(k): 2k frames with their own inputs and outputs issued
     round-robin on k streams (no host sync in between) -> every output and the last frame's gains
     equal the oracle's for that frame, as if stitched one after another (no-blend composite,
-    multi-band and feather: each slot has its own pyramids)."""
+    multi-band and feather: each slot has its own pyramids).  With frames in flight the mapper uses
+    the lean gain feed (closed forms for n <= 3, the workgroup LU above)."""
     import torch
     from octvr_amd import synthetic
-    n = 6
     rig = _ring_rig(n)
     W, H = 512, 256
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
