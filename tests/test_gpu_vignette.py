@@ -24,8 +24,8 @@ def _vignette_rig():
     return rig
 
 
-@pytest.mark.parametrize("blend", [0, 16, -5])
-def test_gpu_vignette_bit_exact(product_lib, blend):
+@pytest.mark.parametrize("blend,inflight", [(0, 1), (16, 1), (-5, 1), (0, 2), (16, 3)])
+def test_gpu_vignette_bit_exact(product_lib, blend, inflight):
     import torch
     from octvr_amd import synthetic
     ox = product_lib
@@ -52,13 +52,19 @@ def test_gpu_vignette_bit_exact(product_lib, blend):
         rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk); seams.append(sm)
     frames = [synthetic.smooth_yuv_frame(w, h, 300 + i) for i, (w, h) in enumerate(sizes)]
     m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True)
-    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
-    m.stitch([torch.from_numpy(f).cuda() for f in frames], out)
+    m.set_frames_in_flight(inflight)  # > 1: the lean gain feed (vignette gathers) and per-slot state
+    dev_frames = [torch.from_numpy(f).cuda() for f in frames]
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(inflight)]
+    streams = [torch.cuda.Stream() for _ in range(inflight)]
+    torch.cuda.synchronize()
+    for k in range(inflight):  # every slot in turn stitches the same frame, each on its own stream
+        m.stitch(dev_frames, outs[k], stream=streams[k])
     torch.cuda.synchronize()
     g = np.array(m.gains())
     want, g_orc = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, blend=blend,
                                  seams=seams, vig=vig, threads=8)
     np.testing.assert_array_equal(g, g_orc)
-    got = out.cpu().numpy()
-    d = got != want
-    assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
+    for out in outs:
+        got = out.cpu().numpy()
+        d = got != want
+        assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
