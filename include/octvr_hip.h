@@ -144,6 +144,10 @@ int octvr_mapper_traffic(const octvr_mapper* mapper, double* bytes_per_frame);
  * the log. */
 int octvr_mapper_set_timing(octvr_mapper* mapper, int enable);
 int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launches);
+/* The same log with frames in flight (launches on several streams overlap): span_ms = summed
+ * start-to-end times, busy_ms = length of the union of the launches' intervals (the wall time some
+ * composite was running).  Synchronizes and resets the log. */
+int octvr_mapper_kernel_busy(octvr_mapper* mapper, double* span_ms, double* busy_ms, int* launches);
 /* Build-time statistics of a mapper as a JSON object (tiles, wide tiles, staged bytes, gain samples). */
 int octvr_mapper_info(const octvr_mapper* mapper, char* buf, size_t len);
 void octvr_mapper_destroy(octvr_mapper* mapper);

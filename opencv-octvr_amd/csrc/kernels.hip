@@ -4,6 +4,7 @@
 // reference's non-FMA x86 arithmetic (the oracle, oracle/octvr_oracle.c, is compiled the same way).
 // No MFMA anywhere: this is a gather + per-pixel fixed-point blend.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cfloat>
 #include <cmath>
@@ -1359,7 +1360,15 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 
 template <int MODE>
 static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
-                                   int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s) {
+                                   int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
+                                   hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+    // timing events: carried by the dispatch packet itself when the tiled kernel is the only launch
+    // (no marker packets between the launches of the timed loop), else recorded around the launches
+    const bool ext_ev = ev0 && lut.n_items > 0 && lut.n_wide == 0 && lut.qpl == 2 && !OCTVR_WIDE_OUT;
+    if (ev0 && !ext_ev) {
+        const hipError_t e = hipEventRecord(ev0, s);
+        if (e != hipSuccess) return e;
+    }
     if (lut.n_items > 0) {
         // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU: 25 KiB LDS each), each
         // walking its XCD band's items
@@ -1399,6 +1408,9 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
         if (OCTVR_QPL == 4 && lut.qpl == 4)                                                                    \
             hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, OCTVR_QPL == 4 ? 4 : 1>), dim3(blocks), dim3(256), \
                                0, s, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);                \
+        else if (lut.qpl == 2 && ext_ev)                                                                       \
+            hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, ev0, ev1, \
+                                  0, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);                \
         else if (lut.qpl == 2)                                                                                 \
             hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, \
                                W, H, gains, use_gain, out, out_pitch, rgba);                                   \
@@ -1422,6 +1434,10 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
     if (lut.n_wide > 0)
         hipLaunchKernelGGL(stitch_wide_kernel<MODE>, dim3(lut.n_wide), dim3(256), 0, s, frames, lut, W, H, gains,
                            use_gain, out, out_pitch, rgba);
+    if (ev0 && !ext_ev) {
+        const hipError_t e = hipEventRecord(ev1, s);
+        if (e != hipSuccess) return e;
+    }
     return hipGetLastError();
 }
 
@@ -1437,8 +1453,8 @@ extern "C" int octvr_debug_stamps(unsigned long long* out, int rows) {
 int composite_qpl() { return OCTVR_QPL; }
 
 hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
-                         int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s) {
-    return launch_composite<0>(frames, lut, W, H, gains, use_gain, out, out_pitch, RgbaOut{}, s);
+                         int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    return launch_composite<0>(frames, lut, W, H, gains, use_gain, out, out_pitch, RgbaOut{}, s, ev0, ev1);
 }
 
 hipError_t launch_mb_remap(const FrameSet& frames, const TiledLut& lut, const double* gains, int use_gain,

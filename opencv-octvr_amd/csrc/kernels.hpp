@@ -196,8 +196,11 @@ constexpr uint32_t kCodeNoGain = 1u << 16;
 // Quads per lane of the blend = 0 composite's items (OCTVR_QPL, default 2: 128 x 16 items).
 int composite_qpl();
 
+// ev0 / ev1 (optional): timing events around the composite (carried by the dispatch packet when it
+// is a single launch)
 hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W, int H,
-                         const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s);
+                         const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s,
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // ---- multi-band blend (blend > 0): MultiBandGPUBlender (blenders.cpp:589-735) ------------------
 // Level l of the blend lives on the "level grid": align_result_roi >> l.  Each camera keeps its

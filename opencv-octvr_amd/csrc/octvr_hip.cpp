@@ -938,7 +938,7 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                 e1 = m->free_events.back().second;
                 m->free_events.pop_back();
             }
-            HIP_CHECK(hipEventRecord(e0, s));
+            if (m->scaled || m->mb) HIP_CHECK(hipEventRecord(e0, s));  // the composite records its own
         }
         if (m->scaled) {
             // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
@@ -955,10 +955,10 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         } else {
             TiledLut view = m->tiles.view;
             view.queue = sl.queue;
-            HIP_CHECK(launch_stitch(fs, view, m->W, m->H, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s));
+            HIP_CHECK(launch_stitch(fs, view, m->W, m->H, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s, e0, e1));
         }
         if (timed) {
-            HIP_CHECK(hipEventRecord(e1, s));
+            if (m->scaled || m->mb) HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
         }
         if (!sl.done) HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
@@ -1483,6 +1483,42 @@ int octvr_mapper_kernel_time(octvr_mapper* m, double* total_ms, int* launches) {
         }
         *launches = (int)m->events.size();
         *total_ms = t;
+        m->events.clear();
+    });
+}
+
+int octvr_mapper_kernel_busy(octvr_mapper* m, double* span_ms, double* busy_ms, int* launches) {
+    return guarded([&] {
+        REQUIRE(m && span_ms && busy_ms && launches, "NULL argument");
+        DeviceGuard dg(m->device);
+        // [start, end] of every recorded launch relative to the first one's start (launches on several
+        // streams may overlap): summed spans and the length of their union
+        std::vector<std::pair<double, double>> iv;
+        double span = 0;
+        for (auto& e : m->events) {
+            HIP_CHECK(hipEventSynchronize(e.second));
+            float a = 0, b = 0;
+            HIP_CHECK(hipEventElapsedTime(&a, m->events[0].first, e.first));
+            HIP_CHECK(hipEventElapsedTime(&b, m->events[0].first, e.second));
+            iv.emplace_back((double)a, (double)b);
+            span += (double)b - (double)a;
+        }
+        std::sort(iv.begin(), iv.end());
+        double busy = 0, cur_a = 0, cur_b = -1e300;
+        for (auto& x : iv) {
+            if (x.first > cur_b) {
+                if (cur_b > cur_a) busy += cur_b - cur_a;
+                cur_a = x.first;
+                cur_b = x.second;
+            } else {
+                cur_b = std::max(cur_b, x.second);
+            }
+        }
+        if (!iv.empty() && cur_b > cur_a) busy += cur_b - cur_a;
+        for (auto& e : m->events) m->free_events.push_back(e);
+        *launches = (int)m->events.size();
+        *span_ms = span;
+        *busy_ms = busy;
         m->events.clear();
     });
 }

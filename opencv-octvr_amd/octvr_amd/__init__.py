@@ -74,6 +74,7 @@ _lib.octvr_mapper_set_frames_in_flight.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
 _lib.octvr_mapper_set_timing.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int)]
+_lib.octvr_mapper_kernel_busy.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]
 _lib.octvr_mapper_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
 _lib.octvr_mapper_destroy.argtypes = [_VP]
 _lib.octvr_mapper_destroy.restype = None
@@ -287,6 +288,12 @@ class Mapper:
         t, k = C.c_double(), C.c_int()
         _check(_lib.octvr_mapper_kernel_time(self._h, C.byref(t), C.byref(k)))
         return t.value, k.value
+
+    def kernel_busy(self):
+        """(summed start-to-end ms, union ms, launches) of the logged launches (synchronizes)."""
+        sp, bu, k = C.c_double(), C.c_double(), C.c_int()
+        _check(_lib.octvr_mapper_kernel_busy(self._h, C.byref(sp), C.byref(bu), C.byref(k)))
+        return sp.value, bu.value, k.value
 
     def close(self):
         if self._h and self._h.value:
