@@ -1442,7 +1442,8 @@ int octvr_mapper_set_frames_in_flight(octvr_mapper* m, int k) {
             m->cur_slot = 0;
         }
         for (size_t i = 1; i < m->slots.size(); i++)
-            if (m->slots[i].done) (void)hipEventDestroy(m->slots[i].done);
+            for (hipEvent_t e : {m->slots[i].done, m->slots[i].feed_in, m->slots[i].feed_done})
+                if (e) (void)hipEventDestroy(e);
         m->slots.resize(1);
         m->slot_bufs.clear();
         std::vector<double> ones(kMaxCams, 1.0);
