@@ -137,7 +137,7 @@ struct CamTemplate {
 // about one workgroup per CU on C2).
 constexpr int kGainMaxCams = 16;
 #ifndef OCTVR_GAIN_PER  // samples per lane of the gain feed
-#define OCTVR_GAIN_PER 6
+#define OCTVR_GAIN_PER 3
 #endif
 constexpr int kGainPer = OCTVR_GAIN_PER;
 constexpr int kGainWaveRun = 64 * kGainPer;  // one wave's samples: contiguous, one camera
