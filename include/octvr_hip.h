@@ -6,7 +6,7 @@
  *
  *   octvr_rig_*      <- vr::MapperTemplate           modules/octvr/include/octvr.hpp:47-91,
  *                                                     modules/octvr/src/template.cpp:23-322
- *   octvr_mapper_*   <- vr::Mapper                   modules/octvr/src/mapper.hpp:386-452,
+ *   octvr_mapper_*   <- vr::Mapper                   modules/octvr/src/mapper.hpp:29-95,
  *                                                     modules/octvr/src/mapper.cpp:47-323
  *   octvr_async_*    <- vr::AsyncMultiMapper         modules/octvr/include/octvr.hpp:103-121,
  *                                                     modules/octvr/src/async.cpp:32-350
@@ -118,18 +118,18 @@ void octvr_rig_destroy(octvr_rig* rig);
 int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                         int enable_gain, int scale_w, int scale_h, octvr_mapper** mapper);
 /* Mapper::stitch (mapper.cpp:193-323) on device-resident YUV420P frames in the "Y over [U|V]"
- * layout of mapper.hpp:432-440: rows [0,H) = Y (W bytes), rows [H, 3H/2) = U in bytes [0, W/2) and
+ * layout of mapper.hpp:75-83: rows [0,H) = Y (W bytes), rows [H, 3H/2) = U in bytes [0, W/2) and
  * V in bytes [W/2, W) of each row; `pitch` = bytes per row (>= W).  gains: NULL = estimate
  * (GainCompensatorGPU::feed), else set_gains (n_gains == n_inputs).  Stream-ordered, no host sync. */
 int octvr_mapper_stitch_yuv420p(octvr_mapper* mapper, const uint8_t* const* in_dev, const size_t* in_pitch,
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream);
-/* Mapper::gains() (mapper.hpp:445-447): gains used by the last stitch (synchronizes the stream). */
+/* Mapper::gains() (mapper.hpp:88-90): gains used by the last stitch (synchronizes the stream). */
 int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
 /* Frames in flight (no reference counterpart: vr::Mapper is not re-entrant, and AsyncMultiMapper
  * serialises its stitches on one compute stream, async.cpp:78-92).  k slots of per-frame device state
  * (gains, gain-feed totals, composite work queue); consecutive stitches take the slots in turn, so
  * stitches issued on different streams overlap (frame k+1's gain feed under frame k's composite).
- * A stitch waits only for its slot's previous stitch when that one was issued on another stream.
+ * A stitch waits (through an event) only for its slot's previous stitch.
  * k > 1 needs the output at template size (no scaled output; OCTVR_E_UNSUPPORTED otherwise);
  * multi-band / feather mappers get per-slot pyramids.  Synchronizes. */
 #define OCTVR_MAX_FRAMES_IN_FLIGHT 4
@@ -148,6 +148,9 @@ int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launch
  * start-to-end times, busy_ms = length of the union of the launches' intervals (the wall time some
  * composite was running).  Synchronizes and resets the log. */
 int octvr_mapper_kernel_busy(octvr_mapper* mapper, double* span_ms, double* busy_ms, int* launches);
+/* The arithmetic behind kernel_busy, on host arrays: span = sum of (end - start), busy = length of the
+ * union of the n intervals [start[k], end[k]] (overlapping, nested, touching or disjoint, any order). */
+int octvr_interval_union(const double* start, const double* end, int n, double* span, double* busy);
 /* Build-time statistics of a mapper as a JSON object (tiles, wide tiles, staged bytes, gain samples). */
 int octvr_mapper_info(const octvr_mapper* mapper, char* buf, size_t len);
 void octvr_mapper_destroy(octvr_mapper* mapper);
@@ -210,6 +213,16 @@ int octvr_fill_poly_u8(uint8_t* img, int w, int h, const int* pts, int npts, uin
 int octvr_png_decode_rgb(const uint8_t* png, size_t n, uint8_t* rgb, size_t rgb_cap, int* w, int* h);
 
 /* ---- self-test hooks (used by tests/, not by the stitching path) ---------------------------------- */
+/* LUT-build bookkeeping of a JSON rig: the number of input i's output pixels whose projection the GPU
+ * build left to the host because a last-ulp device / glibc libm difference could change them
+ * (LutGuard, camera_math.hpp); 0 for rigs from .dat / arrays. */
+int octvr_rig_lut_recomputed(const octvr_rig* rig, int i, uint64_t* n);
+/* The FP64 projection (MapperTemplate::add_input's (x, y) before the f32 rounding, template.cpp:70-95)
+ * of every pixel of an out_w x out_h output for input `input` of a JSON rig, on `device` (where = 0;
+ * fragile[k] = 1 where the guard defers the pixel to the host) or on the host with glibc (where = 1,
+ * fragile unused).  x, y, fragile: host arrays of out_w * out_h.  Include masks are not evaluated. */
+int octvr_debug_project_f64(const char* json, int out_w, int out_h, int input, int device, int where, double* x,
+                            double* y, uint8_t* fragile);
 /* Saturating float -> u8 conversion as the kernels implement it (method 0: rint + clamp in VALU,
  * method 1: v_cvt_pk_u8_f32), for a known-answer test of round-half-even and clamping on device. */
 int octvr_selftest_sat_u8(const float* in_dev, uint8_t* out_dev, int n, int method, void* stream);

@@ -72,10 +72,68 @@ struct CameraParams {
 #define OCTVR_HD __host__ __device__ inline
 constexpr double kPi = 3.14159265358979323846;
 
+// sin(x) and cos(x) of one argument.  The reference is built by gcc, whose sincos pass turns every
+// sin(x) / cos(x) pair of one function into ONE glibc sincos() call, and glibc's sincos differs in the
+// last bit from its (FMA-dispatched) sin and cos at some arguments.  So the host evaluation calls
+// sincos exactly where a reference function computes both (camera.cpp:197-199, fullframe_fisheye_cam.cpp:
+// 191-193 and 244-248, eqarea*.hpp, cvRodrigues2) and plain sin / cos everywhere else (clang never merges
+// them); the device uses OCML's sin and cos (its results are only trusted away from every decision
+// boundary, see LutGuard).
+OCTVR_HD void sin_cos(double x, double* s, double* c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *s = sin(x);
+    *c = cos(x);
+#else
+    ::sincos(x, s, c);
+#endif
+}
+
+// ---- decision guard of the GPU LUT build ---------------------------------------------------------
+// Device libm (OCML) and glibc may differ in the last ulps of sin / cos / atan2 / asin / atan / tan,
+// and so may every quantity derived from them.  The LUT kernel therefore passes a guard through the
+// projection: every comparison whose outcome such a difference could flip (a branch threshold, the
+// [0, 1) image test, a mask pixel index) marks the pixel fragile when its two sides are within
+// kLutGuardTol of each other, and so does a final f64 -> f32 rounding that lies that close to a
+// rounding boundary.  The host then recomputes the fragile pixels with glibc, i.e. with exactly the
+// reference's arithmetic (octvr_hip.cpp build_input), so the LUT is bit-exact.  The host
+// evaluation passes no guard.  Measured device-vs-glibc deviations of the final coordinates are below
+// 1e-14 (tests/test_gpu_lut_exact.py), far inside the tolerance.
+constexpr double kLutGuardTol = 0x1p-36;  // ~1.5e-11 on O(1) quantities
+struct LutGuard {
+    bool hit;
+};
+// a and b (finite) closer than tol: the comparison of a with b may differ between device and host
+OCTVR_HD void guard_near(LutGuard* g, double a, double b, double tol = kLutGuardTol) {
+    if (g && fabs(a - b) <= tol) g->hit = true;
+}
+// v compared with both ends of [lo, hi]
+OCTVR_HD void guard_range(LutGuard* g, double v, double lo, double hi, double tol = kLutGuardTol) {
+    guard_near(g, v, lo, tol);
+    guard_near(g, v, hi, tol);
+}
+// (int)(v) of a mask pixel index: fragile next to an integer (tolerance scaled by the image size)
+OCTVR_HD void guard_index(LutGuard* g, double v, double scale) {
+    if (g && fabs(v - rint(v)) <= kLutGuardTol * (scale > 1 ? scale : 1)) g->hit = true;
+}
+// (float)v: fragile within tol of a rounding boundary (the midpoints between neighbouring floats), and
+// next to 0 (the sign decides the x < 0 test)
+OCTVR_HD bool f32_fragile(double v, double tol = kLutGuardTol) {
+    if (v != v) return false;
+    if (fabs(v) <= tol) return true;
+    const float f = (float)v;
+    if (fabs((double)f) > 3.0e38) return false;  // |v| beyond any image: invalid on both sides
+    const double lo = ((double)f + (double)nextafterf(f, -INFINITY)) * 0.5;
+    const double hi = ((double)f + (double)nextafterf(f, INFINITY)) * 0.5;
+    return v - lo <= tol || hi - v <= tol;
+}
+
 OCTVR_HD void lonlat_to_xyz(double lon, double lat, double* p) {
-    p[0] = cos(lon) * cos(lat);
-    p[1] = sin(lat);
-    p[2] = -sin(lon) * cos(lat);
+    double slon, clon, slat, clat;
+    sin_cos(lon, &slon, &clon);
+    sin_cos(lat, &slat, &clat);
+    p[0] = clon * clat;
+    p[1] = slat;
+    p[2] = -slon * clat;
 }
 
 // rotated = m * r.t() evaluated by cv::gemm's A*B^T loop: s = ((0 + a0 b0) + a1 b1) + a2 b2.
@@ -91,20 +149,31 @@ OCTVR_HD void rotate_rows(const double* r, const double* p, double* q) {
 }
 
 // sphere_xyz_to_lonlat: p = xyz * (1 / norm(xyz)) (camera.cpp:189-192)
-OCTVR_HD void xyz_to_lonlat(const double* xyz, double* lon, double* lat) {
+// Guard: next to a pole (|py| ~ 1) the longitude is ill-conditioned and asin's domain edge is near;
+// atan2's branch cut (pz ~ 0 with px < 0) flips lon between -pi and pi.
+OCTVR_HD void xyz_to_lonlat(const double* xyz, double* lon, double* lat, LutGuard* g = nullptr) {
     double n = sqrt(xyz[0] * xyz[0] + xyz[1] * xyz[1] + xyz[2] * xyz[2]);
     double inv = 1.0 / n;
     double px = xyz[0] * inv, py = xyz[1] * inv, pz = xyz[2] * inv;
+    if (g) {
+        guard_near(g, fabs(py), 1.0, 0x1p-20);
+        if (px < 0) guard_near(g, pz, 0.0);
+    }
     *lon = atan2(-pz, px);
     *lat = asin(py);
 }
-OCTVR_HD void xyz3_to_lonlat(double x, double y, double z, double* lon, double* lat) {
+OCTVR_HD void xyz3_to_lonlat(double x, double y, double z, double* lon, double* lat, LutGuard* g = nullptr) {
     const double p[3] = {x, y, z};
-    xyz_to_lonlat(p, lon, lat);
+    xyz_to_lonlat(p, lon, lat, g);
 }
 
-OCTVR_HD bool valid_longitude(const CameraParams& c, double l) {
-    auto between = [&](double x) { return x >= c.min_lon && x <= c.max_lon; };
+OCTVR_HD bool valid_longitude(const CameraParams& c, double l, LutGuard* g = nullptr) {
+    // the default selection [-pi, pi] (camera.cpp:125-135) holds every atan2 result: no threshold to guard
+    const bool custom = c.min_lon > -kPi || c.max_lon < kPi;
+    auto between = [&](double x) {
+        if (custom) guard_range(g, x, c.min_lon, c.max_lon);
+        return x >= c.min_lon && x <= c.max_lon;
+    };
     return between(l) || between(l + 2 * kPi) || between(l - 2 * kPi) || between(l + 4 * kPi) ||
            between(l - 4 * kPi);
 }
@@ -209,7 +278,8 @@ OCTVR_HD int solve_poly_real(const double* a, int n0, double* re, double* im) {
 
 // FullFrameFisheyeCamera::image_to_obj_single (fullframe_fisheye_cam.cpp:223-253) with
 // do_reverse_radial_distort (:160-185); the crop must be the whole image (checked at rig creation).
-OCTVR_HD void fullframe_fisheye_image_to_obj(const CameraParams& c, double x, double y, double* lon, double* lat) {
+OCTVR_HD void fullframe_fisheye_image_to_obj(const CameraParams& c, double x, double y, double* lon, double* lat,
+                                             LutGuard* g = nullptr) {
     x -= 0.5;
     y -= 0.5;
     x *= (double)c.crop_w;
@@ -232,40 +302,49 @@ OCTVR_HD void fullframe_fisheye_image_to_obj(const CameraParams& c, double x, do
     y = y / scale;
     const double distance = double(c.crop_w) / c.hfov;
     const double alpha = atan2(-y, x);
-    double theta = -y / distance / sin(alpha);
-    if (fabs(sin(alpha)) < 1e-3) theta = -x / distance / cos(alpha);
-    *lon = atan2(sin(theta) * cos(alpha), cos(theta));
+    double sa, ca;
+    sin_cos(alpha, &sa, &ca);
+    double theta = -y / distance / sa;
+    guard_near(g, fabs(sa), 1e-3);
+    if (fabs(sa) < 1e-3) theta = -x / distance / ca;
+    double st, ct;
+    sin_cos(theta, &st, &ct);
+    *lon = atan2(st * ca, ct);
+    guard_near(g, fabs(ca), 0.0, 0x1p-20);  // tan(alpha) changes sign through +-infinity
+    if (g && ct < 0) guard_near(g, st * ca, 0.0);  // atan2's branch cut
     *lat = atan(tan(alpha) * sin(*lon));
 }
 
-OCTVR_HD void image_to_obj_single(const CameraParams& c, double x, double y, double* lon, double* lat) {
+OCTVR_HD void image_to_obj_single(const CameraParams& c, double x, double y, double* lon, double* lat,
+                                  LutGuard* g = nullptr) {
     switch (c.type) {
         case CAM_FULLFRAME_FISHEYE:
-            fullframe_fisheye_image_to_obj(c, x, y, lon, lat);
+            fullframe_fisheye_image_to_obj(c, x, y, lon, lat, g);
             return;
         case CAM_NORMAL: {
             double xx = c.cam_x;
             double yy = c.cam_y - y * 2.0 * c.cam_y;
             double zz = c.cam_z - x * 2.0 * c.cam_z;
-            xyz3_to_lonlat(xx, yy, zz, lon, lat);
+            xyz3_to_lonlat(xx, yy, zz, lon, lat, g);
             return;
         }
         case CAM_PERSPECTIVE: {
             double z = (0.5 - x) * c.aspect;
             double yy = 0.5 - y;
             double xx = 1.0 / c.sf;
-            xyz3_to_lonlat(xx, yy, z, lon, lat);
+            xyz3_to_lonlat(xx, yy, z, lon, lat, g);
             return;
         }
         case CAM_OCAM: {
             double p2[2] = {y * c.height, x * c.width}, p3[3];
             ocam_cam2world(c, p2, p3);
-            xyz3_to_lonlat(-p3[2], -p3[0], -p3[1], lon, lat);
+            xyz3_to_lonlat(-p3[2], -p3[0], -p3[1], lon, lat, g);
             return;
         }
         case CAM_STUPIDOVAL: {
             double la = (0.5 - y) * kPi;
             double lo = (x - 0.5) * kPi * 2.0 / cos(la);
+            guard_range(g, lo, -kPi, kPi);
             if (lo < -kPi || lo > kPi) {
                 *lon = *lat = NAN;
                 return;
@@ -284,19 +363,19 @@ OCTVR_HD void image_to_obj_single(const CameraParams& c, double x, double y, dou
             double px = (x - ix * 1.0 / 3.0) * 3.0 * 2.0 - 1.0;
             double py = (y - iy * 1.0 / 2.0) * 2.0 * 2.0 - 1.0;
             switch (iy * 3 + ix) {
-                case 0: xyz3_to_lonlat(1.0, py, px, lon, lat); return;
-                case 1: xyz3_to_lonlat(-1., py, -px, lon, lat); return;
-                case 2: xyz3_to_lonlat(px, -1., -py, lon, lat); return;
-                case 3: xyz3_to_lonlat(px, 1.0, py, lon, lat); return;
-                case 4: xyz3_to_lonlat(px, py, -1.0, lon, lat); return;
-                default: xyz3_to_lonlat(-px, py, 1.0, lon, lat); return;
+                case 0: xyz3_to_lonlat(1.0, py, px, lon, lat, g); return;
+                case 1: xyz3_to_lonlat(-1., py, -px, lon, lat, g); return;
+                case 2: xyz3_to_lonlat(px, -1., -py, lon, lat, g); return;
+                case 3: xyz3_to_lonlat(px, 1.0, py, lon, lat, g); return;
+                case 4: xyz3_to_lonlat(px, py, -1.0, lon, lat, g); return;
+                default: xyz3_to_lonlat(-px, py, 1.0, lon, lat, g); return;
             }
         }
         case CAM_EQAREA_NORTH: {
             double dx = x - 0.5, dy = y - 0.5;
             double rho = sqrt(dx * dx + dy * dy) * 2;
             *lat = kPi / 2 - (kPi / 2 - c.circle) * rho;
-            *lon = atan2(-dx, -dy);
+            *lon = atan2(-dx, -dy);  // exact arguments: no device / host difference to guard
             return;
         }
         case CAM_EQAREA_SOUTH: {
@@ -318,17 +397,26 @@ OCTVR_HD void equirect_obj_to_image(const CameraParams& c, double lon, double la
     *y = (lat - c.max_lat) / (c.min_lat - c.max_lat);
 }
 
-OCTVR_HD void fullframe_fisheye_obj_to_image(const CameraParams& c, double lon, double lat, double* ox, double* oy) {
-    double s = cos(lat) * cos(lon);
-    double v1 = sin(lat);
-    double v0 = -cos(lat) * sin(lon);
+OCTVR_HD void fullframe_fisheye_obj_to_image(const CameraParams& c, double lon, double lat, double* ox, double* oy,
+                                             LutGuard* g = nullptr) {
+    double slat, clat, slon, clon;
+    sin_cos(lat, &slat, &clat);
+    sin_cos(lon, &slon, &clon);
+    double s = clat * clon;
+    double v1 = slat;
+    double v0 = -clat * slon;
     double r = sqrt(v0 * v0 + v1 * v1);
     double theta = atan2(r, s);
     double distance = double(c.crop_w) / (c.hfov);
     double x = -(theta * v0 / r) * distance;
     double y = -(theta * v1 / r) * distance;
+    if (g) {
+        if (fabs(lat) <= 1e-5 + kLutGuardTol) guard_near(g, fabs(lon), 1e-5);
+        if (fabs(lon) <= 1e-5 + kLutGuardTol) guard_near(g, fabs(lat), 1e-5);
+    }
     if (fabs(lon) < 1e-5 && fabs(lat) < 1e-5) x = y = 0;
     double rr = (sqrt(x * x + y * y)) / c.rad[4];
+    if (g) guard_near(g, rr, c.rad[5], kLutGuardTol * fmax(1.0, fabs(c.rad[5])));
     double scale = (rr < c.rad[5]) ? ((c.rad[3] * rr + c.rad[2]) * rr + c.rad[1]) * rr + c.rad[0] : 1000.0;
     double rx = x * scale, ry = y * scale;
     rx += c.center_dx;
@@ -337,6 +425,7 @@ OCTVR_HD void fullframe_fisheye_obj_to_image(const CameraParams& c, double lon, 
     ry /= double(c.crop_h);
     rx += 0.5;
     ry += 0.5;
+    if (c.crop_circular) guard_near(g, (rx - 0.5) * (rx - 0.5) + (ry - 0.5) * (ry - 0.5), 0.25);
     if (c.crop_circular && (rx - 0.5) * (rx - 0.5) + (ry - 0.5) * (ry - 0.5) > 0.25) {
         *ox = NAN;
         *oy = NAN;
@@ -358,14 +447,16 @@ OCTVR_HD void cubic_face_to_img(int index, double x, double y, double* ox, doubl
     *oy = ry;
 }
 
-OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat, double* ox, double* oy) {
+OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat, double* ox, double* oy,
+                                  LutGuard* g = nullptr) {
     switch (c.type) {
         case CAM_FULLFRAME_FISHEYE:
-            fullframe_fisheye_obj_to_image(c, lon, lat, ox, oy);
+            fullframe_fisheye_obj_to_image(c, lon, lat, ox, oy, g);
             return;
         case CAM_NORMAL: {
             double p[3];
             lonlat_to_xyz(lon, lat, p);
+            guard_near(g, p[0], 0.0);
             if (p[0] < 0) {
                 *ox = *oy = NAN;
                 return;
@@ -381,6 +472,7 @@ OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat,
         case CAM_PERSPECTIVE: {
             double p[3];
             lonlat_to_xyz(lon, lat, p);
+            guard_near(g, p[0], 0.0);  // the projection changes sign through infinity
             double y_ = p[1] * (1.0 / c.sf / p[0]);
             double z_ = p[2] * (1.0 / c.sf / p[0]);
             *ox = 0.5 - z_ / c.aspect;
@@ -404,7 +496,12 @@ OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat,
         case CAM_CUBIC: {
             double p[3], s[3];
             lonlat_to_xyz(lon, lat, p);
-            auto within = [](double a, double b) { return a >= -1.0 && a <= 1.0 && b >= -1.0 && b <= 1.0; };
+            auto within = [g](double a, double b) {
+                guard_range(g, a, -1.0, 1.0);
+                guard_range(g, b, -1.0, 1.0);
+                return a >= -1.0 && a <= 1.0 && b >= -1.0 && b <= 1.0;
+            };
+            for (int k = 0; k < 3; k++) guard_near(g, fabs(p[k]), 1e-2);
             if (fabs(p[0]) > 1e-2) {  // intersect with x = 1 / x = -1
                 const double f = fabs(p[0]);
                 s[0] = p[0] / f;
@@ -448,23 +545,29 @@ OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat,
             return;
         }
         case CAM_EQAREA_NORTH: {
+            guard_near(g, lat, c.circle);
             if (lat < c.circle) {
                 *ox = *oy = NAN;
                 return;
             }
             double rho = (kPi / 2 - lat) / (kPi / 2 - c.circle);
-            *ox = -rho * sin(lon) / 2 + 0.5;
-            *oy = -rho * cos(lon) / 2 + 0.5;
+            double sl, cl;
+            sin_cos(lon, &sl, &cl);
+            *ox = -rho * sl / 2 + 0.5;
+            *oy = -rho * cl / 2 + 0.5;
             return;
         }
         case CAM_EQAREA_SOUTH: {
+            guard_near(g, lat, c.circle);
             if (lat > c.circle) {
                 *ox = *oy = NAN;
                 return;
             }
             double rho = (lat + kPi / 2) / (c.circle + kPi / 2);
-            *ox = rho * sin(lon) / 2 + 0.5;
-            *oy = -rho * cos(lon) / 2 + 0.5;
+            double sl, cl;
+            sin_cos(lon, &sl, &cl);
+            *ox = rho * sl / 2 + 0.5;
+            *oy = -rho * cl / 2 + 0.5;
             return;
         }
         default:
@@ -474,7 +577,8 @@ OCTVR_HD void obj_to_image_single(const CameraParams& c, double lon, double lat,
 }
 
 // Y is the rotated sphere point; Kannala-Brandt projection with zero rvec/tvec and alpha = 0.
-OCTVR_HD void fisheye_project(const CameraParams& c, const double* Y, double* ox, double* oy) {
+OCTVR_HD void fisheye_project(const CameraParams& c, const double* Y, double* ox, double* oy, LutGuard* g = nullptr) {
+    guard_near(g, Y[2], 0.0);
     if (Y[2] <= 0) {
         *ox = NAN;
         *oy = NAN;
@@ -498,7 +602,8 @@ OCTVR_HD void fisheye_project(const CameraParams& c, const double* Y, double* ox
 
 // cvProjectPoints2 for one point with rvec = tvec = 0 (R = I, t = 0) (calibration.cpp:759-793).
 // Y is the rotated sphere point (z <= 0 was mapped to NaN by PinholeCamera::obj_to_image).
-OCTVR_HD void pinhole_project(const CameraParams& c, const double* Y, double* ox, double* oy) {
+OCTVR_HD void pinhole_project(const CameraParams& c, const double* Y, double* ox, double* oy, LutGuard* g = nullptr) {
+    guard_near(g, Y[2], 0.0);
     double X = Y[0], Yy = Y[1], Z = Y[2];
     if (Z <= 0) X = Yy = Z = NAN;
     const double* k = c.dist;
@@ -546,32 +651,42 @@ OCTVR_HD bool selection_excludes(const CameraParams& c, double x, double y) {
 // Output pixel (u, v) in [0,1)^2 -> input camera normalized image point (x, y) or NaN.  With `vis`,
 // also Camera::get_include_mask's verdict for the pixel (camera.cpp:255-294: the same projection
 // without the longitude and exclude tests, then include_mask.at(int(y*rows), int(x*cols))).
+// g (device LUT build): marks the pixel fragile (see LutGuard); the host evaluation passes none.
 OCTVR_HD void project_output_to_input(const CameraParams& out, const CameraParams& in, double u, double v,
-                                      double* x, double* y, bool* vis = nullptr) {
+                                      double* x, double* y, bool* vis = nullptr, LutGuard* g = nullptr) {
     double lon, lat, p[3], q[3];
     if (vis) *vis = false;
     // out->image_to_obj (camera.cpp:296-315)
-    image_to_obj_single(out, u, v, &lon, &lat);
+    image_to_obj_single(out, u, v, &lon, &lat, g);
     lonlat_to_xyz(lon, lat, p);
     rotate_rows(out.Rinv, p, q);
-    xyz_to_lonlat(q, &lon, &lat);
+    xyz_to_lonlat(q, &lon, &lat, g);
     // in->obj_to_image (camera.cpp:212-253; PinholeCamera overrides it, pinhole_cam.cpp:32-50)
     lonlat_to_xyz(lon, lat, p);
-    bool lon_ok = valid_longitude(in, lon);
+    bool lon_ok = valid_longitude(in, lon, g);
     rotate_rows(in.R, p, q);
     if (in.type == CAM_FISHEYE) {
-        fisheye_project(in, q, x, y);
+        fisheye_project(in, q, x, y, g);
         return;
     }
     if (in.type == CAM_PINHOLE) {
-        pinhole_project(in, q, x, y);
+        pinhole_project(in, q, x, y, g);
         return;
     }
     double ll, la;
-    xyz_to_lonlat(q, &ll, &la);
+    xyz_to_lonlat(q, &ll, &la, g);
     double px = NAN, py = NAN;
-    if (lon_ok || (vis && in.incl)) obj_to_image_single(in, ll, la, &px, &py);
+    if (lon_ok || (vis && in.incl)) obj_to_image_single(in, ll, la, &px, &py, g);
     const bool inside = px >= 0 && px < 1 && py >= 0 && py < 1;
+    const bool masked = in.sel || in.excl || (vis && in.incl);
+    if (g && masked) {  // the mask lookups: the [0, 1) test and the pixel indices
+        guard_range(g, px, 0.0, 1.0);
+        guard_range(g, py, 0.0, 1.0);
+        if (inside) {
+            guard_index(g, px * in.width, in.width);
+            guard_index(g, py * in.height, in.height);
+        }
+    }
     const size_t at = inside ? (size_t)(int)(py * in.height) * in.width + (int)(px * in.width) : 0;
     if (vis && in.incl && inside) *vis = in.incl[at] != 0;
     if (!lon_ok) px = py = NAN;

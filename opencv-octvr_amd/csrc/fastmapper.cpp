@@ -32,17 +32,6 @@ struct octvr_fastmapper {
 
 namespace {
 
-template <class F>
-void parallel_for(size_t n, F f) {
-    const size_t T = std::max<size_t>(1, std::min<size_t>(16, std::thread::hardware_concurrency()));
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < T; t++)
-        th.emplace_back([&, t] {
-            for (size_t k = n * t / T; k < n * (t + 1) / T; k++) f(k);
-        });
-    for (auto& x : th) x.join();
-}
-
 int sat_int_rne(float v) {  // saturate_cast<int>(float)
     if (v != v) return INT32_MIN;
     if (v >= 2147483648.f) return INT32_MAX;

@@ -5,11 +5,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <functional>
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels.hpp"
@@ -33,6 +35,22 @@ struct OctvrError : std::runtime_error {
     do {                                                                    \
         if (!(cond)) throw ::octvr::OctvrError(OCTVR_E_INVALID, (msg));     \
     } while (0)
+
+// f(k) for k in [0, n) on up to 16 host threads (contiguous ranges; build-time work only).
+template <class F>
+void parallel_for(size_t n, F f) {
+    const size_t T = std::max<size_t>(1, std::min<size_t>({16, (size_t)std::thread::hardware_concurrency(), n}));
+    if (T <= 1) {
+        for (size_t k = 0; k < n; k++) f(k);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            for (size_t k = n * t / T; k < n * (t + 1) / T; k++) f(k);
+        });
+    for (auto& x : th) x.join();
+}
 
 // octvr_last_error() text of the calling thread (octvr_hip.cpp).
 void set_last_error(const std::string& msg);
@@ -89,6 +107,7 @@ struct RigInput {
     int vig_w = 0, vig_h = 0;
     // morph_controlpoints' triangles (octvr.hpp:60 src_triangles / dst_triangles), 6 floats each
     std::vector<float> src_tris, dst_tris;
+    size_t n_fragile = 0;  // LUT pixels the GPU build left to the host (LutGuard, camera_math.hpp)
 };
 
 struct octvr_rig {

@@ -37,10 +37,13 @@ __device__ unsigned long long g_octvr_stamps[2 * kStampRows * 4];
 // ---------------------------------------------------------------------------------------------
 // LUT build: MapperTemplate::add_input (template.cpp:46-133), one thread per output pixel, FP64.
 // bbox = {min_w, min_h, max_w, max_h} of valid pixels (int atomics, initialised by the host).
+// fragile (optional): pixels whose outcome a last-ulp libm difference could change (LutGuard,
+// camera_math.hpp) are appended as indices (fragile[0] = count, entries from fragile[1], at most
+// cap kept) and left out of bbox and of the visible_mask update: the host recomputes them with glibc.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __restrict__ cams, int W, int H,
                                                         float* map1, float* map2, uint8_t* mask, int32_t* bbox,
-                                                        uint8_t* visible) {
+                                                        uint8_t* visible, uint32_t* fragile, uint32_t cap) {
     const CameraParams& out = cams[0];
     const CameraParams& in = cams[1];
     __shared__ int s_bb[4];
@@ -53,13 +56,20 @@ __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __re
         const int h = (int)(idx / W), w = (int)(idx - (int64_t)h * W);
         double dx, dy;
         bool vis = false;
-        project_output_to_input(out, in, (double)w / W, (double)h / H, &dx, &dy, visible ? &vis : nullptr);
+        LutGuard g{false};
+        project_output_to_input(out, in, (double)w / W, (double)h / H, &dx, &dy, visible ? &vis : nullptr,
+                                fragile ? &g : nullptr);
+        const bool frag = fragile && (g.hit || f32_fragile(dx) || f32_fragile(dy));
+        if (frag) {
+            const uint32_t k = atomicAdd(fragile, 1u);
+            if (k < cap) fragile[1 + k] = (uint32_t)idx;
+        }
         const float x = (float)dx, y = (float)dy;
         // visible_mask arbitration (template.cpp:86-116): a pixel an earlier camera's include mask
         // claimed (1) is rejected; one this camera's include mask claims first is marked 2 so the host
         // clears it from the earlier cameras' masks.
         const bool claimed = visible && visible[idx] == 1;
-        if (visible && vis && !claimed) visible[idx] = 2;
+        if (visible && vis && !claimed && !frag) visible[idx] = 2;
         if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f || claimed) {
             mask[idx] = 0;
             map1[idx] = -1.0f;
@@ -68,10 +78,12 @@ __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __re
             mask[idx] = 255;
             map1[idx] = x;
             map2[idx] = y;
-            lminw = min(lminw, w);
-            lmaxw = max(lmaxw, w);
-            lminh = min(lminh, h);
-            lmaxh = max(lmaxh, h);
+            if (!frag) {
+                lminw = min(lminw, w);
+                lmaxw = max(lmaxw, w);
+                lminh = min(lminh, h);
+                lmaxh = max(lmaxh, h);
+            }
         }
     }
     if (lmaxw >= 0) {
@@ -90,11 +102,38 @@ __global__ void __launch_bounds__(256) lut_build_kernel(const CameraParams* __re
 }
 
 hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
-                            int32_t* bbox, uint8_t* visible, hipStream_t s) {
+                            int32_t* bbox, uint8_t* visible, uint32_t* fragile, uint32_t cap, hipStream_t s) {
     const int64_t total = (int64_t)W * H;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(lut_build_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, W, H, map1, map2, mask, bbox, visible);
+    hipLaunchKernelGGL(lut_build_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, W, H, map1, map2, mask, bbox, visible,
+                       fragile, cap);
+    return hipGetLastError();
+}
+
+// Diagnostics (octvr_debug_project_f64): the FP64 projection of every output pixel before the f32
+// rounding, with the guard's verdict (1 = fragile), for measuring device-vs-glibc deviations.
+__global__ void __launch_bounds__(256) project_f64_kernel(const CameraParams* __restrict__ cams, int W, int H,
+                                                          double* xs, double* ys, uint8_t* fragile) {
+    const int64_t total = (int64_t)W * H;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int h = (int)(idx / W), w = (int)(idx - (int64_t)h * W);
+        double dx, dy;
+        LutGuard g{false};
+        project_output_to_input(cams[0], cams[1], (double)w / W, (double)h / H, &dx, &dy, nullptr, &g);
+        xs[idx] = dx;
+        ys[idx] = dy;
+        fragile[idx] = (g.hit || f32_fragile(dx) || f32_fragile(dy)) ? 1 : 0;
+    }
+}
+
+hipError_t launch_project_f64(const CameraParams* cams_dev, int W, int H, double* x, double* y, uint8_t* fragile,
+                              hipStream_t s) {
+    const int64_t total = (int64_t)W * H;
+    int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(project_f64_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, W, H, x, y, fragile);
     return hipGetLastError();
 }
 
@@ -358,34 +397,59 @@ __device__ __forceinline__ void gain_system_row(const double* I, const int32_t* 
 }
 
 // Gain-feed gathers: per sample the 2 luma and 2 chroma rows of its 2x2 taps as 8-byte buffer loads
-// from 4-byte aligned starts (6 loads instead of 12 byte loads); a frame-sized buffer resource
-// returns 0 past the frame end.  The taps are extracted and converted in feed_taps_finish, after
-// every sample's loads are in flight.
+// from 4-byte aligned starts (6 loads instead of 12 byte loads).  The frame-sized buffer resource
+// range-checks whole dwords, so a load may not reach past the frame's last byte (the last chroma row
+// of a tight-pitch frame whose V row ends mid-dword): every start is clamped to size - 8 and the tap
+// bytes are taken relative to the clamped start.  The taps are extracted and converted in
+// feed_taps_finish, after every sample's loads are in flight.
 struct FeedRaw {
     uint2 y0, y1, u0, u1, v0, v1;
     uint32_t xy, code;
 };
 
+// The six row segments of a sample's taps: row base offsets in the frame (Y row y0, y1; U and V rows
+// y0/2, y1/2) and the clamped 8-byte load starts.
+struct FeedRows {
+    uint32_t by0, by1, bu0, bu1, bv0, bv1;  // offsets of the rows' first bytes
+    uint32_t sy0, sy1, su0, su1, sv0, sv1;  // load starts
+};
+__device__ __forceinline__ FeedRows feed_rows(const SourceFrame& f, const TapCell& tc) {
+    const uint32_t p = (uint32_t)f.pitch;
+    const uint32_t lim = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2) - 8u;  // frames >= 8 B (host check)
+    const uint32_t uo = (uint32_t)f.h * p, vo = uo + (uint32_t)(f.w >> 1);
+    const uint32_t xa = (uint32_t)tc.x0 & ~3u, ca = ((uint32_t)tc.x0 >> 1) & ~3u;
+    FeedRows r;
+    r.by0 = (uint32_t)tc.y0 * p;
+    r.by1 = (uint32_t)tc.y1 * p;
+    r.bu0 = uo + (uint32_t)(tc.y0 >> 1) * p;
+    r.bu1 = uo + (uint32_t)(tc.y1 >> 1) * p;
+    r.bv0 = vo + (uint32_t)(tc.y0 >> 1) * p;
+    r.bv1 = vo + (uint32_t)(tc.y1 >> 1) * p;
+    r.sy0 = min(r.by0 + xa, lim);
+    r.sy1 = min(r.by1 + xa, lim);
+    r.su0 = min(r.bu0 + ca, lim);
+    r.su1 = min(r.bu1 + ca, lim);
+    r.sv0 = min(r.bv0 + ca, lim);
+    r.sv1 = min(r.bv1 + ca, lim);
+    return r;
+}
+
 __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
                                                 uint32_t code, FeedRaw& r) {
-    const TapCell tc = tap_cell(xy, f.w, f.h);
-    const int x0 = tc.x0, y0 = tc.y0, y1 = tc.y1;
-    const uint32_t p = (uint32_t)f.pitch;
-    const uint32_t uo = (uint32_t)f.h * p, vo = uo + (uint32_t)(f.w >> 1);
-    const uint32_t xa = (uint32_t)x0 & ~3u, ca = ((uint32_t)x0 >> 1) & ~3u;
+    const FeedRows w = feed_rows(f, tap_cell(xy, f.w, f.h));
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 t;
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)y0 * p + xa, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sy0, 0, 0);
     r.y0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, (uint32_t)y1 * p + xa, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sy1, 0, 0);
     r.y1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + (uint32_t)(y0 >> 1) * p + ca, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.su0, 0, 0);
     r.u0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + (uint32_t)(y1 >> 1) * p + ca, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.su1, 0, 0);
     r.u1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + (uint32_t)(y0 >> 1) * p + ca, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sv0, 0, 0);
     r.v0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, vo + (uint32_t)(y1 >> 1) * p + ca, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sv1, 0, 0);
     r.v1 = make_uint2(t.x, t.y);
     r.xy = xy;
     r.code = code;
@@ -400,13 +464,16 @@ __device__ __forceinline__ uint32_t seg_byte(const uint2& v, uint32_t k) {
 __device__ __forceinline__ void feed_taps_finish(const SourceFrame& f, const FeedRaw& r, Taps& t) {
     const bool valid = (r.code & 0x8000u) != 0;
     const TapCell tc = tap_cell(r.xy, f.w, f.h);
-    const int x0 = tc.x0, x1 = tc.x1;
-    const uint32_t ky0 = (uint32_t)x0 & 3u, ky1 = ky0 + (uint32_t)(x1 - x0);
-    const uint32_t kc0 = ((uint32_t)x0 >> 1) & 3u, kc1 = kc0 + (uint32_t)((x1 >> 1) - (x0 >> 1));
-    const uint32_t ca = yuv_to_rgba(seg_byte(r.y0, ky0), seg_byte(r.u0, kc0), seg_byte(r.v0, kc0));
-    const uint32_t cb = yuv_to_rgba(seg_byte(r.y0, ky1), seg_byte(r.u0, kc1), seg_byte(r.v0, kc1));
-    const uint32_t cc = yuv_to_rgba(seg_byte(r.y1, ky0), seg_byte(r.u1, kc0), seg_byte(r.v1, kc0));
-    const uint32_t cd = yuv_to_rgba(seg_byte(r.y1, ky1), seg_byte(r.u1, kc1), seg_byte(r.v1, kc1));
+    const FeedRows w = feed_rows(f, tc);
+    const uint32_t x0 = (uint32_t)tc.x0, x1 = (uint32_t)tc.x1, c0 = x0 >> 1, c1 = x1 >> 1;
+    const uint32_t ca = yuv_to_rgba(seg_byte(r.y0, w.by0 + x0 - w.sy0), seg_byte(r.u0, w.bu0 + c0 - w.su0),
+                                    seg_byte(r.v0, w.bv0 + c0 - w.sv0));
+    const uint32_t cb = yuv_to_rgba(seg_byte(r.y0, w.by0 + x1 - w.sy0), seg_byte(r.u0, w.bu0 + c1 - w.su0),
+                                    seg_byte(r.v0, w.bv0 + c1 - w.sv0));
+    const uint32_t cc = yuv_to_rgba(seg_byte(r.y1, w.by1 + x0 - w.sy1), seg_byte(r.u1, w.bu1 + c0 - w.su1),
+                                    seg_byte(r.v1, w.bv1 + c0 - w.sv1));
+    const uint32_t cd = yuv_to_rgba(seg_byte(r.y1, w.by1 + x1 - w.sy1), seg_byte(r.u1, w.bu1 + c1 - w.su1),
+                                    seg_byte(r.v1, w.bv1 + c1 - w.sv1));
     t.c[0] = (valid && tc.ix0 && tc.iy0) ? ca : 0u;
     t.c[1] = (valid && tc.ix1 && tc.iy0) ? cb : 0u;
     t.c[2] = (valid && tc.ix0 && tc.iy1) ? cc : 0u;

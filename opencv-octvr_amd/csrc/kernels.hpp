@@ -145,8 +145,13 @@ constexpr int kGainChunk = 4 * kGainWaveRun;  // one workgroup's samples (4 wave
 constexpr int kGainTotalStride = 32;  // u64 words between pair totals: one 256-B line each
 
 // cams_dev: {output camera, input camera} in device memory (CameraParams holds the ocam polynomials).
+// fragile (optional, cap + 1 words, fragile[0] zero): indices of the pixels the host must recompute
+// (LutGuard, camera_math.hpp); fragile[0] receives their count (entries past cap are dropped).
 hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* map1, float* map2, uint8_t* mask,
-                            int32_t* bbox, uint8_t* visible, hipStream_t s);
+                            int32_t* bbox, uint8_t* visible, uint32_t* fragile, uint32_t cap, hipStream_t s);
+
+hipError_t launch_project_f64(const CameraParams* cams_dev, int W, int H, double* x, double* y, uint8_t* fragile,
+                              hipStream_t s);
 
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
                                 hipStream_t s);
@@ -159,7 +164,7 @@ hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
                             int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s,
-                            bool lean = false);  // lean: <= 32 VGPRs, runs beside a composite (kernels.hip)
+                            bool lean = false);  // lean: <= 80 VGPRs (73 used), runs beside a composite (kernels.hip)
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 

@@ -64,7 +64,9 @@ void rodrigues(double rx, double ry, double rz, double R[9]) {
         return;
     }
     static const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    double c = cos(theta), s = sin(theta), c1 = 1. - c;
+    double c, s;
+    sin_cos(theta, &s, &c);  // gcc builds cvRodrigues2's cos / sin pair as one sincos (camera_math.hpp)
+    const double c1 = 1. - c;
     double itheta = theta ? 1. / theta : 0.;
     rx *= itheta;
     ry *= itheta;
@@ -503,6 +505,7 @@ void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H
     }
     uint8_t* vis_p = visible ? visible->p : nullptr;
     const size_t total = (size_t)W * H;
+    REQUIRE(total < ((size_t)1 << 32), "output frame must have fewer than 2^32 pixels");
     DevBuf<float> m1, m2;
     DevBuf<uint8_t> mk;
     DevBuf<int32_t> bb;
@@ -510,15 +513,78 @@ void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H
     m2.alloc(total);
     mk.alloc(total);
     bb.alloc(4);
-    int32_t init[4] = {INT32_MAX, INT32_MAX, -1, -1};
-    HIP_CHECK(hipMemcpy(bb.p, init, sizeof init, hipMemcpyHostToDevice));
     const CameraParams both[2] = {out_cam, c};
     DevBuf<CameraParams> cams;
     cams.upload(both, 2);
-    HIP_CHECK(launch_lut_build(cams.p, W, H, m1.p, m2.p, mk.p, bb.p, vis_p, nullptr));
-    HIP_CHECK(hipDeviceSynchronize());
+    // fragile pixels (LutGuard, camera_math.hpp): a list of at most `cap` indices, grown and the kernel
+    // re-run if it overflows (the build is idempotent: it writes visible_mask only with 2)
+    uint32_t cap = (uint32_t)std::min<size_t>(total, std::max<size_t>(1 << 16, total / 256));
+    std::vector<uint32_t> frag;
     int32_t b[4];
-    HIP_CHECK(hipMemcpy(b, bb.p, sizeof b, hipMemcpyDeviceToHost));
+    for (;;) {
+        DevBuf<uint32_t> fr;
+        fr.alloc((size_t)cap + 1);
+        HIP_CHECK(hipMemset(fr.p, 0, sizeof(uint32_t)));
+        const int32_t init[4] = {INT32_MAX, INT32_MAX, -1, -1};
+        HIP_CHECK(hipMemcpy(bb.p, init, sizeof init, hipMemcpyHostToDevice));
+        HIP_CHECK(launch_lut_build(cams.p, W, H, m1.p, m2.p, mk.p, bb.p, vis_p, fr.p, cap, nullptr));
+        HIP_CHECK(hipDeviceSynchronize());
+        uint32_t count = 0;
+        HIP_CHECK(hipMemcpy(&count, fr.p, sizeof count, hipMemcpyDeviceToHost));
+        if (count > cap) {
+            cap = count;
+            continue;
+        }
+        frag.resize(count);
+        if (count) HIP_CHECK(hipMemcpy(frag.data(), fr.p + 1, sizeof(uint32_t) * count, hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(b, bb.p, sizeof b, hipMemcpyDeviceToHost));
+        break;
+    }
+    // the fragile pixels with glibc: the reference's arithmetic exactly (camera_math.hpp on the host)
+    std::sort(frag.begin(), frag.end());
+    CameraParams ch = c;
+    ch.excl = excl.empty() ? nullptr : excl.data();
+    ch.incl = (excl.empty() || incl.empty()) ? nullptr : incl.data();
+    struct Fix {
+        float x, y;
+        bool vis;
+    };
+    std::vector<Fix> fix(frag.size());
+    {
+        const bool want_vis = vis_p != nullptr;
+        std::vector<double> fx(frag.size()), fy(frag.size());
+        std::vector<uint8_t> fv(frag.size());
+        parallel_for(frag.size(), [&](size_t k) {
+            const uint32_t idx = frag[k];
+            const int h = (int)(idx / (uint32_t)W), w = (int)(idx - (uint32_t)h * (uint32_t)W);
+            bool v = false;
+            project_output_to_input(out_cam, ch, (double)w / W, (double)h / H, &fx[k], &fy[k], want_vis ? &v : nullptr);
+            fv[k] = v ? 1 : 0;
+        });
+        for (size_t k = 0; k < frag.size(); k++) fix[k] = Fix{(float)fx[k], (float)fy[k], fv[k] != 0};
+    }
+    std::vector<uint8_t> vh;  // visible_mask on the host, when this camera reads or writes it
+    if (vis_p && (!frag.empty() || c.incl)) {
+        vh.resize(total);
+        HIP_CHECK(hipMemcpy(vh.data(), vis_p, total, hipMemcpyDeviceToHost));
+    }
+    std::vector<uint8_t> fvalid(frag.size());
+    for (size_t k = 0; k < frag.size(); k++) {  // lut_build_kernel's per-pixel tail, in index order
+        const uint32_t idx = frag[k];
+        const bool claimed = !vh.empty() && vh[idx] == 1;
+        if (!vh.empty() && fix[k].vis && !claimed) vh[idx] = 2;
+        const float x = fix[k].x, y = fix[k].y;
+        const bool valid = !(std::isnan(x) || std::isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f || claimed);
+        fvalid[k] = valid;
+        if (valid) {
+            const int h = (int)(idx / (uint32_t)W), w = (int)(idx - (uint32_t)h * (uint32_t)W);
+            b[0] = std::min(b[0], w);
+            b[1] = std::min(b[1], h);
+            b[2] = std::max(b[2], w);
+            b[3] = std::max(b[3], h);
+        }
+    }
+    in.n_fragile = frag.size();
     // CV_Assert(min_h <= max_h && min_w <= max_w) (template.cpp:124)
     if (!(b[1] <= b[3] && b[0] <= b[2])) throw OctvrError(OCTVR_E_INVALID, "input camera covers no output pixel");
     int min_w = std::max(0, b[0] - 8), min_h = std::max(0, b[1] - 8);
@@ -540,17 +606,27 @@ void build_input(const CameraParams& out_cam, const JsonValue& cam, int W, int H
     HIP_CHECK(hipMemcpy2D(in.map2.data(), roi[2] * sizeof(float), m2.p + off, W * sizeof(float), roi[2] * sizeof(float),
                           roi[3], hipMemcpyDeviceToHost));
     HIP_CHECK(hipMemcpy2D(in.mask.data(), roi[2], mk.p + off, W, roi[2], roi[3], hipMemcpyDeviceToHost));
+    for (size_t k = 0; k < frag.size(); k++) {  // patch the recomputed pixels (every valid one is in the ROI)
+        const uint32_t idx = frag[k];
+        const int h = (int)(idx / (uint32_t)W), w = (int)(idx - (uint32_t)h * (uint32_t)W);
+        const int rx = w - roi[0], ry = h - roi[1];
+        if (rx < 0 || ry < 0 || rx >= roi[2] || ry >= roi[3]) continue;
+        const size_t j = (size_t)ry * roi[2] + rx;
+        in.mask[j] = fvalid[k] ? 255 : 0;
+        in.map1[j] = fvalid[k] ? fix[k].x : -1.0f;
+        in.map2[j] = fvalid[k] ? fix[k].y : -1.0f;
+    }
     if (c.incl && priors) {  // pixels this camera claimed first (2) leave the earlier cameras' masks
-        std::vector<uint8_t> v(total_px);
-        HIP_CHECK(hipMemcpy(v.data(), vis_p, total_px, hipMemcpyDeviceToHost));
         for (RigInput& p : *priors) {
             if (&p == &in) break;
             for (int y = 0; y < p.roi[3]; y++)
                 for (int x = 0; x < p.roi[2]; x++)
-                    if (v[(size_t)(y + p.roi[1]) * W + x + p.roi[0]] == 2) p.mask[(size_t)y * p.roi[2] + x] = 0;
+                    if (vh[(size_t)(y + p.roi[1]) * W + x + p.roi[0]] == 2) p.mask[(size_t)y * p.roi[2] + x] = 0;
         }
-        for (uint8_t& b : v) b = b ? 1 : 0;
-        HIP_CHECK(hipMemcpy(vis_p, v.data(), total_px, hipMemcpyHostToDevice));
+    }
+    if (c.incl) {
+        for (uint8_t& v : vh) v = v ? 1 : 0;
+        HIP_CHECK(hipMemcpy(vis_p, vh.data(), total, hipMemcpyHostToDevice));
     }
     const JsonValue& o = cam["options"];
     in.in_w = o.has("width") ? o["width"].as_int() : 0;
@@ -619,7 +695,10 @@ struct DatReader {
     void input(RigInput& in, int out_w, int out_h) {
         int64_t roi[4];
         for (int k = 0; k < 4; k++) roi[k] = i64();
-        if (roi[0] < 0 || roi[1] < 0 || roi[2] <= 0 || roi[3] <= 0 || roi[0] + roi[2] > out_w || roi[1] + roi[3] > out_h)
+        // no sums of untrusted int64 fields: each bound is checked against the frame before the next
+        // one is derived from it (roi[0] = INT64_MAX, w = 1 must not wrap into range)
+        if (roi[0] < 0 || roi[1] < 0 || roi[0] > out_w || roi[1] > out_h || roi[2] <= 0 || roi[3] <= 0 ||
+            roi[2] > out_w - roi[0] || roi[3] > out_h - roi[1])
             throw OctvrError(OCTVR_E_PARSE, ".dat: ROI outside the output frame");
         for (int k = 0; k < 4; k++) in.roi[k] = (int)roi[k];
         std::vector<uint8_t> b;
@@ -687,8 +766,7 @@ struct octvr_mapper {
         unsigned long long* totals = nullptr;
         uint32_t* tickets = nullptr;
         uint32_t* queue = nullptr;
-        hipStream_t stream = nullptr;
-        hipEvent_t done = nullptr;  // recorded after the slot's last stitch (the stream may since be gone)
+        hipEvent_t done = nullptr;  // recorded after the slot's last stitch (its stream may since be gone)
         hipEvent_t feed_in = nullptr, feed_done = nullptr;  // hand-over to / from the feed stream
     };
     struct SlotBufs {
@@ -916,14 +994,17 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             // the gain feed reads frames through 32-bit buffer resources
             REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) < 0x7FFFFFFFull,
                     "input frame larger than 2 GiB");
+            // ... in 8-byte segments (kernels.hip feed_rows)
+            REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) >= 8, "input frame below 8 bytes");
             fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
         }
-        // stitches sharing a frame slot (gains, feed totals, work counters) are ordered: one on another
-        // stream waits for the slot's previous stitch (with one slot: for the previous stitch, as
-        // vr::Mapper is not re-entrant either)
+        // stitches sharing a frame slot (gains, feed totals, work counters) are ordered: each waits for
+        // the slot's previous stitch (with one slot: for the previous stitch, as vr::Mapper is not
+        // re-entrant either).  Always through the event, never by comparing stream handles: a destroyed
+        // stream's handle value can come back as a new stream that is not ordered after the old one.
         const int k = (m->cur_slot + 1) % (int)m->slots.size();
         octvr_mapper::FrameSlot& sl = m->slots[k];
-        if (sl.done && sl.stream != s) HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+        if (sl.done) HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
         if (m->use_gain) {
             if (gains_dev) {
                 HIP_CHECK(hipMemcpyAsync(sl.gains, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
@@ -995,7 +1076,6 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         }
         if (!sl.done) HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
         HIP_CHECK(hipEventRecord(sl.done, s));
-        sl.stream = s;
         m->cur_slot = k;
     }
 }
@@ -1502,6 +1582,38 @@ int octvr_mapper_set_timing(octvr_mapper* m, int enable) {
     });
 }
 
+int octvr_interval_union(const double* start, const double* end, int n, double* span, double* busy) {
+    return guarded([&] {
+        REQUIRE(n >= 0 && span && busy && (n == 0 || (start && end)), "bad arguments");
+        std::vector<std::pair<double, double>> iv;
+        double sp = 0;
+        for (int k = 0; k < n; k++) {
+            REQUIRE(end[k] >= start[k], "interval ends before it starts");
+            iv.emplace_back(start[k], end[k]);
+            sp += end[k] - start[k];
+        }
+        // sweep in start order: an interval that starts inside the current run extends it, one that
+        // starts after it closes the run
+        std::sort(iv.begin(), iv.end());
+        double bz = 0;
+        bool open = false;
+        double ra = 0, rb = 0;
+        for (const auto& x : iv) {
+            if (open && x.first <= rb) {
+                rb = std::max(rb, x.second);
+            } else {
+                if (open) bz += rb - ra;
+                ra = x.first;
+                rb = x.second;
+                open = true;
+            }
+        }
+        if (open) bz += rb - ra;
+        *span = sp;
+        *busy = bz;
+    });
+}
+
 int octvr_mapper_kernel_time(octvr_mapper* m, double* total_ms, int* launches) {
     return guarded([&] {
         REQUIRE(m && total_ms && launches, "NULL argument");
@@ -1526,28 +1638,18 @@ int octvr_mapper_kernel_busy(octvr_mapper* m, double* span_ms, double* busy_ms, 
         DeviceGuard dg(m->device);
         // [start, end] of every recorded launch relative to the first one's start (launches on several
         // streams may overlap): summed spans and the length of their union
-        std::vector<std::pair<double, double>> iv;
-        double span = 0;
+        std::vector<double> st, en;
         for (auto& e : m->events) {
             HIP_CHECK(hipEventSynchronize(e.second));
             float a = 0, b = 0;
             HIP_CHECK(hipEventElapsedTime(&a, m->events[0].first, e.first));
             HIP_CHECK(hipEventElapsedTime(&b, m->events[0].first, e.second));
-            iv.emplace_back((double)a, (double)b);
-            span += (double)b - (double)a;
+            st.push_back((double)a);
+            en.push_back((double)b);
         }
-        std::sort(iv.begin(), iv.end());
-        double busy = 0, cur_a = 0, cur_b = -1e300;
-        for (auto& x : iv) {
-            if (x.first > cur_b) {
-                if (cur_b > cur_a) busy += cur_b - cur_a;
-                cur_a = x.first;
-                cur_b = x.second;
-            } else {
-                cur_b = std::max(cur_b, x.second);
-            }
-        }
-        if (!iv.empty() && cur_b > cur_a) busy += cur_b - cur_a;
+        double busy = 0, span = 0;
+        if (octvr_interval_union(st.data(), en.data(), (int)st.size(), &span, &busy) != OCTVR_OK)
+            throw OctvrError(OCTVR_E_HIP, "kernel_busy: inconsistent event timestamps");
         for (auto& e : m->events) m->free_events.push_back(e);
         *launches = (int)m->events.size();
         *span_ms = span;
@@ -1592,6 +1694,65 @@ int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, co
         if (mw == 0 || mh == 0) return;
         HIP_CHECK(launch_remap_u8(src, sw, sh, (int64_t)spitch, cn, map1, map2, mw, mh, (int64_t)mpitch, scale_x,
                                   scale_y, dst, (int64_t)dpitch, (hipStream_t)stream));
+    });
+}
+
+int octvr_rig_lut_recomputed(const octvr_rig* rig, int i, uint64_t* n) {
+    return guarded([&] {
+        REQUIRE(rig && n && i >= 0 && i < (int)rig->inputs.size(), "bad arguments");
+        *n = rig->inputs[i].n_fragile;
+    });
+}
+
+int octvr_debug_project_f64(const char* json, int out_w, int out_h, int input, int device, int where, double* x,
+                            double* y, uint8_t* fragile) {
+    return guarded([&] {
+        REQUIRE(json && x && y && out_w > 0 && out_h > 0 && (where == 0 || where == 1), "bad arguments");
+        JsonValue doc = json_parse(json);
+        const CameraParams out_cam = camera_from_json(doc["output"]);
+        const JsonValue& ins = doc["inputs"];
+        REQUIRE(input >= 0 && input < (int)ins.size(), "bad input index");
+        const JsonValue& cam = ins[(size_t)input];
+        CameraParams c = camera_from_json(cam);
+        std::vector<uint8_t> excl, incl;
+        if (cam.has("options")) build_camera_masks(cam["options"], excl, incl);
+        if (!excl.empty() || !incl.empty()) {
+            c.sel = 0;
+            c.width = cam["options"]["width"].as_int();
+            c.height = cam["options"]["height"].as_int();
+        }
+        const size_t total = (size_t)out_w * out_h;
+        if (where == 1) {  // host, glibc: the evaluation build_input uses for the fragile pixels
+            c.excl = excl.empty() ? nullptr : excl.data();
+            c.incl = nullptr;
+            parallel_for((size_t)out_h, [&](size_t h) {
+                for (int w = 0; w < out_w; w++)
+                    project_output_to_input(out_cam, c, (double)w / out_w, (double)h / out_h, &x[h * out_w + w],
+                                            &y[h * out_w + w]);
+            });
+            return;
+        }
+        REQUIRE(fragile, "fragile is NULL");
+        DeviceGuard dg(device);
+        DevBuf<uint8_t> excl_d;
+        if (!excl.empty()) {
+            excl_d.upload(excl.data(), excl.size());
+            c.excl = excl_d.p;
+        }
+        c.incl = nullptr;
+        const CameraParams both[2] = {out_cam, c};
+        DevBuf<CameraParams> cams;
+        cams.upload(both, 2);
+        DevBuf<double> xd, yd;
+        DevBuf<uint8_t> fd;
+        xd.alloc(total);
+        yd.alloc(total);
+        fd.alloc(total);
+        HIP_CHECK(launch_project_f64(cams.p, out_w, out_h, xd.p, yd.p, fd.p, nullptr));
+        HIP_CHECK(hipDeviceSynchronize());
+        HIP_CHECK(hipMemcpy(x, xd.p, total * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(y, yd.p, total * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_CHECK(hipMemcpy(fragile, fd.p, total, hipMemcpyDeviceToHost));
     });
 }
 

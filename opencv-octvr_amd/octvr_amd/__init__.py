@@ -3,7 +3,7 @@
 Host-side mirror of the reference's octvr API for the stitching path:
 
 * :class:`MapperTemplate`  <- ``vr::MapperTemplate`` (modules/octvr/include/octvr.hpp:47-91)
-* :class:`Mapper`          <- ``vr::Mapper``         (modules/octvr/src/mapper.hpp:386-452)
+* :class:`Mapper`          <- ``vr::Mapper``         (modules/octvr/src/mapper.hpp:29-95)
 
 Device buffers are torch tensors on ``cuda:N`` (PyTorch is plumbing here: allocation, streams,
 torch.distributed); all arithmetic runs in the hand-written HIP kernels of ``liboctvr_hip.so``.
@@ -75,6 +75,9 @@ _lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
 _lib.octvr_mapper_set_timing.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int)]
 _lib.octvr_mapper_kernel_busy.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]
+_lib.octvr_rig_lut_recomputed.argtypes = [_VP, C.c_int, C.POINTER(C.c_uint64)]
+_lib.octvr_debug_project_f64.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP, _VP]
+_lib.octvr_interval_union.argtypes = [_VP, _VP, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.octvr_mapper_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
 _lib.octvr_mapper_destroy.argtypes = [_VP]
 _lib.octvr_mapper_destroy.restype = None
@@ -102,6 +105,31 @@ def lib():
 
 def abi_version():
     return _lib.octvr_abi_version()
+
+
+def debug_project_f64(rig_json, out_w, out_h, input, device=0, where=0):
+    """(x, y, fragile) — the FP64 projection of every output pixel for one input of a JSON rig, on the
+    GPU (where=0; fragile = the LUT guard's verdict) or on the host with glibc (where=1; fragile None)
+    (octvr_debug_project_f64)."""
+    import numpy as _np
+    x = _np.empty((out_h, out_w), _np.float64)
+    y = _np.empty((out_h, out_w), _np.float64)
+    f = _np.zeros((out_h, out_w), _np.uint8)
+    _check(_lib.octvr_debug_project_f64(rig_json.encode() if isinstance(rig_json, str) else rig_json, out_w, out_h,
+                                        int(input), int(device), int(where), x.ctypes.data_as(_VP),
+                                        y.ctypes.data_as(_VP), f.ctypes.data_as(_VP)))
+    return x, y, (f if where == 0 else None)
+
+
+def interval_union(starts, ends):
+    """(summed lengths, length of the union) of the intervals [starts[k], ends[k]]
+    (octvr_interval_union: the arithmetic of Mapper.kernel_busy)."""
+    import numpy as _np
+    a = _np.ascontiguousarray(starts, _np.float64)
+    b = _np.ascontiguousarray(ends, _np.float64)
+    sp, bu = C.c_double(), C.c_double()
+    _check(_lib.octvr_interval_union(a.ctypes.data_as(_VP), b.ctypes.data_as(_VP), len(a), C.byref(sp), C.byref(bu)))
+    return sp.value, bu.value
 
 
 def _stream_ptr(stream):
@@ -150,6 +178,12 @@ class MapperTemplate:
     def dump(self, path):
         """MapperTemplate::dump: VRv11 file (creates the seam masks first if there are none)."""
         _check(_lib.octvr_rig_dump_dat(self._h, os.fsencode(path)))
+
+    def lut_recomputed(self, i):
+        """Output pixels of input i whose projection the GPU LUT build left to the host (glibc)."""
+        n = C.c_uint64()
+        _check(_lib.octvr_rig_lut_recomputed(self._h, i, C.byref(n)))
+        return n.value
 
     def create_masks(self, device=0):
         """MapperTemplate::create_masks(): L2 distance seams (resizes on `device`)."""
@@ -267,7 +301,8 @@ class Mapper:
 
     def set_frames_in_flight(self, k):
         """k slots of per-frame device state: stitches issued on different streams overlap
-        (octvr_mapper_set_frames_in_flight; blend == 0 at template size only)."""
+        (octvr_mapper_set_frames_in_flight).  No scaled output; multi-band / feather mappers get
+        per-slot pyramids."""
         _check(_lib.octvr_mapper_set_frames_in_flight(self._h, int(k)))
 
     def traffic_bytes(self):

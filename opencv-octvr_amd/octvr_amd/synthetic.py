@@ -3,7 +3,7 @@
 Rig JSON follows the reference schema (producer modules/octvr/tools/ptx2json.py):
 `fullframe_fisheye` inputs with a centred circular crop, 200 deg hfov, no radial distortion.
 Frames are uniform-random bytes from splitmix64 (seed = 1000*rig + cam) in the "Y over [U|V]"
-YUV420P layout of mapper.hpp:432-440.
+YUV420P layout of mapper.hpp:75-83.
 """
 import math
 

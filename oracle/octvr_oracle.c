@@ -265,7 +265,10 @@ void orc_camera_set_selection(orc_camera* c, int width, int height, int l, int r
 /* ------------------------------------------------------------------------------------------ */
 /* Sphere helpers (camera.cpp:189-210)                                                         */
 /* ------------------------------------------------------------------------------------------ */
-static void lonlat_to_xyz(double lon, double lat, double* p) {
+/* noinline (and below): gcc merges the sin / cos of one argument within a function into one sincos
+ * call, so the oracle keeps the reference's function boundaries (the reference model methods are separate
+ * functions there) instead of letting inlining pair values the reference never pairs (camera.cpp, cameras/ sources). */
+__attribute__((noinline)) static void lonlat_to_xyz(double lon, double lat, double* p) {
     p[0] = cos(lon) * cos(lat);
     p[1] = sin(lat);
     p[2] = -sin(lon) * cos(lat);
@@ -306,7 +309,7 @@ static void equirect_o2i(const orc_camera* c, double lon, double lat, double* x,
 }
 
 /* FullFrameFisheyeCamera::obj_to_image_single (fullframe_fisheye_cam.cpp:146-221). */
-static void ffisheye_o2i(const orc_camera* c, double lon, double lat, double* ox, double* oy) {
+__attribute__((noinline)) static void ffisheye_o2i(const orc_camera* c, double lon, double lat, double* ox, double* oy) {
     double s = cos(lat) * cos(lon);
     double v1 = sin(lat);
     double v0 = -cos(lat) * sin(lon);
@@ -473,7 +476,7 @@ static int solve_poly(const double* a, int n0, cplx* roots) {
 
 /* FullFrameFisheyeCamera::image_to_obj_single + do_reverse_radial_distort
  * (cameras/fullframe_fisheye_cam.cpp:160-185, 223-253) */
-static void fullframe_image_to_obj(const orc_camera* c, double x, double y, double* lon, double* lat) {
+__attribute__((noinline)) static void fullframe_image_to_obj(const orc_camera* c, double x, double y, double* lon, double* lat) {
     x = (x - 0.5) * (double)c->crop_w - c->center_dx;
     y = (y - 0.5) * (double)c->crop_h - c->center_dy;
     if (fabs(x) < 1e-5 && fabs(y) < 1e-5) { *lon = 0; *lat = 0; return; }
@@ -495,7 +498,7 @@ static void fullframe_image_to_obj(const orc_camera* c, double x, double y, doub
     *lat = atan(tan(alpha) * sin(*lon));
 }
 
-static void image_to_obj_single(const orc_camera* c, double x, double y, double* lon, double* lat) {
+__attribute__((noinline)) static void image_to_obj_single(const orc_camera* c, double x, double y, double* lon, double* lat) {
     switch (c->type) {
     case ORC_FULLFRAME_FISHEYE: fullframe_image_to_obj(c, x, y, lon, lat); return;
     case ORC_NORMAL: /* normal.cpp:24-30 */
@@ -559,8 +562,25 @@ static void cubic_face_to_img(int index, double x, double y, double* ox, double*
     *ox = rx; *oy = ry;
 }
 
+/* The eqarea models' obj_to_image_single, each its own function as in the reference (one sin / cos
+ * pair of one argument per function: gcc builds each pair as one sincos call there). */
+__attribute__((noinline)) static void eqarea_north_o2i(const orc_camera* c, double lon, double lat, double* ox,
+                                                       double* oy) { /* eqareanorthpole.hpp:24-33 */
+    if (lat < c->circle) { *ox = *oy = NAN; return; }
+    double rho = (M_PI / 2 - lat) / (M_PI / 2 - c->circle);
+    *ox = -rho * sin(lon) / 2 + 0.5;
+    *oy = -rho * cos(lon) / 2 + 0.5;
+}
+__attribute__((noinline)) static void eqarea_south_o2i(const orc_camera* c, double lon, double lat, double* ox,
+                                                       double* oy) { /* eqareasouthpole.hpp:23-32 */
+    if (lat > c->circle) { *ox = *oy = NAN; return; }
+    double rho = (lat + M_PI / 2) / (c->circle + M_PI / 2);
+    *ox = rho * sin(lon) / 2 + 0.5;
+    *oy = -rho * cos(lon) / 2 + 0.5;
+}
+
 /* obj_to_image_single of the non-fisheye input camera types. */
-static void obj_to_image_single(const orc_camera* c, double lon, double lat, double* ox, double* oy) {
+__attribute__((noinline)) static void obj_to_image_single(const orc_camera* c, double lon, double lat, double* ox, double* oy) {
     double p[3];
     switch (c->type) {
     case ORC_FULLFRAME_FISHEYE:
@@ -630,20 +650,12 @@ static void obj_to_image_single(const orc_camera* c, double lon, double lat, dou
         *ox = *oy = NAN;
         return;
     }
-    case ORC_EQAREA_NORTH: { /* eqareanorthpole.hpp:24-33 */
-        if (lat < c->circle) { *ox = *oy = NAN; return; }
-        double rho = (M_PI / 2 - lat) / (M_PI / 2 - c->circle);
-        *ox = -rho * sin(lon) / 2 + 0.5;
-        *oy = -rho * cos(lon) / 2 + 0.5;
+    case ORC_EQAREA_NORTH:
+        eqarea_north_o2i(c, lon, lat, ox, oy);
         return;
-    }
-    case ORC_EQAREA_SOUTH: { /* eqareasouthpole.hpp:23-32 */
-        if (lat > c->circle) { *ox = *oy = NAN; return; }
-        double rho = (lat + M_PI / 2) / (c->circle + M_PI / 2);
-        *ox = rho * sin(lon) / 2 + 0.5;
-        *oy = -rho * cos(lon) / 2 + 0.5;
+    case ORC_EQAREA_SOUTH:
+        eqarea_south_o2i(c, lon, lat, ox, oy);
         return;
-    }
     default:
         equirect_o2i(c, lon, lat, ox, oy);
     }
@@ -1159,6 +1171,100 @@ static void parallel_rows(int T, int y0, int y1, row_fn fn, void* ctx) {
         pthread_create(&th[t], NULL, row_worker, &jobs[t]);
     }
     for (int t = 0; t < T; t++) pthread_join(th[t], NULL);
+}
+
+/* orc_lut_build_vis on T threads (row bands): every pixel's computation and the visible_mask update
+ * are per pixel, so the result equals the serial build's; the bands' bounding boxes are merged. */
+typedef struct {
+    const orc_camera *out, *in;
+    int W, H;
+    float *map1, *map2;
+    uint8_t *mask, *visible;
+    int bb[64][4];
+    int next;
+    pthread_mutex_t mu;
+} lut_mt_ctx;
+
+static void lut_mt_rows(void* a, int y0, int y1) {
+    lut_mt_ctx* c = (lut_mt_ctx*)a;
+    int min_h = c->H, max_h = 0, min_w = c->W, max_w = 0;
+    for (int h = y0; h < y1; h++)
+        for (int w = 0; w < c->W; w++) {
+            double dx, dy;
+            int vis = 0;
+            project_pixel_vis(c->out, c->in, (double)w / c->W, (double)h / c->H, &dx, &dy, c->visible ? &vis : NULL);
+            float x = (float)dx, y = (float)dy;
+            size_t idx = (size_t)h * c->W + w;
+            int claimed = c->visible && c->visible[idx] == 1;
+            if (c->visible && vis && !claimed) c->visible[idx] = 2;
+            if (isnan(x) || isnan(y) || x < 0 || x >= 1.0f || y < 0 || y >= 1.0f || claimed) {
+                c->mask[idx] = 0;
+                c->map1[idx] = c->map2[idx] = -1.0f;
+            } else {
+                c->mask[idx] = 255;
+                c->map1[idx] = x;
+                c->map2[idx] = y;
+                if (h < min_h) min_h = h;
+                if (h > max_h) max_h = h;
+                if (w < min_w) min_w = w;
+                if (w > max_w) max_w = w;
+            }
+        }
+    pthread_mutex_lock(&c->mu);
+    int k = c->next++;
+    c->bb[k][0] = min_w; c->bb[k][1] = min_h; c->bb[k][2] = max_w; c->bb[k][3] = max_h;
+    pthread_mutex_unlock(&c->mu);
+}
+
+int orc_lut_build_vis_mt(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
+                         uint8_t* mask, int use_roi, int roi[4], uint8_t* visible, int threads) {
+    lut_mt_ctx c;
+    memset(&c, 0, sizeof c);
+    c.out = out; c.in = in; c.W = W; c.H = H;
+    c.map1 = map1; c.map2 = map2; c.mask = mask; c.visible = visible;
+    pthread_mutex_init(&c.mu, NULL);
+    parallel_rows(threads, 0, H, lut_mt_rows, &c);
+    pthread_mutex_destroy(&c.mu);
+    int min_h = H, max_h = 0, min_w = W, max_w = 0;
+    for (int k = 0; k < c.next; k++) {
+        if (c.bb[k][1] > c.bb[k][3] || c.bb[k][0] > c.bb[k][2]) continue;  /* a band without valid pixels */
+        if (c.bb[k][0] < min_w) min_w = c.bb[k][0];
+        if (c.bb[k][1] < min_h) min_h = c.bb[k][1];
+        if (c.bb[k][2] > max_w) max_w = c.bb[k][2];
+        if (c.bb[k][3] > max_h) max_h = c.bb[k][3];
+    }
+    if (!(min_h <= max_h && min_w <= max_w)) return -1; /* CV_Assert, template.cpp:124 */
+    min_w = min_w - 8 > 0 ? min_w - 8 : 0;
+    min_h = min_h - 8 > 0 ? min_h - 8 : 0;
+    max_w = max_w + 8 < W - 1 ? max_w + 8 : W - 1;
+    max_h = max_h + 8 < H - 1 ? max_h + 8 : H - 1;
+    if (use_roi) {
+        roi[0] = min_w; roi[1] = min_h; roi[2] = max_w + 1 - min_w; roi[3] = max_h + 1 - min_h;
+    } else {
+        roi[0] = 0; roi[1] = 0; roi[2] = W; roi[3] = H;
+    }
+    return 0;
+}
+
+/* The FP64 (x, y) of Camera::obj_to_image for output rows [y0, y1) (template.cpp:70-83), before the
+ * f32 rounding; T threads. */
+typedef struct {
+    const orc_camera *out, *in;
+    int W, H, y0;
+    double *x, *y;
+} proj_ctx;
+static void proj_rows(void* a, int y0, int y1) {
+    proj_ctx* c = (proj_ctx*)a;
+    for (int h = y0; h < y1; h++)
+        for (int w = 0; w < c->W; w++) {
+            size_t idx = (size_t)(h - c->y0) * c->W + w;
+            project_pixel(c->out, c->in, (double)w / c->W, (double)h / c->H, &c->x[idx], &c->y[idx]);
+        }
+}
+void orc_project_f64(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, double* x, double* y,
+                     int threads) {
+    proj_ctx c = {out, in, W, H, y0, x, y};
+    parallel_rows(threads, y0, y1, proj_rows, &c);
 }
 
 typedef struct {

@@ -92,6 +92,12 @@ void orc_fill_poly(uint8_t* img, int w, int h, const int* pts, int count, uint8_
 
 /* Camera::image_to_obj of `from`, then obj_to_image of `to`; nonzero where the reference throws. */
 int orc_project(const orc_camera* from, const orc_camera* to, double u, double v, double* x, double* y);
+/* orc_lut_build_vis on `threads` threads (identical result). */
+int orc_lut_build_vis_mt(const orc_camera* out, const orc_camera* in, int W, int H, float* map1, float* map2,
+                         uint8_t* mask, int use_roi, int roi[4], uint8_t* visible, int threads);
+/* FP64 projection (before the f32 rounding) of output rows [y0, y1), full width. */
+void orc_project_f64(const orc_camera* out, const orc_camera* in, int W, int H, int y0, int y1, double* x, double* y,
+                     int threads);
 /* MapperTemplate::morph_controlpoints (template_morph.cpp:69-237) on ROI-sized LUT planes, in place
  * (octvr_oracle_morph.c).  cps: n_cps x {n0, n1, x0, y0, x1, y1}; src_tris[i] / dst_tris[i] receive
  * camera i's triangles (6 floats each, at most tri_cap), n_tris[i] their count.  Returns the number
@@ -118,7 +124,7 @@ void orc_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, con
                   int mw, int mh, size_t mpitch_elems, float scale_x, float scale_y, uint8_t* dst, size_t dpitch);
 
 /* Own BT.601 definitions standing in for NPP nppiYUV420ToRGB / nppiRGBToYUV420 (parity unpinned,
- * cudaimgproc/src/color.cpp:2269,2306).  Layout "Y over [U|V]" of mapper.hpp:432-440. */
+ * cudaimgproc/src/color.cpp:2269,2306).  Layout "Y over [U|V]" of mapper.hpp:75-83. */
 void orc_yuv420_to_rgba(const uint8_t* yuv, int w, int h, size_t pitch, uint8_t* rgba, size_t rgba_pitch);
 void orc_rgb_to_yuv420(const uint8_t* rgb, int w, int h, size_t rgb_pitch, int rgb_cn, uint8_t* yuv, size_t pitch);
 

@@ -214,10 +214,10 @@ def camera_masks(o):
     return m["excl"], m["incl"]
 
 
-def lut_build(rig, out_w, out_h, use_roi=True):
+def lut_build(rig, out_w, out_h, use_roi=True, threads=1):
     """Per input, then per overlay: (roi, map1, map2, mask) cropped to the ROI, as
     MapperTemplate::add_input, including the include-mask visible_mask arbitration across inputs and
-    overlays (template.cpp:86-116)."""
+    overlays (template.cpp:86-116).  threads > 1: row bands on that many threads (same result)."""
     out = camera_from_json(rig["output"])
     res = []
     visible = None
@@ -231,8 +231,8 @@ def lut_build(rig, out_w, out_h, use_roi=True):
         if visible is None and c.incl:
             visible = np.zeros((out_h, out_w), np.uint8)
         vp = _p(visible) if visible is not None else None
-        rc = lib().orc_lut_build_vis(C.byref(out), C.byref(c), out_w, out_h, _p(m1), _p(m2), _p(mk), int(use_roi),
-                                     roi, vp)
+        rc = lib().orc_lut_build_vis_mt(C.byref(out), C.byref(c), out_w, out_h, _p(m1), _p(m2), _p(mk), int(use_roi),
+                                        roi, vp, int(threads))
         assert rc == 0
         if visible is not None and c.incl:
             for (px, py, pw, ph), _, _, pm in res[:n_inputs]:  # only this->inputs (template.cpp:106)
@@ -286,6 +286,18 @@ def delaunay(points, cap=8192):
     k = L.orc_delaunay_triangles(_p(pts), len(pts) // 2, _p(out), cap)
     assert k >= 0, k
     return out[:k].copy()
+
+
+def project_f64(rig_cam_out, rig_cam_in, W, H, y0=0, y1=None, threads=8):
+    """FP64 (x, y) of output rows [y0, y1) through rig_cam_out's image_to_obj and rig_cam_in's
+    obj_to_image (template.cpp:70-83), before the f32 rounding."""
+    y1 = H if y1 is None else y1
+    out = camera_from_json(rig_cam_out)
+    c = camera_from_json(rig_cam_in)
+    x = np.empty((y1 - y0, W), np.float64)
+    y = np.empty((y1 - y0, W), np.float64)
+    lib().orc_project_f64(C.byref(out), C.byref(c), W, H, y0, y1, _p(x), _p(y), int(threads))
+    return x, y
 
 
 def lut_rows(rig_cam_out, rig_cam_in, W, H, y0, y1):

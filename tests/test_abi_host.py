@@ -110,7 +110,8 @@ def test_dat_reader_accepts_minimal_file(product_lib, tmp_path):
 
 
 @pytest.mark.parametrize("case", ["rows_cols_minus1", "map2_short", "seam_mismatch", "roi_outside", "roi_negative",
-                                  "roi_empty", "out_zero", "negative_count", "truncated_map", "truncated_seam"])
+                                  "roi_empty", "out_zero", "negative_count", "truncated_map", "truncated_seam",
+                                  "roi_x_int64_max", "roi_y_int64_max", "roi_w_int64_max"])
 def test_dat_reader_rejects_malformed(product_lib, tmp_path, case):
     """every Mat must match its input's ROI and every ROI must lie inside the output frame,
     so a malformed .dat fails in the reader instead of reaching the mapper's ROI indexing."""
@@ -129,6 +130,16 @@ def test_dat_reader_rejects_malformed(product_lib, tmp_path, case):
         data = _dat(rois=((-1, 0, 4, 2),))
     elif case == "roi_empty":
         data = _dat(rois=((0, 0, 0, 2),))
+    elif case == "roi_x_int64_max":  # x + w wraps negative and would pass `> out_w`
+        data = _dat(rois=((2 ** 63 - 1, 0, 1, 2),), mats={0: [(5, 2, 1, z4(2, np.float32)), (5, 2, 1, z4(2, np.float32)),
+                                                            (0, 2, 1, z4(2, np.uint8)), (0, 0, 0, b"")]})
+    elif case == "roi_y_int64_max":
+        data = _dat(rois=((0, 2 ** 63 - 1, 4, 1),), mats={0: [(5, 1, 4, z4(4, np.float32)), (5, 1, 4, z4(4, np.float32)),
+                                                            (0, 1, 4, z4(4, np.uint8)), (0, 0, 0, b"")]})
+    elif case == "roi_w_int64_max":
+        data = _dat(rois=((1, 0, 2 ** 63 - 1, 2),), mats={0: [(5, 2, 4, z4(8, np.float32)), (5, 2, 4, z4(8, np.float32)),
+                                                            (0, 2, 4, z4(8, np.uint8)), (0, 0, 0, b"")]},
+                    seams={0: (0, 2, 4, z4(8, np.uint8))})
     elif case == "out_zero":
         data = _dat(out=(0, 4))
     elif case == "negative_count":

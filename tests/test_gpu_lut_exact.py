@@ -1,0 +1,126 @@
+"""Bit-exact GPU LUT build (MapperTemplate::add_input, template.cpp:46-153).
+
+The FP64 LUT kernel evaluates every pixel with device libm (OCML); where a last-ulp difference from
+glibc could change the outcome (a branch threshold, the [0, 1) test, a mask index, the f32 rounding),
+its guard defers the pixel to the host, which recomputes it with glibc (camera_math.hpp LutGuard,
+octvr_hip.cpp build_input).  These tests
+  * measure the device-vs-glibc deviation of the FP64 projection on every model and check that the
+    guard's tolerance covers it with a wide margin (every non-deferred pixel rounds identically);
+  * require the whole LUT (ROI, map1, map2, mask, include-mask arbitration) to equal the oracle's bit
+    for bit — the oracle is pinned to the reference's goldens (test_oracle_golden.py), and the golden
+    rigs are compared with the reference's own fixtures directly (test_gpu_parity.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import camera_rigs as R
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+TOL = 2.0 ** -36  # camera_math.hpp kLutGuardTol
+GOLDEN = ["rigA", "rigB", "rigC", "rigD"]
+
+
+def _golden_text(name):
+    with open(os.path.join(O.ROOT, "tests", "golden", name + ".json")) as f:
+        return f.read()
+
+
+def _rig_cases():
+    cases = [("golden_" + n, _golden_text(n), None) for n in GOLDEN]
+    cases += [("in_" + n, json.dumps(r), (512, 256)) for n, r in sorted(R.input_rigs().items())]
+    cases += [("out_" + n, json.dumps(r), (384, 200)) for n, r in sorted(R.output_rigs().items())]
+    cases += [("mask_" + n, json.dumps(R.mask_rigs()[n]), (512, 256)) for n in ("exclude_poly", "png")]
+    return cases
+
+
+def _size(name, text, wh):
+    if wh:
+        return wh
+    z = np.load(os.path.join(O.ROOT, "tests", "golden", name[len("golden_"):] + ".npz"))
+    return tuple(int(v) for v in z["out_size"])
+
+
+def _deviation(ox, text, W, H, inputs):
+    """max |device - host| of the FP64 projection over the pixels the guard does not defer, and the
+    number of deferred pixels; asserts that every non-deferred pixel has the same NaN-ness and f32."""
+    worst, deferred, total = 0.0, 0, 0
+    for i in inputs:
+        dx, dy, frag = ox.debug_project_f64(text, W, H, i, where=0)
+        hx, hy, _ = ox.debug_project_f64(text, W, H, i, where=1)
+        keep = frag == 0
+        deferred += int((~keep).sum())
+        total += keep.size
+        for d, h in ((dx, hx), (dy, hy)):
+            dn, hn = np.isnan(d), np.isnan(h)
+            assert np.array_equal(dn[keep], hn[keep]), (i, int((dn != hn)[keep].sum()))
+            fin = keep & ~dn
+            if fin.any():
+                worst = max(worst, float(np.abs(d[fin] - h[fin]).max()))
+                assert np.array_equal(d[fin].astype(np.float32), h[fin].astype(np.float32)), i
+    return worst, deferred, total
+
+
+@pytest.mark.parametrize("name,text,wh", _rig_cases(), ids=[c[0] for c in _rig_cases()])
+def test_gpu_projection_deviation_inside_guard(product_lib, name, text, wh):
+    W, H = _size(name, text, wh)
+    n = len(json.loads(text)["inputs"])
+    worst, deferred, total = _deviation(product_lib, text, W, H, range(n))
+    print("%s: max |device - glibc| = %.3g (guard tol %.3g), deferred %d of %d pixels" % (name, worst, TOL, deferred, total))
+    assert worst <= TOL / 64, worst  # the guard's margin: >= 64x the largest deviation seen
+    assert deferred <= max(64, total // 200)
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C4"])
+def test_gpu_projection_deviation_bench_rigs(product_lib, cfg):
+    """Full benchmark geometry, first and last camera."""
+    from octvr_amd import synthetic
+    rig, W, H, _ = synthetic.CONFIGS[cfg]()
+    n = len(rig["inputs"])
+    worst, deferred, total = _deviation(product_lib, json.dumps(rig), W, H, [0, n - 1])
+    print("%s: max |device - glibc| = %.3g, deferred %d of %d pixels" % (cfg, worst, deferred, total))
+    assert worst <= TOL / 64, worst
+    assert deferred <= total // 200
+
+
+def _lut_equal(ox, text, W, H, use_roi=True):
+    """GPU MapperTemplate::from_json == oracle lut_build (inputs and overlays), bit for bit."""
+    rig = O.json_loads_rj(text)  # the doubles the product parses (rapidjson rules, json_lite.hpp)
+    mt = ox.MapperTemplate.from_json(text, W, H, use_roi=use_roi)
+    W, H = mt.out_size
+    want = O.lut_build(rig, W, H, use_roi=use_roi, threads=8)
+    n_in = len(rig["inputs"])
+    got = [mt.input(i)[:4] for i in range(n_in)] + [mt.overlay(i)[:4] for i in range(mt.num_overlays)]
+    assert len(got) == len(want)
+    for k, ((groi, g1, g2, gm), (roi, w1, w2, wm)) in enumerate(zip(got, want)):
+        assert groi == tuple(roi), (k, groi, roi)
+        assert np.array_equal(gm, wm), (k, int((gm != wm).sum()))
+        assert np.array_equal(g1.view(np.int32), w1.view(np.int32)), (k, int((g1.view(np.int32) != w1.view(np.int32)).sum()))
+        assert np.array_equal(g2.view(np.int32), w2.view(np.int32)), (k, int((g2.view(np.int32) != w2.view(np.int32)).sum()))
+    return mt, want
+
+
+@pytest.mark.parametrize("name,text,wh", _rig_cases(), ids=[c[0] for c in _rig_cases()])
+def test_gpu_lut_bit_exact_vs_oracle(product_lib, name, text, wh):
+    W, H = _size(name, text, wh)
+    _lut_equal(product_lib, text, W, H, use_roi=not name.endswith("rigD"))
+
+
+@pytest.mark.parametrize("name", sorted(R.mask_rigs()))
+@pytest.mark.parametrize("use_roi", [False, True])
+def test_gpu_lut_bit_exact_masks_and_arbitration(product_lib, name, use_roi):
+    """selection / exclude / include masks (polygons, PNG) and the include-mask visibility arbitration
+    across inputs and overlays (camera.cpp:96-187, 212-294; template.cpp:86-116)."""
+    _lut_equal(product_lib, json.dumps(R.mask_rigs()[name]), 512, 256, use_roi=use_roi)
+
+
+def test_gpu_lut_recomputed_count(product_lib):
+    """The deferred pixels are a small minority (the device does the build) and are reported."""
+    from octvr_amd import synthetic
+    rig, W, H, _ = synthetic.CONFIGS["C2"]()
+    mt = product_lib.MapperTemplate.from_json(json.dumps(rig), 1920, 960)
+    n = [mt.lut_recomputed(i) for i in range(len(mt))]
+    print("C2 rig at 1920x960: recomputed on the host per camera:", n)
+    assert all(0 <= k <= 1920 * 960 // 200 for k in n)

@@ -1,7 +1,8 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle and the reference goldens.
 
-Bars: integer / byte outputs bit-exact; the FP64 LUT bit-exact against the reference
-except where device libm (OCML) and glibc differ in the last ulp — counted and bounded below.
+Bar: bit-exact everywhere — integer / byte outputs, and the FP64 LUT build too (the
+device defers every pixel a last-ulp OCML / glibc difference could change to the host, which
+recomputes it with glibc: tests/test_gpu_lut_exact.py).
 """
 import json
 import math
@@ -43,16 +44,10 @@ def test_gpu_lut_build_vs_reference(ox, name):
         roi, m1, m2, mk, _ = mt.input(i)
         assert roi == tuple(z["rois"][i])
         g1, g2, gm = z[f"map1_{i}"], z[f"map2_{i}"], z[f"mask_{i}"]
-        d1 = m1.view(np.int32) != g1.view(np.int32)
-        d2 = m2.view(np.int32) != g2.view(np.int32)
-        dm = mk != gm
-        # OCML vs glibc: at most a handful of last-ulp f64 differences survive the f32 rounding
-        assert dm.sum() <= 2, (i, int(dm.sum()))
-        assert d1.sum() + d2.sum() <= max(4, m1.size // 20000), (i, int(d1.sum()), int(d2.sum()))
-        both = (~dm) & (gm > 0)
-        ulp1 = np.abs(m1.view(np.int32)[both].astype(np.int64) - g1.view(np.int32)[both])
-        ulp2 = np.abs(m2.view(np.int32)[both].astype(np.int64) - g2.view(np.int32)[both])
-        assert ulp1.max(initial=0) <= 1 and ulp2.max(initial=0) <= 1
+        # the reference's own LUT, bit for bit (no mask flips, no ulp differences)
+        assert np.array_equal(mk, gm), (i, int((mk != gm).sum()))
+        assert np.array_equal(m1.view(np.int32), g1.view(np.int32)), (i, int((m1.view(np.int32) != g1.view(np.int32)).sum()))
+        assert np.array_equal(m2.view(np.int32), g2.view(np.int32)), (i, int((m2.view(np.int32) != g2.view(np.int32)).sum()))
 
 
 @pytest.mark.parametrize("name", RIGS)
@@ -296,8 +291,7 @@ def c2(ox):
 
 def test_gpu_c2_lut_rows_vs_oracle(ox, c2):
     rig, W, H, sizes, mt = c2
-    bad = 0
-    total = 0
+    rig = O.json_loads_rj(json.dumps(rig))
     for i in (0, 3):
         roi, m1, m2, mk, _ = mt.input(i)
         for y0 in (0, 1237, 1919, 3830):
@@ -307,9 +301,8 @@ def test_gpu_c2_lut_rows_vs_oracle(ox, c2):
             g1[:, roi[0]:roi[0] + roi[2]] = m1[sl]
             g2 = np.zeros_like(r2) - 1
             g2[:, roi[0]:roi[0] + roi[2]] = m2[sl]
-            bad += int((g1.view(np.int32) != r1.view(np.int32)).sum() + (g2.view(np.int32) != r2.view(np.int32)).sum())
-            total += r1.size * 2
-    assert bad <= max(4, total // 20000), (bad, total)
+            assert np.array_equal(g1.view(np.int32), r1.view(np.int32)), (i, y0)
+            assert np.array_equal(g2.view(np.int32), r2.view(np.int32)), (i, y0)
 
 
 def test_gpu_c2_stitch_row_bands_vs_oracle(ox, c2):
@@ -410,3 +403,78 @@ def test_gpu_multiband_bit_exact(ox, name, blend):
         np.testing.assert_array_equal(g_gpu, g_orc)
         d = got != want
         assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_gpu_gain_feed_tight_pitch_last_chroma_cell(ox, k):
+    """the gain feed reads 8-byte row segments through a frame-sized buffer resource whose
+    range check drops whole dwords; with a tight pitch (pitch == w) and w/2 not a multiple of 4 the
+    last V row ends mid-dword.  Width 100 (w/2 = 50), 4 cameras whose samples reach the bottom-right
+    chroma cell: gains (full feed, k = 1; lean feed, k = 2) and output bit-exact vs the oracle."""
+    import torch
+    from octvr_amd import synthetic
+    n, w, h = 4, 100, 76
+    rig = synthetic.fisheye_rig(w, h, [2 * math.pi * i / n for i in range(n)], [0.2 * (-1) ** i for i in range(n)],
+                                circular=False)
+    W, H = 256, 128
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
+    rois, maps1, maps2, masks = [], [], [], []
+    for i in range(n):
+        roi, m1, m2, mk, _ = mt.input(i)
+        rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk)
+    # at this output size the working scale is 1: every pixel of a pairwise intersection is a sample;
+    # make sure some sample's taps touch the last chroma row's last cell (x >= w - 2, y >= h - 2)
+    hit = False
+    for i in range(n):
+        for j in range(n):
+            if i == j:
+                continue
+            (xi, yi, wi, hi), (xj, yj, wj, hj) = rois[i], rois[j]
+            x0, y0, x1, y1 = max(xi, xj), max(yi, yj), min(xi + wi, xj + wj), min(yi + hi, yj + hj)
+            if x0 >= x1 or y0 >= y1:
+                continue
+            both = (masks[i][y0 - yi:y1 - yi, x0 - xi:x1 - xi] > 0) & (masks[j][y0 - yj:y1 - yj, x0 - xj:x1 - xj] > 0)
+            mx = maps1[i][y0 - yi:y1 - yi, x0 - xi:x1 - xi] * w
+            my = maps2[i][y0 - yi:y1 - yi, x0 - xi:x1 - xi] * h
+            hit |= bool((both & (mx >= w - 2) & (my >= h - 2)).any())
+    assert hit
+    m = ox.Mapper(mt, [(w, h)] * n, blend=0, enable_gain=True)
+    m.set_frames_in_flight(k)
+    frames = [synthetic.smooth_yuv_frame(w, h, 40 + i) for i in range(n)]
+    for f in frames:  # a distinctive last V byte: a zeroed dword would change the norm
+        f[-1, -1] = 250
+        f[-1, w // 2 - 1] = 3
+    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    dev = [torch.from_numpy(np.ascontiguousarray(f)).cuda() for f in frames]
+    assert all(t.stride(0) == w for t in dev)
+    m.stitch(dev, out)
+    torch.cuda.synchronize()
+    want, g_orc = O.stitch_frame(frames, [(w, h)] * n, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None)
+    np.testing.assert_array_equal(np.array(m.gains()), np.array(g_orc))
+    assert np.array_equal(out.cpu().numpy(), want)
+
+
+def test_gpu_kernel_busy_log(ox):
+    """octvr_mapper_kernel_busy (the bench's roofline timing): busy <= span, one logged launch per
+    timed stitch, and the log resets."""
+    import torch
+    from octvr_amd import synthetic
+    rig = _ring_rig(6)
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), 512, 256)
+    m = ox.Mapper(mt, [(320, 240)] * 6, blend=0, enable_gain=True)
+    m.set_frames_in_flight(2)
+    frames = [_cuda(synthetic.yuv_frame(320, 240, 9 + i)) for i in range(6)]
+    outs = [torch.zeros((384, 512), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    assert m.kernel_busy()[2] == 0  # empty log
+    m.set_timing(1)
+    for f in range(6):
+        m.stitch(frames, outs[f % 2], stream=streams[f % 2])
+    span, busy, launches = m.kernel_busy()
+    assert launches == 6 and 0 < busy <= span + 1e-9
+    assert m.kernel_busy() == (0.0, 0.0, 0)  # reset
+    m.set_timing(2)  # every 2nd stitch
+    for f in range(6):
+        m.stitch(frames, outs[f % 2], stream=streams[f % 2])
+    assert m.kernel_busy()[2] == 3
+    m.set_timing(0)
