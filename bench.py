@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: independent frame sets stitched round-robin on this many streams "
                          "(octvr_mapper_set_frames_in_flight)")
+    ap.add_argument("--no-async-e2e", action="store_true",
+                    help="skip the AsyncMultiMapper end-to-end (PCIe-inclusive) measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args()
 
@@ -91,6 +93,61 @@ def timed_region(step, steps, sync, dist=None):
 def aggregate_mps(world, steps, frame_px, elapsed):
     """Whole-job throughput: every rank stitched `steps` frames of `frame_px` output pixels."""
     return world * steps * frame_px / 1e6 / elapsed
+
+
+def lib_sha256():
+    import hashlib
+    p = os.path.join(ROOT, "opencv-octvr_amd", "lib", "liboctvr_hip.so")
+    with open(p, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def pmc_traffic(config, blend):
+    """(bytes, source) — per composite launch (blend 0) or per frame over the whole blend sequence
+    (blend > 0) — from the profiles/*_pmc_<config>.json whose so_sha256 is the running library's;
+    (None, reason) when no summary of this binary exists."""
+    import glob
+    sha = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % config))):
+        d = json.load(open(path))
+        if d.get("so_sha256") != sha:
+            continue
+        if blend > 0:
+            return round(d["traffic_per_frame_bytes"]), os.path.basename(path)
+        hit = [v for k, v in d.get("traffic_bytes", {}).items() if "stitch_tiled_kernel" in k]
+        if hit:
+            return round(hit[0]), os.path.basename(path)
+    return None, "no PMC summary of this liboctvr_hip.so (sha256 %s...)" % sha[:12]
+
+
+def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
+    """AsyncMultiMapper end to end (async.cpp:32-193): host YUV420P planes pushed, copied into pinned
+    staging, uploaded, stitched, downloaded and copied out, 3 frames in flight (the reference's
+    BUF_SIZE, async.cpp:261-310).  PCIe-inclusive: reported beside `value`, never as it."""
+    import numpy as np
+    am = ox.AsyncMultiMapper([mt], sizes, (W, H), [blend], [0], [(0.0, 0.0, 1.0, 1.0)], device=dev)
+    ins = [(f[:h], f[h:, :w // 2], f[h:, w // 2:]) for f, (w, h) in zip(frames_np, sizes)]
+    outs = [(np.empty((H, W), np.uint8), np.empty((H // 2, W // 2), np.uint8), np.empty((H // 2, W // 2), np.uint8))
+            for _ in range(4)]
+
+    def run(n):
+        for k in range(n):
+            am.push(ins, outs[k % 4])
+            if am.pending() >= 3:
+                am.pop()
+        while am.pending():
+            am.pop()
+
+    run(4)  # warm-up: pinned buffers, first-touch
+    t0 = time.perf_counter()
+    run(frames)
+    dt = time.perf_counter() - t0
+    am.close()
+    in_b = sum(w * h * 3 // 2 for w, h in sizes)
+    return {"value": round(frames * W * H / 1e6 / dt, 1), "unit": "MP/s", "ms_per_frame": round(dt * 1e3 / frames, 3),
+            "frames": frames, "h2d_bytes_per_frame": in_b, "d2h_bytes_per_frame": W * H * 3 // 2,
+            "note": "AsyncMultiMapper push->pop of host YUV420P planes: copy-in to pinned staging, H2D, stitch, "
+                    "D2H, copy-out, 3 frames in flight; PCIe- and host-copy-inclusive, not the roofline basis"}
 
 
 def cpu_baseline(mt, frames_np, sizes, W, H, blend=0):
@@ -200,15 +257,10 @@ def main():
         f = sum(4.0 ** -l for l in range(1, int(math.ceil(math.log(blend) / math.log(2.)) - 1) + 1))
         survey_b_alg += 12.0 * f * frame_px + 4.0 * f * n_valid
 
-    # HBM traffic of the dominant kernel from the committed PMC summary of this configuration
-    # (scripts/pmc.sh + scripts/pmc_summary.py; rocprofv3 cannot wrap the process that reads it)
-    traffic = None
-    import glob
-    pmc = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % args.config)))
-    if pmc and blend == 0:
-        tb = json.load(open(pmc[-1])).get("traffic_bytes", {})
-        hit = [v for k, v in tb.items() if "stitch_tiled_kernel" in k]
-        traffic = round(hit[0]) if hit else None
+    # HBM traffic of the dominant kernel(s) from the committed PMC summary of THIS binary and config
+    # (scripts/pmc.sh + scripts/pmc_summary.py record the sha256 of the profiled liboctvr_hip.so;
+    # rocprofv3 cannot wrap the process that reads the counters)
+    traffic, traffic_src = pmc_traffic(args.config, blend)
     ncam = len(sizes)
     result = {
         "metric": "stitched megapixels/sec (6x4K->8K equirect)" if args.config in ("C2", "C3") else
@@ -231,7 +283,7 @@ def main():
                                    if blend > 0 else "no-blend composite"),
                    "rigs_per_gpu": 1, "frames_in_flight": inflight, "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "multiband sequence (remap, pyrDown, blend levels)" if blend > 0 else "stitch_kernel",
                      "kernel_us": round(avg_kernel_s * 1e6, 2),
                      "kernel_us_basis": ("union of the launches' HIP-event intervals over %d in-flight streams, per launch"
@@ -249,6 +301,8 @@ def main():
            if serial else {}),
         "mapper": m.info(),
     }
+    if rank == 0 and world == 1 and not args.no_async_e2e:
+        result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend)
     if rank == 0:

@@ -72,8 +72,25 @@ int octvr_stream_sync(void* stream);
  * by a gfx950 FP64 kernel.  out_w/out_h <= 0 derive from the output aspect ratio (template.cpp:32-38).
  * Seam masks are NOT built here (see octvr_rig_create_masks). */
 int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, int device, octvr_rig** rig);
+/* MapperTemplate(to, to_opts, width, height) (template.cpp:23-44): an empty template with the output
+ * camera `out_type` and its options object (JSON text); width / height <= 0 derive from the output
+ * aspect ratio.  flags: OCTVR_JSON_EXACT = numbers are correctly rounded (text printed from doubles with
+ * 17 digits); 0 = rapidjson 1.0.2's own number rules, as the reference parses a config file. */
+#define OCTVR_JSON_EXACT 1
+int octvr_rig_create(const char* out_type, const char* out_opts_json, int out_w, int out_h, int device, int flags,
+                     octvr_rig** rig);
+/* MapperTemplate::add_input(from, from_opts, overlay, use_roi) (template.cpp:46-153): builds input (or
+ * overlay) LUT on the rig's device; include masks clear earlier inputs' masks (visible_mask).  Existing
+ * seam masks are dropped (create_masks again). */
+int octvr_rig_add_input(octvr_rig* rig, const char* type, const char* opts_json, int overlay, int use_roi, int flags);
 /* MapperTemplate(std::ifstream&) — VRv11 reader (template.cpp:258-314). */
 int octvr_rig_load_dat(const char* path, octvr_rig** rig);
+/* The same reader / MapperTemplate::dump writer over caller streams: read(ctx, buf, n) returns the bytes
+ * read (0 = end), write(ctx, data, n) returns n on success. */
+typedef size_t (*octvr_read_fn)(void* ctx, void* buf, size_t n);
+typedef size_t (*octvr_write_fn)(void* ctx, const void* data, size_t n);
+int octvr_rig_load_stream(octvr_read_fn read, void* ctx, octvr_rig** rig);
+int octvr_rig_dump_stream(octvr_rig* rig, octvr_write_fn write, void* ctx);
 /* MapperTemplate::dump — VRv11 writer, byte-compatible (template.cpp:206-256).  Like the reference,
  * creates the seam masks first when the rig has none (template.cpp:209-210). */
 int octvr_rig_dump_dat(octvr_rig* rig, const char* path);
@@ -85,6 +102,11 @@ int octvr_rig_create_masks(octvr_rig* rig, int device);
 int octvr_rig_create_from_arrays(int out_w, int out_h, int n_inputs, const int* rois, const float* const* map1,
                                  const float* const* map2, const uint8_t* const* masks,
                                  const uint8_t* const* seam_masks_or_null, octvr_rig** rig);
+/* inputs[i].vignette (overlay = 0) or overlay_inputs[i].vignette: a w x h f32 gain map, or none
+ * (map NULL, w = h = 0).  Overlay i of a rig made from arrays: */
+int octvr_rig_set_vignette(octvr_rig* rig, int i, int overlay, const float* map, int w, int h);
+int octvr_rig_add_overlay_arrays(octvr_rig* rig, const int* roi, const float* map1, const float* map2,
+                                 const uint8_t* mask);
 int octvr_rig_num_inputs(const octvr_rig* rig, int* n);
 int octvr_rig_out_size(const octvr_rig* rig, int* w, int* h);
 int octvr_rig_get_input(const octvr_rig* rig, int i, octvr_input_view* view);
@@ -123,6 +145,12 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
  * (GainCompensatorGPU::feed), else set_gains (n_gains == n_inputs).  Stream-ordered, no host sync. */
 int octvr_mapper_stitch_yuv420p(octvr_mapper* mapper, const uint8_t* const* in_dev, const size_t* in_pitch,
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream);
+/* The same with Mapper::stitch's preview_output (mapper.cpp:308-312): the RGB result resized
+ * (cuda::resize INTER_LINEAR) into a preview_w x preview_h CV_8UC3 device image (3 bytes per pixel,
+ * row pitch preview_pitch); preview_dev NULL = none.  Needs one frame in flight. */
+int octvr_mapper_stitch_preview(octvr_mapper* mapper, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                uint8_t* out_dev, size_t out_pitch, uint8_t* preview_dev, int preview_w, int preview_h,
+                                size_t preview_pitch, const double* gains, int n_gains, void* stream);
 /* Mapper::gains() (mapper.hpp:88-90): gains used by the last stitch (synchronizes the stream). */
 int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
 /* Frames in flight (no reference counterpart: vr::Mapper is not re-entrant, and AsyncMultiMapper

@@ -122,6 +122,8 @@ struct octvr_rig {
     bool out_cam_masks = false;  // the output camera has exclude / include masks (not kept)
     octvr::CameraParams out_cam{};
     std::vector<octvr::CameraParams> cams;
+    // MapperTemplate::visible_mask (octvr.hpp:67) on the device, allocated once an include mask appears
+    octvr::DevBuf<uint8_t> visible;
 };
 
 namespace octvr {
@@ -135,8 +137,15 @@ int rig_morph_controlpoints(octvr_rig& rig, const JsonValue& control_points);
 void chamfer_l2_3x3(const uint8_t* src, int w, int h, float* dist);
 
 // ---- mapper internals used by the AsyncMultiMapper pipeline (octvr_hip.cpp, async.cpp) -----------
+// preview_output of Mapper::stitch (mapper.cpp:308-312): a CV_8UC3 device image
+struct PreviewOut {
+    uint8_t* dev;
+    int w, h;
+    size_t pitch;
+};
 void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch, uint8_t* out_dev,
-                   size_t out_pitch, const double* gains, int n_gains, const double* gains_dev, hipStream_t s);
+                   size_t out_pitch, const double* gains, int n_gains, const double* gains_dev, hipStream_t s,
+                   const PreviewOut* preview = nullptr);
 int mapper_num_inputs(const octvr_mapper* m);
 bool mapper_has_gain(const octvr_mapper* m);
 const double* mapper_gains_dev(const octvr_mapper* m);

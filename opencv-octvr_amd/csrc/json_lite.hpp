@@ -58,7 +58,9 @@ struct JsonValue {
 
 class JsonParser {
 public:
-    explicit JsonParser(const std::string& s) : s_(s), i_(0) {}
+    // exact: numbers correctly rounded (strtod) instead of rapidjson's rules — for text written from
+    // doubles with 17 significant digits (the C++ API's rapidjson::Value overloads, OCTVR_JSON_EXACT)
+    explicit JsonParser(const std::string& s, bool exact = false) : s_(s), i_(0), exact_(exact) {}
     JsonValue parse() {
         JsonValue v = value();
         ws();
@@ -69,6 +71,7 @@ public:
 private:
     const std::string& s_;
     size_t i_;
+    bool exact_;
 
     [[noreturn]] void fail(const char* what) {
         throw std::runtime_error(std::string("json parse error: ") + what + " at offset " + std::to_string(i_));
@@ -131,7 +134,15 @@ private:
             v.kind = JsonValue::Null;
         } else {
             v.kind = JsonValue::Number;
-            v.num = number();
+            if (exact_) {
+                const char* b = s_.c_str() + i_;
+                char* e = nullptr;
+                v.num = strtod(b, &e);
+                if (e == b) fail("bad number");
+                i_ += (size_t)(e - b);
+            } else {
+                v.num = number();
+            }
         }
         return v;
     }
@@ -261,6 +272,6 @@ private:
     }
 };
 
-inline JsonValue json_parse(const std::string& s) { return JsonParser(s).parse(); }
+inline JsonValue json_parse(const std::string& s, bool exact = false) { return JsonParser(s, exact).parse(); }
 
 }  // namespace octvr

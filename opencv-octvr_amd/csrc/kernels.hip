@@ -813,7 +813,7 @@ struct StageSlot {
 
 __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, int c) {
     StageSlot s;
-    const uint32_t nchunks = m.t < t_end ? ((m.nslots >> 8) & 0xFFu) : 0u;
+    const uint32_t nchunks = (uint32_t)m.t < (uint32_t)t_end ? ((m.nslots >> 8) & 0xFFu) : 0u;
     const int nslots = (int)(m.nslots & 0xFFu);
     s.live = (uint32_t)c < nchunks ? 1u : 0u;
     int q = 0;
@@ -829,6 +829,8 @@ __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, in
     s.by0 = d2 >> 16;
     s.chunk0 = d3 & 0xFFFFu;
     s.f = kernarg_frame(s.cam);
+    // a camera slot without a frame (metadata that is not this launch's) stages nothing
+    if (!s.f.yuv) s.live = 0u;
     return s;
 }
 
@@ -906,8 +908,15 @@ __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rg
         b.z = vig_mul(b.z, sg.g1.z);
         b.w = vig_mul(b.w, sg.g1.w);
     }
+#if OCTVR_STAGE_B64
+    *reinterpret_cast<uint2*>(s_rgb + sg.dst) = make_uint2(a.x, a.y);
+    *reinterpret_cast<uint2*>(s_rgb + sg.dst + 2) = make_uint2(a.z, a.w);
+    *reinterpret_cast<uint2*>(s_rgb + sg.dst + 4) = make_uint2(b.x, b.y);
+    *reinterpret_cast<uint2*>(s_rgb + sg.dst + 6) = make_uint2(b.z, b.w);
+#else
     *reinterpret_cast<uint4*>(s_rgb + sg.dst) = a;
     *reinterpret_cast<uint4*>(s_rgb + sg.dst + 4) = b;
+#endif
 }
 
 #ifndef OCTVR_STITCH_BLOCKS_PER_CU
@@ -966,7 +975,7 @@ constexpr int kStageRegs = OCTVR_STAGE_REGS;
 //
 __device__ __forceinline__ uint4 meta_issue(const TiledLut& lut, int t, int t_end) {  // t: staged item
     const int lane = threadIdx.x & 63;
-    const int tt = t < t_end ? t : 0;
+    const int tt = (uint32_t)t < (uint32_t)t_end ? t : 0;  // unsigned: a negative index is out of range too
     uint4 v;
     if (lane < 1 + kTileSlots)  // exec-masked: the instruction (and its vmcnt) is the same for every wave
         v = lane == 0 ? *reinterpret_cast<const uint4*>(lut.hdr + tt)
@@ -997,7 +1006,7 @@ struct TileData {
 template <bool DWORD_STAGE, bool VIG, int Q, int R>
 __device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& m, int t_end,
                                            const StageSlot (&sl)[R], TileData<Q, R>& d) {
-    const bool live = m.t < t_end;
+    const bool live = (uint32_t)m.t < (uint32_t)t_end;
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
 #pragma unroll
@@ -1270,7 +1279,14 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         // the item two ahead: static on the first iteration, else the claim handed over above
         if (!first) {
 #if OCTVR_DYN
-            const int v = claimed ? dyn0 + (int)uniform((int)s_claim[par]) : t_end;
+            // Global addresses derive from this LDS-handed claim (the item's header, slots and entries,
+            // and through its slots the camera frames), so it is range-checked as unsigned: a value that
+            // is not a claim of this band (the r02 barrier-free ablation read s_claim before wave 0 wrote
+            // it, i.e. uninitialised LDS -> negative item index -> out-of-range header and entry loads and
+            // a null frame pointer, hipErrorIllegalAddress) ends the sequence instead.
+            const uint32_t cv = (uint32_t)uniform((int)s_claim[par]);
+            const int room = t_end - dyn0;
+            const int v = claimed && room > 0 && cv < (uint32_t)room ? dyn0 + (int)cv : t_end;
 #else  // static dealing (round-robin over the band's workgroups)
             const int v = t_n2 < t_end ? t_n2 + step : t_end;
 #endif
@@ -1753,6 +1769,51 @@ hipError_t launch_resize_rgba_yuv420(const uint8_t* rgba, int sw, int sh, int64_
     const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     hipLaunchKernelGGL(resize_rgba_yuv420_kernel, dim3(blocks), dim3(256), 0, s, rgba, sw, sh, spitch, fx, fy, out, dw,
                        dh, out_pitch);
+    return hipGetLastError();
+}
+
+// Preview output (mapper.cpp:308-312): cv::cuda::resize(result, preview_output, preview_size,
+// INTER_LINEAR) of the RGB result into a CV_8UC3 image — the same glob-kernel arithmetic as above,
+// one lane per preview pixel, 3 bytes out.
+__global__ void __launch_bounds__(256) resize_rgba_rgb_kernel(const uint8_t* __restrict__ rgba, int sw, int sh,
+                                                              int64_t spitch, float fx, float fy, uint8_t* out, int dw,
+                                                              int dh, int64_t out_pitch) {
+    const int64_t total = (int64_t)dw * dh;
+    for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < total; k += (int64_t)gridDim.x * blockDim.x) {
+        const int y = (int)(k / dw), x = (int)(k - (int64_t)y * dw);
+        const float src_x = (float)x * fx, src_y = (float)y * fy;
+        const int x1 = (int)floorf(src_x), y1 = (int)floorf(src_y);
+        const int x2 = x1 + 1, y2 = y1 + 1;
+        const int x2r = min(x2, sw - 1), y2r = min(y2, sh - 1);
+        const uint32_t* r1 = reinterpret_cast<const uint32_t*>(rgba + (int64_t)y1 * spitch);
+        const uint32_t* r2 = reinterpret_cast<const uint32_t*>(rgba + (int64_t)y2r * spitch);
+        const uint32_t c00 = r1[x1], c01 = r1[x2r], c10 = r2[x1], c11 = r2[x2r];
+        const float w00 = ((float)x2 - src_x) * ((float)y2 - src_y);
+        const float w01 = (src_x - (float)x1) * ((float)y2 - src_y);
+        const float w10 = ((float)x2 - src_x) * (src_y - (float)y1);
+        const float w11 = (src_x - (float)x1) * (src_y - (float)y1);
+        uint8_t* o3 = out + (int64_t)y * out_pitch + 3 * (int64_t)x;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const uint32_t sh8 = 8u * ch;
+            float o = 0.f;
+            o = __builtin_fmaf((float)((c00 >> sh8) & 255u), w00, o);
+            o = __builtin_fmaf((float)((c01 >> sh8) & 255u), w01, o);
+            o = __builtin_fmaf((float)((c10 >> sh8) & 255u), w10, o);
+            o = __builtin_fmaf((float)((c11 >> sh8) & 255u), w11, o);
+            o3[ch] = (uint8_t)sat_u8_rne(o);
+        }
+    }
+}
+
+hipError_t launch_resize_rgba_rgb(const uint8_t* rgba, int sw, int sh, int64_t spitch, uint8_t* out, int dw, int dh,
+                                  int64_t out_pitch, hipStream_t s) {
+    if (dw <= 0 || dh <= 0) return hipErrorInvalidValue;
+    const float fx = (float)(1.0 / ((double)dw / sw)), fy = (float)(1.0 / ((double)dh / sh));
+    const int64_t total = (int64_t)dw * dh;
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
+    hipLaunchKernelGGL(resize_rgba_rgb_kernel, dim3(blocks), dim3(256), 0, s, rgba, sw, sh, spitch, fx, fy, out, dw, dh,
+                       out_pitch);
     return hipGetLastError();
 }
 

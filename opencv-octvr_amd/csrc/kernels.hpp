@@ -83,6 +83,15 @@ constexpr int kTileSlots = 4;
 #endif
 constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
 constexpr int kTileZeroDwords = 4;
+// Staging stores: 2 x 16 bytes per 8-pixel group (row stride a multiple of 4 dwords), or with
+// OCTVR_STAGE_B64 4 x 8 bytes (stride even), so the tiler may pad rows to 2 mod 4 dwords.
+#ifndef OCTVR_STAGE_B64
+#define OCTVR_STAGE_B64 0
+#endif
+constexpr int kStageAlignDwords = OCTVR_STAGE_B64 ? 2 : 4;
+#ifndef OCTVR_LDS_PAD_DEFAULT
+#define OCTVR_LDS_PAD_DEFAULT 0
+#endif
 // Items whose staged boxes fit half the staging LDS alternate between the two halves, so an item is
 // staged while the previous one is still being read (one barrier per item); larger items carry
 // kHdrBigItem in TileHdr::nslots and take the whole buffer behind an extra barrier.
@@ -312,6 +321,11 @@ hipError_t launch_resize_u8(const uint8_t* src, int sw, int sh, int64_t spitch, 
 // pitch spitch bytes, 4 bytes per pixel) to dw x dh (even), then RGB -> YUV420P into `out`.
 hipError_t launch_resize_rgba_yuv420(const uint8_t* rgba, int sw, int sh, int64_t spitch, uint8_t* out, int dw, int dh,
                                      int64_t out_pitch, hipStream_t s);
+
+// Preview output (mapper.cpp:308-312): cuda::resize INTER_LINEAR of the RGB(A) result to a dw x dh
+// CV_8UC3 image (3 bytes per pixel, pitch out_pitch).
+hipError_t launch_resize_rgba_rgb(const uint8_t* rgba, int sw, int sh, int64_t spitch, uint8_t* out, int dw, int dh,
+                                  int64_t out_pitch, hipStream_t s);
 
 hipError_t launch_selftest_sat(const float* in, uint8_t* out, int n, int method, hipStream_t s);
 

@@ -640,7 +640,7 @@ constexpr const char* kDatMagic = "VRv11";
 constexpr int CV_8UC1 = 0, CV_32FC1 = 5;
 
 struct DatWriter {
-    std::ofstream f;
+    std::ostream& f;
     void i64(int64_t v) { f.write(reinterpret_cast<const char*>(&v), 8); }
     void mat(int type, int rows, int cols, const void* data, size_t elem) {
         i64(type);
@@ -662,7 +662,7 @@ struct DatWriter {
 };
 
 struct DatReader {
-    std::ifstream f;
+    std::istream& f;
     int64_t i64() {
         int64_t v = 0;
         f.read(reinterpret_cast<char*>(&v), 8);
@@ -721,6 +721,132 @@ struct DatReader {
         in.vig_h = r;
     }
 };
+
+// std::streambuf over the C ABI's read / write callbacks (octvr_rig_load_stream / dump_stream).
+struct CbOutBuf : std::streambuf {
+    octvr_write_fn fn;
+    void* ctx;
+    char buf[1 << 16];
+    CbOutBuf(octvr_write_fn f, void* c) : fn(f), ctx(c) { setp(buf, buf + sizeof buf); }
+    bool flush_buf() {
+        const size_t n = (size_t)(pptr() - pbase());
+        if (n && fn(ctx, pbase(), n) != n) return false;
+        setp(buf, buf + sizeof buf);
+        return true;
+    }
+    int overflow(int c) override {
+        if (!flush_buf()) return traits_type::eof();
+        if (c != traits_type::eof()) {
+            *pptr() = (char)c;
+            pbump(1);
+        }
+        return traits_type::not_eof(c);
+    }
+    int sync() override { return flush_buf() ? 0 : -1; }
+};
+struct CbInBuf : std::streambuf {
+    octvr_read_fn fn;
+    void* ctx;
+    char buf[1 << 16];
+    CbInBuf(octvr_read_fn f, void* c) : fn(f), ctx(c) { setg(buf, buf, buf); }
+    int underflow() override {
+        const size_t n = fn(ctx, buf, sizeof buf);
+        if (n == 0) return traits_type::eof();
+        setg(buf, buf, buf + n);
+        return traits_type::to_int_type(buf[0]);
+    }
+};
+
+// MapperTemplate::dump body (template.cpp:206-256)
+void dat_write(octvr_rig& rig, std::ostream& os) {
+    if (rig.seam_masks.empty()) rig_create_masks(rig);  // MapperTemplate::dump (template.cpp:209-210)
+    REQUIRE(rig.seam_masks.size() == rig.inputs.size(), "seam mask count does not match the inputs");
+    DatWriter w{os};
+    w.f.write(kDatMagic, 5);
+    w.i64(rig.out_w);
+    w.i64(rig.out_h);
+    w.i64((int64_t)rig.inputs.size());
+    for (auto& in : rig.inputs) w.input(in);
+    for (size_t i = 0; i < rig.seam_masks.size(); i++) {
+        const RigInput& in = rig.inputs[i];
+        w.mat(CV_8UC1, in.roi[3], in.roi[2], rig.seam_masks[i].data(), 1);
+    }
+    w.i64((int64_t)rig.overlays.size());
+    for (auto& in : rig.overlays) w.input(in);
+    w.f.flush();
+    if (!w.f) throw OctvrError(OCTVR_E_IO, "write failed");
+}
+
+// MapperTemplate(std::ifstream&) body (template.cpp:258-314)
+std::unique_ptr<octvr_rig> dat_read(std::istream& is) {
+    DatReader r{is};
+    char magic[5];
+    r.f.read(magic, 5);
+    if (!r.f || strncmp(magic, kDatMagic, 5) != 0)
+        throw OctvrError(OCTVR_E_PARSE, "Invalid data file (version does not match)");
+    auto rig = std::make_unique<octvr_rig>();
+    const int64_t ow = r.i64(), oh = r.i64();
+    if (ow <= 0 || oh <= 0 || ow > 65535 || oh > 65535) throw OctvrError(OCTVR_E_PARSE, ".dat: bad output size");
+    rig->out_w = (int)ow;
+    rig->out_h = (int)oh;
+    int64_t n = r.i64();
+    if (n < 0 || n > kMaxCams) throw OctvrError(OCTVR_E_PARSE, ".dat: bad input count");
+    rig->inputs.resize(n);
+    for (auto& in : rig->inputs) r.input(in, rig->out_w, rig->out_h);
+    rig->seam_masks.resize(n);
+    for (int64_t i = 0; i < n; i++) {
+        int rr, cc;
+        r.mat(CV_8UC1, rr, cc, rig->seam_masks[i]);
+        // MapperTemplate::dump writes one ROI-sized seam mask per input (template.cpp:245-246)
+        if (rig->seam_masks[i].size() != (size_t)rig->inputs[i].roi[2] * (size_t)rig->inputs[i].roi[3])
+            throw OctvrError(OCTVR_E_PARSE, ".dat: seam mask size does not match ROI");
+    }
+    int64_t no = r.i64();
+    if (no < 0 || no > kMaxCams) throw OctvrError(OCTVR_E_PARSE, ".dat: bad overlay count");
+    rig->overlays.resize(no);
+    for (auto& in : rig->overlays) r.input(in, rig->out_w, rig->out_h);
+    return rig;
+}
+
+// MapperTemplate(to, to_opts, w, h) (template.cpp:23-44): the output camera and size
+std::unique_ptr<octvr_rig> rig_new(const JsonValue& oc, int out_w, int out_h, int device) {
+    CameraParams out_cam = camera_from_json(oc);
+    REQUIRE(!(out_h <= 0 && out_w <= 0), "Output width/height invalid");  // template.cpp:32-33
+    double ar = aspect_ratio(oc);
+    if (out_h <= 0) out_h = int(double(out_w) / ar);
+    if (out_w <= 0) out_w = int(double(out_h) * ar);
+    // the output camera needs image_to_obj_single: fisheye / pinhole throw NotImplemented (camera.hpp:101-103)
+    if (out_cam.type == CAM_FISHEYE || out_cam.type == CAM_PINHOLE)
+        throw OctvrError(OCTVR_E_UNSUPPORTED, "output camera type '" + oc["type"].as_string() + "' is not supported");
+    // CV_Assert(crop.size() == size && crop.tl() == Point(0, 0)) (fullframe_fisheye_cam.cpp:224)
+    if (out_cam.type == CAM_FULLFRAME_FISHEYE)
+        REQUIRE(out_cam.crop_x == 0 && out_cam.crop_y == 0 && out_cam.crop_w == out_cam.width &&
+                    out_cam.crop_h == out_cam.height,
+                "fullframe_fisheye output camera: crop must cover the whole image");
+    auto rig = std::make_unique<octvr_rig>();
+    rig->out_w = out_w;
+    rig->out_h = out_h;
+    rig->device = device;
+    // the camera models stay with the rig for add_input / morph_controlpoints
+    rig->has_cameras = true;
+    rig->out_cam = out_cam;
+    rig->out_cam_masks = oc.has("options") && (oc["options"].has("exclude_masks") || oc["options"].has("include_masks"));
+    return rig;
+}
+
+// MapperTemplate::add_input(from, from_opts, overlay, use_roi) (template.cpp:46-153)
+void rig_add(octvr_rig& rig, const JsonValue& cam, bool overlay, bool use_roi) {
+    REQUIRE(rig.has_cameras, "add_input needs a template built from camera models (not a .dat)");
+    REQUIRE(rig.inputs.size() + rig.overlays.size() < (size_t)kMaxCams, "too many inputs");
+    std::vector<RigInput>& dst = overlay ? rig.overlays : rig.inputs;
+    RigInput in;
+    // overlays go through the same add_input: they share visible_mask and their include masks clear
+    // the (non-overlay) inputs' masks (template.cpp:102-116, 147-150)
+    build_input(rig.out_cam, cam, rig.out_w, rig.out_h, use_roi, rig.device, in, &rig.visible, &rig.inputs);
+    dst.push_back(std::move(in));
+    if (!overlay) rig.cams.push_back(camera_from_json(cam));
+    rig.seam_masks.clear();  // one seam mask per input: create_masks again (dump does)
+}
 
 }  // namespace
 
@@ -975,12 +1101,36 @@ static bool lean_feed() {
     return v;
 }
 
+// The RGB(A) result frame of the scaled-output and preview paths (allocated on first use).
+void ensure_result(octvr_mapper& m) {
+    if (m.result.p) return;
+    REQUIRE((uint64_t)m.W * m.H * 4 < 0x7FFFFF80ull, "stitch frame larger than 2 GiB as RGBA");
+    DeviceGuard dg(m.device);
+    // result = 0 (mapper.cpp:156): pixels no camera writes stay black in every frame
+    m.result.alloc((size_t)m.W * m.H * 4);
+    HIP_CHECK(hipMemset(m.result.p, 0, m.result.n));
+    MbCamLevel v{};
+    v.g_off = 0;
+    v.g_pitch = (uint32_t)m.W * 4;
+    v.w = m.W;
+    v.h = m.H;
+    m.result_view.upload(&v, 1);
+}
+
 // Mapper::stitch (mapper.cpp:193-323).  gains_dev (device, n doubles): gains of another mapper of the
 // same inputs, copied stream-ordered (AsyncMultiMapper's gain_modes chaining, async.cpp:78-86).
 void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch, uint8_t* out_dev,
-                   size_t out_pitch, const double* gains, int n_gains, const double* gains_dev, hipStream_t s) {
+                   size_t out_pitch, const double* gains, int n_gains, const double* gains_dev, hipStream_t s,
+                   const PreviewOut* preview) {
     {
         REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
+        if (preview) {
+            REQUIRE(preview->dev && preview->w > 0 && preview->h > 0 && preview->pitch >= (size_t)preview->w * 3,
+                    "bad preview output");
+            // the preview resizes the whole-frame RGB result, which one frame slot owns
+            REQUIRE(m->slots.size() == 1, "preview output needs one frame in flight");
+            ensure_result(*m);
+        }
         REQUIRE(out_pitch >= (size_t)m->SW, "output pitch smaller than width");
         // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
         REQUIRE((uint64_t)out_pitch * (m->SH + m->SH / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
@@ -1051,11 +1201,11 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                 e1 = m->free_events.back().second;
                 m->free_events.pop_back();
             }
-            if (m->scaled || m->mb) HIP_CHECK(hipEventRecord(e0, s));  // the composite records its own
+            if (m->scaled || m->mb || preview) HIP_CHECK(hipEventRecord(e0, s));  // else the composite records its own
         }
-        if (m->scaled) {
+        if (m->scaled || preview) {
             // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
-            // (one frame slot only: the result frame is shared)
+            // (one frame slot only: the result frame is shared); without scaling the resize is the identity
             if (m->mb)
                 multiband_run(*m->mb, 0, fs, sl.gains, m->use_gain, nullptr, 0, s, m->result.p, (int64_t)m->W * 4);
             else
@@ -1063,6 +1213,9 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                                           RgbaOut{m->result.p, (uint32_t)m->result.n, m->result_view.p}, s));
             HIP_CHECK(launch_resize_rgba_yuv420(m->result.p, m->W, m->H, (int64_t)m->W * 4, out_dev, m->SW, m->SH,
                                                 (int64_t)out_pitch, s));
+            if (preview)  // cuda::resize(result, preview_output, ...) (mapper.cpp:308-312)
+                HIP_CHECK(launch_resize_rgba_rgb(m->result.p, m->W, m->H, (int64_t)m->W * 4, preview->dev, preview->w,
+                                                 preview->h, (int64_t)preview->pitch, s));
         } else if (m->mb) {
             multiband_run(*m->mb, k, fs, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s);
         } else {
@@ -1071,7 +1224,7 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             HIP_CHECK(launch_stitch(fs, view, m->W, m->H, sl.gains, m->use_gain, out_dev, (int64_t)out_pitch, s, e0, e1));
         }
         if (timed) {
-            if (m->scaled || m->mb) HIP_CHECK(hipEventRecord(e1, s));
+            if (m->scaled || m->mb || preview) HIP_CHECK(hipEventRecord(e1, s));
             m->events.emplace_back(e0, e1);
         }
         if (!sl.done) HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
@@ -1150,44 +1303,41 @@ int octvr_rig_create_json(const char* json, int out_w, int out_h, int use_roi, i
     return guarded([&] {
         REQUIRE(json && out, "json/out is NULL");
         JsonValue doc = json_parse(json);
-        const JsonValue& oc = doc["output"];
-        CameraParams out_cam = camera_from_json(oc);
-        REQUIRE(!(out_h <= 0 && out_w <= 0), "Output width/height invalid");  // template.cpp:32-33
-        double ar = aspect_ratio(oc);
-        if (out_h <= 0) out_h = int(double(out_w) / ar);
-        if (out_w <= 0) out_w = int(double(out_h) * ar);
-        // the output camera needs image_to_obj_single: fisheye / pinhole throw NotImplemented (camera.hpp:101-103)
-        if (out_cam.type == CAM_FISHEYE || out_cam.type == CAM_PINHOLE)
-            throw OctvrError(OCTVR_E_UNSUPPORTED, "output camera type '" + oc["type"].as_string() + "' is not supported");
-        // CV_Assert(crop.size() == size && crop.tl() == Point(0, 0)) (fullframe_fisheye_cam.cpp:224)
-        if (out_cam.type == CAM_FULLFRAME_FISHEYE)
-            REQUIRE(out_cam.crop_x == 0 && out_cam.crop_y == 0 && out_cam.crop_w == out_cam.width &&
-                        out_cam.crop_h == out_cam.height,
-                    "fullframe_fisheye output camera: crop must cover the whole image");
-        auto rig = std::make_unique<octvr_rig>();
-        rig->out_w = out_w;
-        rig->out_h = out_h;
-        rig->device = device;
+        auto rig = rig_new(doc["output"], out_w, out_h, device);
+        // apps/octvr/dump.cpp:84-93: every input, then every overlay, through add_input
         const JsonValue& ins = doc["inputs"];
-        rig->inputs.resize(ins.size());
-        // the camera models stay with the rig for morph_controlpoints (its masks are not needed there)
-        rig->has_cameras = true;
-        rig->out_cam = out_cam;
-        rig->out_cam_masks = oc.has("options") && (oc["options"].has("exclude_masks") || oc["options"].has("include_masks"));
-        for (size_t i = 0; i < ins.size(); i++) rig->cams.push_back(camera_from_json(ins[i]));
-        DevBuf<uint8_t> visible;  // template.cpp visible_mask, allocated once an include mask appears
-        for (size_t i = 0; i < ins.size(); i++)
-            build_input(out_cam, ins[i], out_w, out_h, use_roi != 0, device, rig->inputs[i], &visible, &rig->inputs);
+        for (size_t i = 0; i < ins.size(); i++) rig_add(*rig, ins[i], false, use_roi != 0);
         if (doc.has("overlays")) {
             const JsonValue& ov = doc["overlays"];
-            rig->overlays.resize(ov.size());
-            for (size_t i = 0; i < ov.size(); i++)
-                // overlays go through the same add_input: they share visible_mask and their include
-                // masks clear the (non-overlay) inputs' masks (template.cpp:102-116, 147-150)
-                build_input(out_cam, ov[i], out_w, out_h, use_roi != 0, device, rig->overlays[i], &visible,
-                            &rig->inputs);
+            for (size_t i = 0; i < ov.size(); i++) rig_add(*rig, ov[i], true, use_roi != 0);
         }
         *out = rig.release();
+    });
+}
+
+// camera {"type": type, "options": opts} from the C++ API's separate type / options arguments
+static JsonValue camera_json(const char* type, const char* opts_json, int flags) {
+    REQUIRE(type && *type, "camera type is empty");
+    for (const char* c = type; *c; c++)
+        REQUIRE((*c >= 'a' && *c <= 'z') || (*c >= '0' && *c <= '9') || *c == '_', "bad camera type");
+    const std::string text = std::string("{\"type\":\"") + type + "\",\"options\":" +
+                             (opts_json && *opts_json ? opts_json : "{}") + "}";
+    return json_parse(text, (flags & OCTVR_JSON_EXACT) != 0);
+}
+
+int octvr_rig_create(const char* out_type, const char* out_opts_json, int out_w, int out_h, int device, int flags,
+                     octvr_rig** out) {
+    return guarded([&] {
+        REQUIRE(out, "out is NULL");
+        auto rig = rig_new(camera_json(out_type, out_opts_json, flags), out_w, out_h, device);
+        *out = rig.release();
+    });
+}
+
+int octvr_rig_add_input(octvr_rig* rig, const char* type, const char* opts_json, int overlay, int use_roi, int flags) {
+    return guarded([&] {
+        REQUIRE(rig, "rig is NULL");
+        rig_add(*rig, camera_json(type, opts_json, flags), overlay != 0, use_roi != 0);
     });
 }
 
@@ -1225,35 +1375,18 @@ int octvr_rig_create_from_arrays(int out_w, int out_h, int n, const int* rois, c
 int octvr_rig_load_dat(const char* path, octvr_rig** out) {
     return guarded([&] {
         REQUIRE(path && out, "path/out is NULL");
-        DatReader r;
-        r.f.open(path, std::ios::binary);
-        if (!r.f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);
-        char magic[5];
-        r.f.read(magic, 5);
-        if (!r.f || strncmp(magic, kDatMagic, 5) != 0)
-            throw OctvrError(OCTVR_E_PARSE, "Invalid data file (version does not match)");
-        auto rig = std::make_unique<octvr_rig>();
-        const int64_t ow = r.i64(), oh = r.i64();
-        if (ow <= 0 || oh <= 0 || ow > 65535 || oh > 65535) throw OctvrError(OCTVR_E_PARSE, ".dat: bad output size");
-        rig->out_w = (int)ow;
-        rig->out_h = (int)oh;
-        int64_t n = r.i64();
-        if (n < 0 || n > kMaxCams) throw OctvrError(OCTVR_E_PARSE, ".dat: bad input count");
-        rig->inputs.resize(n);
-        for (auto& in : rig->inputs) r.input(in, rig->out_w, rig->out_h);
-        rig->seam_masks.resize(n);
-        for (int64_t i = 0; i < n; i++) {
-            int rr, cc;
-            r.mat(CV_8UC1, rr, cc, rig->seam_masks[i]);
-            // MapperTemplate::dump writes one ROI-sized seam mask per input (template.cpp:245-246)
-            if (rig->seam_masks[i].size() != (size_t)rig->inputs[i].roi[2] * (size_t)rig->inputs[i].roi[3])
-                throw OctvrError(OCTVR_E_PARSE, ".dat: seam mask size does not match ROI");
-        }
-        int64_t no = r.i64();
-        if (no < 0 || no > kMaxCams) throw OctvrError(OCTVR_E_PARSE, ".dat: bad overlay count");
-        rig->overlays.resize(no);
-        for (auto& in : rig->overlays) r.input(in, rig->out_w, rig->out_h);
-        *out = rig.release();
+        std::ifstream f(path, std::ios::binary);
+        if (!f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);
+        *out = dat_read(f).release();
+    });
+}
+
+int octvr_rig_load_stream(octvr_read_fn read, void* ctx, octvr_rig** out) {
+    return guarded([&] {
+        REQUIRE(read && out, "read/out is NULL");
+        CbInBuf buf(read, ctx);
+        std::istream is(&buf);
+        *out = dat_read(is).release();
     });
 }
 
@@ -1268,23 +1401,49 @@ int octvr_rig_create_masks(octvr_rig* rig, int device) {
 int octvr_rig_dump_dat(octvr_rig* rig, const char* path) {
     return guarded([&] {
         REQUIRE(rig && path, "rig/path is NULL");
-        if (rig->seam_masks.empty()) rig_create_masks(*rig);  // MapperTemplate::dump (template.cpp:209-210)
-        REQUIRE(rig->seam_masks.size() == rig->inputs.size(), "seam mask count does not match the inputs");
-        DatWriter w;
-        w.f.open(path, std::ios::binary);
-        if (!w.f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);
-        w.f.write(kDatMagic, 5);
-        w.i64(rig->out_w);
-        w.i64(rig->out_h);
-        w.i64((int64_t)rig->inputs.size());
-        for (auto& in : rig->inputs) w.input(in);
-        for (size_t i = 0; i < rig->seam_masks.size(); i++) {
-            const RigInput& in = rig->inputs[i];
-            w.mat(CV_8UC1, in.roi[3], in.roi[2], rig->seam_masks[i].data(), 1);
-        }
-        w.i64((int64_t)rig->overlays.size());
-        for (auto& in : rig->overlays) w.input(in);
-        if (!w.f) throw OctvrError(OCTVR_E_IO, "write failed");
+        if (rig->seam_masks.empty()) rig_create_masks(*rig);  // before opening: no half-written file on error
+        std::ofstream f(path, std::ios::binary);
+        if (!f) throw OctvrError(OCTVR_E_IO, std::string("cannot open ") + path);
+        dat_write(*rig, f);
+    });
+}
+
+int octvr_rig_dump_stream(octvr_rig* rig, octvr_write_fn write, void* ctx) {
+    return guarded([&] {
+        REQUIRE(rig && write, "rig/write is NULL");
+        CbOutBuf buf(write, ctx);
+        std::ostream os(&buf);
+        dat_write(*rig, os);
+    });
+}
+
+int octvr_rig_set_vignette(octvr_rig* rig, int i, int overlay, const float* map, int w, int h) {
+    return guarded([&] {
+        REQUIRE(rig && i >= 0, "bad arguments");
+        std::vector<RigInput>& v = overlay ? rig->overlays : rig->inputs;
+        REQUIRE(i < (int)v.size(), "bad input index");
+        REQUIRE(map ? (w > 0 && h > 0) : (w == 0 && h == 0), "bad vignette size");
+        v[i].vignette.assign(map, map + (size_t)w * h);
+        v[i].vig_w = w;
+        v[i].vig_h = h;
+    });
+}
+
+int octvr_rig_add_overlay_arrays(octvr_rig* rig, const int* roi, const float* map1, const float* map2,
+                                 const uint8_t* mask) {
+    return guarded([&] {
+        REQUIRE(rig && roi && map1 && map2 && mask, "bad arguments");
+        REQUIRE(rig->inputs.size() + rig->overlays.size() < (size_t)kMaxCams, "too many inputs");
+        REQUIRE(roi[0] >= 0 && roi[1] >= 0 && roi[2] > 0 && roi[3] > 0 && roi[0] <= rig->out_w - roi[2] &&
+                    roi[1] <= rig->out_h - roi[3],
+                "ROI outside the output frame");
+        RigInput in;
+        memcpy(in.roi, roi, sizeof in.roi);
+        const size_t k = (size_t)roi[2] * roi[3];
+        in.map1.assign(map1, map1 + k);
+        in.map2.assign(map2, map2 + k);
+        in.mask.assign(mask, mask + k);
+        rig->overlays.push_back(std::move(in));
     });
 }
 
@@ -1461,17 +1620,7 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             }, m->in_w, m->in_h, qpl));
             m->n_tiles = tx_n * ty_n;
         }
-        if (m->scaled) {
-            // result = 0 (mapper.cpp:156): pixels no camera writes stay black in every frame
-            m->result.alloc((size_t)m->W * m->H * 4);
-            HIP_CHECK(hipMemset(m->result.p, 0, m->result.n));
-            MbCamLevel v{};
-            v.g_off = 0;
-            v.g_pitch = (uint32_t)m->W * 4;
-            v.w = m->W;
-            v.h = m->H;
-            m->result_view.upload(&v, 1);
-        }
+        if (m->scaled) ensure_result(*m);
         m->gains.alloc(kMaxCams);
         std::vector<double> ones(kMaxCams, 1.0);
         HIP_CHECK(hipMemcpy(m->gains.p, ones.data(), kMaxCams * sizeof(double), hipMemcpyHostToDevice));
@@ -1491,6 +1640,16 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream) {
     return guarded([&] {
         mapper_stitch(m, in_dev, in_pitch, out_dev, out_pitch, gains, n_gains, nullptr, (hipStream_t)stream);
+    });
+}
+
+int octvr_mapper_stitch_preview(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                uint8_t* out_dev, size_t out_pitch, uint8_t* preview_dev, int preview_w, int preview_h,
+                                size_t preview_pitch, const double* gains, int n_gains, void* stream) {
+    return guarded([&] {
+        const PreviewOut pv{preview_dev, preview_w, preview_h, preview_pitch};
+        mapper_stitch(m, in_dev, in_pitch, out_dev, out_pitch, gains, n_gains, nullptr, (hipStream_t)stream,
+                      preview_dev ? &pv : nullptr);
     });
 }
 

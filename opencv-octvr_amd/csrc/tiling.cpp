@@ -8,6 +8,7 @@
 // pixel as a 4-byte box-relative LDS byte offset + fractions + slot; jobs that do not
 // fit (> 4 cameras, a box > 256 px, or LDS above kTileLdsBytes) become "wide" with 8-byte entries.
 #include <algorithm>
+#include <cstdlib>
 #include <thread>
 #include <vector>
 
@@ -15,6 +16,16 @@
 #include "kernels.hpp"
 
 namespace octvr {
+
+// Dwords added to every staged row (LDS bank spread): a box whose rows are a multiple of 16 dwords
+// apart puts the taps of vertically adjacent source pixels on 2 of the 32 banks.  OCTVR_LDS_PAD
+// overrides it (experiments); rounded up to the staging stores' alignment.
+static uint32_t tile_lds_pad() {
+    int pad = OCTVR_LDS_PAD_DEFAULT;
+    if (const char* e = getenv("OCTVR_LDS_PAD")) pad = atoi(e);
+    pad = std::max(0, std::min(pad, 64));
+    return (uint32_t)((pad + kStageAlignDwords - 1) / kStageAlignDwords * kStageAlignDwords);
+}
 
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
                               const std::vector<int>& in_h, int qpl) {
@@ -28,6 +39,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     std::vector<uint8_t> is_wide(n_jobs, 0);
     std::vector<std::vector<CompositeEntry>> wide_raw(n_jobs);
     const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const uint32_t pad = tile_lds_pad();
     auto work = [&](int tid) {
         struct Px {
             int slot, x0, y0, fxy, mask, nogain;
@@ -108,6 +120,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
                 groups += (uint32_t)(bws[j] * bhs[j] / 4);
             }
+            if (ns > 0) stride += pad;
             uint32_t lds = kTileZeroDwords, chunks = 0;
             for (int j = 0; j < ns && !wide; j++) {
                 ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);

@@ -69,6 +69,8 @@ _lib.octvr_mapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), 
                                      C.c_int, C.c_int, C.POINTER(_VP)]
 _lib.octvr_mapper_stitch_yuv420p.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t,
                                              C.POINTER(C.c_double), C.c_int, _VP]
+_lib.octvr_mapper_stitch_preview.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP, C.c_int,
+                                             C.c_int, C.c_size_t, C.POINTER(C.c_double), C.c_int, _VP]
 _lib.octvr_mapper_gains.argtypes = [_VP, C.POINTER(C.c_double), C.c_int]
 _lib.octvr_mapper_set_frames_in_flight.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
@@ -281,8 +283,10 @@ class Mapper:
         # output frame size: scale_output, or the template's out_size (mapper.cpp:69)
         self.out_size = tuple(scale_output) if scale_output[0] else mt.out_size
 
-    def stitch(self, inputs, output, gains=None, stream=None):
-        """inputs: list of uint8 cuda tensors (1.5H x W "Y over [U|V]"); output likewise."""
+    def stitch(self, inputs, output, gains=None, stream=None, preview=None):
+        """inputs: list of uint8 cuda tensors (1.5H x W "Y over [U|V]"); output likewise.  preview: an
+        optional (h, w, 3) uint8 cuda tensor receiving Mapper::stitch's preview_output (the RGB result
+        resized, mapper.cpp:308-312)."""
         n = len(inputs)
         ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
         pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
@@ -291,8 +295,15 @@ class Mapper:
         if gains is not None:
             g = (C.c_double * len(gains))(*gains)
             ng = len(gains)
-        _check(_lib.octvr_mapper_stitch_yuv420p(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()),
-                                                output.stride(0), g, ng, _stream_ptr(stream)))
+        if preview is None:
+            _check(_lib.octvr_mapper_stitch_yuv420p(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()),
+                                                    output.stride(0), g, ng, _stream_ptr(stream)))
+        else:
+            assert preview.dim() == 3 and preview.shape[2] == 3 and preview.stride(1) == 3 and preview.stride(2) == 1
+            _check(_lib.octvr_mapper_stitch_preview(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()),
+                                                    output.stride(0), C.c_void_p(preview.data_ptr()),
+                                                    preview.shape[1], preview.shape[0], preview.stride(0), g, ng,
+                                                    _stream_ptr(stream)))
 
     def gains(self):
         g = (C.c_double * self.n)()

@@ -1433,6 +1433,9 @@ int orc_stitch_frame(const orc_frame* f) {
         stage_ctx c = {f, 0, NULL, NULL, 1.f, result, rb, re};
         parallel_rows(T, rb / 2, re / 2, out_rows, &c);
     }
+    if (f->preview && f->preview_w > 0 && f->preview_h > 0)  /* mapper.cpp:308-312 */
+        orc_resize_linear_cuda_u8c(result, f->out_w, f->out_h, (size_t)f->out_w * 3, 3, f->preview, f->preview_w,
+                                   f->preview_h, f->preview_pitch);
     for (int i = 0; i < n; i++) free(warped[i]);
     free(warped); free(gains); free(result);
     return rc;
@@ -1464,5 +1467,43 @@ void orc_resize_linear_cuda_f32(const float* src, int sw, int sh, float* dst, in
             o = fmaf(src[(size_t)y2r * sw + x1], (x2 - src_x) * (src_y - y1), o);
             o = fmaf(src[(size_t)y2r * sw + x2r], (src_x - x1) * (src_y - y1), o);
             dst[(size_t)y * dw + x] = o;
+        }
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* A12: CUDA fastRemap's texture bilinear, for measuring its distance from the adopted A13    */
+/* ------------------------------------------------------------------------------------------ */
+/* fast_remap<uchar4> (cudawarping/src/cuda/fast_remap.cu:21-44) through a texture object with
+ * normalized coordinates, clamp addressing, linear filtering and cudaReadModeNormalizedFloat
+ * (cudev/ptr2d/texture.hpp:124-160).  The filtering is CUDA hardware behaviour, not in the reference
+ * repository; modelled after the CUDA Programming Guide's "Texture Fetching" appendix: x = u W - 0.5,
+ * i = floor(x), alpha = frac(x) held with 8 fractional bits (truncated here), taps clamped to the
+ * image, the weighted sum of the normalized texels in f32, then saturate_cast<uchar>(v * 255) (round
+ * half to even).  map1 < 0 -> 0 (fill_zero).  Test infrastructure for the documented A12 tolerance
+ * only: no product path follows these semantics (arithmetic contract). */
+void orc_fast_remap_tex_rgba(const uint8_t* src, int w, int h, size_t spitch, const float* map1, const float* map2,
+                             int mw, int mh, size_t mpitch, uint8_t* dst, size_t dpitch) {
+    for (int y = 0; y < mh; y++)
+        for (int x = 0; x < mw; x++) {
+            float u = map1[(size_t)y * mpitch + x], v = map2[(size_t)y * mpitch + x];
+            uint8_t* o = dst + (size_t)y * dpitch + (size_t)x * 4;
+            if (u < 0) { o[0] = o[1] = o[2] = o[3] = 0; continue; }
+            float xb = u * (float)w - 0.5f, yb = v * (float)h - 0.5f;
+            float fx = floorf(xb), fy = floorf(yb);
+            float a = floorf((xb - fx) * 256.f) / 256.f, b = floorf((yb - fy) * 256.f) / 256.f;
+            int i0 = (int)fx, j0 = (int)fy, i1 = i0 + 1, j1 = j0 + 1;
+            i0 = i0 < 0 ? 0 : i0 > w - 1 ? w - 1 : i0;
+            i1 = i1 < 0 ? 0 : i1 > w - 1 ? w - 1 : i1;
+            j0 = j0 < 0 ? 0 : j0 > h - 1 ? h - 1 : j0;
+            j1 = j1 < 0 ? 0 : j1 > h - 1 ? h - 1 : j1;
+            const uint8_t* t00 = src + (size_t)j0 * spitch + (size_t)i0 * 4;
+            const uint8_t* t10 = src + (size_t)j0 * spitch + (size_t)i1 * 4;
+            const uint8_t* t01 = src + (size_t)j1 * spitch + (size_t)i0 * 4;
+            const uint8_t* t11 = src + (size_t)j1 * spitch + (size_t)i1 * 4;
+            for (int c = 0; c < 4; c++) {
+                float val = (1.f - a) * (1.f - b) * (t00[c] / 255.f) + a * (1.f - b) * (t10[c] / 255.f) +
+                            (1.f - a) * b * (t01[c] / 255.f) + a * b * (t11[c] / 255.f);
+                o[c] = (uint8_t)sat_u8_rne(val * 255.f);
+            }
         }
 }

@@ -161,8 +161,15 @@ typedef struct {
     const float* const* vig;         /* per camera: vignette gains at input size (in_w x in_h) or NULL; may be NULL */
     int scale_w, scale_h;            /* scaled output size (mapper.cpp:69, 290-306); 0,0 = out_w x out_h.  When
                                         set, out_yuv / out_pitch describe the scaled frame and row_begin/end are ignored */
+    uint8_t* preview;                /* preview_output (mapper.cpp:308-312): cuda::resize INTER_LINEAR of the RGB result
+                                        to preview_w x preview_h, u8x3 rows of preview_pitch bytes; NULL = none */
+    int preview_w, preview_h;
+    size_t preview_pitch;
 } orc_frame;
 int orc_stitch_frame(const orc_frame* f);
+/* A12 CUDA fastRemap texture bilinear on RGBA (for the documented A12-vs-A13 tolerance only). */
+void orc_fast_remap_tex_rgba(const uint8_t* src, int w, int h, size_t spitch, const float* map1, const float* map2,
+                             int mw, int mh, size_t mpitch, uint8_t* dst, size_t dpitch);
 
 /* ---- GPU blenders (octvr_oracle_blend.c) ----------------------------------- */
 void orc_fast_pyr_down_u8x4(const uint8_t* src, int sw, int sh, uint8_t* dst, int threads);           /* K2 */

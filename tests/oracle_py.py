@@ -63,6 +63,9 @@ class OrcFrame(C.Structure):
         ("seams", C.POINTER(C.c_void_p)),
         ("vig", C.POINTER(C.c_void_p)),
         ("scale_w", C.c_int), ("scale_h", C.c_int),
+        ("preview", C.c_void_p),
+        ("preview_w", C.c_int), ("preview_h", C.c_int),
+        ("preview_pitch", C.c_size_t),
     ]
 
 
@@ -324,6 +327,19 @@ def remap_u8(src, map1, map2, scale_x, scale_y):
     return dst
 
 
+def fast_remap_tex_rgba(rgba, map1, map2):
+    """A12: CUDA fastRemap texture bilinear (normalized maps) -> u8x4 (oracle model, parity unpinned)."""
+    rgba = np.ascontiguousarray(rgba)
+    h, w = rgba.shape[:2]
+    m1 = np.ascontiguousarray(map1, np.float32)
+    m2 = np.ascontiguousarray(map2, np.float32)
+    mh, mw = m1.shape
+    out = np.zeros((mh, mw, 4), np.uint8)
+    lib().orc_fast_remap_tex_rgba(_p(rgba), w, h, C.c_size_t(w * 4), _p(m1), _p(m2), mw, mh, C.c_size_t(mw), _p(out),
+                                  C.c_size_t(mw * 4))
+    return out
+
+
 def bilinear_tab():
     t = np.zeros(4096, np.int16)
     lib().orc_bilinear_tab(_p(t))
@@ -449,7 +465,9 @@ def gain_feed(rois, warped, masks, out_w, out_h):
 
 
 def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enable_gain=True, gains=None,
-                 threads=1, row_band=None, blend=0, seams=None, vig=None, scale=None):
+                 threads=1, row_band=None, blend=0, seams=None, vig=None, scale=None, preview=None):
+    """One Mapper::stitch -> (YUV420P output, gains); preview=(w, h): also the preview_output image,
+    returned as a third value."""
     n = len(in_yuv)
     keep = []
 
@@ -498,9 +516,15 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
         vig = [None if v is None else np.ascontiguousarray(v, np.float32) for v in vig]
         keep.append(vig)
         f.vig = arr(C.c_void_p, [None if v is None else v.ctypes.data for v in vig])
+    pv = None
+    if preview:
+        pv = np.zeros((preview[1], preview[0], 3), np.uint8)
+        f.preview = pv.ctypes.data
+        f.preview_w, f.preview_h = preview
+        f.preview_pitch = preview[0] * 3
     rc = lib().orc_stitch_frame(C.byref(f))
     assert rc == 0
-    return out, gout
+    return (out, gout, pv) if preview else (out, gout)
 
 
 def fastmapper_nv12(in_nv12, in_sizes, map1s, map2s, masks, out_w, out_h):

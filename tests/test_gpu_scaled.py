@@ -50,3 +50,40 @@ def test_gpu_scaled_output_rejects_odd_size(product_lib):
     for bad in ((511, 256), (512, 0), (0, 256)):
         with pytest.raises(ox.OctvrError):
             ox.Mapper(mt, [(256, 144)] * 2, scale_output=bad)
+
+
+@pytest.mark.parametrize("scale", [None, (384, 192)])
+@pytest.mark.parametrize("blend", [0, 16, -5])
+def test_gpu_preview_output_bit_exact(product_lib, blend, scale):
+    """Mapper::stitch's preview_output (mapper.cpp:308-312): the RGB result (before any output scaling)
+    resized with cuda::resize INTER_LINEAR into a CV_8UC3 image — and the YUV output unchanged by it."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    rig, z = O.load_rig("rigB")
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    sizes = [(rig["inputs"][i]["options"]["width"], rig["inputs"][i]["options"]["height"]) for i in range(n)]
+    maps1 = [z[f"map1_{i}"] for i in range(n)]
+    maps2 = [z[f"map2_{i}"] for i in range(n)]
+    masks = [z[f"mask_{i}"] for i in range(n)]
+    seams = [z[f"seam_{i}"] for i in range(n)]
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks, seams)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, scale_output=scale)
+    sw, sh = scale or (W, H)
+    frames = [synthetic.smooth_yuv_frame(w, h, 900 + i) for i, (w, h) in enumerate(sizes)]
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    for pw, ph in ((320, 180), (W, H), (1000, 500)):
+        out = torch.zeros((sh * 3 // 2, sw), dtype=torch.uint8, device="cuda")
+        pv = torch.zeros((ph, pw, 3), dtype=torch.uint8, device="cuda")
+        m.stitch(dev, out, preview=pv)
+        plain = torch.zeros_like(out)
+        m.stitch(dev, plain)
+        torch.cuda.synchronize()
+        want, _, want_pv = O.stitch_frame(frames, sizes, z["rois"].tolist(), maps1, maps2, masks, W, H,
+                                          enable_gain=True, blend=blend, seams=seams, threads=8, scale=scale,
+                                          preview=(pw, ph))
+        assert np.array_equal(out.cpu().numpy(), want)
+        assert torch.equal(out, plain)
+        d = pv.cpu().numpy() != want_pv
+        assert not d.any(), ((pw, ph), int(d.sum()))
