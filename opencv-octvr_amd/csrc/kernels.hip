@@ -813,7 +813,7 @@ struct StageSlot {
 
 __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, int c) {
     StageSlot s;
-    const uint32_t nchunks = (uint32_t)m.t < (uint32_t)t_end ? ((m.nslots >> 8) & 0xFFu) : 0u;
+    const uint32_t nchunks = m.t < t_end ? ((m.nslots >> 8) & 0xFFu) : 0u;
     const int nslots = (int)(m.nslots & 0xFFu);
     s.live = (uint32_t)c < nchunks ? 1u : 0u;
     int q = 0;
@@ -829,8 +829,6 @@ __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, in
     s.by0 = d2 >> 16;
     s.chunk0 = d3 & 0xFFFFu;
     s.f = kernarg_frame(s.cam);
-    // a camera slot without a frame (metadata that is not this launch's) stages nothing
-    if (!s.f.yuv) s.live = 0u;
     return s;
 }
 
@@ -975,7 +973,7 @@ constexpr int kStageRegs = OCTVR_STAGE_REGS;
 //
 __device__ __forceinline__ uint4 meta_issue(const TiledLut& lut, int t, int t_end) {  // t: staged item
     const int lane = threadIdx.x & 63;
-    const int tt = (uint32_t)t < (uint32_t)t_end ? t : 0;  // unsigned: a negative index is out of range too
+    const int tt = t < t_end ? t : 0;  // t >= 0: every item index derives from bounded claims
     uint4 v;
     if (lane < 1 + kTileSlots)  // exec-masked: the instruction (and its vmcnt) is the same for every wave
         v = lane == 0 ? *reinterpret_cast<const uint4*>(lut.hdr + tt)
@@ -1006,7 +1004,7 @@ struct TileData {
 template <bool DWORD_STAGE, bool VIG, int Q, int R>
 __device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& m, int t_end,
                                            const StageSlot (&sl)[R], TileData<Q, R>& d) {
-    const bool live = (uint32_t)m.t < (uint32_t)t_end;
+    const bool live = m.t < t_end;
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
 #pragma unroll
@@ -1284,9 +1282,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
             // is not a claim of this band (the r02 barrier-free ablation read s_claim before wave 0 wrote
             // it, i.e. uninitialised LDS -> negative item index -> out-of-range header and entry loads and
             // a null frame pointer, hipErrorIllegalAddress) ends the sequence instead.
-            const uint32_t cv = (uint32_t)uniform((int)s_claim[par]);
-            const int room = t_end - dyn0;
-            const int v = claimed && room > 0 && cv < (uint32_t)room ? dyn0 + (int)cv : t_end;
+            // (one scalar min: dyn0 + cv then cannot wrap negative, and t_n2 below stays in [0, t_end])
+            const uint32_t cv = min((uint32_t)uniform((int)s_claim[par]), 0x3FFFFFFFu);
+            const int v = claimed ? dyn0 + (int)cv : t_end;
 #else  // static dealing (round-robin over the band's workgroups)
             const int v = t_n2 < t_end ? t_n2 + step : t_end;
 #endif
@@ -1319,9 +1317,24 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         const uint32_t ent[4] = {e4[h].x, e4[h].y, e4[h].z, e4[h].w};
         uint32_t rgb[4][3];
         f32x2_t gain[4];
+#if OCTVR_TAPS_FIRST  // the quad's 8 LDS reads issued before any of its arithmetic
+        uint32_t t00[4], t01[4], t10[4], t11[4];
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + (ent[p] & 0x7FFFu);
+            const uint8_t* r1 = r0 + 4u * S;
+            t00[p] = reinterpret_cast<const uint32_t*>(r0)[0];
+            t01[p] = reinterpret_cast<const uint32_t*>(r0)[1];
+            t10[p] = reinterpret_cast<const uint32_t*>(r1)[0];
+            t11[p] = reinterpret_cast<const uint32_t*>(r1)[1];
+        }
+#endif
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint32_t e = ent[p];
+#if OCTVR_TAPS_FIRST
+            const uint32_t c00 = t00[p], c01 = t01[p], c10 = t10[p], c11 = t11[p];
+#else
             // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
             const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + (e & 0x7FFFu);
             const uint8_t* r1 = r0 + 4u * S;
@@ -1329,6 +1342,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
             const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
             const uint32_t c10 = reinterpret_cast<const uint32_t*>(r1)[0];
             const uint32_t c11 = reinterpret_cast<const uint32_t*>(r1)[1];
+#endif
 #if OCTVR_DIAG_NOTAPS
             (void)c00; (void)c01; (void)c10; (void)c11;
             rgb[p][0] = e & 255u; rgb[p][1] = (e >> 8) & 255u; rgb[p][2] = (e >> 16) & 255u;

@@ -234,6 +234,53 @@ struct alignas(16) UpQuad {  // one quad row (or column) of a pyrUp output; 16 B
 };
 static_assert(sizeof(UpQuad) == 16, "UpQuad layout");
 
+// The same taps computed in registers instead of read from the UpQuad tables (no dependent table
+// load between the camera record and the tap loads).  For the quad at even level-grid index g, local
+// pixels o0 = g - off and o0 + 1 (up_taps / up_table in multiband_host.cpp, pyr_up.cu:55-166):
+//   o0 even (o0 = 2h):   sources h-1, h, h+1+k   w0 = 1 6 1, w1 = 0 4 4    k: rows, o0 % 8 == 6
+//   o0 odd  (o0 = 2h+1): sources h, h+1, h+2+k'  w0 = 4 4 0, w1 = 1 6 1    k': rows, o0 % 8 == 5
+//                                   (rows, o0 % 8 == 7: the odd pixel reads h, h+2: w0 = 4 0 4)
+// A pixel outside [0, n_local) weighs 0; sources are |u| clamped to n_src - 1.  Zero-weight slots
+// may hold a different (in-range) source than the table's, so the weighted sums are identical.
+__host__ __device__ inline int up_clamp(int u, int n_src) {
+    u = u < 0 ? -u : u;
+    return u < n_src - 1 ? u : n_src - 1;
+}
+struct UpArith {
+    int idx[3];
+    int w0[3], w1[3];
+};
+__host__ __device__ inline UpArith up_arith(int g, int off, int n_local, int n_src, bool rows) {
+    UpArith e;
+    const int o0 = g - off;
+    const int h = o0 >> 1;  // floor
+    const bool odd = (o0 & 1) != 0;
+    const int m8 = o0 & 7;
+    const bool v0 = o0 >= 0 && o0 < n_local, v1 = o0 + 1 >= 0 && o0 + 1 < n_local;
+    int u0, u2;
+    if (!odd) {
+        u0 = h - 1;
+        u2 = h + 1 + ((rows && m8 == 6) ? 1 : 0);
+        e.w0[0] = 1, e.w0[1] = 6, e.w0[2] = 1;
+        e.w1[0] = 0, e.w1[1] = 4, e.w1[2] = 4;
+    } else {
+        u0 = h;
+        u2 = h + 2 + ((rows && m8 == 5) ? 1 : 0);
+        const bool q7 = rows && m8 == 7;
+        e.w0[0] = 4, e.w0[1] = q7 ? 0 : 4, e.w0[2] = q7 ? 4 : 0;
+        e.w1[0] = 1, e.w1[1] = 6, e.w1[2] = 1;
+    }
+    e.idx[0] = up_clamp(u0, n_src);
+    e.idx[1] = up_clamp(u0 + 1, n_src);
+    e.idx[2] = up_clamp(u2, n_src);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        e.w0[j] = v0 ? e.w0[j] : 0;
+        e.w1[j] = v1 ? e.w1[j] : 0;
+    }
+    return e;
+}
+
 struct MbCamLevel {       // one camera at one level
     uint32_t g_off;        // byte offset of the camera's G in the level's pyramid allocation
     uint32_t g_pitch;      // bytes per row of G (4 * w)

@@ -130,10 +130,11 @@ struct Up9 {
 // 3 x 3 union taps, per-pixel integer weights over them (UpQuad).  The 1-D weights of a quad row /
 // column sum to 8 (1 6 1 or 4 4), so with s16 sources every product and partial sum fits 24 bits:
 // 24-bit multiplies (full rate; a 32-bit v_mul_lo is quarter rate).
-__device__ __forceinline__ void up_weigh(const UpQuad& ur, const UpQuad& uc, const int (&v)[3][3][3], Up9& o) {
+template <class QR, class QC>
+__device__ __forceinline__ void up_weigh(const QR& ur, const QC& uc, const int (&v)[3][3][3], Up9& o) {
 #pragma unroll
     for (int pc = 0; pc < 2; pc++) {
-        const uint8_t* wx = pc ? uc.w1 : uc.w0;
+        const auto& wx = pc ? uc.w1 : uc.w0;
         int h[3][3];  // [row][ch]
 #pragma unroll
         for (int j = 0; j < 3; j++)
@@ -143,7 +144,7 @@ __device__ __forceinline__ void up_weigh(const UpQuad& ur, const UpQuad& uc, con
                            __mul24((int)wx[2], v[j][2][ch]);
 #pragma unroll
         for (int pr = 0; pr < 2; pr++) {
-            const uint8_t* wy = pr ? ur.w1 : ur.w0;
+            const auto& wy = pr ? ur.w1 : ur.w0;
 #pragma unroll
             for (int ch = 0; ch < 3; ch++)
                 o.s[pr * 2 + pc][ch] = __mul24((int)wy[0], h[0][ch]) + __mul24((int)wy[1], h[1][ch]) +
@@ -178,8 +179,8 @@ template <class T>
 struct Taps9 {
     T t[3][3];
 };
-template <class T>
-__device__ __forceinline__ void up_taps_issue(const UpQuad& ur, const UpQuad& uc, const uint8_t* base, int64_t pitch,
+template <class T, class QR, class QC>
+__device__ __forceinline__ void up_taps_issue(const QR& ur, const QC& uc, const uint8_t* base, int64_t pitch,
                                               Taps9<T>& o) {
 #pragma unroll
     for (int j = 0; j < 3; j++) {
@@ -188,8 +189,8 @@ __device__ __forceinline__ void up_taps_issue(const UpQuad& ur, const UpQuad& uc
         for (int k = 0; k < 3; k++) o.t[j][k] = *reinterpret_cast<const T*>(row + (int64_t)uc.idx[k] * sizeof(T));
     }
 }
-template <class T, class UNPACK>
-__device__ __forceinline__ void up_quad_taps(const UpQuad& ur, const UpQuad& uc, const Taps9<T>& tp, UNPACK unpack,
+template <class T, class UNPACK, class QR, class QC>
+__device__ __forceinline__ void up_quad_taps(const QR& ur, const QC& uc, const Taps9<T>& tp, UNPACK unpack,
                                              Up9& o) {
     int v[3][3][3];
 #pragma unroll
@@ -234,6 +235,9 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
 
 #ifndef MB_RUP_EARLY
 #define MB_RUP_EARLY 0
+#endif
+#ifndef MB_ARITH_TAPS  // direct taps: computed in registers (up_arith), not read from the UpQuad tables
+#define MB_ARITH_TAPS 1
 #endif
 #ifndef MB_BLEND_WAVES  // waves per SIMD the blend is compiled for (register budget)
 #define MB_BLEND_WAVES 7
@@ -348,7 +352,11 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
                 for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
             };
 #if MB_DIRECT_TAPS
+#if MB_ARITH_TAPS
+            const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
+#else
             const UpQuad ur = c.up_rows[y >> 1], uc = load_up(c.up_cols, x >> 1);
+#endif
             Taps9<uint32_t> tp;
             up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
             up_quad_taps(ur, uc, tp, unpack, u);
@@ -401,7 +409,9 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             o[2] = (int)(int16_t)(v.y & 0xFFFFu);
         };
 #if MB_DIRECT_TAPS
-#if MB_RUP_EARLY
+#if MB_ARITH_TAPS
+        const UpArith ur = up_arith(y, 0, a.H, a.H_next, true), uc = up_arith(x, 0, a.W, a.W_next, false);
+#elif MB_RUP_EARLY
         asm volatile("" : "+v"(ucR_raw.x), "+v"(ucR_raw.y), "+v"(ucR_raw.z), "+v"(ucR_raw.w));
         const UpQuad ur = a.rup_rows[y >> 1], uc = __builtin_bit_cast(UpQuad, ucR_raw);
 #else

@@ -138,6 +138,31 @@ std::vector<UpQuad> up_table(int n_grid, int off, int n_local, int n_src, bool r
     return t;
 }
 
+// mb_blend computes its taps in registers (up_arith, kernels.hpp); check once per rig that they weigh
+// the same sources as the tables: per quad pixel, the summed weight of every source index.
+void check_up_arith(const std::vector<UpQuad>& t, int off, int n_local, int n_src, bool rows) {
+    for (size_t q = 0; q < t.size(); q++) {
+        const UpArith e = up_arith((int)(2 * q), off, n_local, n_src, rows);
+        for (int p = 0; p < 2; p++) {
+            int wt[6] = {0}, we[6] = {0}, it[6], ie[6];
+            for (int j = 0; j < 3; j++) {
+                it[j] = t[q].idx[j], wt[j] = p ? t[q].w1[j] : t[q].w0[j];
+                ie[j] = e.idx[j], we[j] = p ? e.w1[j] : e.w0[j];
+                REQUIRE(ie[j] >= 0 && ie[j] < n_src, "pyrUp tap outside the source");
+            }
+            auto weight_of = [](const int* idx, const int* w, int v) {
+                int s = 0;
+                for (int j = 0; j < 3; j++) s += idx[j] == v ? w[j] : 0;
+                return s;
+            };
+            for (int j = 0; j < 3; j++)
+                REQUIRE(weight_of(it, wt, it[j]) == weight_of(ie, we, it[j]) &&
+                            weight_of(it, wt, ie[j]) == weight_of(ie, we, ie[j]),
+                        "pyrUp register taps differ from the tap table");
+        }
+    }
+}
+
 // Origin of each tile's staged pyrUp patch (kernels.hpp kUpPatchRows x kUpPatchCols): the smallest
 // source index any weighted tap of the tile's quads reads; the span must fit the patch.
 std::vector<int32_t> patch_origins(const std::vector<UpQuad>& t, int quads_per_tile, int n_tiles, int limit) {
@@ -371,6 +396,8 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             // size index them too (their weights are 0, their taps clamped in range)
             ur[l][i] = up_table(L.ty_n * kTileH, c.oy, c.h, Ln.cams_h[i].h, true);
             uc[l][i] = up_table(L.tx_n * kTileW, c.ox, c.w, Ln.cams_h[i].w, false);
+            check_up_arith(ur[l][i], c.oy, c.h, Ln.cams_h[i].h, true);
+            check_up_arith(uc[l][i], c.ox, c.w, Ln.cams_h[i].w, false);
             ro[i] = all.size();
             all.insert(all.end(), ur[l][i].begin(), ur[l][i].end());
             co[i] = all.size();
@@ -395,6 +422,8 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         }
         std::vector<UpQuad> rr = up_table(L.ty_n * kTileH, 0, L.H, Ln.H, true),
                             rc = up_table(L.tx_n * kTileW, 0, L.W, Ln.W, false);
+        check_up_arith(rr, 0, L.H, Ln.H, true);
+        check_up_arith(rc, 0, L.W, Ln.W, false);
         {
             auto r0 = patch_origins(rr, kTileH / 2, L.ty_n, kUpPatchRows);
             auto c0 = patch_origins(rc, kTileW / 2, L.tx_n, kUpPatchCols);
