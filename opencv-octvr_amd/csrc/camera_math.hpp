@@ -96,8 +96,9 @@ OCTVR_HD void sin_cos(double x, double* s, double* c) {
 // kLutGuardTol of each other, and so does a final f64 -> f32 rounding that lies that close to a
 // rounding boundary.  The host then recomputes the fragile pixels with glibc, i.e. with exactly the
 // reference's arithmetic (octvr_hip.cpp build_input), so the LUT is bit-exact.  The host
-// evaluation passes no guard.  Measured device-vs-glibc deviations of the final coordinates are below
-// 1e-14 (tests/test_gpu_lut_exact.py), far inside the tolerance.
+// evaluation passes no guard.  Measured device-vs-glibc deviations of the final coordinates in and
+// next to the image: <= 1e-13 on every model but the tilted k1-k4 pinhole (6.9e-13), at least 20x
+// inside the tolerance (tests/test_gpu_lut_exact.py).
 constexpr double kLutGuardTol = 0x1p-36;  // ~1.5e-11 on O(1) quantities
 struct LutGuard {
     bool hit;

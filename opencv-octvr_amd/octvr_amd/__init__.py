@@ -274,6 +274,7 @@ class Mapper:
         n = len(in_sizes)
         w = (C.c_int * n)(*[s[0] for s in in_sizes])
         h = (C.c_int * n)(*[s[1] for s in in_sizes])
+        scale_output = tuple(scale_output) if scale_output else (0, 0)  # None / () = unscaled
         hd = _VP()
         _check(_lib.octvr_mapper_create(mt._h, device, n, w, h, blend, int(enable_gain), scale_output[0],
                                         scale_output[1], C.byref(hd)))
