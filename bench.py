@@ -218,6 +218,12 @@ def main():
         torch.cuda.synchronize(dev)
         return
 
+    # setup: one stitch per stream first, so every stream's hardware queue exists before the W warmup
+    # steps (the first launch on a new stream costs ~8 ms: with W < inflight it used to land inside the
+    # timed region — the "four in flight" cliff of round 2, profiles/r03_kt_inflight_cliff.md)
+    for j in range(inflight):
+        step(j)
+    torch.cuda.synchronize(dev)
     for k in range(args.warmup):
         step(k)
     torch.cuda.synchronize(dev)

@@ -17,13 +17,12 @@
 
 namespace octvr {
 
-// round half to even of S / 2^sh (S of any sign)
+// round half to even of S / 2^sh (S of any sign): floor((S + half - 1 + bit_sh(S)) / 2^sh) — below
+// the half the sum stays under the next multiple, at the half it reaches it only for an odd quotient
 template <int SH>
 __device__ __forceinline__ int rne_shr(int S) {
-    const int q = S >> SH;
-    const int r = S - (q << SH);
     constexpr int half = 1 << (SH - 1);
-    return q + ((r > half || (r == half && (q & 1))) ? 1 : 0);
+    return (S + (half - 1) + (int)(((uint32_t)S >> SH) & 1u)) >> SH;
 }
 
 __device__ __forceinline__ uint32_t ch_of(uint32_t v, int c) { return (v >> (8 * c)) & 255u; }
@@ -200,6 +199,52 @@ __device__ __forceinline__ void up_quad_taps(const QR& ur, const QC& uc, const T
     up_weigh(ur, uc, v, o);
 }
 
+// pyrUp of a quad of u8x4 taps (the Gaussian level), rounded: R and B ride as the two 16-bit halves of
+// one word, G alone.  Column sums first with the row weights (wave-uniform), then the per-lane column
+// weights; every partial sum is <= 64 * 255 per half, so the 32-bit adds never carry across halves,
+// the 24-bit multiplies see operands < 2^24, and the round (S + 31 + bit6) / 64 stays inside its half.
+// Out: per pixel (R | B << 16) and G of sat_u8(rne(S / 64)) (the clamp is a no-op: S <= 64 * 255).
+__device__ __forceinline__ void up_g_packed(const UpArith& ur, const UpArith& uc, const Taps9<uint32_t>& tp,
+                                            uint32_t (&rb)[4], uint32_t (&gg)[4]) {
+    uint32_t vrb[2][3], vg[2][3];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        uint32_t RB[3], G[3];
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            RB[j] = tp.t[j][k] & 0x00FF00FFu;
+            G[j] = (tp.t[j][k] >> 8) & 255u;
+        }
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++) {
+            const auto& wy = pr ? ur.w1 : ur.w0;
+            vrb[pr][k] = __umul24((uint32_t)wy[0], RB[0]) + __umul24((uint32_t)wy[1], RB[1]) +
+                         __umul24((uint32_t)wy[2], RB[2]);  // halves <= 8 * 255
+            vg[pr][k] = __umul24((uint32_t)wy[0], G[0]) + __umul24((uint32_t)wy[1], G[1]) +
+                        __umul24((uint32_t)wy[2], G[2]);
+        }
+    }
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int pc = 0; pc < 2; pc++) {
+        const auto& wx = pc ? uc.w1 : uc.w0;
+        const u16x2 w0 = {(unsigned short)wx[0], (unsigned short)wx[0]}, w1 = {(unsigned short)wx[1], (unsigned short)wx[1]},
+                    w2 = {(unsigned short)wx[2], (unsigned short)wx[2]};
+#pragma unroll
+        for (int pr = 0; pr < 2; pr++) {
+            // halves <= 8 * 2040: 16-bit packed multiply-adds (v_pk_mad_u16)
+            const u16x2 s = __builtin_bit_cast(u16x2, vrb[pr][0]) * w0 + __builtin_bit_cast(u16x2, vrb[pr][1]) * w1 +
+                            __builtin_bit_cast(u16x2, vrb[pr][2]) * w2;
+            const uint32_t S = __builtin_bit_cast(uint32_t, s);
+            const uint32_t S2 = S + 0x001F001Fu + ((S >> 6) & 0x00010001u);
+            rb[pr * 2 + pc] = (S2 >> 6) & 0x00FF00FFu;
+            const uint32_t Sg = __umul24((uint32_t)wx[0], vg[pr][0]) + __umul24((uint32_t)wx[1], vg[pr][1]) +
+                                __umul24((uint32_t)wx[2], vg[pr][2]);
+            gg[pr * 2 + pc] = (Sg + 31u + ((Sg >> 6) & 1u)) >> 6;
+        }
+    }
+}
+
 // Cooperative load of an 8 x 72 patch (rows r0.., cols c0.., clamped to the source) into registers:
 // entries tid, tid + 256, tid + 512 (< 576).
 constexpr int kPatchN = kUpPatchRows * kUpPatchCols;
@@ -236,6 +281,9 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
 #ifndef MB_RUP_EARLY
 #define MB_RUP_EARLY 0
 #endif
+#ifndef MB_PACKED_UP  // the Gaussian pyrUp in packed 16-bit halves (up_g_packed)
+#define MB_PACKED_UP 1
+#endif
 #ifndef MB_ARITH_TAPS  // direct taps: computed in registers (up_arith), not read from the UpQuad tables
 #define MB_ARITH_TAPS 1
 #endif
@@ -267,13 +315,13 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
                            rc0, rp);
     }
 #endif
-    int D[4][3];
+    float D[4][3];  // the Laplacian accumulator (a CV_16S sum in the reference; exact here, see below)
     float wsum[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         wsum[p] = 1e-5f;
 #pragma unroll
-        for (int ch = 0; ch < 3; ch++) D[p][ch] = 0;
+        for (int ch = 0; ch < 3; ch++) D[p][ch] = 0.f;
     }
 #if MB_RUP_EARLY  // the collapse's per-column tap table loaded before the camera loop, kept raw
     uint4 ucR_raw = make_uint4(0u, 0u, 0u, 0u);
@@ -343,9 +391,22 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             w[p] = in ? wv_ : 0.f;
             gv[p] = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + cx * 4);
         }
-        int g[4][3];
+        float g[4][3];  // G - pyrUp(G_next) (G at the top level): small exact integers
         if (!top) {
             const MbCamLevel cn = a.cams_next[n];
+#if MB_DIRECT_TAPS && MB_ARITH_TAPS && MB_PACKED_UP
+            const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
+            Taps9<uint32_t> tp;
+            up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
+            uint32_t urb[4], ug[4];
+            up_g_packed(ur, uc, tp, urb, ug);
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                g[p][0] = (float)ch_of(gv[p], 0) - (float)(urb[p] & 255u);
+                g[p][1] = (float)ch_of(gv[p], 1) - (float)ug[p];
+                g[p][2] = (float)ch_of(gv[p], 2) - (float)(urb[p] >> 16);
+            }
+#else
             Up9 u;
             auto unpack = [](uint32_t v, int (&o)[3]) {
 #pragma unroll
@@ -373,20 +434,23 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             for (int p = 0; p < 4; p++)
 #pragma unroll
                 for (int ch = 0; ch < 3; ch++)
-                    g[p][ch] = (int)ch_of(gv[p], ch) - min(max(rne_shr<6>(u.s[p][ch]), 0), 255);  // sat u8
+                    g[p][ch] = (float)((int)ch_of(gv[p], ch) - min(max(rne_shr<6>(u.s[p][ch]), 0), 255));  // sat u8
+#endif
         } else {
 #pragma unroll
             for (int p = 0; p < 4; p++)
 #pragma unroll
-                for (int ch = 0; ch < 3; ch++) g[p][ch] = (int)ch_of(gv[p], ch);
+                for (int ch = 0; ch < 3; ch++) g[p][ch] = (float)ch_of(gv[p], ch);
         }
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             if (w[p] == 0.f) continue;
 #pragma unroll
             for (int ch = 0; ch < 3; ch++) {
-                const int sub = (int)__builtin_truncf((float)g[p][ch] * w[p]);  // (short) of a small value
-                D[p][ch] = (int)(int16_t)(D[p][ch] + sub);                      // short += short wraps
+                // (short)(g * w), then short += short.  |g * w| <= 255 * w and the weights of a pixel sum
+                // to <= 1 (multi-band) or <= n (feather, n <= 32): |D| <= 8160 at every step, so the
+                // short adds never wrap and the sum is exact in f32
+                D[p][ch] = D[p][ch] + __builtin_truncf(g[p][ch] * w[p]);
             }
             wsum[p] = wsum[p] + w[p];
         }
@@ -399,7 +463,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
         const float rcp = a.feather ? a.out_scale : 1.0f / wsum[p];
 #pragma unroll
         for (int ch = 0; ch < 3; ch++)
-            R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf((float)D[p][ch] * rcp), -32768.f, 32767.f);
+            R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf(D[p][ch] * rcp), -32768.f, 32767.f);
     }
     if (!top) {
         Up9 u;
