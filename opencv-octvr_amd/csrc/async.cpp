@@ -9,13 +9,17 @@
 //     instead of round-tripping them through the host (async.cpp:78-86);
 //   * worker threads are joinable and exit when the object is destroyed (the reference's five
 //     threads loop forever and its destructor clears joinable std::threads, async.cpp:87-90,337-349);
-//   * a failing frame carries its status to pop() instead of asserting.
+//   * a failing frame carries its status to pop() instead of asserting;
+//   * the two host-copy stages split their rows over a few helper threads (RowPool): one thread's
+//     memcpy from pageable memory (~15 GB/s) otherwise bounds the whole pipeline (C2: 75 MB in per
+//     frame, scripts/async_trace.py).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -105,6 +109,72 @@ struct Job {
     std::string error;
 };
 
+// Helper threads of one host-copy stage: run(n, f) calls f(lo, hi) over n rows split into contiguous
+// ranges, the calling thread taking the last one, and returns when all are done.  One run at a time
+// (each stage owns its pool); f must not throw (memcpy only).
+class RowPool {
+public:
+    explicit RowPool(int helpers) {
+        for (int i = 0; i < helpers; i++) th_.emplace_back([this, i] { loop(i); });
+    }
+    ~RowPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            quit_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    template <class F>
+    void run(size_t n, F f) {
+        const size_t T = th_.size() + 1;
+        std::function<void(size_t, size_t)> fn = f;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            job_ = &fn;
+            n_ = n;
+            left_ = th_.size();
+            gen_++;
+        }
+        cv_.notify_all();
+        fn(n * (T - 1) / T, n);
+        std::unique_lock<std::mutex> g(mu_);
+        done_.wait(g, [&] { return left_ == 0; });
+        job_ = nullptr;
+    }
+
+private:
+    void loop(int i) {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(size_t, size_t)>* f;
+            size_t n, T;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return quit_ || gen_ != seen; });
+                if (quit_) return;
+                seen = gen_;
+                f = job_;
+                n = n_;
+                T = th_.size() + 1;
+            }
+            (*f)(n * (size_t)i / T, n * (size_t)(i + 1) / T);
+            {
+                std::lock_guard<std::mutex> g(mu_);
+                if (--left_ == 0) done_.notify_all();
+            }
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    const std::function<void(size_t, size_t)>* job_ = nullptr;
+    size_t n_ = 0, left_ = 0;
+    uint64_t gen_ = 0;
+    bool quit_ = false;
+};
+constexpr int kCopyHelpers = 5;  // per host-copy stage (the GPU box grants ~16 host threads per GPU)
+
 template <class F>
 void stage(Job& j, F&& f) {  // run a stage unless the frame already failed; record the first failure
     if (j.status != OCTVR_OK) return;
@@ -134,6 +204,7 @@ struct octvr_async {
     Channel<std::shared_ptr<Job>> q_in, q_up, q_map, q_down, q_out, q_done;
     Channel<int> free_slots;
     std::vector<std::thread> threads;
+    RowPool copy_in_pool{kCopyHelpers}, copy_out_pool{kCopyHelpers};
     int pending = 0;  // pushed, not popped (caller thread only)
 
     ~octvr_async() {
@@ -165,12 +236,20 @@ struct octvr_async {
                 const int w = in_w[i], h = in_h[i];
                 uint8_t* dst = slots[s].in_host[i]->p;
                 const uint8_t *Y = j.in_planes[3 * i], *U = j.in_planes[3 * i + 1], *V = j.in_planes[3 * i + 2];
-                for (int y = 0; y < h; y++) memcpy(dst + (size_t)y * w, Y + (size_t)y * j.in_pitches[3 * i], w);
-                for (int y = 0; y < h / 2; y++) {
-                    uint8_t* row = dst + (size_t)(h + y) * w;
-                    memcpy(row, U + (size_t)y * j.in_pitches[3 * i + 1], w / 2);
-                    memcpy(row + w / 2, V + (size_t)y * j.in_pitches[3 * i + 2], w / 2);
-                }
+                const size_t py = j.in_pitches[3 * i], pu = j.in_pitches[3 * i + 1], pv = j.in_pitches[3 * i + 2];
+                // rows 0..h-1: Y; h..h+h/2-1: U | V side by side
+                copy_in_pool.run((size_t)(h + h / 2), [&](size_t lo, size_t hi) {
+                    for (size_t y = lo; y < hi; y++) {
+                        uint8_t* row = dst + y * (size_t)w;
+                        if (y < (size_t)h) {
+                            memcpy(row, Y + y * py, w);
+                        } else {
+                            const size_t c = y - (size_t)h;
+                            memcpy(row, U + c * pu, w / 2);
+                            memcpy(row + w / 2, V + c * pv, w / 2);
+                        }
+                    }
+                });
             }
         });
     }
@@ -228,13 +307,18 @@ struct octvr_async {
                 const Rect& r = regions[k];
                 const Rect& c = regions_uv[k];
                 const uint8_t* src = sl.out_host[k]->p;
-                for (int y = 0; y < r.h; y++)
-                    memcpy(j.out_planes[0] + (size_t)(r.y + y) * j.out_pitches[0] + r.x, src + (size_t)y * r.w, r.w);
-                for (int y = 0; y < c.h; y++) {
-                    const uint8_t* row = src + (size_t)(r.h + y) * r.w;
-                    memcpy(j.out_planes[1] + (size_t)(c.y + y) * j.out_pitches[1] + c.x, row, c.w);
-                    memcpy(j.out_planes[2] + (size_t)(c.y + y) * j.out_pitches[2] + c.x, row + r.w / 2, c.w);
-                }
+                copy_out_pool.run((size_t)(r.h + c.h), [&](size_t lo, size_t hi) {
+                    for (size_t y = lo; y < hi; y++) {
+                        if (y < (size_t)r.h) {
+                            memcpy(j.out_planes[0] + (size_t)(r.y + (int)y) * j.out_pitches[0] + r.x, src + y * r.w, r.w);
+                        } else {
+                            const size_t cy = y - (size_t)r.h;
+                            const uint8_t* row = src + (size_t)(r.h + (int)cy) * r.w;
+                            memcpy(j.out_planes[1] + (size_t)(c.y + (int)cy) * j.out_pitches[1] + c.x, row, c.w);
+                            memcpy(j.out_planes[2] + (size_t)(c.y + (int)cy) * j.out_pitches[2] + c.x, row + r.w / 2, c.w);
+                        }
+                    }
+                });
             }
         });
     }

@@ -29,20 +29,19 @@ def run(cfg, frames):
 
 
 def analyze(d):
+    """Busy time (interval union) per copy direction and of the stitch kernels, and their pairwise
+    overlaps.  Uploads appear as HOST_TO_DEVICE copies (SDMA); the downloads into pinned host memory
+    run as `__amd_rocclr_copyBuffer` blit kernels on the download stream."""
     def rows(name):
         p = os.path.join(d, name)
         return list(csv.DictReader(open(p))) if os.path.exists(p) else []
     ker = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows("run_kernel_trace.csv")]
-    cpy = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Direction", r.get("Operation", "")), int(r.get("Bytes", r.get("Size", 0)) or 0))
+    cpy = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Direction"].replace("MEMORY_COPY_", ""))
            for r in rows("run_memory_copy_trace.csv")]
-    stitch = sorted((s, e) for s, e, n in ker if "stitch_tiled" in n or "mb_blend" in n)
-    h2d = sorted((s, e, b) for s, e, k, b in cpy if "HOST_TO_DEVICE" in k.upper() and b >= 1 << 20)
-    d2h = sorted((s, e, b) for s, e, k, b in cpy if "DEVICE_TO_HOST" in k.upper() and b >= 1 << 20)
 
     def union(iv):
-        iv = sorted(iv)
         tot, cs, ce = 0, None, None
-        for s, e in iv:
+        for s, e in sorted(iv):
             if cs is None or s > ce:
                 if cs is not None:
                     tot += ce - cs
@@ -53,15 +52,23 @@ def analyze(d):
 
     def overlap(a, b):
         return union(a) + union(b) - union(a + b)
-    h = [(s, e) for s, e, _ in h2d]
-    o = [(s, e) for s, e, _ in d2h]
-    t0 = min(x[0] for x in stitch + h + o)
-    t1 = max(x[1] for x in stitch + h + o)
-    out = {"window_us": (t1 - t0) / 1e3, "stitch_busy_us": union(stitch) / 1e3, "h2d_busy_us": union(h) / 1e3,
-           "d2h_busy_us": union(o) / 1e3, "h2d_copies": len(h), "d2h_copies": len(o),
-           "h2d_GBps": sum(b for _, _, b in h2d) / max(union(h), 1), "d2h_GBps": sum(b for _, _, b in d2h) / max(union(o), 1),
-           "stitch_under_h2d_us": overlap(stitch, h) / 1e3, "stitch_under_d2h_us": overlap(stitch, o) / 1e3,
-           "h2d_under_d2h_us": overlap(h, o) / 1e3}
+    stitch = [(s, e) for s, e, n in ker if "stitch" in n or "mb_" in n]
+    t_first = min(s for s, _ in stitch)  # the pipeline's window: from the first stitch on
+    groups = {"stitch": stitch}
+    for s, e, k in cpy:
+        if e >= t_first:
+            groups.setdefault(k, []).append((s, e))
+    groups["DEVICE_TO_HOST (blit kernel)"] = [(s, e) for s, e, n in ker if "copyBuffer" in n and e >= t_first]
+    t0 = min(s for v in groups.values() for s, _ in v)
+    t1 = max(e for v in groups.values() for _, e in v)
+    out = {"window_us": round((t1 - t0) / 1e3, 1),
+           "busy_us": {k: round(union(v) / 1e3, 1) for k, v in groups.items()},
+           "count": {k: len(v) for k, v in groups.items()},
+           "overlap_us": {}}
+    keys = sorted(groups)
+    for i in range(len(keys)):
+        for j in range(i + 1, len(keys)):
+            out["overlap_us"][keys[i] + "|" + keys[j]] = round(overlap(groups[keys[i]], groups[keys[j]]) / 1e3, 1)
     print(json.dumps(out, indent=1))
 
 
