@@ -290,6 +290,11 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
 #ifndef MB_BLEND_WAVES  // waves per SIMD the blend is compiled for (register budget)
 #define MB_BLEND_WAVES 7
 #endif
+// 1e-5f + 1.0f (one weight-1 camera: (float)(1. / 255) * 255.0f rounds to exactly 1.0f) and the
+// correctly rounded reciprocals of the two common weight sums (constant-folded)
+constexpr float kWsumOwned = 1e-5f + 1.0f, kRcpOwned = 1.0f / kWsumOwned, kRcpNone = 1.0f / 1e-5f;
+static_assert((float)(1. / 255) * 255.0f == 1.0f, "seam weight 255 / 255");
+
 __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendArgs a) {
 #if !MB_DIRECT_TAPS
     __shared__ uint2 s_r[kPatchN];     // collapsed coarser level (s16x4)
@@ -442,9 +447,10 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 #pragma unroll
                 for (int ch = 0; ch < 3; ch++) g[p][ch] = (float)ch_of(gv[p], ch);
         }
+        // only where w != 0 in the reference; a zero weight adds +-0 to D and 0 to the weight sum, so the
+        // sums are the same without a per-pixel branch
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            if (w[p] == 0.f) continue;
 #pragma unroll
             for (int ch = 0; ch < 3; ch++) {
                 // (short)(g * w), then short += short.  |g * w| <= 255 * w and the weights of a pixel sum
@@ -460,7 +466,10 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     for (int p = 0; p < 4; p++) {
         // feather: convertTo(CV_8UC3, 1/n) = sat_u8(alpha * D) (clamped to u8 below); multi-band:
         // DivOpSpecial<short3> with the correctly rounded reciprocal (hipcc default, as CUDA's 1.0f / b)
-        const float rcp = a.feather ? a.out_scale : 1.0f / wsum[p];
+        float rcp = a.feather ? a.out_scale : kRcpOwned;
+        // level 0 with 0 / 255 seams: one camera of weight 1 (or none) per pixel, i.e. the two sums below;
+        // any other sum takes the division (a branch only the lanes that need it execute)
+        if (!a.feather && wsum[p] != kWsumOwned) rcp = wsum[p] == 1e-5f ? kRcpNone : 1.0f / wsum[p];
 #pragma unroll
         for (int ch = 0; ch < 3; ch++)
             R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf(D[p][ch] * rcp), -32768.f, 32767.f);
@@ -474,7 +483,15 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
         };
 #if MB_DIRECT_TAPS
 #if MB_ARITH_TAPS
-        const UpArith ur = up_arith(y, 0, a.H, a.H_next, true), uc = up_arith(x, 0, a.W, a.W_next, false);
+        // x and y are even on the level grid: every quad has the even tap pattern (1 6 1 | 0 4 4) as
+        // constants; the zero weights up_arith gives pixels outside the level only matter for pixels
+        // that are never stored (W, H even at level 0; level > 0 stores valid pixels only)
+        UpArith ur = up_arith(y, 0, a.H, a.H_next, true), uc = up_arith(x, 0, a.W, a.W_next, false);
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            ur.w0[j] = uc.w0[j] = j == 1 ? 6 : 1;
+            ur.w1[j] = uc.w1[j] = j == 0 ? 0 : 4;
+        }
 #elif MB_RUP_EARLY
         asm volatile("" : "+v"(ucR_raw.x), "+v"(ucR_raw.y), "+v"(ucR_raw.z), "+v"(ucR_raw.w));
         const UpQuad ur = a.rup_rows[y >> 1], uc = __builtin_bit_cast(UpQuad, ucR_raw);
