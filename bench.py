@@ -237,7 +237,7 @@ def main():
     m.set_timing(False)
     span_ms, busy_ms, launches = m.kernel_busy()
     kern_ms = busy_ms if inflight > 1 else span_ms
-    serial = None
+    serial = serial_step = None
     if inflight > 1 and not dist:
         # supplementary, after the timed region: the composite kernel's duration with one frame in
         # flight (with two, the events on a stream also span the other stream's kernels).  The mapper
@@ -254,6 +254,11 @@ def main():
         s_ms, s_n = m.kernel_time()
         m.set_timing(False)
         serial = s_ms / 1e3 / max(s_n, 1)
+        t0 = time.perf_counter()  # and the wall time per frame of serial stitches (feed + composite)
+        for k in range(16):
+            m.stitch(frame_sets[0], outs[0], stream=streams[0])
+        torch.cuda.synchronize(dev)
+        serial_step = (time.perf_counter() - t0) / 16
 
     gains = m.gains()
     frame_px = W * H
@@ -309,7 +314,12 @@ def main():
         **({"roofline_one_in_flight": {"kernel_us": round(serial * 1e6, 2),
                                         "achieved": round(bytes_per_launch / serial / 1e9, 1),
                                         "frac": round(bytes_per_launch / serial / 1e9 / HBM_PEAK_GBPS, 4),
-                                        "note": "8 stitches after the timed region with set_frames_in_flight(1): feed then composite, nothing beside them"}}
+                                        "step_us": round(serial_step * 1e6, 1),
+                                        "note": "after the timed region with set_frames_in_flight(1): kernel_us = the "
+                                                "composite's packet-attached HIP events over 8 stitches (they read "
+                                                "~10 us above rocprof's kernel duration here, profiles/r03_*_inflight1_"
+                                                "kernel_stats.csv); step_us = wall time per frame of 16 serial stitches "
+                                                "(gain feed + composite)"}}
            if serial else {}),
         "mapper": m.info(),
     }
