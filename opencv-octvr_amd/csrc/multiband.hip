@@ -281,6 +281,12 @@ __device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
 #ifndef MB_RUP_EARLY
 #define MB_RUP_EARLY 0
 #endif
+#ifndef MB_LOADS_FIRST  // a camera's loads all issued before their first use (one round trip per camera)
+#define MB_LOADS_FIRST 1
+#endif
+#ifndef MB_COLLAPSE_FIRST
+#define MB_COLLAPSE_FIRST 0
+#endif
 #ifndef MB_PACKED_UP  // the Gaussian pyrUp in packed 16-bit halves (up_g_packed)
 #define MB_PACKED_UP 1
 #endif
@@ -332,46 +338,93 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     uint4 ucR_raw = make_uint4(0u, 0u, 0u, 0u);
     if (!top) ucR_raw = *reinterpret_cast<const uint4*>(a.rup_cols + (x >> 1));
 #endif
+#if MB_COLLAPSE_FIRST
+    // the collapse's 9 taps issued before the camera loop: their latency overlaps the first camera's
+    // loads instead of following the loop (18 VGPRs held across it)
+    UpArith urR = up_arith(y, 0, a.H, a.H_next, true), ucR = up_arith(x, 0, a.W, a.W_next, false);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        urR.w0[j] = ucR.w0[j] = j == 1 ? 6 : 1;
+        urR.w1[j] = ucR.w1[j] = j == 0 ? 0 : 4;
+    }
+    Taps9<uint2> tpR;
+    if (!top) {
+        up_taps_issue<uint2>(urR, ucR, reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, tpR);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) tpR.t[j][k] = make_uint2(0u, 0u);
+    }
+#endif
     uint32_t m = (uint32_t)uniform((int)a.tile_cams[tile]);
     while (m) {
         const int n = __builtin_ctz(m);
         m &= m - 1;
         const MbCamLevel c = a.cams[n];
         const int xl = x - c.ox, yl = y - c.oy;  // camera-local quad origin (any parity)
-        // all of this camera's loads at once: weights, G, and the coarser level's taps
         float w[4];
-        uint32_t gv[4];
-#if MB_PAIR_LOADS
+        float g[4][3];  // G - pyrUp(G_next) (G at the top level): small exact integers
+#if MB_LOADS_FIRST
         if (c.w >= 2) {
-            // per quad row one 8-byte load of G and of the weights at the clamped pair start x0:
-            // pixel px is element px - x0 (0 or 1 whenever it lies inside the camera)
+            // Every load of this camera is issued before any of them is used — the G pairs and weight
+            // pairs of both quad rows and the 9 pyrUp taps — so a camera costs one memory round trip.
+            // Per quad row one 8-byte load of G and of the weights at the clamped pair start x0: pixel
+            // px is element px - x0 (0 or 1 whenever it lies inside the camera).  One buffer resource
+            // serves both weight kinds: the u8 level-0 seam from the dword at or below the pair (dword
+            // loads ignore the low address bits; reads past the end return 0), or the f32 level.
             const int x0 = min(max(xl, 0), c.w - 2);
-            // u8 level-0 weights: an 8-byte buffer load from the dword at or below the pair (dword loads
-            // ignore the low address bits, so the resource starts at the dword below the weights and
-            // reads past the end return 0)
-            const uint32_t dlt = (uint32_t)(reinterpret_cast<uintptr_t>(c.weight) & 3u);
+            const uint32_t dlt = a.w_u8 ? (uint32_t)(reinterpret_cast<uintptr_t>(c.weight) & 3u) : 0u;
             const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint8_t*>(static_cast<const uint8_t*>(c.weight) - dlt), 0,
-                (int)(c.w * c.h + dlt), 0x00020000);
+                (int)(a.w_u8 ? (uint32_t)(c.w * c.h) + dlt : (uint32_t)(c.w * c.h) * 4u), 0x00020000);
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            // (plain scalars, no arrays: a private array here is promoted to LDS and waited on)
+            const int cy0 = min(max(yl, 0), c.h - 1), cy1 = min(max(yl + 1, 0), c.h - 1);
+            const uint2 gp0 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy0 * c.g_pitch + x0 * 4);
+            const uint2 gp1 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy1 * c.g_pitch + x0 * 4);
+            const uint32_t at0 = dlt + (uint32_t)(cy0 * c.w + x0), at1 = dlt + (uint32_t)(cy1 * c.w + x0);
+#if MB_LF_F32_GLOBAL
+            u32x2 wq0, wq1;
+            if (a.w_u8) {
+                wq0 = __builtin_amdgcn_raw_buffer_load_b64(wr, at0 & ~3u, 0, 0);
+                wq1 = __builtin_amdgcn_raw_buffer_load_b64(wr, at1 & ~3u, 0, 0);
+            } else {
+                const uint2 t0 = *reinterpret_cast<const uint2*>(static_cast<const float*>(c.weight) + at0);
+                const uint2 t1 = *reinterpret_cast<const uint2*>(static_cast<const float*>(c.weight) + at1);
+                wq0 = u32x2{t0.x, t0.y};
+                wq1 = u32x2{t1.x, t1.y};
+            }
+#else
+            const u32x2 wq0 = __builtin_amdgcn_raw_buffer_load_b64(wr, a.w_u8 ? at0 & ~3u : at0 * 4u, 0, 0);
+            const u32x2 wq1 = __builtin_amdgcn_raw_buffer_load_b64(wr, a.w_u8 ? at1 & ~3u : at1 * 4u, 0, 0);
+#endif
+            // unconditionally (the top level reads its own G as a stand-in, unused): a branch here would
+            // let the compiler merge it with the one below, after the weight decode's waits
+            const MbCamLevel cn = *(top ? a.cams + n : a.cams_next + n);
+            const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
+            Taps9<uint32_t> tp;
+            up_taps_issue<uint32_t>(ur, uc, (top ? a.g : a.g_next) + cn.g_off, cn.g_pitch, tp);
+            uint32_t gv[4];
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                const int py = yl + r, cy = min(max(py, 0), c.h - 1);
-                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                const uint2 gp = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + x0 * 4);
+                const int py = yl + r;
+                const u32x2 wq = r ? wq1 : wq0;
+                const uint2 gp = r ? gp1 : gp0;
+                const uint32_t at = r ? at1 : at0;
                 float wp[2];
                 if (a.w_u8) {
-                    const uint32_t at = dlt + (uint32_t)(cy * c.w + x0), a4 = at & ~3u;
-                    const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(wr, a4, 0, 0);
-                    const uint64_t q = ((uint64_t)t.y << 32) | t.x;
-                    const uint32_t sh = 8u * (at - a4);
+                    const uint64_t q = ((uint64_t)wq.y << 32) | wq.x;
+                    const uint32_t sh = 8u * (at & 3u);
                     // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
                     wp[0] = (float)(1. / 255) * (float)(uint32_t)((q >> sh) & 255u);
                     wp[1] = (float)(1. / 255) * (float)(uint32_t)((q >> (sh + 8u)) & 255u);
-                } else {  // f32 levels: in-bounds 8-byte load at the pair start
-                    const float2 t = *reinterpret_cast<const float2*>(static_cast<const float*>(c.weight) +
-                                                                      (int64_t)cy * c.w + x0);
-                    wp[0] = t.x;
-                    wp[1] = t.y;
+                } else {
+                    // (__uint_as_float of a copied scalar: __builtin_bit_cast of an ext-vector component
+                    // reads the vector's first element with this compiler)
+                    const uint32_t lo = wq.x, hi = wq.y;
+                    wp[0] = __uint_as_float(lo);
+                    wp[1] = __uint_as_float(hi);
                 }
 #pragma unroll
                 for (int pc = 0; pc < 2; pc++) {
@@ -382,70 +435,131 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
                     gv[p] = hi ? gp.y : gp.x;
                 }
             }
+            if (!top) {
+                uint32_t urb[4], ug[4];
+                up_g_packed(ur, uc, tp, urb, ug);
+#pragma unroll
+                for (int p = 0; p < 4; p++) {
+                    g[p][0] = (float)ch_of(gv[p], 0) - (float)(urb[p] & 255u);
+                    g[p][1] = (float)ch_of(gv[p], 1) - (float)ug[p];
+                    g[p][2] = (float)ch_of(gv[p], 2) - (float)(urb[p] >> 16);
+                }
+            } else {
+#pragma unroll
+                for (int p = 0; p < 4; p++)
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) g[p][ch] = (float)ch_of(gv[p], ch);
+            }
         } else
 #endif
+        {
+            // (cameras 1 pixel wide at this level, or the MB_LOADS_FIRST = 0 build)
+            uint32_t gv[4];
+#if MB_PAIR_LOADS
+            if (c.w >= 2) {
+                // per quad row one 8-byte load of G and of the weights at the clamped pair start x0:
+                // pixel px is element px - x0 (0 or 1 whenever it lies inside the camera)
+                const int x0 = min(max(xl, 0), c.w - 2);
+                // u8 level-0 weights: an 8-byte buffer load from the dword at or below the pair (dword loads
+                // ignore the low address bits, so the resource starts at the dword below the weights and
+                // reads past the end return 0)
+                const uint32_t dlt = (uint32_t)(reinterpret_cast<uintptr_t>(c.weight) & 3u);
+                const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<uint8_t*>(static_cast<const uint8_t*>(c.weight) - dlt), 0,
+                    (int)(c.w * c.h + dlt), 0x00020000);
 #pragma unroll
-        for (int p = 0; p < 4; p++) {
-            const int px = xl + (p & 1), py = yl + (p >> 1);
-            const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
-            const int cx = min(max(px, 0), c.w - 1), cy = min(max(py, 0), c.h - 1);
-            const int64_t k = (int64_t)cy * c.w + cx;
-            // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
-            const float wv_ = a.w_u8 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
-                                     : static_cast<const float*>(c.weight)[k];
-            w[p] = in ? wv_ : 0.f;
-            gv[p] = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + cx * 4);
-        }
-        float g[4][3];  // G - pyrUp(G_next) (G at the top level): small exact integers
-        if (!top) {
-            const MbCamLevel cn = a.cams_next[n];
-#if MB_DIRECT_TAPS && MB_ARITH_TAPS && MB_PACKED_UP
-            const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
-            Taps9<uint32_t> tp;
-            up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
-            uint32_t urb[4], ug[4];
-            up_g_packed(ur, uc, tp, urb, ug);
+                for (int r = 0; r < 2; r++) {
+                    const int py = yl + r, cy = min(max(py, 0), c.h - 1);
+                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                    const uint2 gp = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + x0 * 4);
+                    float wp[2];
+                    if (a.w_u8) {
+                        const uint32_t at = dlt + (uint32_t)(cy * c.w + x0), a4 = at & ~3u;
+                        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(wr, a4, 0, 0);
+                        const uint64_t q = ((uint64_t)t.y << 32) | t.x;
+                        const uint32_t sh = 8u * (at - a4);
+                        // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
+                        wp[0] = (float)(1. / 255) * (float)(uint32_t)((q >> sh) & 255u);
+                        wp[1] = (float)(1. / 255) * (float)(uint32_t)((q >> (sh + 8u)) & 255u);
+                    } else {  // f32 levels: in-bounds 8-byte load at the pair start
+                        const float2 t = *reinterpret_cast<const float2*>(static_cast<const float*>(c.weight) +
+                                                                          (int64_t)cy * c.w + x0);
+                        wp[0] = t.x;
+                        wp[1] = t.y;
+                    }
+#pragma unroll
+                    for (int pc = 0; pc < 2; pc++) {
+                        const int p = 2 * r + pc, px = xl + pc;
+                        const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
+                        const bool hi = ((px - x0) & 1) != 0;
+                        w[p] = in ? (hi ? wp[1] : wp[0]) : 0.f;
+                        gv[p] = hi ? gp.y : gp.x;
+                    }
+                }
+            } else
+#endif
 #pragma unroll
             for (int p = 0; p < 4; p++) {
-                g[p][0] = (float)ch_of(gv[p], 0) - (float)(urb[p] & 255u);
-                g[p][1] = (float)ch_of(gv[p], 1) - (float)ug[p];
-                g[p][2] = (float)ch_of(gv[p], 2) - (float)(urb[p] >> 16);
+                const int px = xl + (p & 1), py = yl + (p >> 1);
+                const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
+                const int cx = min(max(px, 0), c.w - 1), cy = min(max(py, 0), c.h - 1);
+                const int64_t k = (int64_t)cy * c.w + cx;
+                // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
+                const float wv_ = a.w_u8 ? (float)(1. / 255) * (float)static_cast<const uint8_t*>(c.weight)[k]
+                                         : static_cast<const float*>(c.weight)[k];
+                w[p] = in ? wv_ : 0.f;
+                gv[p] = *reinterpret_cast<const uint32_t*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + cx * 4);
             }
-#else
-            Up9 u;
-            auto unpack = [](uint32_t v, int (&o)[3]) {
+            if (!top) {
+                const MbCamLevel cn = a.cams_next[n];
+#if MB_DIRECT_TAPS && MB_ARITH_TAPS && MB_PACKED_UP
+                const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
+                Taps9<uint32_t> tp;
+                up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
+                uint32_t urb[4], ug[4];
+                up_g_packed(ur, uc, tp, urb, ug);
 #pragma unroll
-                for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
-            };
+                for (int p = 0; p < 4; p++) {
+                    g[p][0] = (float)ch_of(gv[p], 0) - (float)(urb[p] & 255u);
+                    g[p][1] = (float)ch_of(gv[p], 1) - (float)ug[p];
+                    g[p][2] = (float)ch_of(gv[p], 2) - (float)(urb[p] >> 16);
+                }
+#else
+                Up9 u;
+                auto unpack = [](uint32_t v, int (&o)[3]) {
+#pragma unroll
+                    for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
+                };
 #if MB_DIRECT_TAPS
 #if MB_ARITH_TAPS
-            const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
+                const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
 #else
-            const UpQuad ur = c.up_rows[y >> 1], uc = load_up(c.up_cols, x >> 1);
+                const UpQuad ur = c.up_rows[y >> 1], uc = load_up(c.up_cols, x >> 1);
 #endif
-            Taps9<uint32_t> tp;
-            up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
-            up_quad_taps(ur, uc, tp, unpack, u);
+                Taps9<uint32_t> tp;
+                up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
+                up_quad_taps(ur, uc, tp, unpack, u);
 #else
-            PatchRegs<uint32_t> gp;
-            const int gr0 = c.up_r0[ty], gc0 = c.up_c0[tx];
-            patch_issue<uint32_t>(a.g_next + cn.g_off, cn.g_pitch, cn.h, cn.w, gr0, gc0, gp);
-            __syncthreads();  // the previous camera's patch readers are done
-            patch_store(gp, s_g);
-            __syncthreads();
-            up_quad_lds(c.up_rows[y >> 1], c.up_cols[x >> 1], gr0, gc0, s_g, unpack, u);
+                PatchRegs<uint32_t> gp;
+                const int gr0 = c.up_r0[ty], gc0 = c.up_c0[tx];
+                patch_issue<uint32_t>(a.g_next + cn.g_off, cn.g_pitch, cn.h, cn.w, gr0, gc0, gp);
+                __syncthreads();  // the previous camera's patch readers are done
+                patch_store(gp, s_g);
+                __syncthreads();
+                up_quad_lds(c.up_rows[y >> 1], c.up_cols[x >> 1], gr0, gc0, s_g, unpack, u);
 #endif
 #pragma unroll
-            for (int p = 0; p < 4; p++)
+                for (int p = 0; p < 4; p++)
 #pragma unroll
-                for (int ch = 0; ch < 3; ch++)
-                    g[p][ch] = (float)((int)ch_of(gv[p], ch) - min(max(rne_shr<6>(u.s[p][ch]), 0), 255));  // sat u8
+                    for (int ch = 0; ch < 3; ch++)
+                        g[p][ch] = (float)((int)ch_of(gv[p], ch) - min(max(rne_shr<6>(u.s[p][ch]), 0), 255));  // sat u8
 #endif
-        } else {
+            } else {
 #pragma unroll
-            for (int p = 0; p < 4; p++)
+                for (int p = 0; p < 4; p++)
 #pragma unroll
-                for (int ch = 0; ch < 3; ch++) g[p][ch] = (float)ch_of(gv[p], ch);
+                    for (int ch = 0; ch < 3; ch++) g[p][ch] = (float)ch_of(gv[p], ch);
+            }
         }
         // only where w != 0 in the reference; a zero weight adds +-0 to D and 0 to the weight sum, so the
         // sums are the same without a per-pixel branch
@@ -481,7 +595,9 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             o[1] = (int)(int16_t)(v.x >> 16);
             o[2] = (int)(int16_t)(v.y & 0xFFFFu);
         };
-#if MB_DIRECT_TAPS
+#if MB_DIRECT_TAPS && MB_COLLAPSE_FIRST
+        up_quad_taps(urR, ucR, tpR, unpack, u);
+#elif MB_DIRECT_TAPS
 #if MB_ARITH_TAPS
         // x and y are even on the level grid: every quad has the even tap pattern (1 6 1 | 0 4 4) as
         // constants; the zero weights up_arith gives pixels outside the level only matter for pixels

@@ -210,6 +210,9 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     M.feather = feather_border > 0;
     if (M.feather) M.B = bands = 0;
     const int B = bands;
+    // tile camera sets are 32-bit masks, and the blend's f32 Laplacian sum is exact only while
+    // |D| <= 255 * sum(w) stays below 2^15 (sum(w) <= n <= 32, multiband.hip)
+    REQUIRE(n >= 1 && n <= 32, "multi-band / feather blend: 1..32 inputs");
     if (!M.feather) {
         REQUIRE(B >= 1 && B <= kMbMaxBands, "multi-band blend: band count out of range (blend must be >= 3)");
         REQUIRE(rig.seam_masks.size() == (size_t)n,
