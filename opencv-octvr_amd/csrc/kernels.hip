@@ -950,6 +950,9 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
                       // 65.5 vs 63.7 us: the barrier is not what the item loop waits on), 0: off
 #define OCTVR_LDS_DB 0
 #endif
+#ifndef OCTVR_ISSUE_EARLY  // 1: the next item's loads issued before this item's second barrier
+#define OCTVR_ISSUE_EARLY 0
+#endif
 #ifndef OCTVR_WIDE_OUT  // 1: LDS-staged 16-byte output stores (measured no faster on C2; off)
 #define OCTVR_WIDE_OUT 0
 #endif
@@ -1271,6 +1274,11 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
                 stage_store<VIG>(sg, s_stage);
             }
         }
+#if OCTVR_ISSUE_EARLY
+        // the next item's entry and staging loads before the barrier (their registers are free once
+        // staged): their latency then also covers the barrier wait, not only this item's compute
+        data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
+#endif
         OCTVR_PHASE(1);
         __syncthreads();
         OCTVR_PHASE(2);
@@ -1300,7 +1308,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
                 store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
 #endif
+#if !OCTVR_ISSUE_EARLY
         data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
+#endif
         mv = meta_issue(lut, t_n2, t_end);
         t_mv = t_n2;
         claimed = OCTVR_DYN && t_n2 < t_end;  // claim the item after it (only while the sequence is live)
