@@ -63,6 +63,45 @@ def test_gpu_async_multimapper_bit_exact(product_lib, out_size, blends, gain_mod
     am.close()
 
 
+def test_gpu_async_side_by_side_regions(product_lib):
+    """Regions split horizontally (x offsets, pitched output rows): the copy-out stage's row ranges
+    over its helper threads (async.cpp RowPool) write each region's rows at its own column offset."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    rig, z = O.load_rig("rigB")
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    sizes = [(rig["inputs"][i]["options"]["width"], rig["inputs"][i]["options"]["height"]) for i in range(n)]
+    maps1 = [z[f"map1_{i}"] for i in range(n)]
+    maps2 = [z[f"map2_{i}"] for i in range(n)]
+    masks = [z[f"mask_{i}"] for i in range(n)]
+    mts = [ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks) for _ in range(2)]
+    OW, OH = 2 * W, H  # two template-size regions side by side
+    am = ox.AsyncMultiMapper(mts, sizes, (OW, OH), [0, 0], [0, 0], [(0.0, 0.0, 0.5, 1.0), (0.5, 0.0, 0.5, 1.0)])
+    frames, outs = [], []
+    for f in range(7):
+        fr = [synthetic.smooth_yuv_frame(w, h, 300 + 10 * f + i) for i, (w, h) in enumerate(sizes)]
+        out = (np.zeros((OH, OW), np.uint8), np.zeros((OH // 2, OW // 2), np.uint8), np.zeros((OH // 2, OW // 2), np.uint8))
+        am.push([_planes(x, w, h) for x, (w, h) in zip(fr, sizes)], out)
+        frames.append(fr)
+        outs.append(out)
+        if am.pending() >= 3:
+            am.pop()
+    while am.pending():
+        am.pop()
+    for f in range(7):
+        want, _ = O.stitch_frame(frames[f], sizes, z["rois"].tolist(), maps1, maps2, masks, W, H,
+                                 enable_gain=True, threads=8)
+        for k in range(2):
+            x0 = k * W
+            assert np.array_equal(outs[f][0][:, x0:x0 + W], want[:H]), (f, k, "Y")
+            assert np.array_equal(outs[f][1][:, x0 // 2:(x0 + W) // 2], want[H:, :W // 2]), (f, k, "U")
+            assert np.array_equal(outs[f][2][:, x0 // 2:(x0 + W) // 2], want[H:, W // 2:]), (f, k, "V")
+    am.close()
+
+
 def test_gpu_async_rejects_bad_regions(product_lib):
     ox = product_lib
     rig, z = O.load_rig("rigA")
