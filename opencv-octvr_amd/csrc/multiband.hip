@@ -326,14 +326,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
                            rc0, rp);
     }
 #endif
-    float D[4][3];  // the Laplacian accumulator (a CV_16S sum in the reference; exact here, see below)
-    float wsum[4];
-#pragma unroll
-    for (int p = 0; p < 4; p++) {
-        wsum[p] = 1e-5f;
-#pragma unroll
-        for (int ch = 0; ch < 3; ch++) D[p][ch] = 0.f;
-    }
 #if MB_RUP_EARLY  // the collapse's per-column tap table loaded before the camera loop, kept raw
     uint4 ucR_raw = make_uint4(0u, 0u, 0u, 0u);
     if (!top) ucR_raw = *reinterpret_cast<const uint4*>(a.rup_cols + (x >> 1));
@@ -357,7 +349,42 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             for (int k = 0; k < 3; k++) tpR.t[j][k] = make_uint2(0u, 0u);
     }
 #endif
+    int R[4][3];
     uint32_t m = (uint32_t)uniform((int)a.tile_cams[tile]);
+    // Level-0 tiles owned by one camera (its seam is 255 on every tile pixel, tile_owned): the
+    // weight is 1.0f everywhere, so D = G - pyrUp(G_next) exactly, the weight sum is kWsumOwned and
+    // rint(D * kRcpOwned) = D (|D| <= 255): the Laplacian is taken as is, no weight loads or sums.
+    if (a.owned != nullptr && !top && a.owned[tile] != 0) {
+        const int n = __builtin_ctz(m);
+        const MbCamLevel c = a.cams[n];
+        const int xl = x - c.ox, yl = y - c.oy;  // inside the camera (seam pixels), even
+        const int x0 = min(max(xl, 0), c.w - 2);
+        const int cy0 = min(max(yl, 0), c.h - 1), cy1 = min(max(yl + 1, 0), c.h - 1);
+        const uint2 gp0 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy0 * c.g_pitch + x0 * 4);
+        const uint2 gp1 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy1 * c.g_pitch + x0 * 4);
+        const MbCamLevel cn = a.cams_next[n];
+        const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
+        Taps9<uint32_t> tp;
+        up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
+        uint32_t urb[4], ug[4];
+        up_g_packed(ur, uc, tp, urb, ug);
+#pragma unroll
+        for (int p = 0; p < 4; p++) {
+            const uint2 gp = (p >> 1) ? gp1 : gp0;
+            const uint32_t gv = ((xl + (p & 1) - x0) & 1) ? gp.y : gp.x;
+            R[p][0] = (int)ch_of(gv, 0) - (int)(urb[p] & 255u);
+            R[p][1] = (int)ch_of(gv, 1) - (int)ug[p];
+            R[p][2] = (int)ch_of(gv, 2) - (int)(urb[p] >> 16);
+        }
+    } else {
+    float D[4][3];  // the Laplacian accumulator (a CV_16S sum in the reference; exact here, see below)
+    float wsum[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        wsum[p] = 1e-5f;
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) D[p][ch] = 0.f;
+    }
     while (m) {
         const int n = __builtin_ctz(m);
         m &= m - 1;
@@ -575,7 +602,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             wsum[p] = wsum[p] + w[p];
         }
     }
-    int R[4][3];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         // feather: convertTo(CV_8UC3, 1/n) = sat_u8(alpha * D) (clamped to u8 below); multi-band:
@@ -587,6 +613,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 #pragma unroll
         for (int ch = 0; ch < 3; ch++)
             R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf(D[p][ch] * rcp), -32768.f, 32767.f);
+    }
     }
     if (!top) {
         Up9 u;

@@ -53,6 +53,8 @@ class MultiBand {
         DevBuf<float> wts;              // level > 0: f32 weights over each align_roi >> l
         DevBuf<uint32_t> tile_cams;
         std::vector<uint32_t> tile_cams_h;
+        DevBuf<uint8_t> owned;          // level 0 multi-band: per tile, one camera with seam 255 throughout
+        int n_owned = 0;
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
         int rup_rows = 0;
@@ -317,6 +319,8 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         for (int i = 0; i < n; i++) L0.cams_h[i].weight = L0.wts.p + woff[i];
     }
     // ---- weights: level 0 = seam (u8), levels >= 1 = K4 pyrDown of seam/255 ------------------
+    std::vector<uint8_t> seam_h;      // level-0 seams over each align_roi (host copy, for tile_owned)
+    std::vector<size_t> seam_off;
     if (!M.feather) {
         auto& L0 = M.lv[0];
         size_t tot = 0;
@@ -337,6 +341,8 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                 }
         }
         L0.seam0.upload(s0.data(), s0.size());
+        seam_h = s0;
+        seam_off = woff;
         for (int i = 0; i < n; i++) L0.cams_h[i].weight = L0.seam0.p + woff[i];
         DevBuf<float> prev;
         prev.upload(f0.data(), f0.size());
@@ -383,6 +389,31 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                         L.tile_cams_h[(size_t)(by * kBlk / kTileH) * L.tx_n + bx * kBlk / kTileW] |= 1u << i;
         }
         L.tile_cams.upload(L.tile_cams_h.data(), L.tile_cams_h.size());
+        if (l == 0 && !M.feather && B >= 1) {
+            // tile_owned: one camera with a non-zero seam in the tile, and its seam is 255 on every
+            // tile pixel of the level grid (so each pixel's weight is exactly 1 for it, 0 for the rest)
+            std::vector<uint8_t> owned((size_t)L.tx_n * L.ty_n, 0);
+            for (int ty = 0; ty < L.ty_n; ty++)
+                for (int tx = 0; tx < L.tx_n; tx++) {
+                    const uint32_t msk = L.tile_cams_h[(size_t)ty * L.tx_n + tx];
+                    if (__builtin_popcount(msk) != 1) continue;
+                    const int i = __builtin_ctz(msk);
+                    const auto& c = L.cams_h[i];
+                    bool all = true;
+                    for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
+                        for (int x = tx * kTileW; x < std::min((tx + 1) * kTileW, L.W); x++) {
+                            const int xl = x - c.ox, yl = y - c.oy;
+                            if (xl < 0 || yl < 0 || xl >= c.w || yl >= c.h ||
+                                seam_h[seam_off[i] + (size_t)yl * c.w + xl] != 255) {
+                                all = false;
+                                break;
+                            }
+                        }
+                    owned[(size_t)ty * L.tx_n + tx] = all ? 1 : 0;
+                    L.n_owned += all ? 1 : 0;
+                }
+            L.owned.upload(owned.data(), owned.size());
+        }
     }
     // ---- pyrUp tap tables -------------------------------------------------------------------
     std::vector<std::vector<std::vector<UpQuad>>> ur(B), uc(B);  // [level][camera]
@@ -608,6 +639,7 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
         a.H = L.H;
         a.tiles_x = L.tx_n;
         a.tile_cams = L.tile_cams.p;
+        a.owned = l == 0 ? L.owned.p : nullptr;
         a.cams = L.cams.p;
         a.g = G(l);
         if (l < M.B) {
@@ -668,9 +700,10 @@ std::string multiband_info(const MultiBand& M) {
         const auto& L = M.lv[l];
         size_t cam_tiles = 0;
         for (uint32_t m : L.tile_cams_h) cam_tiles += (size_t)__builtin_popcount(m);
-        char buf[160];
-        snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d}",
-                 l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down);
+        char buf[224];
+        snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d%s}",
+                 l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down,
+                 l == 0 && L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned)).c_str() : "");
         s += buf;
     }
     return s + "]";
