@@ -953,6 +953,9 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #ifndef OCTVR_ISSUE_EARLY  // 1: the next item's loads issued before this item's second barrier
 #define OCTVR_ISSUE_EARLY 0
 #endif
+#ifndef OCTVR_PRIO_STAGE  // > 0: s_setprio for the staging phase (the waves its barrier waits for)
+#define OCTVR_PRIO_STAGE 0
+#endif
 #ifndef OCTVR_WIDE_OUT  // 1: LDS-staged 16-byte output stores (measured no faster on C2; off)
 #define OCTVR_WIDE_OUT 0
 #endif
@@ -1243,6 +1246,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         // (or one after a big item) overlaps it and first waits for its readers.
         const bool big = !OCTVR_LDS_DB || (cur.nslots & kHdrBigItem) != 0u;
         if (big || prev_big) __syncthreads();
+#if OCTVR_PRIO_STAGE  // the staging phase (between the item's two barriers) at raised wave priority
+        __builtin_amdgcn_s_setprio(OCTVR_PRIO_STAGE);
+#endif
         uint32_t* const s_stage = s_rgb + (big ? 0u : half * (uint32_t)(kTileHalfBytes / 4));
         if (tid < kTileZeroDwords) s_stage[tid] = 0u;  // black pixels read offset 0 of the region
         OCTVR_PHASE(0);
@@ -1281,6 +1287,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #endif
         OCTVR_PHASE(1);
         __syncthreads();
+#if OCTVR_PRIO_STAGE
+        __builtin_amdgcn_s_setprio(0);
+#endif
         OCTVR_PHASE(2);
         // the item two ahead: static on the first iteration, else the claim handed over above
         if (!first) {

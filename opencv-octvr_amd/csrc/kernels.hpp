@@ -312,7 +312,7 @@ struct MbBlendArgs {
     int W, H;                       // level grid
     int tiles_x;
     const uint32_t* tile_cams;      // bit n: camera n has a non-zero weight in the tile
-    const uint8_t* owned;           // level 0 multi-band (or NULL): the tile's one camera has seam 255 on every tile pixel
+    const uint8_t* owned;           // multi-band (or NULL): the tile's one camera has weight 1 on every tile pixel
     const MbCamLevel* cams;         // this level
     const MbCamLevel* cams_next;    // level + 1 (NULL at the top)
     const uint8_t* g;               // this level's pyramid allocation

@@ -351,10 +351,11 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 #endif
     int R[4][3];
     uint32_t m = (uint32_t)uniform((int)a.tile_cams[tile]);
-    // Level-0 tiles owned by one camera (its seam is 255 on every tile pixel, tile_owned): the
-    // weight is 1.0f everywhere, so D = G - pyrUp(G_next) exactly, the weight sum is kWsumOwned and
-    // rint(D * kRcpOwned) = D (|D| <= 255): the Laplacian is taken as is, no weight loads or sums.
-    if (a.owned != nullptr && !top && a.owned[tile] != 0) {
+    // Tiles owned by one camera (its weight is exactly 1.0f on every tile pixel: seam 255 at level 0,
+    // the f32 pyramid's 1.0f above; tile_owned): D = G - pyrUp(G_next) (G at the top level) exactly,
+    // the weight sum is kWsumOwned and rint(D * kRcpOwned) = D (|D| <= 255), so the Laplacian is taken
+    // as is, with no weight loads or sums.
+    if (a.owned != nullptr && a.owned[tile] != 0) {
         const int n = __builtin_ctz(m);
         const MbCamLevel c = a.cams[n];
         const int xl = x - c.ox, yl = y - c.oy;  // inside the camera (seam pixels), even
@@ -362,19 +363,21 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
         const int cy0 = min(max(yl, 0), c.h - 1), cy1 = min(max(yl + 1, 0), c.h - 1);
         const uint2 gp0 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy0 * c.g_pitch + x0 * 4);
         const uint2 gp1 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy1 * c.g_pitch + x0 * 4);
-        const MbCamLevel cn = a.cams_next[n];
+        // (the top level reads its own G as a stand-in for the unused taps, as the general path)
+        const MbCamLevel cn = *(top ? a.cams + n : a.cams_next + n);
         const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
         Taps9<uint32_t> tp;
-        up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
+        up_taps_issue<uint32_t>(ur, uc, (top ? a.g : a.g_next) + cn.g_off, cn.g_pitch, tp);
         uint32_t urb[4], ug[4];
         up_g_packed(ur, uc, tp, urb, ug);
 #pragma unroll
         for (int p = 0; p < 4; p++) {
             const uint2 gp = (p >> 1) ? gp1 : gp0;
             const uint32_t gv = ((xl + (p & 1) - x0) & 1) ? gp.y : gp.x;
-            R[p][0] = (int)ch_of(gv, 0) - (int)(urb[p] & 255u);
-            R[p][1] = (int)ch_of(gv, 1) - (int)ug[p];
-            R[p][2] = (int)ch_of(gv, 2) - (int)(urb[p] >> 16);
+            const uint32_t u0 = top ? 0u : urb[p] & 255u, u1 = top ? 0u : ug[p], u2 = top ? 0u : urb[p] >> 16;
+            R[p][0] = (int)ch_of(gv, 0) - (int)u0;
+            R[p][1] = (int)ch_of(gv, 1) - (int)u1;
+            R[p][2] = (int)ch_of(gv, 2) - (int)u2;
         }
     } else {
     float D[4][3];  // the Laplacian accumulator (a CV_16S sum in the reference; exact here, see below)

@@ -53,7 +53,7 @@ class MultiBand {
         DevBuf<float> wts;              // level > 0: f32 weights over each align_roi >> l
         DevBuf<uint32_t> tile_cams;
         std::vector<uint32_t> tile_cams_h;
-        DevBuf<uint8_t> owned;          // level 0 multi-band: per tile, one camera with seam 255 throughout
+        DevBuf<uint8_t> owned;          // multi-band: per tile, one camera of weight exactly 1 throughout
         int n_owned = 0;
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
@@ -389,9 +389,15 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                         L.tile_cams_h[(size_t)(by * kBlk / kTileH) * L.tx_n + bx * kBlk / kTileW] |= 1u << i;
         }
         L.tile_cams.upload(L.tile_cams_h.data(), L.tile_cams_h.size());
-        if (l == 0 && !M.feather && B >= 1) {
-            // tile_owned: one camera with a non-zero seam in the tile, and its seam is 255 on every
-            // tile pixel of the level grid (so each pixel's weight is exactly 1 for it, 0 for the rest)
+        if (!M.feather) {
+            // tile_owned: one camera with a non-zero weight in the tile, and its weight is exactly 1 on
+            // every tile pixel of the level grid (level 0: seam 255; above: the f32 pyramid's 1.0f), so
+            // each pixel's Laplacian is that camera's alone with weight 1 (mb_blend's fast path)
+            std::vector<float> wl;  // level l > 0: the f32 weights of every camera (host copy)
+            if (l > 0) {
+                wl.resize(L.wts.n);
+                HIP_CHECK(hipMemcpy(wl.data(), L.wts.p, wl.size() * sizeof(float), hipMemcpyDeviceToHost));
+            }
             std::vector<uint8_t> owned((size_t)L.tx_n * L.ty_n, 0);
             for (int ty = 0; ty < L.ty_n; ty++)
                 for (int tx = 0; tx < L.tx_n; tx++) {
@@ -399,12 +405,14 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                     if (__builtin_popcount(msk) != 1) continue;
                     const int i = __builtin_ctz(msk);
                     const auto& c = L.cams_h[i];
-                    bool all = true;
+                    const size_t woff = l == 0 ? seam_off[i] : (size_t)(static_cast<const float*>(c.weight) - L.wts.p);
+                    bool all = c.w >= 2;  // the fast path reads pixel pairs
                     for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
                         for (int x = tx * kTileW; x < std::min((tx + 1) * kTileW, L.W); x++) {
                             const int xl = x - c.ox, yl = y - c.oy;
+                            const size_t k = woff + (size_t)yl * c.w + xl;
                             if (xl < 0 || yl < 0 || xl >= c.w || yl >= c.h ||
-                                seam_h[seam_off[i] + (size_t)yl * c.w + xl] != 255) {
+                                (l == 0 ? seam_h[k] != 255 : wl[k] != 1.0f)) {
                                 all = false;
                                 break;
                             }
@@ -639,7 +647,7 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
         a.H = L.H;
         a.tiles_x = L.tx_n;
         a.tile_cams = L.tile_cams.p;
-        a.owned = l == 0 ? L.owned.p : nullptr;
+        a.owned = L.owned.p;
         a.cams = L.cams.p;
         a.g = G(l);
         if (l < M.B) {
@@ -703,7 +711,7 @@ std::string multiband_info(const MultiBand& M) {
         char buf[224];
         snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d%s}",
                  l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down,
-                 l == 0 && L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned)).c_str() : "");
+                 L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned)).c_str() : "");
         s += buf;
     }
     return s + "]";
