@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--no-async-e2e", action="store_true",
                     help="skip the AsyncMultiMapper end-to-end (PCIe-inclusive) measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--no-gain", action="store_true", help=argparse.SUPPRESS)  # diagnostic: composite alone
     return ap.parse_args()
 
 
@@ -194,7 +195,7 @@ def main():
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=True, device=dev)
     if blend > 0:
         mt.create_masks(dev)  # MapperTemplate::create_masks (DistanceSeamFinder), as octvr_dump does
-    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, device=dev)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=not args.no_gain, device=dev)
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
     inflight = max(1, args.inflight)

@@ -94,6 +94,35 @@ __device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t
     }
 }
 
+// bilerp_rgba at weight scale 2^16, straight from a tiled entry (fx bits 15-19, fy 20-24), channel
+// values returned as floats.  X = {64 (32 - fx), 64 fx} (one 24-bit multiply-add), w0 = X (32 - fy) and
+// w1 = X fy per 16-bit half, so (sum + 2^15) >> 16 is bilerp_rgba's (sum' + 2^9) >> 10 exactly
+// (w = 64 w').  Every half stays <= 63,488 except code 0's (fx = fy = 0) 65,536: w0 is formed as
+// X (31 - fy) + X with a saturating packed add (v_pk_add_u16 clamp; gfx950 ignores the clamp bit of
+// v_pk_mul_lo_u16, scripts/clamp_probe.hip), so that half becomes 65,535 and
+// (65535 c00 + 2^15) >> 16 = c00 for c00 <= 255 — the table's own {32767, 0, 0, 1} result.  The sum
+// stays below 2^24, so the result is byte 2 of it: v_cvt_f32_ubyte2, no shift (5 VALU per channel
+// instead of 6: perm, perm, dot2, dot2, cvt).
+__device__ __forceinline__ void bilerp_rgba_f(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint32_t e,
+                                              float (&rgb)[3]) {
+    const uint32_t fx = (e >> 15) & 31u, fy = (e >> 20) & 31u;
+    const uint32_t X = __umul24(fx, 0x3FFFC0u) + 2048u;  // (2048 - 64 fx) | (64 fx) << 16
+    const u16x2_t Xv = __builtin_bit_cast(u16x2_t, X);
+    const unsigned short gy = (unsigned short)(31u - fy);
+    const u16x2_t w0v = __builtin_elementwise_add_sat(Xv * u16x2_t{gy, gy}, Xv);
+    const uint32_t w0 = __builtin_bit_cast(uint32_t, w0v);
+    const u16x2_t w1 = Xv * u16x2_t{(unsigned short)fy, (unsigned short)fy};
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const uint32_t sel = 0x0C000C00u | ((4u + ch) << 16) | (uint32_t)ch;  // {lo.ch, 0, hi.ch, 0}
+        const u16x2_t top = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c01, c00, sel));
+        const u16x2_t bot = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c11, c10, sel));
+        const uint32_t S = __builtin_amdgcn_udot2(
+            bot, w1, __builtin_amdgcn_udot2(top, __builtin_bit_cast(u16x2_t, w0), 32768u, false), false);
+        rgb[ch] = (float)((S >> 16) & 255u);
+    }
+}
+
 // Direct (global-memory) bilinear sample of one camera at an 8-byte composite entry — the gain feed
 // samples and "wide" tiles.  Every load is issued unconditionally from a clamped in-image address;
 // taps outside the image and invalid entries are zeroed afterwards.
@@ -170,6 +199,30 @@ __device__ __forceinline__ QuadOut finish_quad2(const uint32_t (&rgb)[4][3], con
         br.x = __builtin_amdgcn_fmed3f(__builtin_rintf(br.x), 0.f, 255.f);
         br.y = __builtin_amdgcn_fmed3f(__builtin_rintf(br.y), 0.f, 255.f);
         const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain2[p].x), 0.f, 255.f);
+        const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
+        if (p < 2) y01 = pack_u8(Yf, p, y01);
+        else y23 = pack_u8(Yf, p - 2, y23);
+        uv = __builtin_elementwise_fma(kuv, br - Yf, uv);
+    }
+    QuadOut q;
+    q.y01 = y01;
+    q.y23 = y23;
+    q.u = pack_u8(__builtin_fmaf(uv.x, 0.25f, 128.f), 0, 0u);
+    q.v = pack_u8(__builtin_fmaf(uv.y, 0.25f, 128.f), 0, 0u);
+    return q;
+}
+
+// finish_quad2 from channel values already in f32
+__device__ __forceinline__ QuadOut finish_quad2f(const float (&rgb)[4][3], const f32x2_t (&gain2)[4]) {
+    uint32_t y01 = 0, y23 = 0;
+    f32x2_t uv = {0.f, 0.f};  // (us, vs)
+    const f32x2_t kuv = {0.492f, 0.877f};
+#pragma unroll
+    for (int p = 0; p < 4; p++) {
+        f32x2_t br = f32x2_t{rgb[p][2], rgb[p][0]} * gain2[p];
+        br.x = __builtin_amdgcn_fmed3f(__builtin_rintf(br.x), 0.f, 255.f);
+        br.y = __builtin_amdgcn_fmed3f(__builtin_rintf(br.y), 0.f, 255.f);
+        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf(rgb[p][1] * gain2[p].x), 0.f, 255.f);
         const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
         if (p < 2) y01 = pack_u8(Yf, p, y01);
         else y23 = pack_u8(Yf, p - 2, y23);

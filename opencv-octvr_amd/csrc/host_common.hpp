@@ -174,8 +174,7 @@ struct TiledLutBuild {
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
                               const std::vector<int>& in_h, int qpl = 1);
 struct TiledLutDev {
-    DevBuf<TileHdr> hdr;
-    DevBuf<TileSlot> slots;
+    DevBuf<TileHdr> meta;  // kMetaWords 16-byte words per staged item (kernels.hpp TiledLut::meta)
     DevBuf<uint32_t> entries;
     DevBuf<CompositeEntry> wide;
     DevBuf<uint32_t> wide_tiles;

@@ -953,6 +953,7 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #ifndef OCTVR_ISSUE_EARLY  // 1: the next item's loads issued before this item's second barrier
 #define OCTVR_ISSUE_EARLY 0
 #endif
+constexpr int kGainTables = OCTVR_LDS_DB ? 2 : 1;
 #ifndef OCTVR_PRIO_STAGE  // > 0: s_setprio for the staging phase (the waves its barrier waits for)
 #define OCTVR_PRIO_STAGE 0
 #endif
@@ -977,13 +978,18 @@ constexpr int kStageRegs = OCTVR_STAGE_REGS;
 // same vector-memory operations in the same order (clamped addresses instead of branches), so the
 // compiler's wait counts stay exact across the loop.
 //
-__device__ __forceinline__ uint4 meta_issue(const TiledLut& lut, int t, int t_end) {  // t: staged item
+// One buffer load by lanes 0..kMetaWords-1: the voffset (lane * 16) is loop-invariant, the item's
+// record offset a scalar, so no per-lane 64-bit address is held across the loop.
+__device__ __forceinline__ uint4 meta_issue(const __amdgpu_buffer_rsrc_t& mr, int t, int t_end) {  // t: staged item
     const int lane = threadIdx.x & 63;
     const int tt = t < t_end ? t : 0;  // t >= 0: every item index derives from bounded claims
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     uint4 v;
-    if (lane < 1 + kTileSlots)  // exec-masked: the instruction (and its vmcnt) is the same for every wave
-        v = lane == 0 ? *reinterpret_cast<const uint4*>(lut.hdr + tt)
-                      : *reinterpret_cast<const uint4*>(lut.slots + (int64_t)tt * kTileSlots + (lane - 1));
+    if (lane < kMetaWords) {  // exec-masked: the instruction (and its vmcnt) is the same for every wave
+        const u32x4 r = __builtin_amdgcn_raw_buffer_load_b128(mr, (uint32_t)lane * 16u,
+                                                              (uint32_t)uniform(tt) * (uint32_t)(kMetaWords * 16), 0);
+        v = uint4{r.x, r.y, r.z, r.w};
+    }
     return v;
 }
 
@@ -1043,16 +1049,16 @@ __device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& 
 // Mapper::stitch hands to the blender, mapper.cpp:233-262); pixels outside the camera's aligned ROI
 // are dropped.  Either way a quad's result is 4 dwords.
 template <int MODE>
-__device__ __forceinline__ QuadOut finish_any(const uint32_t (&rgb)[4][3], const f32x2_t (&gain)[4]) {
+__device__ __forceinline__ QuadOut finish_any(const float (&rgb)[4][3], const f32x2_t (&gain)[4]) {
     if constexpr (MODE == 0) {
-        return finish_quad2(rgb, gain);
+        return finish_quad2f(rgb, gain);
     } else {
         uint32_t px[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            uint32_t v = pack_u8((float)rgb[p][0] * gain[p].x, 0, 0u);
-            v = pack_u8((float)rgb[p][1] * gain[p].x, 1, v);
-            px[p] = pack_u8((float)rgb[p][2] * gain[p].x, 2, v);
+            uint32_t v = pack_u8(rgb[p][0] * gain[p].x, 0, 0u);
+            v = pack_u8(rgb[p][1] * gain[p].x, 1, v);
+            px[p] = pack_u8(rgb[p][2] * gain[p].x, 2, v);
         }
         return QuadOut{px[0], px[1], px[2], px[3]};
     }
@@ -1139,7 +1145,10 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     __shared__ float s_gain[kMaxCams];
     // per iteration parity: written before an item's staging barrier, read after it (the next write
     // to the same entry is two items later, behind the next barrier)
-    __shared__ f32x2_t s_slot_gain[2][kTileSlots];  // {g, g} per slot (finish_quad2)
+    // {g, g} per slot (finish_quad2f).  Written after an item's first barrier and read after its
+    // second; the next write comes after the next item's first barrier, i.e. after every wave's last
+    // read, so one table suffices (two, by iteration parity, when OCTVR_LDS_DB may skip that barrier).
+    __shared__ f32x2_t s_slot_gain[kGainTables][kTileSlots];
     __shared__ uint32_t s_claim[2];
     // MODE 2: the previous item's YUV420P output, staged in LDS and written with one 16-byte store
     // per lane (store_item_wide) instead of four 1-2-byte stores per quad
@@ -1158,6 +1167,8 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     const int step = (gridDim.x - g + groups - 1) / groups;
     const int t_begin = lut.bands[g];
     const int t_end = lut.bands[g + 1];
+    const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<TileHdr*>(lut.meta), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kMetaWords * 16)), 0x00020000);
     OutFrame of{};
     RgbaSink ro{};
     if constexpr (SM == 0)
@@ -1183,7 +1194,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     const int dyn0 = t_begin + 3 * step;  // item of claim value 0
     uint32_t* const q = lut.queue + g * kQueueStride;
     const int wave = uniform(tid >> 6);
-    TileMeta cur = meta_read(meta_issue(lut, t0, t_end), t0);
+    TileMeta cur = meta_read(meta_issue(mrsrc, t0, t_end), t0);
     __syncthreads();
     TileData<QPL, R> d;
     {
@@ -1194,7 +1205,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     }
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
-    uint4 mv = meta_issue(lut, t_mv, t_end);
+    uint4 mv = meta_issue(mrsrc, t_mv, t_end);
     uint32_t claim = 0u;  // lane 0 of wave 0: returned value of the claim in flight
     bool claimed = false; // a claim for the item after t_n2 is in flight (uniform)
     bool first = true;
@@ -1245,7 +1256,11 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         // Staging region: a small item takes the LDS half the previous item does not read; a big item
         // (or one after a big item) overlaps it and first waits for its readers.
         const bool big = !OCTVR_LDS_DB || (cur.nslots & kHdrBigItem) != 0u;
+#if OCTVR_DIAG_NOBAR  // diagnostic (wrong output, timing only): no item barriers, static dealing only
+        static_assert(!OCTVR_DYN, "the claim hand-over through LDS needs the barriers");
+#else
         if (big || prev_big) __syncthreads();
+#endif
 #if OCTVR_PRIO_STAGE  // the staging phase (between the item's two barriers) at raised wave priority
         __builtin_amdgcn_s_setprio(OCTVR_PRIO_STAGE);
 #endif
@@ -1259,7 +1274,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
-            if (tid < kTileSlots) s_slot_gain[par][tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
+            if (tid < kTileSlots) s_slot_gain[kGainTables > 1 ? par : 0][tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
         }
         if (claimed && tid == 0) s_claim[par] = claim;  // issued one iteration ago
 #if !OCTVR_DIAG_NOSTAGE
@@ -1286,7 +1301,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
 #endif
         OCTVR_PHASE(1);
+#if !OCTVR_DIAG_NOBAR
         __syncthreads();
+#endif
 #if OCTVR_PRIO_STAGE
         __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1320,7 +1337,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #if !OCTVR_ISSUE_EARLY
         data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
 #endif
-        mv = meta_issue(lut, t_n2, t_end);
+        mv = meta_issue(mrsrc, t_n2, t_end);
         t_mv = t_n2;
         claimed = OCTVR_DYN && t_n2 < t_end;  // claim the item after it (only while the sequence is live)
         if (claimed && tid == 0) {
@@ -1334,7 +1351,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #pragma unroll
         for (int h = 0; h < QPL; h++) {
         const uint32_t ent[4] = {e4[h].x, e4[h].y, e4[h].z, e4[h].w};
-        uint32_t rgb[4][3];
+        float rgb[4][3];
         f32x2_t gain[4];
 #if OCTVR_TAPS_FIRST  // the quad's 8 LDS reads issued before any of its arithmetic
         uint32_t t00[4], t01[4], t10[4], t11[4];
@@ -1364,15 +1381,17 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #endif
 #if OCTVR_DIAG_NOTAPS
             (void)c00; (void)c01; (void)c10; (void)c11;
-            rgb[p][0] = e & 255u; rgb[p][1] = (e >> 8) & 255u; rgb[p][2] = (e >> 16) & 255u;
+            rgb[p][0] = (float)(e & 255u); rgb[p][1] = (float)((e >> 8) & 255u); rgb[p][2] = (float)((e >> 16) & 255u);
 #else
-            bilerp_rgba(c00, c01, c10, c11, (e >> 15) & 31u, (e >> 20) & 31u, rgb[p]);
+            bilerp_rgba_f(c00, c01, c10, c11, e, rgb[p]);
 #endif
-            gain[p] = s_slot_gain[par][(e >> 25) & 3u];
+            // slot << 3 = e >> 27 (bits 25-29 of a composite entry are zero; kernels.hpp)
+            gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain[kGainTables > 1 ? par : 0]) +
+                                                        (e >> 27));
             if (SM == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
         }
 #if OCTVR_DIAG_NOCOMPUTE
-        prev[h] = QuadOut{rgb[0][0] ^ rgb[1][1], rgb[2][2] ^ rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
+        prev[h] = QuadOut{(uint32_t)rgb[0][0] ^ (uint32_t)rgb[1][1], (uint32_t)rgb[2][2] ^ (uint32_t)rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
 #else
         prev[h] = finish_any<SM>(rgb, gain);
 #endif
@@ -1471,7 +1490,12 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
         gain[p] = f32x2_t{gp, gp};
     }
     const uint32_t cam = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;
-    store_any<MODE>(of, ro, finish_any<MODE>(rgb, gain), cam, x, y, x < W && y < H);
+    float rgbf[4][3];
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) rgbf[p][ch] = (float)rgb[p][ch];
+    store_any<MODE>(of, ro, finish_any<MODE>(rgbf, gain), cam, x, y, x < W && y < H);
 }
 
 template <int MODE>

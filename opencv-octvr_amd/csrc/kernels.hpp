@@ -74,7 +74,9 @@ __host__ __device__ inline TapCell tap_cell(uint32_t xy, int w, int h) {
 // the source image: staging writes RGBA 0 for box pixels outside the image (BORDER_CONSTANT), so
 // every tap is read from LDS at off, off + 4, off + 4 S, off + 4 S + 4 (S = row stride) unmasked.
 // The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel:
-//   bits 0-14 LDS byte offset of tap (x, y); 15-19 fx; 20-24 fy; 25-26 slot; 29 "no gain".
+//   bits 0-14 LDS byte offset of tap (x, y); 15-19 fx; 20-24 fy; 25 "no gain" (RGBA mode); 26-29
+//   zero; 30-31 slot (so the slot's gain sits at byte offset e >> 27 of a 4-slot table of f32 pairs:
+//   one shift per pixel, kernels.hip).
 // A pixel with no camera, or with every tap outside, is entry 0 and comes out black.
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
@@ -178,8 +180,7 @@ hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* sample
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 
 struct TiledLut {
-    const TileHdr* hdr;           // per staged item
-    const TileSlot* slots;        // kTileSlots per staged item
+    const TileHdr* meta;          // per staged item kMetaWords 16-byte words: the TileHdr, then kTileSlots TileSlots
     const uint32_t* entries;      // kTilePx per staged item, quad-major inside the tile
     int n_items;
     const uint32_t* wide_tiles;   // tile column | row << 16 of each wide tile
@@ -191,6 +192,7 @@ struct TiledLut {
                                   // zero before a launch, left zero by its last workgroup
     int qpl;                      // quads per lane: an item is 128 x (8 qpl) pixels, qpl * kTilePx entries
 };
+constexpr int kMetaWords = 1 + kTileSlots;
 constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter
 // The staged items are cut into one contiguous band per XCD (locality: neighbouring tiles share
 // source boxes in that XCD's L2), balanced by cost = base + chunk weight x staging chunks.  Measured
@@ -201,10 +203,11 @@ constexpr int kStitchBands = 8;
 #ifndef OCTVR_BAND_CHUNK_WEIGHT
 #define OCTVR_BAND_CHUNK_WEIGHT 0
 #endif
-// 4-byte tiled entries: bit 29 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
+// 4-byte tiled entries: bit 25 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
 // in-image map value; mul_scalar_with_mask, exposure_compensate.cu:15-30).  8-byte CompositeEntry
 // records carry the same flag in code bit 16.  TileHdr.nslots bits 16-20: output camera (RGBA mode).
-constexpr uint32_t kEntryNoGain = 1u << 29;
+constexpr uint32_t kEntryNoGain = 1u << 25;
+constexpr int kEntrySlotShift = 30;
 constexpr uint32_t kCodeNoGain = 1u << 16;
 
 // Quads per lane of the blend = 0 composite's items (OCTVR_QPL, default 2: 128 x 16 items).

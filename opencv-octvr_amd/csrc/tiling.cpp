@@ -8,6 +8,7 @@
 // pixel as a 4-byte box-relative LDS byte offset + fractions + slot; jobs that do not
 // fit (> 4 cameras, a box > 256 px, or LDS above kTileLdsBytes) become "wide" with 8-byte entries.
 #include <algorithm>
+#include <cstring>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -147,7 +148,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 const TileSlot& sl = ts[px[k].slot];
                 const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
                 out[k] = off * 4u | ((uint32_t)(px[k].fxy & 31) << 15) | ((uint32_t)(px[k].fxy >> 5) << 20) |
-                         ((uint32_t)px[k].slot << 25) | (px[k].nogain ? kEntryNoGain : 0u);
+                         ((uint32_t)px[k].slot << kEntrySlotShift) | (px[k].nogain ? kEntryNoGain : 0u);
             }
         }
     };
@@ -234,8 +235,15 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
 }
 
 void TiledLutDev::upload(const TiledLutBuild& b) {
-    hdr.upload(b.hdr.data(), b.hdr.size());
-    slots.upload(b.slots.data(), b.slots.size());
+    // per staged item one 80-byte record: its TileHdr, then its kTileSlots TileSlots (lane q of the
+    // metadata load reads 16-byte word q)
+    static_assert(sizeof(TileHdr) == 16 && sizeof(TileSlot) == 16, "16-byte metadata words");
+    std::vector<TileHdr> m(b.hdr.size() * kMetaWords);
+    for (size_t t = 0; t < b.hdr.size(); t++) {
+        m[t * kMetaWords] = b.hdr[t];
+        std::memcpy(&m[t * kMetaWords + 1], &b.slots[t * kTileSlots], kTileSlots * sizeof(TileSlot));
+    }
+    meta.upload(m.data(), m.size());
     entries.upload(b.entries.data(), b.entries.size());
     wide.upload(b.wide.data(), b.wide.size());
     wide_tiles.upload(b.wide_tiles.data(), b.wide_tiles.size());
@@ -245,7 +253,7 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     HIP_CHECK(hipMemset(queue.p, 0, queue.n * sizeof(uint32_t)));
     staged_bytes = b.staged_bytes;
     stats = b.stats;
-    view = TiledLut{hdr.p, slots.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
+    view = TiledLut{meta.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
                     b.qpl};
 }
 

@@ -1,0 +1,19 @@
+#!/bin/bash
+# Round 3 A/B 2: which part of the VALU diet helps (weights decode / scalar staging / scalar finish).
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+V=$PWD/opencv-octvr_amd/lib/variants
+b() {  # name cfg [env...]
+  local name=$1 cfg=$2; shift 2
+  env "$@" timeout -k 10 240 python bench.py --config $cfg --steps 60 --warmup 5 --no-cpu-baseline --no-async-e2e \
+      > gpurun_out/ab2_$name.log 2>&1 || { echo "$name rc=$?"; tail -5 gpurun_out/ab2_$name.log; exit 1; }
+  python3 -c "import json; d=json.loads(open('gpurun_out/ab2_$name.log').read().strip().splitlines()[-1]); r=d['roofline']; o=d.get('roofline_one_in_flight',{}); print('$name', d['value'], d['ms_per_step'], r['kernel_us'], r['frac_at_step_time'], o.get('kernel_us'), o.get('step_us'))"
+}
+for rep in 1 2 3; do
+  b base_$rep C2 OCTVR_HIP_LIB=$V/base.so
+  b wonly_$rep C2 OCTVR_HIP_LIB=$V/wonly.so
+  b wstage_$rep C2 OCTVR_HIP_LIB=$V/wstage.so
+  b wfin_$rep C2 OCTVR_HIP_LIB=$V/wfin.so
+done
+echo done
