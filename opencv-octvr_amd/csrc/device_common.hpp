@@ -107,6 +107,7 @@ __device__ __forceinline__ void bilerp_rgba_f(uint32_t c00, uint32_t c01, uint32
                                               float (&rgb)[3]) {
     const uint32_t fx = (e >> 15) & 31u, fy = (e >> 20) & 31u;
     const uint32_t X = __umul24(fx, 0x3FFFC0u) + 2048u;  // (2048 - 64 fx) | (64 fx) << 16
+    // (X is 28 bits wide, beyond __umul24's operands: packed 16-bit multiplies)
     const u16x2_t Xv = __builtin_bit_cast(u16x2_t, X);
     const unsigned short gy = (unsigned short)(31u - fy);
     const u16x2_t w0v = __builtin_elementwise_add_sat(Xv * u16x2_t{gy, gy}, Xv);
@@ -212,7 +213,11 @@ __device__ __forceinline__ QuadOut finish_quad2(const uint32_t (&rgb)[4][3], con
     return q;
 }
 
-// finish_quad2 from channel values already in f32
+// finish_quad2 from channel values already in f32, for gains already clamped to [0, FLT_MAX] (NaN -> 0):
+// the products are then >= 0 (or NaN only for 0 * NaN, which cannot occur), so sat_u8(rne(x)) is
+// min(rint(x), 255) — v_min_f32 instead of v_med3_f32.  The composite clamps its slot gains so
+// (clamping changes no result: sat_u8 maps every negative or NaN product to 0, as 0 * g' does, and a
+// product beyond 255 to 255 either way).
 __device__ __forceinline__ QuadOut finish_quad2f(const float (&rgb)[4][3], const f32x2_t (&gain2)[4]) {
     uint32_t y01 = 0, y23 = 0;
     f32x2_t uv = {0.f, 0.f};  // (us, vs)
@@ -220,9 +225,9 @@ __device__ __forceinline__ QuadOut finish_quad2f(const float (&rgb)[4][3], const
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         f32x2_t br = f32x2_t{rgb[p][2], rgb[p][0]} * gain2[p];
-        br.x = __builtin_amdgcn_fmed3f(__builtin_rintf(br.x), 0.f, 255.f);
-        br.y = __builtin_amdgcn_fmed3f(__builtin_rintf(br.y), 0.f, 255.f);
-        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf(rgb[p][1] * gain2[p].x), 0.f, 255.f);
+        br.x = __builtin_fminf(__builtin_rintf(br.x), 255.f);
+        br.y = __builtin_fminf(__builtin_rintf(br.y), 255.f);
+        const float G = __builtin_fminf(__builtin_rintf(rgb[p][1] * gain2[p].x), 255.f);
         const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
         if (p < 2) y01 = pack_u8(Yf, p, y01);
         else y23 = pack_u8(Yf, p - 2, y23);

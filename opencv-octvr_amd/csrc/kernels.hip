@@ -954,6 +954,9 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #define OCTVR_ISSUE_EARLY 0
 #endif
 constexpr int kGainTables = OCTVR_LDS_DB ? 2 : 1;
+#ifndef OCTVR_FAST_STORE  // 1: scalar-offset output stores for items wholly inside the frame (MODE 0)
+#define OCTVR_FAST_STORE 1
+#endif
 #ifndef OCTVR_PRIO_STAGE  // > 0: s_setprio for the staging phase (the waves its barrier waits for)
 #define OCTVR_PRIO_STAGE 0
 #endif
@@ -1225,6 +1228,12 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #pragma unroll
     for (int h = 0; h < QPL; h++) prev[h] = QuadOut{0u, 0u, 0u, 0u};
     int px = 0, py = 0;  // the previous item's quad of this lane in its first half
+    // MODE 0 stores of items wholly inside the frame: the lane's part of the byte offsets is
+    // loop-invariant (voffset), the item's part a scalar (soffset) — no per-lane address arithmetic
+    constexpr bool kFastStore = OCTVR_FAST_STORE && SM == 0 && !kWideOut && !kStoreLate;
+    const uint32_t lane_y = (uint32_t)(2 * qy) * of.pitch + (uint32_t)(2 * qx), lane_c = (uint32_t)qy * of.pitch + (uint32_t)qx;
+    int pox = 0, poy = 0;  // the previous item's origin (uniform)
+    bool pfull = false;    // the previous item lies wholly inside W x H (uniform)
     uint32_t pcam = 0;
     bool pin = false;
     uint32_t par = 0, half = 0;  // iteration parity; LDS half of the next small item
@@ -1274,7 +1283,11 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
-            if (tid < kTileSlots) s_slot_gain[kGainTables > 1 ? par : 0][tid] = f32x2_t{s_gain[cw & 31u], s_gain[cw & 31u]};
+            // clamped to [0, FLT_MAX] (NaN -> 0) for finish_quad2f's min-only saturation (MODE 0);
+            // the RGBA sink saturates with v_cvt_pk_u8_f32 and takes the gain as is
+            const float gs = s_gain[cw & 31u];
+            const float gc = SM == 0 ? __builtin_fminf(__builtin_fmaxf(gs, 0.f), FLT_MAX) : gs;
+            if (tid < kTileSlots) s_slot_gain[kGainTables > 1 ? par : 0][tid] = f32x2_t{gc, gc};
         }
         if (claimed && tid == 0) s_claim[par] = claim;  // issued one iteration ago
 #if !OCTVR_DIAG_NOSTAGE
@@ -1328,6 +1341,22 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #if !OCTVR_DIAG_NOSTORE
         if constexpr (kWideOut) {
             store_item_wide<QPL>(of, s_out, px - 2 * qx, py - 2 * qy, pin, H);
+        } else if constexpr (kFastStore) {
+            if (pfull) {
+#pragma unroll
+                for (int h = 0; h < QPL; h++) {
+                    const uint32_t sy = (uint32_t)uniform((poy + h * kTileH) * (int)of.pitch + pox);
+                    const uint32_t sc = (uint32_t)uniform(((poy + h * kTileH) >> 1) * (int)of.pitch + (pox >> 1));
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)prev[h].y01, of.rsrc, lane_y, sy, OCTVR_OUT_POLICY);
+                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)prev[h].y23, of.rsrc, lane_y, sy + of.pitch, OCTVR_OUT_POLICY);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)prev[h].u, of.rsrc, lane_c, sc + of.u_off, OCTVR_OUT_POLICY);
+                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)prev[h].v, of.rsrc, lane_c, sc + of.v_off, OCTVR_OUT_POLICY);
+                }
+            } else {
+#pragma unroll
+                for (int h = 0; h < QPL; h++)
+                    store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+            }
         } else if constexpr (!kStoreLate) {
 #pragma unroll
             for (int h = 0; h < QPL; h++)
@@ -1393,6 +1422,54 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #if OCTVR_DIAG_NOCOMPUTE
         prev[h] = QuadOut{(uint32_t)rgb[0][0] ^ (uint32_t)rgb[1][1], (uint32_t)rgb[2][2] ^ (uint32_t)rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
 #else
+#if OCTVR_DIAG_XOP  // diagnostic: 16 extra independent instructions of one opcode per quad (4 per pixel), to
+                    // price an opcode inside this loop (scripts/r3_diag4.sh); the results feed nothing
+#if OCTVR_DIAG_XOP == 1
+#define OCTVR_XOP_ASM "v_xor_b32 %0, %0, %1"
+#elif OCTVR_DIAG_XOP == 2
+#define OCTVR_XOP_ASM "v_pk_mul_lo_u16 %0, %0, %1"
+#elif OCTVR_DIAG_XOP == 3
+#define OCTVR_XOP_ASM "v_perm_b32 %0, %0, %1, %1"
+#elif OCTVR_DIAG_XOP == 4
+#define OCTVR_XOP_ASM "v_mul_u32_u24 %0, %0, %1"
+#elif OCTVR_DIAG_XOP == 5
+#define OCTVR_XOP_ASM "v_dot2_u32_u16 %0, %1, %1, %0"
+#elif OCTVR_DIAG_XOP == 6
+#define OCTVR_XOP_ASM "v_pk_add_u16 %0, %0, %1"
+#elif OCTVR_DIAG_XOP == 7
+#define OCTVR_XOP_ASM "v_cvt_pk_u8_f32 %0, %1, 1, %0"
+#elif OCTVR_DIAG_XOP == 8
+#define OCTVR_XOP_ASM "v_fmac_f32 %0, %1, %1"
+#elif OCTVR_DIAG_XOP == 9
+#define OCTVR_XOP_ASM "v_rndne_f32 %0, %0"
+#elif OCTVR_DIAG_XOP == 10
+#define OCTVR_XOP_ASM "v_med3_f32 %0, %0, %1, %1"
+#elif OCTVR_DIAG_XOP == 11
+#define OCTVR_XOP_ASM "v_min_f32 %0, %0, %1"
+#elif OCTVR_DIAG_XOP == 12
+#define OCTVR_XOP_ASM "v_bfe_u32 %0, %0, 3, 5"
+#elif OCTVR_DIAG_XOP == 13
+#define OCTVR_XOP_ASM "v_cvt_f32_ubyte1 %0, %0"
+#elif OCTVR_DIAG_XOP == 14
+#define OCTVR_XOP_ASM "v_mul_f32 %0, %0, %1"
+#elif OCTVR_DIAG_XOP == 16
+#define OCTVR_XOP_ASM "v_mul_lo_u32 %0, %0, %1"
+#else
+#define OCTVR_XOP_ASM "v_mov_b32 %0, %1"
+#endif
+        {
+            uint32_t z0 = ent[0], z1 = ent[1], z2 = ent[2], z3 = ent[3];
+            const uint32_t k = ent[0] ^ ent[3];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                asm volatile(OCTVR_XOP_ASM : "+v"(z0) : "v"(k));
+                asm volatile(OCTVR_XOP_ASM : "+v"(z1) : "v"(k));
+                asm volatile(OCTVR_XOP_ASM : "+v"(z2) : "v"(k));
+                asm volatile(OCTVR_XOP_ASM : "+v"(z3) : "v"(k));
+            }
+            asm volatile("" ::"v"(z0), "v"(z1), "v"(z2), "v"(z3));
+        }
+#endif
         prev[h] = finish_any<SM>(rgb, gain);
 #endif
         // MODE 2: staged for the wide stores after the next barrier
@@ -1404,6 +1481,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         OCTVR_PHASE(4);
         px = x;
         py = y;
+        pox = (int)(cur.tile & 0xFFFFu) * kTileW;
+        poy = (int)(cur.tile >> 16) * kItemH;
+        pfull = pox + kTileW <= W && poy + kItemH <= H;
         pcam = (cur.nslots >> 16) & 31u;
         pin = x < W && y < H;
 #if !OCTVR_DIAG_NOSTORE
@@ -1486,7 +1566,8 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 #pragma unroll
     for (int p = 0; p < 4; p++) {
         bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
-        const float gp = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
+        float gp = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
+        if (MODE == 0) gp = __builtin_fminf(__builtin_fmaxf(gp, 0.f), FLT_MAX);  // finish_quad2f's contract
         gain[p] = f32x2_t{gp, gp};
     }
     const uint32_t cam = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;
