@@ -954,6 +954,10 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #define OCTVR_ISSUE_EARLY 0
 #endif
 constexpr int kGainTables = OCTVR_LDS_DB ? 2 : 1;
+#ifndef OCTVR_SLN_LATE  // 1: the next item's staging slots resolved after the second barrier, right before
+                        // its loads (27 -> 5 SGPR spills, 30 -> 15 v_readlane per iteration; C2 +3 %)
+#define OCTVR_SLN_LATE 1
+#endif
 #ifndef OCTVR_FAST_STORE  // 1: scalar-offset output stores for items wholly inside the frame (MODE 0)
 #define OCTVR_FAST_STORE 1
 #endif
@@ -1016,9 +1020,12 @@ struct TileData {
 
 // Issue an item's entry loads and the staging loads of its first R chunks per wave (sl[r]: the
 // slots of chunks r * 4 + wave, from stage_slot).
+// er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
+// scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
+// that the entries fit 32-bit offsets)
 template <bool DWORD_STAGE, bool VIG, int Q, int R>
-__device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& m, int t_end,
-                                           const StageSlot (&sl)[R], TileData<Q, R>& d) {
+__device__ __forceinline__ void data_issue(const TiledLut& lut, const __amdgpu_buffer_rsrc_t& er, const TileMeta& m,
+                                           int t_end, const StageSlot (&sl)[R], TileData<Q, R>& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
@@ -1032,7 +1039,11 @@ __device__ __forceinline__ void data_issue(const TiledLut& lut, const TileMeta& 
             reinterpret_cast<const u32x4_t*>(lut.entries + ((int64_t)(live ? m.t : 0) * Q + h) * kTilePx) + tid);
         d.e4[h] = uint4{v.x, v.y, v.z, v.w};
 #else
-        d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + ((int64_t)(live ? m.t : 0) * Q + h) * kTilePx)[tid];
+        typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+        const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * Q + h) * (uint32_t)(kTilePx * 4);
+        const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
+        d.e4[h] = uint4{v.x, v.y, v.z, v.w};
+        (void)lut;
 #endif
     }
 #pragma unroll
@@ -1170,6 +1181,8 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     const int step = (gridDim.x - g + groups - 1) / groups;
     const int t_begin = lut.bands[g];
     const int t_end = lut.bands[g + 1];
+    const __amdgpu_buffer_rsrc_t ersrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(QPL * kTilePx * 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<TileHdr*>(lut.meta), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kMetaWords * 16)), 0x00020000);
     OutFrame of{};
@@ -1204,7 +1217,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         StageSlot sl[R];
 #pragma unroll
         for (int r = 0; r < R; r++) sl[r] = stage_slot(cur, t_end, r * 4 + wave);
-        data_issue<DWORD_STAGE, VIG>(lut, cur, t_end, sl, d);
+        data_issue<DWORD_STAGE, VIG>(lut, ersrc, cur, t_end, sl, d);
     }
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
@@ -1279,8 +1292,10 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         const TileMeta nxt = meta_read(mv, t_mv);
         // the next item's staging slots (+ their frames' kernarg loads), used after the barrier below
         StageSlot sln[R];
+#if !OCTVR_SLN_LATE
 #pragma unroll
         for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
+#endif
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
             // clamped to [0, FLT_MAX] (NaN -> 0) for finish_quad2f's min-only saturation (MODE 0);
@@ -1311,7 +1326,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #if OCTVR_ISSUE_EARLY
         // the next item's entry and staging loads before the barrier (their registers are free once
         // staged): their latency then also covers the barrier wait, not only this item's compute
-        data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
+        data_issue<DWORD_STAGE, VIG>(lut, ersrc, nxt, t_end, sln, d);
 #endif
         OCTVR_PHASE(1);
 #if !OCTVR_DIAG_NOBAR
@@ -1364,7 +1379,11 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         }
 #endif
 #if !OCTVR_ISSUE_EARLY
-        data_issue<DWORD_STAGE, VIG>(lut, nxt, t_end, sln, d);
+#if OCTVR_SLN_LATE  // the next item's slots resolved only now (shorter scalar live ranges, exposed kernarg loads)
+#pragma unroll
+        for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
+#endif
+        data_issue<DWORD_STAGE, VIG>(lut, ersrc, nxt, t_end, sln, d);
 #endif
         mv = meta_issue(mrsrc, t_n2, t_end);
         t_mv = t_n2;

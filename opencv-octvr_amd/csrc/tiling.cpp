@@ -244,6 +244,8 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
         std::memcpy(&m[t * kMetaWords + 1], &b.slots[t * kTileSlots], kTileSlots * sizeof(TileSlot));
     }
     meta.upload(m.data(), m.size());
+    // the composite addresses the entries through a buffer resource with 32-bit offsets
+    REQUIRE(b.entries.size() * sizeof(uint32_t) < (size_t)1 << 32, "tiled LUT entries exceed 4 GiB");
     entries.upload(b.entries.data(), b.entries.size());
     wide.upload(b.wide.data(), b.wide.size());
     wide_tiles.upload(b.wide_tiles.data(), b.wide_tiles.size());
