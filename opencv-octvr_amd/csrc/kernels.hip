@@ -795,6 +795,7 @@ struct TileMeta {
     int t;
     uint4 v;
     uint32_t tile, nslots, stride;
+    uint32_t map;  // slot of staging chunk c < 4 in bits 2c, 2c + 1 (TiledLutDev::upload)
 };
 
 // dword j (0-3) of slot q (wave-uniform)
@@ -811,14 +812,20 @@ struct StageSlot {
     SourceFrame f;
 };
 
+// FIRST: c < 4 (a wave's first chunk), whose slot the host stored in m.map; else searched.
+template <bool FIRST = false>
 __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, int c) {
     StageSlot s;
     const uint32_t nchunks = m.t < t_end ? ((m.nslots >> 8) & 0xFFu) : 0u;
-    const int nslots = (int)(m.nslots & 0xFFu);
     s.live = (uint32_t)c < nchunks ? 1u : 0u;
     int q = 0;
+    if constexpr (FIRST) {
+        q = (int)((m.map >> (2 * c)) & 3u);
+    } else {
+        const int nslots = (int)(m.nslots & 0xFFu);
 #pragma unroll
-    for (int j = 1; j < kTileSlots; j++) q += (j < nslots && c >= (int)(slot_word(m, j, 3) & 0xFFFFu)) ? 1 : 0;
+        for (int j = 1; j < kTileSlots; j++) q += (j < nslots && c >= (int)(slot_word(m, j, 3) & 0xFFFFu)) ? 1 : 0;
+    }
     const uint32_t d0 = slot_word(m, q, 0), d1 = slot_word(m, q, 1);
     const uint32_t d2 = slot_word(m, q, 2), d3 = slot_word(m, q, 3);
     s.cam = s.live ? (d0 & 31u) : 0u;
@@ -1007,6 +1014,7 @@ __device__ __forceinline__ TileMeta meta_read(const uint4& v, int t) {
     m.tile = (uint32_t)__builtin_amdgcn_readlane((int)v.x, 0);
     m.nslots = (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0);
     m.stride = (uint32_t)__builtin_amdgcn_readlane((int)v.w, 0);
+    m.map = (uint32_t)__builtin_amdgcn_readlane((int)v.z, 0);
     return m;
 }
 
@@ -1216,7 +1224,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     {
         StageSlot sl[R];
 #pragma unroll
-        for (int r = 0; r < R; r++) sl[r] = stage_slot(cur, t_end, r * 4 + wave);
+        for (int r = 0; r < R; r++) sl[r] = r == 0 ? stage_slot<true>(cur, t_end, wave) : stage_slot(cur, t_end, r * 4 + wave);
         data_issue<DWORD_STAGE, VIG>(lut, ersrc, cur, t_end, sl, d);
     }
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
@@ -1294,7 +1302,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         StageSlot sln[R];
 #if !OCTVR_SLN_LATE
 #pragma unroll
-        for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
+        for (int r = 0; r < R; r++) sln[r] = r == 0 ? stage_slot<true>(nxt, t_end, wave) : stage_slot(nxt, t_end, r * 4 + wave);
 #endif
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
@@ -1381,7 +1389,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #if !OCTVR_ISSUE_EARLY
 #if OCTVR_SLN_LATE  // the next item's slots resolved only now (shorter scalar live ranges, exposed kernarg loads)
 #pragma unroll
-        for (int r = 0; r < R; r++) sln[r] = stage_slot(nxt, t_end, r * 4 + wave);
+        for (int r = 0; r < R; r++) sln[r] = r == 0 ? stage_slot<true>(nxt, t_end, wave) : stage_slot(nxt, t_end, r * 4 + wave);
 #endif
         data_issue<DWORD_STAGE, VIG>(lut, ersrc, nxt, t_end, sln, d);
 #endif

@@ -241,6 +241,16 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     std::vector<TileHdr> m(b.hdr.size() * kMetaWords);
     for (size_t t = 0; t < b.hdr.size(); t++) {
         m[t * kMetaWords] = b.hdr[t];
+        // word 2 on the device: the slot of each staging chunk c < 4 (2 bits at 2c), as stage_slot's
+        // search over the slots' first chunks would find it (stage_groups is host-side statistics)
+        uint32_t map = 0;
+        const int ns = (int)(b.hdr[t].nslots & 0xFFu);
+        for (int c = 0; c < 4; c++) {
+            int q = 0;
+            for (int j = 1; j < kTileSlots; j++) q += (j < ns && c >= (int)b.slots[t * kTileSlots + j].chunk0) ? 1 : 0;
+            map |= (uint32_t)q << (2 * c);
+        }
+        m[t * kMetaWords].stage_groups = map;
         std::memcpy(&m[t * kMetaWords + 1], &b.slots[t * kTileSlots], kTileSlots * sizeof(TileSlot));
     }
     meta.upload(m.data(), m.size());
