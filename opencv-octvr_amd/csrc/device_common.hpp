@@ -54,6 +54,19 @@ __device__ __forceinline__ void yuv2_to_rgba(uint32_t y0, uint32_t y1, uint32_t 
     p1 = pack_u8(B.y, 2, pack_u8(G.y, 1, pack_u8(R.y, 0, 0u)));
 }
 
+// yuv2_to_rgba with the chroma already as the floats u - 128, v - 128
+__device__ __forceinline__ void yuv2_to_rgba_c(uint32_t y0, uint32_t y1, float Uf, float Vf, uint32_t& p0,
+                                               uint32_t& p1) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 Y = {(float)y0, (float)y1};
+    const f2 R = __builtin_elementwise_fma(f2{1.140f, 1.140f}, f2{Vf, Vf}, Y);
+    const f2 G = __builtin_elementwise_fma(f2{-0.581f, -0.581f}, f2{Vf, Vf},
+                                           __builtin_elementwise_fma(f2{-0.394f, -0.394f}, f2{Uf, Uf}, Y));
+    const f2 B = __builtin_elementwise_fma(f2{2.032f, 2.032f}, f2{Uf, Uf}, Y);
+    p0 = pack_u8(B.x, 2, pack_u8(G.x, 1, pack_u8(R.x, 0, 0u)));
+    p1 = pack_u8(B.y, 2, pack_u8(G.y, 1, pack_u8(R.y, 0, 0u)));
+}
+
 // Vignette correction of a source pixel: multiply(rgba, vignette_map) = MulOpSpecial_c4
 // (cudaarithm/src/cuda/mul_mat.cu:198-214): saturate_cast<uchar>(c * g) per channel.
 __device__ __forceinline__ uint32_t vig_mul(uint32_t rgba, float g) {

@@ -897,12 +897,14 @@ __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rg
     if (sg.dst < 0) return;
     const bool black = (sg.flags & kStageBlack) != 0;  // Y = 0, U = V = 128 -> RGBA 0
     const uint32_t y0 = black ? 0u : sg.y0, y1 = black ? 0u : sg.y1;
-    const uint32_t uq = black ? 0x80808080u : sg.uq, vq = black ? 0x80808080u : sg.vq;
+    // chroma bytes xor 0x80 read as signed bytes are u - 128: one v_cvt_f32_i32_sdwa (sext) each
+    const uint32_t uq = black ? 0u : sg.uq ^ 0x80808080u, vq = black ? 0u : sg.vq ^ 0x80808080u;
+    auto ch = [](uint32_t w, int k) { return (float)(signed char)((w >> (8 * k)) & 255u); };
     uint4 a, b;
-    yuv2_to_rgba(y0 & 255u, (y0 >> 8) & 255u, uq & 255u, vq & 255u, a.x, a.y);
-    yuv2_to_rgba((y0 >> 16) & 255u, y0 >> 24, (uq >> 8) & 255u, (vq >> 8) & 255u, a.z, a.w);
-    yuv2_to_rgba(y1 & 255u, (y1 >> 8) & 255u, (uq >> 16) & 255u, (vq >> 16) & 255u, b.x, b.y);
-    yuv2_to_rgba((y1 >> 16) & 255u, y1 >> 24, uq >> 24, vq >> 24, b.z, b.w);
+    yuv2_to_rgba_c(y0 & 255u, (y0 >> 8) & 255u, ch(uq, 0), ch(vq, 0), a.x, a.y);
+    yuv2_to_rgba_c((y0 >> 16) & 255u, y0 >> 24, ch(uq, 1), ch(vq, 1), a.z, a.w);
+    yuv2_to_rgba_c(y1 & 255u, (y1 >> 8) & 255u, ch(uq, 2), ch(vq, 2), b.x, b.y);
+    yuv2_to_rgba_c((y1 >> 16) & 255u, y1 >> 24, ch(uq, 3), ch(vq, 3), b.z, b.w);
     if (VIG && !(sg.flags & kStageNoVig)) {
         a.x = vig_mul(a.x, sg.g0.x);
         a.y = vig_mul(a.y, sg.g0.y);
