@@ -195,63 +195,55 @@ struct QuadOut {
     uint32_t u, v;
 };
 
-// Per pixel the (B, R) pair goes through packed f32 ops (v_pk_mul_f32 / v_pk_add_f32 / v_pk_fma_f32:
-// two lanes' worth per instruction, each element rounded exactly like the scalar op) and the chroma
-// sums accumulate as the pair (us, vs) in the same pixel order.
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-// gain2[p] = {g, g}: the pair the packed multiply reads, held in two defined registers (a scalar
-// gain broadcast by op_sel would make the multiply read the register after it, and the compiler
-// then waits for whatever load is in flight into that one).
-__device__ __forceinline__ QuadOut finish_quad2(const uint32_t (&rgb)[4][3], const f32x2_t (&gain2)[4]) {
-    uint32_t y01 = 0, y23 = 0;
-    f32x2_t uv = {0.f, 0.f};  // (us, vs)
-    const f32x2_t kuv = {0.492f, 0.877f};
+
+// The library's own RGB -> YUV420P (it stands in for NPP's closed nppiRGBToYUV420; oracle/octvr_oracle.c
+// rgb_quad_to_yuv is the same definition): full-range BT.601 in 8-bit fixed point,
+//   Y = (77 R + 150 G + 29 B + 128) >> 8                                   (0..255, no clamp needed)
+//   U = (sum over the quad of -43 R' - 84 G' + 127 B' + 131584) >> 10      (1..255)
+//   V = (sum over the quad of 127 R' - 106 G' - 21 B' + 131584) >> 10
+// with R' = R - 128 etc. (the U / V coefficients sum to 0, so they equal the same sums over R, G, B).
+// Per pixel one v_dot4_u32_u8 (Y lands in byte 1) and two v_dot4c_i32_i8 on the pixel xor 0x808080.
+// px[p]: R | G << 8 | B << 16 (byte 3 is ignored: every coefficient vector has byte 3 = 0).
+__device__ __forceinline__ QuadOut quad_yuv(const uint32_t (&px)[4]) {
+    uint32_t yr[4];
+    int au = 0, av = 0;
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        // gain: saturate_cast<uchar>(px * g), kept as an exact float of the saturated integer
-        f32x2_t br = f32x2_t{(float)rgb[p][2], (float)rgb[p][0]} * gain2[p];
-        br.x = __builtin_amdgcn_fmed3f(__builtin_rintf(br.x), 0.f, 255.f);
-        br.y = __builtin_amdgcn_fmed3f(__builtin_rintf(br.y), 0.f, 255.f);
-        const float G = __builtin_amdgcn_fmed3f(__builtin_rintf((float)rgb[p][1] * gain2[p].x), 0.f, 255.f);
-        const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
-        if (p < 2) y01 = pack_u8(Yf, p, y01);
-        else y23 = pack_u8(Yf, p - 2, y23);
-        uv = __builtin_elementwise_fma(kuv, br - Yf, uv);
+        const uint32_t c = px[p];  // byte 3 meets coefficient 0 in all three products
+        yr[p] = __builtin_amdgcn_udot4(c, 0x001D964Du, 128u, false);  // {77, 150, 29, 0}
+        const int s = (int)(c ^ 0x00808080u);
+        au = __builtin_amdgcn_sdot4(s, 0x007FACD5, au, false);  // {-43, -84, 127, 0}
+        av = __builtin_amdgcn_sdot4(s, 0x00EB967F, av, false);  // {127, -106, -21, 0}
     }
     QuadOut q;
-    q.y01 = y01;
-    q.y23 = y23;
-    q.u = pack_u8(__builtin_fmaf(uv.x, 0.25f, 128.f), 0, 0u);
-    q.v = pack_u8(__builtin_fmaf(uv.y, 0.25f, 128.f), 0, 0u);
+    q.y01 = __builtin_amdgcn_perm(yr[1], yr[0], 0x0C0C0501u);  // byte 1 of each
+    q.y23 = __builtin_amdgcn_perm(yr[3], yr[2], 0x0C0C0501u);
+    q.u = (uint32_t)(au + 131584) >> 10;
+    q.v = (uint32_t)(av + 131584) >> 10;
     return q;
 }
 
-// finish_quad2 from channel values already in f32, for gains already clamped to [0, FLT_MAX] (NaN -> 0):
-// the products are then >= 0 (or NaN only for 0 * NaN, which cannot occur), so sat_u8(rne(x)) is
-// min(rint(x), 255) — v_min_f32 instead of v_med3_f32.  The composite clamps its slot gains so
-// (clamping changes no result: sat_u8 maps every negative or NaN product to 0, as 0 * g' does, and a
-// product beyond 255 to 255 either way).
+// gain + pack: sat_u8(rne(c * g)) per channel with v_cvt_pk_u8_f32 (round half to even, saturating,
+// NaN -> 0), then quad_yuv.  gain2[p] = {g, g}: (B, R) go through one v_pk_mul_f32.
 __device__ __forceinline__ QuadOut finish_quad2f(const float (&rgb)[4][3], const f32x2_t (&gain2)[4]) {
-    uint32_t y01 = 0, y23 = 0;
-    f32x2_t uv = {0.f, 0.f};  // (us, vs)
-    const f32x2_t kuv = {0.492f, 0.877f};
+    uint32_t px[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        f32x2_t br = f32x2_t{rgb[p][2], rgb[p][0]} * gain2[p];
-        br.x = __builtin_fminf(__builtin_rintf(br.x), 255.f);
-        br.y = __builtin_fminf(__builtin_rintf(br.y), 255.f);
-        const float G = __builtin_fminf(__builtin_rintf(rgb[p][1] * gain2[p].x), 255.f);
-        const float Yf = __builtin_fmaf(0.114f, br.x, __builtin_fmaf(0.587f, G, 0.299f * br.y));
-        if (p < 2) y01 = pack_u8(Yf, p, y01);
-        else y23 = pack_u8(Yf, p - 2, y23);
-        uv = __builtin_elementwise_fma(kuv, br - Yf, uv);
+        const f32x2_t br = f32x2_t{rgb[p][2], rgb[p][0]} * gain2[p];
+        const float G = rgb[p][1] * gain2[p].x;
+        px[p] = pack_u8(br.x, 2, pack_u8(G, 1, pack_u8(br.y, 0, 0u)));
     }
-    QuadOut q;
-    q.y01 = y01;
-    q.y23 = y23;
-    q.u = pack_u8(__builtin_fmaf(uv.x, 0.25f, 128.f), 0, 0u);
-    q.v = pack_u8(__builtin_fmaf(uv.y, 0.25f, 128.f), 0, 0u);
-    return q;
+    return quad_yuv(px);
+}
+
+__device__ __forceinline__ QuadOut finish_quad2(const uint32_t (&rgb)[4][3], const f32x2_t (&gain2)[4]) {
+    float f[4][3];
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) f[p][ch] = (float)rgb[p][ch];
+    return finish_quad2f(f, gain2);
 }
 
 __device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {

@@ -1308,8 +1308,8 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #endif
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
-            // clamped to [0, FLT_MAX] (NaN -> 0) for finish_quad2f's min-only saturation (MODE 0);
-            // the RGBA sink saturates with v_cvt_pk_u8_f32 and takes the gain as is
+            // clamped to [0, FLT_MAX] (NaN -> 0) in MODE 0; no result depends on it (finish_quad2f
+            // saturates with v_cvt_pk_u8_f32, which maps negative and NaN products to 0 either way)
             const float gs = s_gain[cw & 31u];
             const float gc = SM == 0 ? __builtin_fminf(__builtin_fmaxf(gs, 0.f), FLT_MAX) : gs;
             if (tid < kTileSlots) s_slot_gain[kGainTables > 1 ? par : 0][tid] = f32x2_t{gc, gc};
@@ -1596,7 +1596,6 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
     for (int p = 0; p < 4; p++) {
         bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
         float gp = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
-        if (MODE == 0) gp = __builtin_fminf(__builtin_fmaxf(gp, 0.f), FLT_MAX);  // finish_quad2f's contract
         gain[p] = f32x2_t{gp, gp};
     }
     const uint32_t cam = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;

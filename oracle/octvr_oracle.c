@@ -889,18 +889,22 @@ static inline void yuv_px_to_rgb(int y, int u, int v, uint8_t* o) {
     o[2] = sat_u8_rne(fmaf(2.032f, Uf, Yf));
 }
 
-/* 2x2 RGB quad -> 4 Y + 1 U + 1 V (U, V from the mean of the per-pixel chroma differences). */
+/* 2x2 RGB quad -> 4 Y + 1 U + 1 V: full-range BT.601 in 8-bit fixed point (the library's own
+ * definition, device_common.hpp quad_yuv; it stands in for NPP's closed nppiRGBToYUV420):
+ *   Y = (77 R + 150 G + 29 B + 128) >> 8,
+ *   U = (sum over the quad of -43 R - 84 G + 127 B, + 131584) >> 10,
+ *   V = (sum over the quad of 127 R - 106 G - 21 B, + 131584) >> 10
+ * (the U / V coefficients sum to 0; every intermediate fits an int and U, V land in 1..255). */
 static inline void rgb_quad_to_yuv(const uint8_t* const p[4], uint8_t Y[4], uint8_t* U, uint8_t* V) {
-    float us = 0.f, vs = 0.f;
+    int au = 0, av = 0;
     for (int k = 0; k < 4; k++) {
-        float R = p[k][0], G = p[k][1], B = p[k][2];
-        float Yf = fmaf(0.114f, B, fmaf(0.587f, G, 0.299f * R));
-        Y[k] = sat_u8_rne(Yf);
-        us = fmaf(0.492f, B - Yf, us);
-        vs = fmaf(0.877f, R - Yf, vs);
+        const int R = p[k][0], G = p[k][1], B = p[k][2];
+        Y[k] = (uint8_t)((77 * R + 150 * G + 29 * B + 128) >> 8);
+        au += -43 * R - 84 * G + 127 * B;
+        av += 127 * R - 106 * G - 21 * B;
     }
-    *U = sat_u8_rne(fmaf(us, 0.25f, 128.f));
-    *V = sat_u8_rne(fmaf(vs, 0.25f, 128.f));
+    *U = (uint8_t)((au + 131584) >> 10);
+    *V = (uint8_t)((av + 131584) >> 10);
 }
 
 void orc_yuv420_to_rgba(const uint8_t* yuv, int w, int h, size_t pitch, uint8_t* rgba, size_t rgba_pitch) {
