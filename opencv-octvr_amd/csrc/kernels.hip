@@ -963,6 +963,9 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #define OCTVR_ISSUE_EARLY 0
 #endif
 constexpr int kGainTables = OCTVR_LDS_DB ? 2 : 1;
+#ifndef OCTVR_ENT_LATE  // 1: the next item's entries loaded after this item's computation (not after its barrier)
+#define OCTVR_ENT_LATE 0
+#endif
 #ifndef OCTVR_SLN_LATE  // 1: the next item's staging slots resolved after the second barrier, right before
                         // its loads (27 -> 5 SGPR spills, 30 -> 15 v_readlane per iteration; C2 +3 %)
 #define OCTVR_SLN_LATE 1
@@ -1033,7 +1036,7 @@ struct TileData {
 // er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
 // scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
 // that the entries fit 32-bit offsets)
-template <bool DWORD_STAGE, bool VIG, int Q, int R>
+template <bool DWORD_STAGE, bool VIG, int Q, int R, bool ENTRIES = true>
 __device__ __forceinline__ void data_issue(const TiledLut& lut, const __amdgpu_buffer_rsrc_t& er, const TileMeta& m,
                                            int t_end, const StageSlot (&sl)[R], TileData<Q, R>& d) {
     const bool live = m.t < t_end;
@@ -1041,6 +1044,7 @@ __device__ __forceinline__ void data_issue(const TiledLut& lut, const __amdgpu_b
     const int wave = uniform(tid >> 6);
 #pragma unroll
     for (int h = 0; h < Q; h++) {
+        if constexpr (!ENTRIES) break;
 #if OCTVR_DIAG_HOTENT  // diagnostic: every item reads item 0's entries (L2-resident)
         d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + (int64_t)h * kTilePx)[tid];
 #elif OCTVR_ENT_NT  // entries stream once: non-temporal loads (keep the source boxes in L2)
@@ -1393,7 +1397,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #pragma unroll
         for (int r = 0; r < R; r++) sln[r] = r == 0 ? stage_slot<true>(nxt, t_end, wave) : stage_slot(nxt, t_end, r * 4 + wave);
 #endif
-        data_issue<DWORD_STAGE, VIG>(lut, ersrc, nxt, t_end, sln, d);
+        data_issue<DWORD_STAGE, VIG, QPL, R, !OCTVR_ENT_LATE>(lut, ersrc, nxt, t_end, sln, d);
 #endif
         mv = meta_issue(mrsrc, t_n2, t_end);
         t_mv = t_n2;
@@ -1507,6 +1511,20 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         asm volatile("" : "+v"(prev[h].y01), "+v"(prev[h].y23), "+v"(prev[h].u), "+v"(prev[h].v));
 #endif
         }
+#if OCTVR_ENT_LATE
+        // the next item's entries only now, after this item's last use of its own: no copy of the
+        // in-flight entries is held across the computation (they land during the staging phase)
+        {
+            const bool nlive = nxt.t < t_end;
+#pragma unroll
+            for (int h = 0; h < QPL; h++) {
+                typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+                const uint32_t so = (uint32_t)uniform((nlive ? nxt.t : 0) * QPL + h) * (uint32_t)(kTilePx * 4);
+                const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(ersrc, (uint32_t)tid * 16u, so, 0);
+                d.e4[h] = uint4{v.x, v.y, v.z, v.w};
+            }
+        }
+#endif
         OCTVR_PHASE(4);
         px = x;
         py = y;
