@@ -246,6 +246,14 @@ __device__ __forceinline__ QuadOut finish_quad2(const uint32_t (&rgb)[4][3], con
     return finish_quad2f(f, gain2);
 }
 
+// quad_yuv of channel values already in 0..255 (no gain): packed directly
+__device__ __forceinline__ QuadOut finish_quad_u8(const uint32_t (&rgb)[4][3]) {
+    uint32_t px[4];
+#pragma unroll
+    for (int p = 0; p < 4; p++) px[p] = rgb[p][0] | (rgb[p][1] << 8) | (rgb[p][2] << 16);
+    return quad_yuv(px);
+}
+
 __device__ __forceinline__ QuadOut finish_quad(const uint32_t (&rgb)[4][3], const float (&gain)[4]) {
     const f32x2_t g2[4] = {{gain[0], gain[0]}, {gain[1], gain[1]}, {gain[2], gain[2]}, {gain[3], gain[3]}};
     return finish_quad2(rgb, g2);

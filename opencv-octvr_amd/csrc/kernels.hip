@@ -1911,7 +1911,6 @@ __global__ void __launch_bounds__(256) resize_rgba_yuv420_kernel(const uint8_t* 
     const OutFrame of = make_out_frame(out, dw, dh, out_pitch);
     const int qw = dw >> 1, qh = dh >> 1;
     const int64_t total = (int64_t)qw * qh;
-    const float one[4] = {1.f, 1.f, 1.f, 1.f};
     for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (int64_t)gridDim.x * blockDim.x) {
         const int qy = (int)(q / qw), qx = (int)(q - (int64_t)qy * qw);
         uint32_t rgb[4][3];
@@ -1940,7 +1939,7 @@ __global__ void __launch_bounds__(256) resize_rgba_yuv420_kernel(const uint8_t* 
                 rgb[p][ch] = (uint32_t)sat_u8_rne(o);
             }
         }
-        store_quad(of, finish_quad(rgb, one), 2 * qx, 2 * qy, true);
+        store_quad(of, finish_quad_u8(rgb), 2 * qx, 2 * qy, true);  // rgb already 0..255
     }
 }
 

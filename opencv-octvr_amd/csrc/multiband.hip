@@ -688,9 +688,8 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
         }
         return;
     }
-    const float one[4] = {1.f, 1.f, 1.f, 1.f};
     const OutFrame of = make_out_frame(a.out, a.out_w, a.out_h, a.out_pitch);
-    store_quad(of, finish_quad(rgb, one), ox, oy, in);
+    store_quad(of, finish_quad_u8(rgb), ox, oy, in);  // rgb already 0..255
 }
 
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s) {
