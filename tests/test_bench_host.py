@@ -1,0 +1,61 @@
+"""bench.py's roofline bookkeeping on the CPU: `roofline.traffic` comes only from a PMC summary whose
+so_sha256 is the running library's (a summary of another binary is never used), and the committed
+summaries under profiles/ have the shape bench.pmc_traffic reads."""
+import glob
+import json
+import os
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERNEL = "void octvr::stitch_tiled_kernel<false, 0, false, 2>(octvr::FrameSet, ...)"
+
+
+def _write(d, name, sha, per_launch=1000.0, per_frame=5000.0):
+    os.makedirs(d / "profiles", exist_ok=True)
+    (d / "profiles" / name).write_text(json.dumps({
+        "so_sha256": sha, "traffic_per_frame_bytes": per_frame,
+        "traffic_bytes": {"octvr::gain_feed_lean_kernel(...)": 7.0, KERNEL: per_launch}}))
+
+
+@pytest.fixture
+def bench_at(tmp_path, monkeypatch):
+    import bench
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    monkeypatch.setattr(bench, "lib_sha256", lambda: "a" * 64)
+    return bench, tmp_path
+
+
+def test_pmc_traffic_keyed_to_library(bench_at):
+    bench, d = bench_at
+    _write(d, "r01_pmc_C2.json", "b" * 64, per_launch=1.0)  # another binary: skipped
+    _write(d, "r02_pmc_C2.json", "a" * 64, per_launch=1234.4, per_frame=99.6)
+    assert bench.pmc_traffic("C2", 0) == (1234, "r02_pmc_C2.json")  # the composite launch
+    assert bench.pmc_traffic("C2", 3) == (100, "r02_pmc_C2.json")  # the whole blend sequence per frame
+
+
+def test_pmc_traffic_absent_for_other_binaries(bench_at):
+    bench, d = bench_at
+    _write(d, "r01_pmc_C3.json", "b" * 64)
+    v, why = bench.pmc_traffic("C3", 3)
+    assert v is None and "no PMC summary" in why and "aaaaaaaaaaaa" in why
+    assert bench.pmc_traffic("C4", 0)[0] is None  # no summary of that config at all
+
+
+def test_committed_pmc_summaries_are_well_formed():
+    # (round 1-2 summaries predate the sha256 key; bench.pmc_traffic skips them)
+    paths = [p for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_*.json")))
+             if "so_sha256" in json.load(open(p))]
+    assert len(paths) >= 3
+    for p in paths:
+        d = json.load(open(p))
+        assert len(d["so_sha256"]) == 64, p
+        assert d["traffic_per_frame_bytes"] > 0, p
+        assert any("stitch_tiled_kernel" in k for k in d["traffic_bytes"]), p
+        # per launch: 2 x FETCH_SIZE + WRITE_SIZE, the medians over the profiled launches, KiB -> bytes
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            for k, t in d["traffic_bytes"].items():
+                f, w = d["FETCH_SIZE"].get(k), d["WRITE_SIZE"].get(k)
+                if f and w:
+                    want = (2 * f["kib_median"] + w["kib_median"]) * 1024
+                    assert t == pytest.approx(want, rel=1e-6), (p, k)
