@@ -355,7 +355,12 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     // the f32 pyramid's 1.0f above; tile_owned): D = G - pyrUp(G_next) (G at the top level) exactly,
     // the weight sum is kWsumOwned and rint(D * kRcpOwned) = D (|D| <= 255), so the Laplacian is taken
     // as is, with no weight loads or sums.
-    if (a.owned != nullptr && a.owned[tile] != 0) {
+    // Deep tiles (owned = 2, multiband_host.cpp): R = G on every pixel, by induction over the levels
+    // above (one camera of weight 1 on all the pyrUp taps, with the camera's and the collapse's taps
+    // identical), so neither pyrUp is taken.
+    const int own = a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
+    const bool deep = own == 2;
+    if (own != 0) {
         const int n = __builtin_ctz(m);
         const MbCamLevel c = a.cams[n];
         const int xl = x - c.ox, yl = y - c.oy;  // inside the camera (seam pixels), even
@@ -363,6 +368,15 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
         const int cy0 = min(max(yl, 0), c.h - 1), cy1 = min(max(yl + 1, 0), c.h - 1);
         const uint2 gp0 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy0 * c.g_pitch + x0 * 4);
         const uint2 gp1 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy1 * c.g_pitch + x0 * 4);
+        if (deep) {
+#pragma unroll
+            for (int p = 0; p < 4; p++) {
+                const uint2 gp = (p >> 1) ? gp1 : gp0;
+                const uint32_t gv = ((xl + (p & 1) - x0) & 1) ? gp.y : gp.x;
+#pragma unroll
+                for (int ch = 0; ch < 3; ch++) R[p][ch] = (int)ch_of(gv, ch);
+            }
+        } else {
         // (the top level reads its own G as a stand-in for the unused taps, as the general path)
         const MbCamLevel cn = *(top ? a.cams + n : a.cams_next + n);
         const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
@@ -378,6 +392,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             R[p][0] = (int)ch_of(gv, 0) - (int)u0;
             R[p][1] = (int)ch_of(gv, 1) - (int)u1;
             R[p][2] = (int)ch_of(gv, 2) - (int)u2;
+        }
         }
     } else {
     float D[4][3];  // the Laplacian accumulator (a CV_16S sum in the reference; exact here, see below)
@@ -618,7 +633,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             R[p][ch] = (int)__builtin_amdgcn_fmed3f(__builtin_rintf(D[p][ch] * rcp), -32768.f, 32767.f);
     }
     }
-    if (!top) {
+    if (!top && !deep) {
         Up9 u;
         auto unpack = [](uint2 v, int (&o)[3]) {
             o[0] = (int)(int16_t)(v.x & 0xFFFFu);

@@ -21,6 +21,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -54,7 +55,9 @@ class MultiBand {
         DevBuf<uint32_t> tile_cams;
         std::vector<uint32_t> tile_cams_h;
         DevBuf<uint8_t> owned;          // multi-band: per tile, one camera of weight exactly 1 throughout
+                                        // (1), and R = G on every tile pixel (2, the deep pass)
         int n_owned = 0;
+        int n_deep = 0;                 // owned tiles with R = G at this level (owned = 2)
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
         int rup_rows = 0;
@@ -370,6 +373,10 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     // ---- weight activity per 8x8 block, then per tile (bit n: camera n) -------------------------
     constexpr int kBlk = 8;
     std::vector<std::vector<std::vector<uint8_t>>> act(B + 1);  // [level][camera][block]
+    // per level: the owner of each level-grid pixel (the one camera with a non-zero weight, that weight
+    // exactly 1; -1 otherwise) and the tiles' owned flags (uploaded after the deep pass below)
+    std::vector<std::vector<int8_t>> own_map(B + 1);
+    std::vector<std::vector<uint8_t>> owned_h(B + 1);
     for (int l = 0; l <= B; l++) {
         auto& L = M.lv[l];
         const int bx_n = (L.W + kBlk - 1) / kBlk, by_n = (L.H + kBlk - 1) / kBlk;
@@ -398,6 +405,27 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                 wl.resize(L.wts.n);
                 HIP_CHECK(hipMemcpy(wl.data(), L.wts.p, wl.size() * sizeof(float), hipMemcpyDeviceToHost));
             }
+            auto& om = own_map[l];
+            om.assign((size_t)L.W * L.H, (int8_t)-2);
+            for (int i = 0; i < n; i++) {
+                const auto& c = L.cams_h[i];
+                const size_t woff = l == 0 ? seam_off[i] : (size_t)(static_cast<const float*>(c.weight) - L.wts.p);
+                for (int yl = 0; yl < c.h; yl++) {
+                    const int y = yl + c.oy;
+                    if (y < 0 || y >= L.H) continue;
+                    for (int xl = 0; xl < c.w; xl++) {
+                        const int x = xl + c.ox;
+                        if (x < 0 || x >= L.W) continue;
+                        const size_t k = woff + (size_t)yl * c.w + xl;
+                        const bool nz = l == 0 ? seam_h[k] != 0 : wl[k] != 0.f;
+                        const bool one = l == 0 ? seam_h[k] == 255 : wl[k] == 1.0f;
+                        if (!nz) continue;
+                        int8_t& o = om[(size_t)y * L.W + x];
+                        o = (o == -2 && one) ? (int8_t)i : (int8_t)-1;
+                    }
+                }
+            }
+            for (int8_t& o : om) o = o < 0 ? (int8_t)-1 : o;
             std::vector<uint8_t> owned((size_t)L.tx_n * L.ty_n, 0);
             for (int ty = 0; ty < L.ty_n; ty++)
                 for (int tx = 0; tx < L.tx_n; tx++) {
@@ -420,11 +448,12 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                     owned[(size_t)ty * L.tx_n + tx] = all ? 1 : 0;
                     L.n_owned += all ? 1 : 0;
                 }
-            L.owned.upload(owned.data(), owned.size());
+            owned_h[l] = std::move(owned);
         }
     }
     // ---- pyrUp tap tables -------------------------------------------------------------------
     std::vector<std::vector<std::vector<UpQuad>>> ur(B), uc(B);  // [level][camera]
+    std::vector<std::vector<UpQuad>> rup_r(B), rup_c(B);             // [level]: the collapse's
     for (int l = 0; l < B; l++) {
         auto& L = M.lv[l];
         const auto& Ln = M.lv[l + 1];
@@ -473,8 +502,92 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             L.rup_org.upload(r0.data(), r0.size());
         }
         L.rup_rows = (int)rr.size();
+        rup_r[l] = rr;
+        rup_c[l] = rc;
         rr.insert(rr.end(), rc.begin(), rc.end());
         L.rup.upload(rr.data(), rr.size());
+    }
+    // ---- deep tiles: R = G (mb_blend skips the pyrUps) -------------------------------------------
+    // A pixel of level l is deep for camera n when n owns it (one camera of weight exactly 1), the
+    // camera's pyrUp of G_{l+1} there reads the same sources with the same weights as the collapse's
+    // pyrUp of R_{l+1}, and every such source is deep for n at level l + 1 (at the top level: owned).
+    // Then R_l = G_l exactly, by induction from the top: L_l = G_l - up(G_{l+1}) (weight 1, the
+    // normalisation exact for |D| <= 255), R_l = L_l + up(R_{l+1}) with R_{l+1} = G_{l+1} on every tap,
+    // and the two pyrUps round identically (the u8 and s16 saturations are no-ops for 0..255).  A tile
+    // whose pixels are all deep (owned = 2) takes R = G at its level: no taps, no collapse.
+    // (OCTVR_MB_NO_DEEP=1: measurement / cross-check knob, every owned tile takes the pyrUp path)
+    const bool deep_on = std::getenv("OCTVR_MB_NO_DEEP") == nullptr;
+    if (!M.feather) {
+        // nonzero-weight (source, weight) pairs of grid pixel 2q + p, sources shifted by `sh`, merged
+        auto taps_of = [](const UpQuad& u, int p, int sh, int (&src)[3], int (&wt)[3]) {
+            int k = 0;
+            for (int j = 0; j < 3; j++) {
+                const int w = p ? u.w1[j] : u.w0[j];
+                if (!w) continue;
+                const int v = (int)u.idx[j] + sh;
+                int m = 0;
+                while (m < k && src[m] != v) m++;
+                if (m == k) src[k] = v, wt[k++] = 0;
+                wt[m] += w;
+            }
+            for (int a = 1; a < k; a++)  // sorted by source
+                for (int b = a; b > 0 && src[b - 1] > src[b]; b--) std::swap(src[b], src[b - 1]), std::swap(wt[b], wt[b - 1]);
+            return k;
+        };
+        auto same_taps = [&](const UpQuad& cu, int sh, const UpQuad& gu, int p) {
+            int s1[3], w1[3], s2[3], w2[3];
+            const int k1 = taps_of(cu, p, sh, s1, w1), k2 = taps_of(gu, p, 0, s2, w2);
+            if (k1 != k2 || k1 == 0) return false;
+            for (int j = 0; j < k1; j++)
+                if (s1[j] != s2[j] || w1[j] != w2[j]) return false;
+            return true;
+        };
+        std::vector<int8_t> deep_next = own_map[B];
+        for (int l = B - 1; l >= 0; l--) {
+            auto& L = M.lv[l];
+            const auto& Ln = M.lv[l + 1];
+            std::vector<std::vector<uint8_t>> rok(n), cok(n);
+            for (int i = 0; i < n; i++) {
+                rok[i].resize(L.H);
+                cok[i].resize(L.W);
+                for (int y = 0; y < L.H; y++)
+                    rok[i][y] = same_taps(ur[l][i][y >> 1], Ln.cams_h[i].oy, rup_r[l][y >> 1], y & 1);
+                for (int x = 0; x < L.W; x++)
+                    cok[i][x] = same_taps(uc[l][i][x >> 1], Ln.cams_h[i].ox, rup_c[l][x >> 1], x & 1);
+            }
+            auto deep_px = [&](int x, int y) -> bool {
+                const int c = own_map[l][(size_t)y * L.W + x];
+                if (c < 0 || !rok[c][y] || !cok[c][x]) return false;
+                int rs[3], rw[3], cs[3], cw[3];
+                const int kr = taps_of(rup_r[l][y >> 1], y & 1, 0, rs, rw), kc = taps_of(rup_c[l][x >> 1], x & 1, 0, cs, cw);
+                for (int a = 0; a < kr; a++)
+                    for (int b = 0; b < kc; b++)
+                        if (deep_next[(size_t)rs[a] * Ln.W + cs[b]] != c) return false;
+                return true;
+            };
+            std::vector<int8_t> deep;
+            if (l > 0) {  // every pixel (the finer level's test reads them)
+                deep.assign((size_t)L.W * L.H, (int8_t)-1);
+                for (int y = 0; y < L.H; y++)
+                    for (int x = 0; x < L.W; x++)
+                        if (deep_px(x, y)) deep[(size_t)y * L.W + x] = own_map[l][(size_t)y * L.W + x];
+            }
+            for (int ty = 0; ty < L.ty_n; ty++)
+                for (int tx = 0; tx < L.tx_n; tx++) {
+                    uint8_t& t = owned_h[l][(size_t)ty * L.tx_n + tx];
+                    if (!t) continue;
+                    bool all = true;
+                    for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
+                        for (int x = tx * kTileW; x < std::min((tx + 1) * kTileW, L.W); x++)
+                            if (l > 0 ? deep[(size_t)y * L.W + x] < 0 : !deep_px(x, y)) {
+                                all = false;
+                                break;
+                            }
+                    if (all && deep_on) t = 2, L.n_deep++;
+                }
+            deep_next = std::move(deep);
+        }
+        for (int l = 0; l <= B; l++) M.lv[l].owned.upload(owned_h[l].data(), owned_h[l].size());
     }
     // ---- required 8x8 blocks per camera and level, then tiles ------------------------------------
     // need(l) = weight blocks(l) + pyrUp support of weight blocks(l-1) + pyrDown support of need(l+1)
@@ -708,10 +821,11 @@ std::string multiband_info(const MultiBand& M) {
         const auto& L = M.lv[l];
         size_t cam_tiles = 0;
         for (uint32_t m : L.tile_cams_h) cam_tiles += (size_t)__builtin_popcount(m);
-        char buf[224];
+        char buf[288];
         snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d%s}",
                  l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down,
-                 L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned)).c_str() : "");
+                 L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned) + ", \"deep_tiles\": " +
+                              std::to_string(L.n_deep)).c_str() : "");
         s += buf;
     }
     return s + "]";

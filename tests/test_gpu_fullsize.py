@@ -91,3 +91,33 @@ def test_gpu_fullsize_bit_exact(product_lib, cfg):
         _, g_orc = O.stitch_frame(sets[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None,
                                   blend=0, threads=THREADS, row_band=(0, 2))
         np.testing.assert_array_equal(np.array(m.gains()), np.array(g_orc))
+
+
+def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch):
+    """C3 at full size: the deep tiles' R = G shortcut (multiband_host.cpp) against the same mapper with it
+    off (OCTVR_MB_NO_DEEP, every owned tile through both pyrUps), on noise frames (every level's
+    Laplacian non-zero): bit-identical output."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    rig, W, H, sizes = synthetic.CONFIGS["C3"]()
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
+    mt.create_masks(0)
+    rng = np.random.default_rng(11)
+    frames = [torch.from_numpy(rng.integers(0, 256, size=(h * 3 // 2, w), dtype=np.uint8)).cuda() for w, h in sizes]
+    outs = []
+    deep = []
+    for off in (False, True):
+        if off:
+            monkeypatch.setenv("OCTVR_MB_NO_DEEP", "1")
+        m = ox.Mapper(mt, sizes, blend=synthetic.BLEND["C3"], enable_gain=True)
+        deep.append([t["deep_tiles"] for t in m.info()["level_tiles"]])
+        out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+        m.stitch(frames, out, gains=[1.0] * len(sizes))
+        torch.cuda.synchronize()
+        outs.append(out.cpu().numpy())
+        del m
+    print(deep)
+    assert deep[0][0] > 0 and sum(deep[1]) == 0
+    d = outs[0] != outs[1]
+    assert not d.any(), (int(d.sum()), np.argwhere(d)[:4].tolist())

@@ -84,7 +84,7 @@ def test_gpu_remap_edges(ox):
     assert np.array_equal(got, want)
 
 
-def _stitch_case(ox, name, frames_fn, gains, blend=0):
+def _stitch_case(ox, name, frames_fn, gains, blend=0, info=None):
     rig, z = O.load_rig(name)
     W, H = (int(v) for v in z["out_size"])
     n = len(z["rois"])
@@ -96,6 +96,8 @@ def _stitch_case(ox, name, frames_fn, gains, blend=0):
     seams = [z[f"seam_{i}"] for i in range(n)]
     mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks, seams)
     m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True)
+    if info is not None:
+        info.append(m.info())
     import torch
     out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
     m.stitch([_cuda(f) for f in frames], out, gains=gains)
@@ -403,6 +405,24 @@ def test_gpu_multiband_bit_exact(ox, name, blend):
         np.testing.assert_array_equal(g_gpu, g_orc)
         d = got != want
         assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
+
+
+def test_gpu_multiband_deep_tiles(ox):
+    """Deep tiles (R = G at their level, no pyrUp taps; multiband_host.cpp) occur on the golden rigs and
+    the output stays bit-exact with them."""
+    from octvr_amd import synthetic
+    deep = {}
+    for name in RIGS:
+        for blend in (4, 16):
+            info = []
+            got, want, _, _ = _stitch_case(ox, name, synthetic.smooth_yuv_frame, None, blend=blend, info=info)
+            lv = info[0]["level_tiles"]
+            deep[(name, blend)] = [t.get("deep_tiles", 0) for t in lv]
+            assert all(t["deep_tiles"] <= t["owned_tiles"] for t in lv)
+            d = got != want
+            assert not d.any(), (name, blend, int(d.sum()), np.argwhere(d)[:5].tolist())
+    print(deep)
+    assert sum(v[0] for v in deep.values()) > 0, deep
 
 
 @pytest.mark.parametrize("k", [1, 2])
