@@ -359,6 +359,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     // above (one camera of weight 1 on all the pyrUp taps, with the camera's and the collapse's taps
     // identical), so neither pyrUp is taken.
     const int own = a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
+    if (own == 3) return;  // no collapse reads this tile (levels >= 1)
     const bool deep = own == 2;
     if (own != 0) {
         const int n = __builtin_ctz(m);

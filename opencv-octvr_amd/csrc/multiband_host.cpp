@@ -55,9 +55,10 @@ class MultiBand {
         DevBuf<uint32_t> tile_cams;
         std::vector<uint32_t> tile_cams_h;
         DevBuf<uint8_t> owned;          // multi-band: per tile, one camera of weight exactly 1 throughout
-                                        // (1), and R = G on every tile pixel (2, the deep pass)
+                                        // (1), and R = G on every tile pixel (2, the deep pass); 3: read by no collapse
         int n_owned = 0;
         int n_deep = 0;                 // owned tiles with R = G at this level (owned = 2)
+        int n_skip = 0;                 // tiles no collapse reads (owned = 3)
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
         int rup_rows = 0;
@@ -587,6 +588,37 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                 }
             deep_next = std::move(deep);
         }
+        // Tiles of level l >= 1 that no collapse reads (every level-(l-1) tile whose pyrUp taps reach them
+        // is deep or itself unread): owned = 3, mb_blend returns at once there, and their Gaussian blocks
+        // are not required for them (below).
+        for (int l = 1; deep_on && l <= B; l++) {
+            auto& L = M.lv[l];
+            const auto& Lf = M.lv[l - 1];
+            std::vector<uint8_t> read((size_t)L.tx_n * L.ty_n, 0);
+            for (int ty = 0; ty < Lf.ty_n; ty++)
+                for (int tx = 0; tx < Lf.tx_n; tx++) {
+                    const uint8_t t = owned_h[l - 1][(size_t)ty * Lf.tx_n + tx];
+                    if (t == 2 || t == 3) continue;
+                    int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
+                    for (int q = ty * kTileH / 2; q < (ty + 1) * kTileH / 2; q++)
+                        for (int j = 0; j < 3; j++)
+                            if (rup_r[l - 1][q].w0[j] | rup_r[l - 1][q].w1[j])
+                                r0 = std::min(r0, (int)rup_r[l - 1][q].idx[j]), r1 = std::max(r1, (int)rup_r[l - 1][q].idx[j]);
+                    for (int q = tx * kTileW / 2; q < (tx + 1) * kTileW / 2; q++)
+                        for (int j = 0; j < 3; j++)
+                            if (rup_c[l - 1][q].w0[j] | rup_c[l - 1][q].w1[j])
+                                c0 = std::min(c0, (int)rup_c[l - 1][q].idx[j]), c1 = std::max(c1, (int)rup_c[l - 1][q].idx[j]);
+                    if (r1 < 0 || c1 < 0) continue;
+                    for (int y = r0 / kTileH; y <= std::min(r1 / kTileH, L.ty_n - 1); y++)
+                        for (int x = c0 / kTileW; x <= std::min(c1 / kTileW, L.tx_n - 1); x++) read[(size_t)y * L.tx_n + x] = 1;
+                }
+            for (size_t t = 0; t < read.size(); t++)
+                if (!read[t]) {
+                    L.n_deep -= owned_h[l][t] == 2 ? 1 : 0;
+                    owned_h[l][t] = 3;
+                    L.n_skip++;
+                }
+        }
         for (int l = 0; l <= B; l++) M.lv[l].owned.upload(owned_h[l].data(), owned_h[l].size());
     }
     // ---- required 8x8 blocks per camera and level, then tiles ------------------------------------
@@ -599,6 +631,13 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         for (int i = 0; i < n; i++) {
             const auto& c = L.cams_h[i];
             std::vector<uint8_t> need = act[l][i];
+            auto tile_of = [&](int lv_, int bx, int by) {  // owned flag of the tile holding block (bx, by)
+                const auto& Lt = M.lv[lv_];
+                return owned_h[lv_].empty() ? 0 : (int)owned_h[lv_][(size_t)(by * kBlk / kTileH) * Lt.tx_n + bx * kBlk / kTileW];
+            };
+            for (int by = 0; by < by_n; by++)  // blocks of unread tiles: no blend reads G there
+                for (int bx = 0; bx < bx_n; bx++)
+                    if (tile_of(l, bx, by) == 3) need[(size_t)by * bx_n + bx] = 0;
             auto mark = [&](int x0, int y0, int x1, int y1) {  // level-grid pixel rectangle, inclusive
                 x0 = std::max(x0, 0), y0 = std::max(y0, 0);
                 x1 = std::min(x1, bx_n * kBlk - 1), y1 = std::min(y1, by_n * kBlk - 1);
@@ -611,6 +650,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                 for (int by = 0; by < fby; by++)
                     for (int bx = 0; bx < fbx; bx++) {
                         if (!act[l - 1][i][(size_t)by * fbx + bx]) continue;
+                        if (tile_of(l - 1, bx, by) >= 2) continue;  // deep / unread: no pyrUp of G_l there
                         int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
                         for (int q = by * kBlk / 2; q < (by + 1) * kBlk / 2; q++) {
                             const UpQuad& u = ur[l - 1][i][q];
@@ -825,7 +865,7 @@ std::string multiband_info(const MultiBand& M) {
         snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d%s}",
                  l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down,
                  L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned) + ", \"deep_tiles\": " +
-                              std::to_string(L.n_deep)).c_str() : "");
+                              std::to_string(L.n_deep) + ", \"unread_tiles\": " + std::to_string(L.n_skip)).c_str() : "");
         s += buf;
     }
     return s + "]";
