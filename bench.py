@@ -29,7 +29,8 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one GPU each); without a launcher's WORLD_SIZE, bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
@@ -172,21 +173,82 @@ def cpu_baseline(mt, frames_np, sizes, W, H, blend=0):
                                                  dt, cpu_model())}
 
 
-def main():
+def visible_gpus():
+    """Number of GPUs this process may use, counted without initialising HIP (the parent of a
+    multi-rank launch must not touch the GPU before it starts its ranks)."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def launch_ranks(n, argv, check_devices=True):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this same script (one per
+    GPU, SURVEY.md §8e: independent rigs, no data-path collective), each with RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR / MASTER_PORT in its environment, and wait for them.  Rank 0 prints the
+    one JSON line.  Runs before anything touches the GPU; returns the worst child exit status."""
+    import socket
+    if check_devices:
+        have = visible_gpus()
+        if n > have:
+            sys.stderr.write("bench.py: --gpus %d but only %d GPU(s) visible\n" % (n, have))
+            return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(argv[0])] + list(argv[1:]), env=env))
+    # a rank that fails leaves the others waiting in a barrier: stop them, and report its status
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [c for c in rcs if c not in (None, 0)]
+        if bad or all(c is not None for c in rcs):
+            break
+        time.sleep(0.2)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    return bad[0] if bad else 0
+
+
+def main(rank_body=None, check_devices=True):
+    """rank_body(args, world, rank, local_rank, dist) -> result dict (rank 0) — the GPU stitch by
+    default; tests/bench_standin.py passes a CPU stand-in to exercise the launcher and the harness."""
     args = parse()
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv, check_devices))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
-    import torch
-    import octvr_amd as ox
-    from octvr_amd import synthetic
-
+    if args.gpus is not None and world != args.gpus:
+        sys.stderr.write("bench.py: --gpus %d but WORLD_SIZE=%d\n" % (args.gpus, world))
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
         # no data-path collective: gloo carries only the barrier and the max-over-ranks time
         dist.init_process_group("gloo")
+    result = (rank_body or gpu_rank)(args, world, rank, local_rank, dist)
+    if rank == 0:
+        assert result["n_gpus"] == world
+        print(json.dumps(result), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def gpu_rank(args, world, rank, local_rank, dist):
+    import numpy as np  # noqa: F401
+    import torch
+    import octvr_amd as ox
+    from octvr_amd import synthetic
+
     torch.cuda.set_device(local_rank)
     dev = local_rank
 
@@ -217,7 +279,7 @@ def main():
         for k in range(max(args.steps, 1)):
             step(k)
         torch.cuda.synchronize(dev)
-        return
+        sys.exit(0)
 
     # setup: one stitch per stream first, so every stream's hardware queue exists before the W warmup
     # steps (the first launch on a new stream costs ~8 ms: with W < inflight it used to land inside the
@@ -328,10 +390,7 @@ def main():
         result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
-    if dist:
-        dist.destroy_process_group()
+    return result
 
 
 if __name__ == "__main__":

@@ -198,12 +198,17 @@ struct QuadOut {
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
 // The library's own RGB -> YUV420P (it stands in for NPP's closed nppiRGBToYUV420; oracle/octvr_oracle.c
-// rgb_quad_to_yuv is the same definition): full-range BT.601 in 8-bit fixed point,
-//   Y = (77 R + 150 G + 29 B + 128) >> 8                                   (0..255, no clamp needed)
-//   U = (sum over the quad of -43 R' - 84 G' + 127 B' + 131584) >> 10      (1..255)
-//   V = (sum over the quad of 127 R' - 106 G' - 21 B' + 131584) >> 10
-// with R' = R - 128 etc. (the U / V coefficients sum to 0, so they equal the same sums over R, G, B).
-// Per pixel one v_dot4_u32_u8 (Y lands in byte 1) and two v_dot4c_i32_i8 on the pixel xor 0x808080.
+// rgb_quad_to_yuv is the same definition).  NPP documents (and its YUV -> RGB, yuv_to_rgba above,
+// inverts) Y = 0.299 R + 0.587 G + 0.114 B, U = 0.492 (B - Y) + 128, V = 0.877 (R - Y) + 128, i.e.
+// U' = -0.147 R - 0.289 G + 0.436 B, V' = 0.615 R - 0.515 G - 0.100 B.  In fixed point, chroma as the
+// quad's mean (4:2:0):
+//   Y = (77 R + 150 G + 29 B + 128) >> 8                                  (0..255, no clamp needed)
+//   U = (sum over the quad of -38 R' - 74 G' + 112 B' + 131584) >> 10     (scale 256; 16..240)
+//   V = clamp((sum over the quad of 79 R' - 66 G' - 13 B' + 65792) >> 9, 0, 255)   (scale 128)
+// with R' = R - 128 etc. (each chroma vector sums to 0, so grey is exact; V's scale-128 vector fits
+// i8).  Every coefficient is within 0.002 of NPP's; a YUV -> RGB -> YUV round trip through the
+// staging conversion keeps U and V within +-1 (tests/test_oracle_color.py).  Per pixel one
+// v_dot4_u32_u8 (Y lands in byte 1) and two v_dot4c_i32_i8 on the pixel xor 0x808080.
 // px[p]: R | G << 8 | B << 16 (byte 3 is ignored: every coefficient vector has byte 3 = 0).
 __device__ __forceinline__ QuadOut quad_yuv(const uint32_t (&px)[4]) {
     uint32_t yr[4];
@@ -213,14 +218,14 @@ __device__ __forceinline__ QuadOut quad_yuv(const uint32_t (&px)[4]) {
         const uint32_t c = px[p];  // byte 3 meets coefficient 0 in all three products
         yr[p] = __builtin_amdgcn_udot4(c, 0x001D964Du, 128u, false);  // {77, 150, 29, 0}
         const int s = (int)(c ^ 0x00808080u);
-        au = __builtin_amdgcn_sdot4(s, 0x007FACD5, au, false);  // {-43, -84, 127, 0}
-        av = __builtin_amdgcn_sdot4(s, 0x00EB967F, av, false);  // {127, -106, -21, 0}
+        au = __builtin_amdgcn_sdot4(s, 0x0070B6DA, au, false);  // {-38, -74, 112, 0}
+        av = __builtin_amdgcn_sdot4(s, 0x00F3BE4F, av, false);  // {79, -66, -13, 0}
     }
     QuadOut q;
     q.y01 = __builtin_amdgcn_perm(yr[1], yr[0], 0x0C0C0501u);  // byte 1 of each
     q.y23 = __builtin_amdgcn_perm(yr[3], yr[2], 0x0C0C0501u);
     q.u = (uint32_t)(au + 131584) >> 10;
-    q.v = (uint32_t)(av + 131584) >> 10;
+    q.v = (uint32_t)min(max((av + 65792) >> 9, 0), 255);
     return q;
 }
 

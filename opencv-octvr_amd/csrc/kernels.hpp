@@ -84,6 +84,7 @@ constexpr int kTileSlots = 4;
 #define OCTVR_TILE_LDS_BYTES (20 * 1024)  // 20 KiB: 7 workgroups fit by LDS, so the composite can take a 7-wave register budget
 #endif
 constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
+static_assert(kTileLdsBytes <= (1 << 15), "the tiled entry holds the LDS byte offset in bits 0-14");
 constexpr int kTileZeroDwords = 4;
 // Staging stores: 2 x 16 bytes per 8-pixel group (row stride a multiple of 4 dwords), or with
 // OCTVR_STAGE_B64 4 x 8 bytes (stride even), so the tiler may pad rows to 2 mod 4 dwords.

@@ -1354,7 +1354,7 @@ int octvr_rig_create_from_arrays(int out_w, int out_h, int n, const int* rois, c
             RigInput& in = rig->inputs[i];
             memcpy(in.roi, rois + 4 * i, 4 * sizeof(int));
             REQUIRE(in.roi[0] >= 0 && in.roi[1] >= 0 && in.roi[2] > 0 && in.roi[3] > 0 &&
-                        in.roi[0] + in.roi[2] <= out_w && in.roi[1] + in.roi[3] <= out_h,
+                        in.roi[0] <= out_w - in.roi[2] && in.roi[1] <= out_h - in.roi[3],  // no int overflow
                     "ROI outside the output frame");
             size_t k = (size_t)in.roi[2] * in.roi[3];
             in.map1.assign(map1[i], map1[i] + k);

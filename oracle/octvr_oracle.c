@@ -889,22 +889,25 @@ static inline void yuv_px_to_rgb(int y, int u, int v, uint8_t* o) {
     o[2] = sat_u8_rne(fmaf(2.032f, Uf, Yf));
 }
 
-/* 2x2 RGB quad -> 4 Y + 1 U + 1 V: full-range BT.601 in 8-bit fixed point (the library's own
- * definition, device_common.hpp quad_yuv; it stands in for NPP's closed nppiRGBToYUV420):
+/* 2x2 RGB quad -> 4 Y + 1 U + 1 V (the library's own definition, device_common.hpp quad_yuv; it
+ * stands in for NPP's closed nppiRGBToYUV420, color.cpp:2306): NPP's documented BT.601 matrix,
+ * Y = 0.299 R + 0.587 G + 0.114 B, U = 0.492 (B - Y) + 128, V = 0.877 (R - Y) + 128 (the inverse of
+ * yuv_px_to_rgb above), in fixed point with the chroma as the quad's mean:
  *   Y = (77 R + 150 G + 29 B + 128) >> 8,
- *   U = (sum over the quad of -43 R - 84 G + 127 B, + 131584) >> 10,
- *   V = (sum over the quad of 127 R - 106 G - 21 B, + 131584) >> 10
- * (the U / V coefficients sum to 0; every intermediate fits an int and U, V land in 1..255). */
+ *   U = (sum over the quad of -38 R - 74 G + 112 B, + 131584) >> 10             (16..240),
+ *   V = clamp((sum over the quad of 79 R - 66 G - 13 B, + 65792) >> 9, 0, 255)
+ * (each chroma vector sums to 0, so R - 128 etc. may replace R in the sums). */
 static inline void rgb_quad_to_yuv(const uint8_t* const p[4], uint8_t Y[4], uint8_t* U, uint8_t* V) {
     int au = 0, av = 0;
     for (int k = 0; k < 4; k++) {
         const int R = p[k][0], G = p[k][1], B = p[k][2];
         Y[k] = (uint8_t)((77 * R + 150 * G + 29 * B + 128) >> 8);
-        au += -43 * R - 84 * G + 127 * B;
-        av += 127 * R - 106 * G - 21 * B;
+        au += -38 * R - 74 * G + 112 * B;
+        av += 79 * R - 66 * G - 13 * B;
     }
+    const int v = (av + 65792) >> 9;
     *U = (uint8_t)((au + 131584) >> 10);
-    *V = (uint8_t)((av + 131584) >> 10);
+    *V = (uint8_t)(v < 0 ? 0 : v > 255 ? 255 : v);
 }
 
 void orc_yuv420_to_rgba(const uint8_t* yuv, int w, int h, size_t pitch, uint8_t* rgba, size_t rgba_pitch) {

@@ -152,3 +152,12 @@ def test_dat_reader_rejects_malformed(product_lib, tmp_path, case):
     p.write_bytes(data)
     with pytest.raises(product_lib.OctvrError):
         product_lib.MapperTemplate.load(str(p))
+
+
+@pytest.mark.parametrize("roi", [(2 ** 31 - 1, 0, 1, 1), (0, 2 ** 31 - 1, 1, 1), (1, 0, 2 ** 31 - 1, 1)])
+def test_from_arrays_rejects_overflowing_roi(product_lib, roi):
+    """octvr_rig_create_from_arrays compares x <= out_w - w (no int overflow), so an
+    ROI at INT_MAX is rejected instead of wrapping negative and passing."""
+    one_f = np.zeros(1, np.float32)
+    with pytest.raises(product_lib.OctvrError):
+        product_lib.MapperTemplate.from_arrays(8, 4, [roi], [one_f], [one_f], [np.zeros(1, np.uint8)])

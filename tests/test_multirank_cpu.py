@@ -72,7 +72,54 @@ def test_bench_harness_two_ranks_gloo(tmp_path):
     assert r[0]["value"] == pytest.approx(world * 3 * r[0]["px"] / 1e6 / r[0]["elapsed"])
 
 
+def test_bench_entry_point_gpus2_standin():
+    """bench.py's own `--gpus 2` path (no WORLD_SIZE: bench.launch_ranks starts the ranks itself),
+    with the oracle standing in for the HIP stitch: one JSON line, n_gpus 2, both ranks' frames."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(here, "bench_standin.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2
+    assert sorted(r["rank"] for r in d["ranks"]) == [0, 1]
+    assert sorted(r["local_rank"] for r in d["ranks"]) == [0, 1]
+    assert all(r["frames"] == 2 for r in d["ranks"])
+    assert d["ranks"][0]["digest"] != d["ranks"][1]["digest"]  # independent rigs (rank-seeded frames)
+    assert d["value"] == pytest.approx(2 * 2 * d["frame_px"] / 1e6 / d["elapsed"])
+
+
+def test_bench_entry_point_rejects_mismatch():
+    """--gpus that disagrees with a launcher's WORLD_SIZE is an error, not a silent 1-GPU run."""
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(here, "bench_standin.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "0"], env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "WORLD_SIZE=1" in p.stderr
+
+
 def test_frame_seeds_are_distinct():
     import bench
     seeds = {bench.frame_seed(r, j, i) for r in range(8) for j in range(4) for i in range(16)}
     assert len(seeds) == 8 * 4 * 16
+
+
+def test_bench_refuses_more_ranks_than_gpus():
+    """bench.py --gpus N with fewer visible GPUs fails with a clear error before touching any GPU
+    (this container has none)."""
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("needs a host with fewer than 2 GPUs")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode == 2 and "GPU(s) visible" in p.stderr
