@@ -17,8 +17,8 @@
  * Errors: bad JSON / .dat throw std::string as the reference's template code does (template.cpp:30,33,
  * 53,262); everything else throws cv::Exception (the reference's CV_Assert).  Differences from the
  * reference, all deliberate:
- *   - MapperTemplate copies are safe (the reference double-deletes its camera pointers);
- *     output_cam / input_cams stay null (camera models live behind the C ABI).
+ *   - MapperTemplate copies are independent deep copies (octvr_rig_clone; the reference double-deletes
+ *     its camera pointers); output_cam / input_cams stay null (camera models live behind the C ABI).
  *   - create_masks(imgs) with images needs GraphCutSeamFinder: not on the path, throws.
  *   - AsyncMultiMapper's preview_size (Qt shared-memory preview) is ignored; its worker threads are
  *     joined on destruction instead of running forever (async.cpp:337-349).
@@ -27,6 +27,7 @@
 #ifndef OCTVR_HPP
 #define OCTVR_HPP
 
+#include <charconv>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -98,6 +99,26 @@ struct RigDeleter {
 };
 typedef std::shared_ptr<octvr_rig> RigPtr;
 inline RigPtr own(octvr_rig* r) { return RigPtr(r, RigDeleter()); }
+inline RigPtr clone(const RigPtr& r) {
+    if (!r) return RigPtr();
+    octvr_rig* c = nullptr;
+    check(octvr_rig_clone(r.get(), &c));
+    return own(c);
+}
+
+// The camera-model rig behind a MapperTemplate: copying a template copies it (the reference copies its
+// Input vectors by value, so add_input / morph_controlpoints on one copy never reach another).
+struct OwnedRig {
+    RigPtr p;
+    OwnedRig() = default;
+    OwnedRig(const OwnedRig& o) : p(clone(o.p)) {}
+    OwnedRig& operator=(const OwnedRig& o) {
+        if (this != &o) p = clone(o.p);
+        return *this;
+    }
+    OwnedRig(OwnedRig&&) = default;
+    OwnedRig& operator=(OwnedRig&&) = default;
+};
 
 // a tightly packed copy of `n` elements of T from a caller array into a new Mat
 template <typename T>
@@ -111,8 +132,10 @@ inline cv::Mat mat_copy(const T* src, int rows, int cols, int type) {
 inline cv::Mat packed(const cv::Mat& m) { return m.isContinuous() ? m : m.clone(); }
 
 #ifdef OCTVR_HAVE_RAPIDJSON
-// a rapidjson value as JSON text with every number printed to 17 significant digits, parsed back with
-// correct rounding (OCTVR_JSON_EXACT): the doubles the caller's rapidjson holds, unchanged
+// a rapidjson value as JSON text with every number in its shortest round-trip form (std::to_chars),
+// parsed back with correct rounding (OCTVR_JSON_EXACT, std::from_chars): the doubles the caller's
+// rapidjson holds, unchanged.  Both conversions are locale-independent (a Qt caller has called
+// setlocale(LC_ALL, ""); printf / strtod would write and read "1,5" under a comma locale).
 inline void write_exact(const rapidjson::Value& v, std::string& out) {
     char buf[64];
     if (v.IsObject()) {
@@ -149,8 +172,8 @@ inline void write_exact(const rapidjson::Value& v, std::string& out) {
         snprintf(buf, sizeof buf, "%llu", (unsigned long long)v.GetUint64());
         out += buf;
     } else {
-        snprintf(buf, sizeof buf, "%.17g", v.GetDouble());
-        out += buf;
+        const std::to_chars_result r = std::to_chars(buf, buf + sizeof buf, v.GetDouble());
+        out.append(buf, r.ptr);
     }
 }
 inline std::string json_exact(const rapidjson::Value& v) {
@@ -257,28 +280,28 @@ public:
     detail::RigPtr rig() const { return from_fields(true); }
 
 private:
-    detail::RigPtr cams_;  // the rig with the camera models (JSON-built templates), for add_input / morph
+    detail::OwnedRig cams_;  // the rig with the camera models (JSON-built templates), for add_input / morph
 
     void create(const std::string& to, const std::string& opts, int w, int h, int flags) {
         octvr_rig* r = nullptr;
         detail::check(octvr_rig_create(to.c_str(), opts.c_str(), w, h, detail::device(), flags, &r));
-        cams_ = detail::own(r);
+        cams_.p = detail::own(r);
         out_type = to;
         int ow = 0, oh = 0;
         detail::check(octvr_rig_out_size(r, &ow, &oh));
         out_size = cv::Size(ow, oh);
     }
     void add(const std::string& from, const std::string& opts, bool overlay, bool use_roi, int flags) {
-        if (!cams_) throw cv::Exception(OCTVR_E_UNSUPPORTED, "add_input needs a template created from an output camera");
-        detail::check(octvr_rig_add_input(cams_.get(), from.c_str(), opts.c_str(), overlay ? 1 : 0, use_roi ? 1 : 0,
+        if (!cams_.p) throw cv::Exception(OCTVR_E_UNSUPPORTED, "add_input needs a template created from an output camera");
+        detail::check(octvr_rig_add_input(cams_.p.get(), from.c_str(), opts.c_str(), overlay ? 1 : 0, use_roi ? 1 : 0,
                                           flags));
-        pull(cams_.get());
+        pull(cams_.p.get());
     }
     void morph(const std::string& cps) {
-        if (!cams_) throw cv::Exception(OCTVR_E_UNSUPPORTED, "morph_controlpoints needs the camera models (a JSON-built template)");
+        if (!cams_.p) throw cv::Exception(OCTVR_E_UNSUPPORTED, "morph_controlpoints needs the camera models (a JSON-built template)");
         int kept = 0;
-        detail::check(octvr_rig_morph_controlpoints(cams_.get(), cps.c_str(), &kept));
-        pull(cams_.get());
+        detail::check(octvr_rig_morph_controlpoints(cams_.p.get(), cps.c_str(), &kept));
+        pull(cams_.p.get());
     }
 
     static Input input_of(const octvr_rig* r, int i, bool overlay, const uint8_t** seam) {

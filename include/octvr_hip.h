@@ -130,6 +130,10 @@ int octvr_rig_morph_controlpoints(octvr_rig* rig, const char* control_points_jso
  * y2, normalized output coordinates) per triangle.  *n = count; src / dst may be NULL (count only). */
 int octvr_rig_get_triangles(const octvr_rig* rig, int i, float* src, float* dst, int cap, int* n);
 void octvr_rig_destroy(octvr_rig* rig);
+/* An independent deep copy of a rig (camera models, LUTs, seams, include-mask visibility state): what
+ * copying a vr::MapperTemplate copies (its Input vectors, octvr.hpp:56-64), so add_input / morph on
+ * one copy leave the other unchanged. */
+int octvr_rig_clone(const octvr_rig* rig, octvr_rig** out);
 
 /* ---- vr::Mapper ---------------------------------------------------------------------------- */
 /* Mapper(mt, in_sizes, blend, enable_gain, scale_output) (mapper.cpp:47-191).

@@ -3,6 +3,7 @@
 // rig schema needs: objects, arrays, numbers, strings, true/false/null.  Throws std::runtime_error.
 #pragma once
 
+#include <charconv>
 #include <cstdint>
 #include <cstdlib>
 #include <cstdio>
@@ -134,12 +135,17 @@ private:
             v.kind = JsonValue::Null;
         } else {
             v.kind = JsonValue::Number;
-            if (exact_) {
-                const char* b = s_.c_str() + i_;
-                char* e = nullptr;
-                v.num = strtod(b, &e);
-                if (e == b) fail("bad number");
-                i_ += (size_t)(e - b);
+            if (exact_) {  // std::from_chars: correctly rounded and locale-independent (strtod reads the
+                           // C library's LC_NUMERIC radix: "1,5" under a comma locale)
+                const char* b = s_.data() + i_;
+                const char* e = s_.data() + s_.size();
+                if (b < e && *b == '-' && b + 1 < e && !(b[1] >= '0' && b[1] <= '9')) fail("bad number");
+                if (b < e && !(*b == '-' || (*b >= '0' && *b <= '9'))) fail("bad number");
+                double x = 0.0;
+                const std::from_chars_result r = std::from_chars(b, e, x, std::chars_format::general);
+                if (r.ec != std::errc() || r.ptr == b) fail("bad number");
+                v.num = x;
+                i_ += (size_t)(r.ptr - b);
             } else {
                 v.num = number();
             }
@@ -228,7 +234,7 @@ private:
         }
         if (useDouble) {
             int p = exp + expFrac;
-            auto pow10 = [](int n) { double r = 1.0; static const double t[] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22}; if (n <= 22) return t[n]; char buf[16]; snprintf(buf, sizeof buf, "1e%d", n); r = strtod(buf, nullptr); return r; };
+            auto pow10 = [](int n) { double r = 1.0; static const double t[] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22}; if (n <= 22) return t[n]; char buf[16]; const int k = snprintf(buf, sizeof buf, "1e%d", n); std::from_chars(buf, buf + k, r); return r; };
             auto fast = [&](double sig, int e) { return e < -308 ? 0.0 : e >= 0 ? sig * pow10(e) : sig / pow10(-e); };
             if (p < -308) { d = fast(d, -308); d = fast(d, p + 308); }
             else d = fast(d, p);

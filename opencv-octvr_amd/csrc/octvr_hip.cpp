@@ -1532,6 +1532,29 @@ int octvr_rig_get_triangles(const octvr_rig* rig, int i, float* src, float* dst,
 
 void octvr_rig_destroy(octvr_rig* rig) { delete rig; }
 
+int octvr_rig_clone(const octvr_rig* src, octvr_rig** out) {
+    return guarded([&] {
+        REQUIRE(src && out, "NULL argument");
+        auto r = std::make_unique<octvr_rig>();
+        r->out_w = src->out_w;
+        r->out_h = src->out_h;
+        r->device = src->device;
+        r->inputs = src->inputs;
+        r->overlays = src->overlays;
+        r->seam_masks = src->seam_masks;
+        r->has_cameras = src->has_cameras;
+        r->out_cam_masks = src->out_cam_masks;
+        r->out_cam = src->out_cam;
+        r->cams = src->cams;
+        if (src->visible.p) {  // the include-mask visibility state (template.cpp:86-116) travels with the copy
+            DeviceGuard dg(src->device);
+            r->visible.alloc(src->visible.n);
+            HIP_CHECK(hipMemcpy(r->visible.p, src->visible.p, src->visible.n, hipMemcpyDeviceToDevice));
+        }
+        *out = r.release();
+    });
+}
+
 int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                         int enable_gain, int scale_w, int scale_h, octvr_mapper** out) {
     return guarded([&] {

@@ -70,6 +70,29 @@ int main(int argc, char** argv) {
         std::cerr << "dumped " << mt.inputs.size() << " inputs, " << mt.out_size.width << "x" << mt.out_size.height
                   << ", seam masks " << mt.seam_masks.size() << std::endl;
 
+        // ---- template copies are independent: the reference copies its Input vectors by value -------
+        {
+            vr::MapperTemplate a(out_type, out_opts, W, H);
+            a.add_input(types[0], opts[0], false, use_roi != 0);
+            vr::MapperTemplate b(a);  // copy construction
+            vr::MapperTemplate c(out_type, out_opts, W, H);
+            c = a;  // copy assignment
+            a.add_input(types[n - 1], opts[n - 1], false, use_roi != 0);
+            b.add_input(types[0], opts[0], false, use_roi != 0);
+            if (a.inputs.size() != 2 || b.inputs.size() != 2 || c.inputs.size() != 1)
+                throw std::runtime_error("MapperTemplate copies share their inputs");
+            const cv::Rect& r0 = a.inputs[0].roi;
+            const cv::Rect& rb = b.inputs[1].roi;
+            const cv::Rect& ra = a.inputs[1].roi;
+            const cv::Rect& rn = mt.inputs[n - 1].roi;
+            if (rb.x != r0.x || rb.y != r0.y || rb.width != r0.width || rb.height != r0.height ||
+                ra.x != rn.x || ra.y != rn.y || ra.width != rn.width || ra.height != rn.height)
+                throw std::runtime_error("a template copy received another copy's input");
+            c.add_input(types[n - 1], opts[n - 1], false, use_roi != 0);
+            if (c.inputs.size() != 2 || b.inputs.size() != 2) throw std::runtime_error("copy assignment shares inputs");
+            std::cerr << "template copies independent" << std::endl;
+        }
+
         // ---- a template loaded from .dat, vr::Mapper on GpuMats -------------------------------------
         std::ifstream in_dat(d + "rig.dat", std::ios::binary);
         vr::MapperTemplate mt2(in_dat);

@@ -147,3 +147,34 @@ def test_gpu_cpp_api_drop_in(product_lib, tmp_path, name, blend):
         nv12.append(m)
     want = O.fastmapper_nv12(nv12, sizes, [l[1] for l in luts], [l[2] for l in luts], [l[3] for l in luts], W, H)
     assert np.array_equal(np.fromfile(os.path.join(d, "out_fast.nv12"), np.uint8).reshape(H * 3 // 2, W), want)
+
+
+RJ_BIN = os.path.join(O.ROOT, "opencv-octvr_amd", "lib", "vr_dump_rj")
+
+
+@pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
+def test_gpu_rapidjson_dump_flow(tmp_path, name):
+    """apps/octvr/dump.cpp:71-113 verbatim in shape (rapidjson::Document -> MapperTemplate(type,
+    options["output"]["options"], w, h) -> add_input(type, (*i)["options"], false, roi) -> dump) through
+    the rapidjson::Value overloads (OCTVR_JSON_EXACT): the .dat equals the reference's own bytes, also
+    with a comma-decimal locale active in the caller (a Qt caller's setlocale(LC_ALL, ""))."""
+    if not os.path.exists(RJ_BIN):
+        pytest.skip("vr_dump_rj is built only where rapidjson's headers exist (build container)")
+    import test_json_locale as L
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    man = json.load(open(os.path.join(O.ROOT, "tests", "golden", "manifest.json")))["rigs"][name]
+    cfg = os.path.join(O.ROOT, "tests", "golden", name + ".json")
+    envs = [{"LC_ALL": "C"}]
+    loc = L.comma_locale(tmp_path)
+    if loc:
+        envs.append(loc)
+    for k, env in enumerate(envs):
+        out = str(tmp_path / ("rig%d.dat" % k))
+        args = [RJ_BIN, "-w", str(W), "-h", str(H), "-o", out, cfg]
+        if name == "rigD":
+            args.insert(1, "-n")  # rigD's golden .dat was dumped with -n (template.cpp:126-133)
+        r = subprocess.run(args, capture_output=True, text=True, timeout=300, env=dict(os.environ, **env))
+        assert r.returncode == 0, r.stderr[-2000:]
+        dat = open(out, "rb").read()
+        assert len(dat) == man["dat_bytes"] and hashlib.sha256(dat).hexdigest() == man["dat_sha256"], env
