@@ -152,10 +152,10 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
                     "D2H, copy-out, 3 frames in flight; PCIe- and host-copy-inclusive, not the roofline basis"}
 
 
-def cpu_baseline(mt, frames_np, sizes, W, H, blend=0):
+def cpu_baseline(mt, frames_np, sizes, W, H, blend=0, gain=True):
     """The reference CPU path restated by the oracle (YUV->RGBA, fixed-point cv::remap of every
     camera over its full ROI, gain feed + apply, copyTo(mask) or the multi-band blender,
-    RGB->YUV420P) on this host."""
+    RGB->YUV420P) on this host.  gain=False: the C1 plumbing case (cv::remap + the seam-mask copy)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as O  # test infrastructure: used only as the timed CPU baseline
     rois, m1s, m2s, masks, seams = [], [], [], [], []
@@ -164,13 +164,17 @@ def cpu_baseline(mt, frames_np, sizes, W, H, blend=0):
         rois.append(roi); m1s.append(m1); m2s.append(m2); masks.append(mk); seams.append(sm)
     T = host_threads()
     t0 = time.perf_counter()
-    O.stitch_frame(frames_np, sizes, rois, m1s, m2s, masks, W, H, enable_gain=True, gains=None, threads=T,
+    O.stitch_frame(frames_np, sizes, rois, m1s, m2s, masks, W, H, enable_gain=gain, gains=None, threads=T,
                    blend=blend, seams=seams if blend > 0 else None)
     dt = time.perf_counter() - t0
-    return {"value": round(W * H / 1e6 / dt, 3), "unit": "MP/s", "cores": T, "kind": "port",
-            "sample": "one full %dx%d frame (%d cameras, gain estimated%s) through the oracle (oracle/*.c), "
-                      "%.2f s, host CPU: %s" % (W, H, len(sizes), ", multi-band blend=%d" % blend if blend else "",
-                                                 dt, cpu_model())}
+    r = {"value": round(W * H / 1e6 / dt, 3), "unit": "MP/s", "cores": T, "kind": "port",
+         "sample": "one full %dx%d frame (%d cameras, %s%s) through the oracle (oracle/*.c), "
+                   "%.2f s, host CPU: %s" % (W, H, len(sizes), "gain estimated" if gain else "no gain",
+                                              ", multi-band blend=%d" % blend if blend else "", dt, cpu_model())}
+    if not gain and blend == 0 and len(sizes) == 2:
+        r["survey_reference"] = ("SURVEY.md §6: the reference's own CPU cv::remap + seam copy at this geometry, "
+                                 "192-204 MP/s on 8 threads of an 8-core Xeon VM (YUV<->RGB not included there)")
+    return r
 
 
 def visible_gpus():
@@ -243,12 +247,89 @@ def main(rank_body=None, check_devices=True):
         dist.destroy_process_group()
 
 
+def nv12_of(yuv420p):
+    """The same frame as NV12 (interleaved U, V rows), as FastMapper takes it."""
+    import numpy as np
+    h = yuv420p.shape[0] * 2 // 3
+    w = yuv420p.shape[1]
+    m = np.empty_like(yuv420p)
+    m[:h] = yuv420p[:h]
+    m[h:, 0::2] = yuv420p[h:, : w // 2]
+    m[h:, 1::2] = yuv420p[h:, w // 2:]
+    return m
+
+
+def fast_rank(args, world, rank, local_rank, dist):
+    """--config F2: vr::FastMapper::stitch_nv12 (mapper_fast.cpp:153-195) on the C2 rig built without ROI
+    (octvr_dump -n), NV12 in / out, feather weights; a step = one stitch_nv12 of one frame set."""
+    import torch
+    import octvr_amd as ox
+    from octvr_amd import synthetic
+
+    torch.cuda.set_device(local_rank)
+    dev = local_rank
+    rig, W, H, sizes = synthetic.CONFIGS[args.config]()
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=False, device=dev)
+    fm = ox.FastMapper(mt, sizes, device=dev)
+    frames_np = [nv12_of(synthetic.yuv_frame(w, h, frame_seed(rank, 0, i))) for i, (w, h) in enumerate(sizes)]
+    frames = [torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]
+    out = torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}")
+    stream = torch.cuda.current_stream(dev)
+
+    def step(k):
+        fm.stitch_nv12(frames, out, stream=stream)
+
+    if args.pmc_child:
+        for k in range(max(args.steps, 1)):
+            step(k)
+        torch.cuda.synchronize(dev)
+        sys.exit(0)
+    for k in range(max(args.warmup, 1)):
+        step(k)
+    torch.cuda.synchronize(dev)
+    elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
+    # kernel time: events around 16 back-to-back stitches (both plane launches) after the timed region
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for k in range(16):
+        step(k)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_s = e0.elapsed_time(e1) / 1e3 / 16
+    b = fm.traffic_bytes()
+    traffic, traffic_src = pmc_traffic(args.config, 1)
+    result = {
+        "metric": "stitched megapixels/sec (6x4K->8K equirect, FastMapper NV12)",
+        "value": round(aggregate_mps(world, args.steps, W * H, elapsed), 1), "unit": "MP/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (splitmix64 frames as NV12, SURVEY.md §8d rig)",
+        "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
+                               "template without ROI), NV12 in/out" % (len(sizes), sizes[0][0], sizes[0][1], W, H),
+                   "rigs_per_gpu": 1, "frames_in_flight": 1, "parallelism": "independent rig per GPU"},
+        "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
+                     "kernel": "fast_y_kernel + fast_uv_kernel", "kernel_us": round(kern_s * 1e6, 2),
+                     "kernel_us_basis": "torch events around 16 back-to-back stitch_nv12 on the launch stream",
+                     "bytes_per_launch": b,
+                     "bytes_basis": "8 B per (camera, 256-px run) entry block pixel, 1.5 B out per px, source bytes the "
+                                    "weighted taps reach (octvr_fastmapper_traffic)",
+                     "frac_at_step_time": round(b / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "frac_traffic": round(traffic / kern_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None},
+    }
+    # (no cpu_baseline: F2 is not a BASELINE configuration, and the oracle's FastMapper restatement
+    # rebuilds the per-rig feather weights inside every call)
+    return result
+
+
 def gpu_rank(args, world, rank, local_rank, dist):
     import numpy as np  # noqa: F401
     import torch
     import octvr_amd as ox
     from octvr_amd import synthetic
 
+    if args.config == "F2":
+        return fast_rank(args, world, rank, local_rank, dist)
     torch.cuda.set_device(local_rank)
     dev = local_rank
 
@@ -257,7 +338,8 @@ def gpu_rank(args, world, rank, local_rank, dist):
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=True, device=dev)
     if blend > 0:
         mt.create_masks(dev)  # MapperTemplate::create_masks (DistanceSeamFinder), as octvr_dump does
-    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=not args.no_gain, device=dev)
+    use_gain = synthetic.GAIN[args.config] and not args.no_gain
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=use_gain, device=dev)
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
     inflight = max(1, args.inflight)
@@ -356,9 +438,9 @@ def gpu_rank(args, world, rank, local_rank, dist):
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 YUV420P frames, SURVEY.md §8d rig)",
-        "config": {"workload": "%s: %d x %dx%d fullframe_fisheye -> %dx%d equirect, remap + gain (estimated per "
-                               "frame) + %s, YUV420P in/out" % (
+        "config": {"workload": "%s: %d x %dx%d fullframe_fisheye -> %dx%d equirect, remap + %s + %s, YUV420P in/out" % (
                                    args.config, len(sizes), sizes[0][0], sizes[0][1], W, H,
+                                   "gain (estimated per frame)" if use_gain else "no gain",
                                    "multi-band blend=%d (%d bands)" % (blend, int(math.ceil(math.log(blend) / math.log(2.)) - 1))
                                    if blend > 0 else "no-blend composite"),
                    "rigs_per_gpu": 1, "frames_in_flight": inflight, "parallelism": "independent rig per GPU"},
@@ -370,9 +452,18 @@ def gpu_rank(args, world, rank, local_rank, dist):
                                          % inflight) if inflight > 1 else "HIP-event start-to-end, every 4th launch",
                      "kernel_us_span": round(span_ms / 1e3 / max(launches, 1) * 1e6, 2),
                      "bytes_per_launch": bytes_per_launch,
-                     "survey_b_alg_bytes": survey_b_alg,
-                     "survey_b_alg_frac_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
-                     "frac_at_step_time": round(bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4)},
+                     "bytes_basis": "algorithmic: what each launch must move, each byte once (DESIGN.md §4; "
+                                    "octvr_mapper_traffic)" + ("; per launch of the sequence in bytes_parts" if blend > 0 else ""),
+                     **({"bytes_parts": m.info().get("traffic_parts")} if blend > 0 else {}),
+                     "frac_at_step_time": round(bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
+                     # the counter-based fraction: PMC HBM bytes of the same binary over the same kernel time
+                     "frac_traffic": round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
+                     "traffic_over_bytes": round(traffic / bytes_per_launch, 3) if traffic else None},
+        "survey_b_alg": {"bytes": survey_b_alg,
+                         "gbps_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9, 1),
+                         "note": "SURVEY.md §8(d) B_alg (per-camera maps re-read for every valid (camera, pixel)); "
+                                 "this design moves fewer bytes for the same output, so this is a rate of the survey's "
+                                 "model, not a fraction of HBM peak"},
         "gains": [round(g, 6) for g in gains],
         **({"roofline_one_in_flight": {"kernel_us": round(serial * 1e6, 2),
                                         "achieved": round(bytes_per_launch / serial / 1e9, 1),
@@ -389,7 +480,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
     if rank == 0 and world == 1 and not args.no_async_e2e:
         result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend)
+        result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend, gain=use_gain)
     return result
 
 

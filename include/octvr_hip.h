@@ -226,6 +226,9 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
  * channel order (merge of the V-then-U accumulators).  Stream-ordered. */
 int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fastmapper, const uint8_t* const* in_dev, const size_t* in_pitch,
                                  uint8_t* out_dev, size_t out_pitch, void* stream);
+/* Algorithmic bytes one stitch_nv12 moves (entries read, output written, source bytes its weighted taps
+ * reach): the roofline basis of bench.py --config F2. */
+int octvr_fastmapper_traffic(const octvr_fastmapper* fastmapper, double* bytes);
 void octvr_fastmapper_destroy(octvr_fastmapper* fastmapper);
 
 /* ---- standalone kernels --------------------------------------------------------------------- */

@@ -4,7 +4,10 @@
 //     (cv::resize of the f32 maps, 2x area fast path), imgwarp.cpp:4831-5044, 2284-2460;
 //   feather weights w_i = max(distanceTransform(mask_i) - 5, 0), u8 = sat(rne(255 * w_i / (1e-5 + sum w))),
 //     half-size weights by the u8 area fast path (mapper_fast.cpp:75-94);
-//   per 256-pixel run, the bit mask of cameras with a non-zero weight.
+//   per 256-pixel run, the bit mask of cameras with a non-zero weight, and the entries of exactly those
+//   (camera, run) pairs as consecutive 256-entry blocks (camera order), so the per-frame kernels read no
+//   entry of a camera that has zero weight on the whole run (C2 full frame: ~1.3 blocks per run instead of
+//   one per camera).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -18,16 +21,18 @@
 using namespace octvr;
 
 namespace octvr {
-hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint32_t* runs_y,
-                                  const uint2* ent_uv, const uint32_t* runs_uv, int W, int H, uint8_t* out,
+hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint2* runs_y,
+                                  const uint2* ent_uv, const uint2* runs_uv, int W, int H, uint8_t* out,
                                   int64_t out_pitch, hipStream_t s);
 }
 
 struct octvr_fastmapper {
     int device = 0, n = 0, W = 0, H = 0;
     std::vector<int> in_w, in_h;
-    DevBuf<uint2> ent_y, ent_uv;
-    DevBuf<uint32_t> runs_y, runs_uv;
+    DevBuf<uint2> ent_y, ent_uv;     // per (run, camera with weight in the run): 256 entries
+    DevBuf<uint2> runs_y, runs_uv;   // per run: camera mask, first block
+    double bytes = 0;                // algorithmic bytes per stitch (octvr_fastmapper_traffic)
+    size_t blocks = 0;               // 256-entry (camera, run) blocks, Y + UV
 };
 
 namespace {
@@ -104,29 +109,54 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
             }
             total[k] = t;
         });
-        std::vector<uint2> ey(npx * n), euv(nh * n);
         const size_t runs_y = (npx + 255) / 256, runs_uv = (nh + 255) / 256;
         std::vector<uint32_t> my(runs_y, 0u), muv(runs_uv, 0u);
-        std::vector<uint8_t> fmask(npx), hmask(nh);
-        std::vector<float> h1(nh), h2(nh);
+        std::vector<std::vector<uint8_t>> fmask(n, std::vector<uint8_t>(npx)), hmask(n, std::vector<uint8_t>(nh));
         for (int i = 0; i < n; i++) {
-            const RigInput& in = rig->inputs[i];
             // divide(weight_i, dst_weight_map) then convertTo(CV_8U, 255): fma(r, 255, 0), rne, saturate
+            uint8_t* fm_i = fmask[i].data();
             parallel_for(npx, [&](size_t k) {
                 const float e2 = total[k];
                 const float r = e2 != 0.f ? wt[i][k] / e2 : 0.f;
-                fmask[k] = sat_u8_rte(fmaf(r, 255.f, 0.f));
+                fm_i[k] = sat_u8_rte(fmaf(r, 255.f, 0.f));
             });
             // cv::resize(feather_mask, half): u8 area fast path (a + b + c + d + 2) >> 2
+            uint8_t* hm_i = hmask[i].data();
             parallel_for(hh, [&](size_t y) {
                 for (size_t x = 0; x < hw; x++) {
-                    const uint8_t* s = fmask.data() + (2 * y) * W + 2 * x;
-                    hmask[y * hw + x] = (uint8_t)((s[0] + s[1] + s[W] + s[W + 1] + 2) >> 2);
+                    const uint8_t* s = fm_i + (2 * y) * W + 2 * x;
+                    hm_i[y * hw + x] = (uint8_t)((s[0] + s[1] + s[W] + s[W + 1] + 2) >> 2);
                 }
             });
+            for (size_t k = 0; k < npx; k++)
+                if (fm_i[k]) my[k / 256] |= 1u << i;
+            for (size_t k = 0; k < nh; k++)
+                if (hm_i[k]) muv[k / 256] |= 1u << i;
+        }
+        // blocks: run r's cameras (ascending) at first[r], first[r] + 1, ...
+        auto blocks = [](const std::vector<uint32_t>& m, std::vector<uint2>& runs) {
+            runs.resize(m.size());
+            uint32_t b = 0;
+            for (size_t r = 0; r < m.size(); r++) {
+                runs[r] = make_uint2(m[r], b);
+                b += (uint32_t)__builtin_popcount(m[r]);
+            }
+            return (size_t)b;
+        };
+        std::vector<uint2> ry, ruv;
+        const size_t by = blocks(my, ry), buv = blocks(muv, ruv);
+        REQUIRE(std::max(by, buv) * 256 < ((size_t)1 << 32), "FastMapper entries exceed 2^32");
+        std::vector<uint2> ey(std::max<size_t>(by, 1) * 256, make_uint2(0u, 0u)), euv(std::max<size_t>(buv, 1) * 256, make_uint2(0u, 0u));
+        std::vector<float> h1(nh), h2(nh);
+        for (int i = 0; i < n; i++) {
+            const RigInput& in = rig->inputs[i];
             const float sx = (float)in_w[i], sy = (float)in_h[i];
-            parallel_for(npx, [&](size_t k) {
-                ey[(size_t)i * npx + k] = make_entry(in.map1[k], in.map2[k], sx, sy, fmask[k]);
+            const uint8_t* fm_i = fmask[i].data();
+            parallel_for(runs_y, [&](size_t r) {
+                if (!(my[r] >> i & 1u)) return;
+                const size_t blk = ry[r].y + (size_t)__builtin_popcount(my[r] & ((1u << i) - 1u));
+                for (size_t k = r * 256; k < std::min(npx, (r + 1) * 256); k++)
+                    ey[blk * 256 + (k - r * 256)] = make_entry(in.map1[k], in.map2[k], sx, sy, fm_i[k]);
             });
             const int vec = (int)(hw / 4 * 4);
             parallel_for(hh, [&](size_t y) {
@@ -139,17 +169,50 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
             });
             // r_map * (in_size / 2): integer halving first (mapper_fast.cpp:62-64)
             const float hx = (float)(in_w[i] / 2), hy = (float)(in_h[i] / 2);
-            parallel_for(nh, [&](size_t k) { euv[(size_t)i * nh + k] = make_entry(h1[k], h2[k], hx, hy, hmask[k]); });
-            for (size_t k = 0; k < npx; k++)
-                if (fmask[k]) my[k / 256] |= 1u << i;
-            for (size_t k = 0; k < nh; k++)
-                if (hmask[k]) muv[k / 256] |= 1u << i;
+            const uint8_t* hm_i = hmask[i].data();
+            parallel_for(runs_uv, [&](size_t r) {
+                if (!(muv[r] >> i & 1u)) return;
+                const size_t blk = ruv[r].y + (size_t)__builtin_popcount(muv[r] & ((1u << i) - 1u));
+                for (size_t k = r * 256; k < std::min(nh, (r + 1) * 256); k++)
+                    euv[blk * 256 + (k - r * 256)] = make_entry(h1[k], h2[k], hx, hy, hm_i[k]);
+            });
         }
+        // per stitch: 8 B per entry read, 1.5 B per output pixel written, and the source bytes the
+        // weighted taps reach (each once: luma pixels 1 B, interleaved chroma pairs 2 B)
+        fm->bytes = 8.0 * (double)(by + buv) * 256 + 1.5 * (double)npx;
+        for (int i = 0; i < n; i++) {
+            const int w = in_w[i], h = in_h[i];
+            std::vector<uint8_t> ty((size_t)w * h, 0), tuv((size_t)(w / 2) * (h / 2), 0);
+            auto touch = [](std::vector<uint8_t>& t, int tw, int th, uint2 e) {
+                const int sx = (int)(int16_t)(e.x & 0xFFFFu), sy = (int)(int16_t)(e.x >> 16);
+                for (int k = 0; k < 4; k++) {
+                    const int x = sx + (k & 1), y = sy + (k >> 1);
+                    if (x >= 0 && y >= 0 && x < tw && y < th) t[(size_t)y * tw + x] = 1;
+                }
+            };
+            for (size_t r = 0; r < runs_y; r++) {
+                if (!(my[r] >> i & 1u)) continue;
+                const size_t blk = ry[r].y + (size_t)__builtin_popcount(my[r] & ((1u << i) - 1u));
+                for (size_t k = 0; k < 256; k++)
+                    if (ey[blk * 256 + k].y >> 16) touch(ty, w, h, ey[blk * 256 + k]);
+            }
+            for (size_t r = 0; r < runs_uv; r++) {
+                if (!(muv[r] >> i & 1u)) continue;
+                const size_t blk = ruv[r].y + (size_t)__builtin_popcount(muv[r] & ((1u << i) - 1u));
+                for (size_t k = 0; k < 256; k++)
+                    if (euv[blk * 256 + k].y >> 16) touch(tuv, w / 2, h / 2, euv[blk * 256 + k]);
+            }
+            double c = 0;
+            for (uint8_t v : ty) c += v;
+            for (uint8_t v : tuv) c += 2.0 * v;
+            fm->bytes += c;
+        }
+        fm->blocks = by + buv;
         DeviceGuard dg(device);
         fm->ent_y.upload(ey.data(), ey.size());
         fm->ent_uv.upload(euv.data(), euv.size());
-        fm->runs_y.upload(my.data(), my.size());
-        fm->runs_uv.upload(muv.data(), muv.size());
+        fm->runs_y.upload(ry.data(), ry.size());
+        fm->runs_uv.upload(ruv.data(), ruv.size());
         *out = fm.release();
         return OCTVR_OK;
     } catch (const OctvrError& e) {
@@ -180,6 +243,15 @@ int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_
         set_last_error(e.what());
         return e.code;
     }
+}
+
+int octvr_fastmapper_traffic(const octvr_fastmapper* fm, double* bytes) {
+    if (!fm || !bytes) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    *bytes = fm->bytes;
+    return OCTVR_OK;
 }
 
 void octvr_fastmapper_destroy(octvr_fastmapper* fm) {

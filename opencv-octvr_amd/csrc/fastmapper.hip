@@ -8,7 +8,8 @@
 // a register (u16 adds wrap, so the camera order does not matter) and writes the final u8 directly:
 // no u16 accumulator planes in HBM, no separate convert pass.
 //
-// Per (camera, pixel) entry (uint2, built on the host from convertMaps + the feather weights):
+// Per (camera, pixel) entry (uint2, built on the host from convertMaps + the feather weights; stored only
+// for the (camera, 256-pixel run) pairs where the camera has a non-zero weight somewhere in the run):
 //   x = sx | sy << 16 (s16 each, convertMaps' integer tap), y = code (10-bit fractions) | weight << 16.
 #include <hip/hip_runtime.h>
 
@@ -50,18 +51,22 @@ __device__ __forceinline__ uint8_t convert_out(uint32_t acc) {  // convertTo(CV_
 
 }  // namespace
 
+// runs[r] = {camera mask, first block}: run r's cameras (ascending) own blocks first, first + 1, ... of
+// 256 entries (fastmapper.cpp)
 __global__ void __launch_bounds__(256) fast_y_kernel(FrameSet frames, const uint2* __restrict__ ent,
-                                                     const uint32_t* __restrict__ runs, int W, int H, uint8_t* out,
+                                                     const uint2* __restrict__ runs, int W, int H, uint8_t* out,
                                                      int64_t out_pitch) {
     const int64_t npx = (int64_t)W * H;
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t m = (uint32_t)uniform((int)runs[blockIdx.x]);
+    const uint2 rr = runs[blockIdx.x];
+    uint32_t m = (uint32_t)uniform((int)rr.x);
+    uint32_t blk = (uint32_t)uniform((int)rr.y);
     if (idx >= npx) return;
     uint32_t acc = 0;
     while (m) {
         const int c = __builtin_ctz(m);
         m &= m - 1;
-        const uint2 e = ent[(int64_t)c * npx + idx];
+        const uint2 e = ent[(int64_t)(blk++) * 256 + threadIdx.x];
         if ((e.y >> 16) == 0) continue;
         const SourceFrame& f = frames.f[c];
         acc += weighted_tap(f.yuv, f.w, f.h, f.pitch, 1, e);
@@ -71,18 +76,20 @@ __global__ void __launch_bounds__(256) fast_y_kernel(FrameSet frames, const uint
 }
 
 __global__ void __launch_bounds__(256) fast_uv_kernel(FrameSet frames, const uint2* __restrict__ ent,
-                                                      const uint32_t* __restrict__ runs, int W, int H, uint8_t* out,
+                                                      const uint2* __restrict__ runs, int W, int H, uint8_t* out,
                                                       int64_t out_pitch) {
     const int hw = W / 2, hh = H / 2;
     const int64_t npx = (int64_t)hw * hh;
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    uint32_t m = (uint32_t)uniform((int)runs[blockIdx.x]);
+    const uint2 rr = runs[blockIdx.x];
+    uint32_t m = (uint32_t)uniform((int)rr.x);
+    uint32_t blk = (uint32_t)uniform((int)rr.y);
     if (idx >= npx) return;
     uint32_t accV = 0, accU = 0;
     while (m) {
         const int c = __builtin_ctz(m);
         m &= m - 1;
-        const uint2 e = ent[(int64_t)c * npx + idx];
+        const uint2 e = ent[(int64_t)(blk++) * 256 + threadIdx.x];
         if ((e.y >> 16) == 0) continue;
         const SourceFrame& f = frames.f[c];
         const uint8_t* uv = f.yuv + (int64_t)f.h * f.pitch;  // interleaved U, V rows (NV12)
@@ -95,8 +102,8 @@ __global__ void __launch_bounds__(256) fast_uv_kernel(FrameSet frames, const uin
     o[1] = convert_out(accU);
 }
 
-hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint32_t* runs_y,
-                                  const uint2* ent_uv, const uint32_t* runs_uv, int W, int H, uint8_t* out,
+hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint2* runs_y,
+                                  const uint2* ent_uv, const uint2* runs_uv, int W, int H, uint8_t* out,
                                   int64_t out_pitch, hipStream_t s) {
     const int64_t ny = (int64_t)W * H, nuv = (int64_t)(W / 2) * (H / 2);
     hipLaunchKernelGGL(fast_y_kernel, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0, s, frames, ent_y, runs_y, W, H,

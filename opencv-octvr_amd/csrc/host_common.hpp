@@ -155,6 +155,7 @@ void mapper_out_size(const octvr_mapper* m, int* w, int* h);
 struct TileJob {
     int tx, ty;  // 128 x (8 qpl) item of the output (or level-0) grid
     int cam;     // RGBA mode: the camera whose pyramid image the tile is written to
+    uint32_t flags = 0;  // RGBA mode: per half kItemResult / kItemNoG0 (kernels.hpp)
 };
 // entry(job, x, y): the 8-byte CompositeEntry of grid pixel (x, y) for that job ({0,0} = black)
 using EntryFn = std::function<CompositeEntry(int job, int x, int y)>;
@@ -164,11 +165,13 @@ struct TiledLutBuild {
     std::vector<uint32_t> entries;
     std::vector<CompositeEntry> wide;
     std::vector<uint32_t> wide_tiles;
-    std::vector<uint8_t> wide_cams;
+    std::vector<uint8_t> wide_cams;  // camera | result << 5 | no-G0 << 6 (RGBA mode)
+    std::vector<uint8_t> item_flags;  // per staged item: its job's flags (RGBA mode)
     std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
     int qpl = 1;  // 128x8 halves per item (kernels.hpp TiledLut::qpl)
-    double staged_bytes = 0;
+    double staged_bytes = 0;  // YUV bytes staged, summed over items (boxes of neighbouring items overlap)
+    double source_bytes = 0;  // unique source bytes: the union of the staged boxes (+ wide tiles' taps)
     std::string stats;  // JSON fragment: staged items by staging chunks / LDS bytes, per-band chunk sums
 };
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
@@ -182,6 +185,9 @@ struct TiledLutDev {
     DevBuf<int32_t> bands;
     DevBuf<uint32_t> queue;
     double staged_bytes = 0;
+    double source_bytes = 0;
+    double g0_bytes = 0;      // RGBA mode: G0 bytes the items write (halves without kItemNoG0)
+    double result_bytes = 0;  // RGBA mode: result pixels the items write (kItemResult halves)
     std::string stats;
     TiledLut view{};
     void upload(const TiledLutBuild& b);

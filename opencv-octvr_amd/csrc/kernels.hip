@@ -1097,6 +1097,32 @@ struct RgbaSink {
     const MbCamLevel* cams;
 };
 
+// MODE 1: the deep tiles' result frame as an OutFrame from the level-0 grid origin (RgbaOut::res), in
+// the registers MODE 0's output frame takes
+__device__ __forceinline__ OutFrame make_result_frame(const RgbaOut& r) {
+    OutFrame o;
+    o.rsrc = __builtin_amdgcn_make_buffer_rsrc(r.res, 0, (int)r.res_bytes, 0x00020000);
+    o.pitch = r.res_pitch;
+    o.u_off = r.res_u_off;
+    o.v_off = r.res_v_off;
+    return o;
+}
+
+// A deep level-0 quad's final result straight from the remap (mb_blend level 0 for owned = 4: R = G0,
+// convertTo(CV_8UC3) into result(align_result_roi) and RGB -> YUV420P, or the RGBA result image of a
+// scaled output).  q holds the quad's four packed RGB pixels; (x, y): the quad on the level-0 grid.
+__device__ __forceinline__ void store_result(const OutFrame& o, bool rgba, const QuadOut& q, int x, int y, bool in) {
+    if (rgba) {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        const uint32_t off = in ? (uint32_t)y * o.pitch + (uint32_t)x * 4u : kDropOffset;
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{q.y01, q.y23}, o.rsrc, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{q.u, q.v}, o.rsrc, in ? off + o.pitch : kDropOffset, 0, 0);
+        return;
+    }
+    const uint32_t px[4] = {q.y01, q.y23, q.u, q.v};
+    store_quad(o, quad_yuv(px), x, y, in);
+}
+
 __device__ __forceinline__ void store_rgba(const RgbaSink& o, const QuadOut& q, uint32_t cam, int x, int y, bool in) {
     const MbCamLevel* c = o.cams + cam;
     const int xl = x - c->ox, yl = y - c->oy;
@@ -1115,6 +1141,20 @@ __device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro
         store_quad(of, q, x, y, in);
     else
         store_rgba(ro, q, cam, x, y, in);
+}
+
+// One half of an item: MODE 0 the YUV quad into `of`; MODE 1 the G0 quad unless the item's flags
+// (uniform, kItemNoG0) say nothing reads it, and the final result into `of` (the result frame) where they
+// say the tile is deep (kItemResult)
+template <int MODE>
+__device__ __forceinline__ void store_half(const OutFrame& of, const RgbaSink& ro, bool res_rgba, const QuadOut& q,
+                                           uint32_t cam, uint32_t flags, int h, int x, int y, bool in) {
+    if constexpr (MODE == 0) {
+        store_quad(of, q, x, y, in);
+    } else {
+        if (!((flags >> h) & kItemNoG0)) store_rgba(ro, q, cam, x, y, in);
+        if ((flags >> h) & kItemResult) store_result(of, res_rgba, q, x, y, in);
+    }
 }
 
 // MODE 2 output staging: one item's YUV420P output (Q halves of 128 x 8) in LDS as Y rows 0..8Q-1
@@ -1201,10 +1241,14 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         const_cast<TileHdr*>(lut.meta), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kMetaWords * 16)), 0x00020000);
     OutFrame of{};
     RgbaSink ro{};
-    if constexpr (SM == 0)
+    bool res_rgba = false;
+    if constexpr (SM == 0) {
         of = make_out_frame(out, W, H, out_pitch);
-    else
+    } else {
         ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
+        of = make_result_frame(rgba);
+        res_rgba = rgba.res_rgba != 0;
+    }
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
 #if OCTVR_STAMPS == 1
@@ -1261,7 +1305,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     const uint32_t lane_y = (uint32_t)(2 * qy) * of.pitch + (uint32_t)(2 * qx), lane_c = (uint32_t)qy * of.pitch + (uint32_t)qx;
     int pox = 0, poy = 0;  // the previous item's origin (uniform)
     bool pfull = false;    // the previous item lies wholly inside W x H (uniform)
-    uint32_t pcam = 0;
+    uint32_t pcam = 0, pfl = 0;  // the previous item's RGBA-mode camera and flags (kItemResult / kItemNoG0)
     bool pin = false;
     uint32_t par = 0, half = 0;  // iteration parity; LDS half of the next small item
     bool prev_big = true;
@@ -1389,7 +1433,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         } else if constexpr (!kStoreLate) {
 #pragma unroll
             for (int h = 0; h < QPL; h++)
-                store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+                store_half<SM>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
 #endif
 #if !OCTVR_ISSUE_EARLY
@@ -1532,6 +1576,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         poy = (int)(cur.tile >> 16) * kItemH;
         pfull = pox + kTileW <= W && poy + kItemH <= H;
         pcam = (cur.nslots >> 16) & 31u;
+        pfl = SM == 1 ? (cur.map >> 8) & 0xFFu : 0u;
         pin = x < W && y < H;
 #if !OCTVR_DIAG_NOSTORE
         if constexpr (kStoreLate && !kWideOut) {  // youngest ops of the iteration (see kStoreLate)
@@ -1571,7 +1616,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     } else if constexpr (!kStoreLate) {
 #pragma unroll
         for (int h = 0; h < QPL; h++)
-            store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+            store_half<SM>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
     }
 #if OCTVR_STAMPS == 1
     if (MODE != 1 && tid == 0 && blockIdx.x < kStampRows) {
@@ -1595,10 +1640,12 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
     __syncthreads();
     OutFrame of{};
     RgbaSink ro{};
-    if constexpr (MODE == 0)
+    if constexpr (MODE == 0) {
         of = make_out_frame(out, W, H, out_pitch);
-    else
+    } else {
         ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
+        of = make_result_frame(rgba);
+    }
     const uint32_t tile = (uint32_t)uniform((int)lut.wide_tiles[blockIdx.x]);
     const int x = (int)(tile & 0xFFFFu) * kTileW + (tid & 63) * 2, y = (int)(tile >> 16) * kTileH + (tid >> 6) * 2;
     const uint4* wp = reinterpret_cast<const uint4*>(lut.wide + (int64_t)blockIdx.x * kTilePx) + tid * 2;
@@ -1616,13 +1663,15 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
         float gp = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
         gain[p] = f32x2_t{gp, gp};
     }
-    const uint32_t cam = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;
+    const uint32_t camb = MODE == 1 ? (uint32_t)uniform((int)lut.wide_cams[blockIdx.x]) : 0u;
     float rgbf[4][3];
 #pragma unroll
     for (int p = 0; p < 4; p++)
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) rgbf[p][ch] = (float)rgb[p][ch];
-    store_any<MODE>(of, ro, finish_any<MODE>(rgbf, gain), cam, x, y, x < W && y < H);
+    // camera byte: camera | result << 5 | no-G0 << 6 (tiling.cpp), i.e. the item flags of half 0
+    const uint32_t fl = ((camb >> 5) & 1u ? kItemResult : 0u) | ((camb >> 6) & 1u ? kItemNoG0 : 0u);
+    store_half<MODE>(of, ro, rgba.res_rgba != 0, finish_any<MODE>(rgbf, gain), camb & 31u, fl, 0, x, y, x < W && y < H);
 }
 
 template <int MODE>

@@ -301,7 +301,21 @@ struct RgbaOut {
     uint8_t* base;
     uint32_t bytes;        // allocation size (< 2^31)
     const MbCamLevel* cams;
+    // Deep level-0 tiles (multi-band, owned = 4 on the host: the result there is exactly the owner
+    // camera's G0): items flagged kItemResult write their halves' final result from the remap itself,
+    // so the level-0 blend skips those tiles; items flagged kItemNoG0 write no G0 for that half (nothing
+    // reads it).  The result frame is addressed from the level-0 grid origin (align_result_roi's
+    // top-left): `res` points there, YUV420P with the U / V planes at res_u_off / res_v_off bytes
+    // (res_rgba = 0), or the RGBA result image of a scaled output (res_rgba = 1).  Flagged tiles lie
+    // wholly inside the crop and the frame (multiband_create), so the stores need no bounds.
+    uint8_t* res;
+    uint32_t res_bytes;    // addressable bytes from `res` (< 2^31)
+    uint32_t res_pitch, res_u_off, res_v_off;
+    int res_rgba;
 };
+// Per-item flags of the MODE-1 remap (bits 8-15 of the item header's device word 2, see TiledLutDev::upload;
+// bits 5 / 6 of a wide tile's camera byte): half h writes its result (1 << h), half h writes no G0 (16 << h).
+constexpr uint32_t kItemResult = 1u, kItemNoG0 = 16u;
 
 hipError_t launch_mb_remap(const FrameSet& frames, const TiledLut& lut, const double* gains, int use_gain,
                            const RgbaOut& out, hipStream_t s);
@@ -334,6 +348,7 @@ struct MbBlendArgs {
     int ax, ay, crop_w, crop_h;     // align_result_roi origin in the output frame, crop size
     uint8_t* rgba;                  // level 0, scaled output: the RGB result as RGBA (out_w x out_h) instead of YUV
     int64_t rgba_pitch;
+    // level 0, multi-band: owned = 4 marks deep tiles whose result the remap wrote (kItemResult)
 };
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s);
 // Build time: K4 pyrDown<float, BrdReflect101> with nvcc's FMA contraction (pyr_down.cu:55-192).

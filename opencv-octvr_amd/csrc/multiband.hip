@@ -361,6 +361,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     const int own = a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
     if (own == 3) return;  // no collapse reads this tile (levels >= 1)
     const bool deep = own == 2;
+    if (own == 4) return;  // level 0: a deep tile whose result the remap wrote (kItemResult)
     if (own != 0) {
         const int n = __builtin_ctz(m);
         const MbCamLevel c = a.cams[n];

@@ -80,6 +80,8 @@ class MultiBand {
     };
     std::vector<std::unique_ptr<FrameBufs>> extra;
     bool feather = false;  // FeatherGPUBlender instead of MultiBandGPUBlender
+    bool deep_in_remap = false;  // deep level-0 tiles are written by the remap (kItemResult, owned 4)
+    int n_result = 0;            // level-0 tiles the remap writes
     bool full_cover = true;
     int crop_w = 0, crop_h = 0;
 };
@@ -598,7 +600,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             for (int ty = 0; ty < Lf.ty_n; ty++)
                 for (int tx = 0; tx < Lf.tx_n; tx++) {
                     const uint8_t t = owned_h[l - 1][(size_t)ty * Lf.tx_n + tx];
-                    if (t == 2 || t == 3) continue;
+                    if (t >= 2) continue;  // deep (2, 4) or unread (3): no collapse reads level l there
                     int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
                     for (int q = ty * kTileH / 2; q < (ty + 1) * kTileH / 2; q++)
                         for (int j = 0; j < 3; j++)
@@ -621,8 +623,33 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         }
         for (int l = 0; l <= B; l++) M.lv[l].owned.upload(owned_h[l].data(), owned_h[l].size());
     }
+    // ---- deep level-0 tiles: the remap writes their result (kItemResult) ----------------------------
+    // A deep level-0 tile's result is its one camera's G0 (R = G, above), so the MODE-1 remap item of that
+    // camera converts it to YUV420P (or the RGBA result) right away and mb_blend skips the tile (owned 4):
+    // its G0 is then needed only where a level-1 pyrDown reads it.  Only tiles wholly inside the crop and
+    // the output frame qualify (the remap's result stores take no bounds).  (OCTVR_MB_NO_REMAP_RESULT=1:
+    // measurement / cross-check knob, the level-0 blend writes every tile.)
+    std::vector<int8_t> deep0_owner;  // per level-0 tile: the camera of a remap-result tile, else -1
+    if (!M.feather && deep_on && std::getenv("OCTVR_MB_NO_REMAP_RESULT") == nullptr) {
+        auto& L0 = M.lv[0];
+        deep0_owner.assign((size_t)L0.tx_n * L0.ty_n, (int8_t)-1);
+        for (int ty = 0; ty < L0.ty_n; ty++)
+            for (int tx = 0; tx < L0.tx_n; tx++) {
+                const size_t t = (size_t)ty * L0.tx_n + tx;
+                const int x1 = (tx + 1) * kTileW, y1 = (ty + 1) * kTileH;
+                if (owned_h[0][t] != 2 || x1 > M.crop_w || y1 > M.crop_h || M.arr.x + x1 > rig.out_w ||
+                    M.arr.y + y1 > rig.out_h)
+                    continue;
+                deep0_owner[t] = (int8_t)__builtin_ctz(L0.tile_cams_h[t]);
+                owned_h[0][t] = 4;
+                M.n_result++;
+            }
+        M.deep_in_remap = M.n_result > 0;
+        L0.owned.upload(owned_h[0].data(), owned_h[0].size());
+    }
     // ---- required 8x8 blocks per camera and level, then tiles ------------------------------------
     // need(l) = weight blocks(l) + pyrUp support of weight blocks(l-1) + pyrDown support of need(l+1)
+    // (level 0 with deep tiles written by the remap: their weight blocks need no G0)
     std::vector<std::vector<Bitmap>> req(B + 1, std::vector<Bitmap>(n));  // tiles
     std::vector<std::vector<uint8_t>> need_next(n);                       // blocks of level l + 1
     for (int l = B; l >= 0; l--) {
@@ -637,7 +664,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             };
             for (int by = 0; by < by_n; by++)  // blocks of unread tiles: no blend reads G there
                 for (int bx = 0; bx < bx_n; bx++)
-                    if (tile_of(l, bx, by) == 3) need[(size_t)by * bx_n + bx] = 0;
+                    if (tile_of(l, bx, by) == 3 || tile_of(l, bx, by) == 4) need[(size_t)by * bx_n + bx] = 0;
             auto mark = [&](int x0, int y0, int x1, int y1) {  // level-grid pixel rectangle, inclusive
                 x0 = std::max(x0, 0), y0 = std::max(y0, 0);
                 x1 = std::min(x1, bx_n * kBlk - 1), y1 = std::min(y1, by_n * kBlk - 1);
@@ -718,14 +745,23 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         auto& L0 = M.lv[0];
         // items of qpl vertically adjacent tiles (128 x 8 qpl), kept when any of them is required
         const int qpl = composite_qpl();
+        // per half: G0 written where required (else kItemNoG0), the result where the tile is deep and
+        // this camera owns it (kItemResult)
         std::vector<TileJob> jobs;
         for (int i = 0; i < n; i++)
             for (int ty = 0; ty < (L0.ty_n + qpl - 1) / qpl; ty++)
                 for (int tx = 0; tx < L0.tx_n; tx++) {
                     bool any = false;
-                    for (int h = 0; h < qpl && ty * qpl + h < L0.ty_n; h++)
-                        any |= req[0][i].b[(size_t)(ty * qpl + h) * L0.tx_n + tx] != 0;
-                    if (any) jobs.push_back(TileJob{tx, ty, i});
+                    uint32_t fl = 0;
+                    for (int h = 0; h < qpl; h++) {
+                        const size_t t = (size_t)(ty * qpl + h) * L0.tx_n + tx;
+                        const bool in = ty * qpl + h < L0.ty_n;
+                        const bool g0 = in && req[0][i].b[t] != 0;
+                        const bool res = in && !deep0_owner.empty() && deep0_owner[t] == i;
+                        any |= g0 || res;
+                        fl |= (g0 ? 0u : kItemNoG0 << h) | (res ? kItemResult << h : 0u);
+                    }
+                    if (any) jobs.push_back(TileJob{tx, ty, i, fl});
                 }
         const Rect arr = M.arr;
         auto entry = [&](int job, int x, int y) -> CompositeEntry {
@@ -774,11 +810,7 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
     auto& L0 = M.lv[0];
     TiledLut view = M.remap.view;
     if (fb) view.queue = fb->queue.p;
-    HIP_CHECK(launch_mb_remap(frames, view, gains_dev, use_gain, RgbaOut{G(0), (uint32_t)L0.g_bytes, L0.cams.p}, s));
-    for (int l = 1; l <= M.B; l++) {
-        auto& L = M.lv[l];
-        HIP_CHECK(launch_mb_down(L.down_items.p, L.n_down, L.cams.p, M.lv[l - 1].cams.p, G(l - 1), G(l), s));
-    }
+    // (first: the remap writes the deep tiles' results into the output)
     if (!M.full_cover) {  // result pixels outside the blended ROI stay 0 (mapper.cpp:155): Y 0, U = V = 128
         if (rgba) {
             HIP_CHECK(hipMemset2DAsync(rgba, rgba_pitch, 0, (size_t)M.out_w * 4, M.out_h, s));
@@ -786,6 +818,36 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
             HIP_CHECK(hipMemset2DAsync(out, out_pitch, 0, M.out_w, M.out_h, s));
             HIP_CHECK(hipMemset2DAsync(out + (int64_t)M.out_h * out_pitch, out_pitch, 128, M.out_w, M.out_h / 2, s));
         }
+    }
+    RgbaOut ro{};
+    ro.base = G(0);
+    ro.bytes = (uint32_t)L0.g_bytes;
+    ro.cams = L0.cams.p;
+    if (M.deep_in_remap) {  // the result frame from the level-0 grid origin (align_result_roi's top-left)
+        if (rgba) {
+            const int64_t o = (int64_t)M.arr.y * rgba_pitch + (int64_t)M.arr.x * 4;
+            const int64_t total = rgba_pitch * M.out_h;
+            REQUIRE(total < ((int64_t)1 << 31) - 64 && rgba_pitch < ((int64_t)1 << 31), "result image exceeds 2 GiB");
+            ro.res = rgba + o;
+            ro.res_bytes = (uint32_t)(total - o);
+            ro.res_pitch = (uint32_t)rgba_pitch;
+            ro.res_rgba = 1;
+        } else {
+            const int64_t o = (int64_t)M.arr.y * out_pitch + M.arr.x;
+            const int64_t total = out_pitch * (M.out_h + M.out_h / 2);
+            REQUIRE(total < ((int64_t)1 << 31) - 64, "output frame exceeds 2 GiB");
+            const int64_t u = (int64_t)M.out_h * out_pitch + (int64_t)(M.arr.y / 2) * out_pitch + M.arr.x / 2;
+            ro.res = out + o;
+            ro.res_bytes = (uint32_t)(total - o);
+            ro.res_pitch = (uint32_t)out_pitch;
+            ro.res_u_off = (uint32_t)(u - o);
+            ro.res_v_off = (uint32_t)(u - o + M.out_w / 2);
+        }
+    }
+    HIP_CHECK(launch_mb_remap(frames, view, gains_dev, use_gain, ro, s));
+    for (int l = 1; l <= M.B; l++) {
+        auto& L = M.lv[l];
+        HIP_CHECK(launch_mb_down(L.down_items.p, L.n_down, L.cams.p, M.lv[l - 1].cams.p, G(l - 1), G(l), s));
     }
     for (int l = M.B; l >= 0; l--) {
         auto& L = M.lv[l];
@@ -833,22 +895,61 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
     }
 }
 
-double multiband_traffic(const MultiBand& M) {
-    // remap: tiled entries + level-0 pyramid writes; pyrDown: source reads + writes; blend: per
-    // (camera, pixel) of every weight tile G + weight + 9/4 coarser taps, R reads/writes, output
-    const auto& L0 = M.lv[0];
+// Algorithmic bytes per frame, per launch of the sequence: what each launch must move, every byte
+// counted once per launch that needs it (re-reads of a neighbour's halo from L2 are not counted).
+//   remap:   4 B tiled entry per item pixel (8 B wide), the G0 halves it writes (4 B / px), the deep
+//            tiles' results (1.5 B / px YUV420P), the unique source bytes of its staged boxes, metadata;
+//   down l:  4 B written per level-l item pixel, its 2 x 2 level-(l-1) source (16 B / px);
+//   blend l: per tile by kind — unread (owned 3): nothing; deep (2): G 4 B + R 8 B (level 0: nothing
+//            when the remap wrote it, else 1.5 B out); owned (1): G 4 B + coarser G taps 1 B + collapsed
+//            coarser level 2 B + R 8 B / out 1.5 B; general: per weighted camera G 4 B + weight (1 B u8
+//            seam at level 0, else 4 B f32) + coarser G 1 B, then coarser R 2 B + R 8 B / out 1.5 B.
+std::vector<std::pair<std::string, double>> multiband_traffic_parts(const MultiBand& M) {
+    std::vector<std::pair<std::string, double>> parts;
     const TiledLut& t = M.remap.view;
-    double b = (4.0 + 4.0) * t.n_items * kTilePx * t.qpl + (8.0 + 4.0) * t.n_wide * kTilePx;
-    for (int l = 1; l <= M.B; l++) b += (double)M.lv[l].n_down * kTilePx * (16.0 + 4.0);
-    for (int l = 0; l <= M.B; l++) {
+    const TiledLutDev& r = M.remap;
+    parts.emplace_back("remap", 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + r.g0_bytes +
+                                    1.5 * r.result_bytes + r.source_bytes +
+                                    (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)));
+    for (int l = 1; l <= M.B; l++) parts.emplace_back("down" + std::to_string(l), (double)M.lv[l].n_down * kTilePx * (16.0 + 4.0));
+    for (int l = M.B; l >= 0; l--) {
         const auto& L = M.lv[l];
-        size_t cam_tiles = 0;
-        for (uint32_t m : L.tile_cams_h) cam_tiles += (size_t)__builtin_popcount(m);
-        b += (double)cam_tiles * kTilePx * (4.0 + (l ? 4.0 : 1.0) + (l < M.B ? 1.0 : 0.0));
-        if (l > 0) b += 8.0 * L.W * L.H * 1.25;  // R written, read back by the finer level's pyrUp
+        const bool up = l < M.B;
+        const double out_b = l ? 8.0 : 1.5;
+        std::vector<uint8_t> own;
+        if (L.owned.p) {
+            own.resize(L.owned.n);
+            HIP_CHECK(hipMemcpy(own.data(), L.owned.p, own.size(), hipMemcpyDeviceToHost));
+        }
+        double b = 0;
+        for (size_t k = 0; k < L.tile_cams_h.size(); k++) {
+            const uint32_t m = L.tile_cams_h[k];
+            const int o = own.empty() ? 0 : own[k];
+            double px_b = 0;
+            if (o == 3) {
+                px_b = 0;
+            } else if (o == 4) {
+                px_b = 0;  // level 0: the remap wrote the result
+            } else if (o == 2) {
+                px_b = 4.0 + out_b;
+            } else if (o == 1) {
+                px_b = 4.0 + (up ? 1.0 + 2.0 : 0.0) + out_b;
+            } else if (m) {
+                px_b = __builtin_popcount(m) * (4.0 + ((l == 0 && !M.feather) ? 1.0 : 4.0) + (up ? 1.0 : 0.0)) +
+                       (up ? 2.0 : 0.0) + out_b;
+            } else {
+                px_b = (up ? 2.0 : 0.0) + out_b;  // no camera: the collapse alone
+            }
+            b += px_b * kTilePx;
+        }
+        parts.emplace_back("blend" + std::to_string(l), b);
     }
-    b += 1.5 * M.out_w * M.out_h;
-    (void)L0;
+    return parts;
+}
+
+double multiband_traffic(const MultiBand& M) {
+    double b = 0;
+    for (const auto& p : multiband_traffic_parts(M)) b += p.second;
     return b;
 }
 
@@ -856,7 +957,18 @@ std::string multiband_info(const MultiBand& M) {
     std::string s = std::string(M.feather ? "\"feather\": 1, " : "") + "\"bands\": " + std::to_string(M.B) + ", \"align_result_roi\": [" + std::to_string(M.arr.x) + ", " +
                     std::to_string(M.arr.y) + ", " + std::to_string(M.arr.w) + ", " + std::to_string(M.arr.h) +
                     "], \"remap_items\": " + std::to_string(M.remap.view.n_items) +
-                    ", \"remap_wide\": " + std::to_string(M.remap.view.n_wide) + ", \"level_tiles\": [";
+                    ", \"remap_wide\": " + std::to_string(M.remap.view.n_wide) +
+                    ", \"remap_result_tiles\": " + std::to_string(M.n_result) + ", \"traffic_parts\": {";
+    {
+        bool first = true;
+        for (const auto& p : multiband_traffic_parts(M)) {
+            char buf[96];
+            snprintf(buf, sizeof buf, "%s\"%s\": %.0f", first ? "" : ", ", p.first.c_str(), p.second);
+            s += buf;
+            first = false;
+        }
+    }
+    s += "}, \"level_tiles\": [";
     for (int l = 0; l <= M.B; l++) {
         const auto& L = M.lv[l];
         size_t cam_tiles = 0;

@@ -1741,18 +1741,17 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
     return guarded([&] {
         REQUIRE(m && bytes, "NULL argument");
         // composite kernel: 4 B tiled-LUT entry (8 B in wide tiles) + 1.5 B YUV420 output per output
-        // pixel, every source frame read once (1.5 B per input pixel), tile headers/slots
+        // pixel, the unique source bytes its staged boxes cover (YUV420P, 1.5 B per luma pixel: the
+        // circular crops leave the rest of each frame unread), tile headers / slots.  Multi-band: the
+        // sum over the sequence's launches (multiband_traffic_parts).
         if (m->mb) {
-            double b = multiband_traffic(*m->mb);
-            for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
-            *bytes = b;
+            *bytes = multiband_traffic(*m->mb);
             return;
         }
         const TiledLut& t = m->tiles.view;
-        double b = 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
-                   (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide;
-        for (int i = 0; i < m->n; i++) b += 1.5 * m->in_w[i] * m->in_h[i];
-        *bytes = b;
+        *bytes = 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
+                 (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide +
+                 m->tiles.source_bytes;
     });
 }
 
@@ -1846,10 +1845,10 @@ int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
         char tmp[512];
         snprintf(tmp, sizeof tmp,
                  "{\"inputs\": %d, \"out\": [%d, %d], \"blend\": %d, \"tiles\": %d, \"wide_tiles\": %d, "
-                 "\"staged_bytes\": %.0f, \"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, "
+                 "\"staged_bytes\": %.0f, \"source_bytes\": %.0f, \"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, "
                  "\"gain_chunks\": %d, \"scaled_out\": [%d, %d]",
                  m->n, m->W, m->H, m->blend, m->n_tiles, m->tiles.view.n_wide,
-                 m->mb ? 0.0 : m->tiles.staged_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks, m->SW, m->SH);
+                 m->mb ? 0.0 : m->tiles.staged_bytes, m->mb ? 0.0 : m->tiles.source_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks, m->SW, m->SH);
         std::string js = tmp;
         if (m->mb) js += ", " + multiband_info(*m->mb);
         else if (!m->tiles.stats.empty()) js += ", " + m->tiles.stats;

@@ -162,7 +162,8 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             const TileJob& J = jobs[t];
             for (int h = 0; h < qpl; h++) {
                 b.wide_tiles.push_back((uint32_t)J.tx | ((uint32_t)(J.ty * qpl + h) << 16));
-                b.wide_cams.push_back((uint8_t)J.cam);
+                b.wide_cams.push_back((uint8_t)(J.cam | ((J.flags >> h) & kItemResult ? 32 : 0) |
+                                                 ((J.flags >> h) & kItemNoG0 ? 64 : 0)));
                 b.wide.insert(b.wide.end(), wide_raw[t].begin() + (size_t)h * kTilePx,
                               wide_raw[t].begin() + (size_t)(h + 1) * kTilePx);
             }
@@ -176,10 +177,41 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                       b.entries.begin() + (size_t)n_items * item_px);
         }
         b.staged_bytes += 8.0 * b.hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes per 4-pixel group
+        b.item_flags.push_back((uint8_t)jobs[t].flags);
         n_items++;
     }
     b.n_items = n_items;
     b.n_wide = (int)b.wide_tiles.size();
+    {  // unique source bytes the launch reads: the union over items of each camera's staged boxes (8 x 2
+       // luma cells, 1.5 B per luma pixel of YUV420P), plus the wide tiles' tap cells
+        const int nc = (int)in_w.size();
+        std::vector<std::vector<uint8_t>> cell(nc);
+        std::vector<int> cw(nc);
+        for (int c = 0; c < nc; c++) {
+            cw[c] = (in_w[c] + 7) / 8;
+            cell[c].assign((size_t)cw[c] * ((in_h[c] + 1) / 2), 0);
+        }
+        auto mark = [&](int c, int x, int y) {
+            if (c < 0 || c >= nc || x < 0 || y < 0 || x >= in_w[c] || y >= in_h[c]) return;
+            cell[c][(size_t)(y / 2) * cw[c] + x / 8] = 1;
+        };
+        for (int t = 0; t < n_items; t++)
+            for (int j = 0; j < (int)(b.hdr[t].nslots & 0xFFu); j++) {
+                const TileSlot& sl = b.slots[(size_t)t * kTileSlots + j];
+                for (int y = sl.by0; y < sl.by0 + sl.bh; y += 2)
+                    for (int x = sl.bx0; x < sl.bx0 + sl.bw; x += 8) mark(sl.cam, x, y);
+            }
+        for (const CompositeEntry& e : b.wide) {
+            if (!(e.code & 0x8000u)) continue;
+            const int c = (int)((e.code >> 10) & 31u);
+            const int sx = (int)(int16_t)(e.xy & 0xFFFFu), sy = (int)(int16_t)(e.xy >> 16);
+            for (int k = 0; k < 4; k++) mark(c, sx + (k & 1), sy + (k >> 1));
+        }
+        double cells = 0;
+        for (auto& v : cell)
+            for (uint8_t x : v) cells += x;
+        b.source_bytes = cells * 16 * 1.5;
+    }
     {  // cost-balanced XCD bands over the staged items
         std::vector<double> cum(n_items + 1, 0.0);
         for (int t = 0; t < n_items; t++) {
@@ -250,6 +282,7 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
             for (int j = 1; j < kTileSlots; j++) q += (j < ns && c >= (int)b.slots[t * kTileSlots + j].chunk0) ? 1 : 0;
             map |= (uint32_t)q << (2 * c);
         }
+        if (t < b.item_flags.size()) map |= (uint32_t)b.item_flags[t] << 8;  // RGBA mode: kItemResult / kItemNoG0
         m[t * kMetaWords].stage_groups = map;
         std::memcpy(&m[t * kMetaWords + 1], &b.slots[t * kTileSlots], kTileSlots * sizeof(TileSlot));
     }
@@ -264,6 +297,20 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     queue.alloc((size_t)(kStitchBands + 1) * kQueueStride);
     HIP_CHECK(hipMemset(queue.p, 0, queue.n * sizeof(uint32_t)));
     staged_bytes = b.staged_bytes;
+    source_bytes = b.source_bytes;
+    result_bytes = 0;
+    g0_bytes = 0;
+    for (size_t t = 0; t < b.item_flags.size(); t++)
+        for (int h = 0; h < b.qpl; h++) {
+            const uint32_t f = (uint32_t)b.item_flags[t] >> h;
+            g0_bytes += (f & kItemNoG0) ? 0.0 : 4.0 * kTilePx;
+            result_bytes += (f & kItemResult) ? 1.0 * kTilePx : 0.0;  // result pixels (bytes: x 1.5 or 4)
+        }
+    for (uint8_t c : b.wide_cams) {
+        g0_bytes += (c & 64) ? 0.0 : 4.0 * kTilePx;
+        result_bytes += (c & 32) ? 1.0 * kTilePx : 0.0;
+    }
+    if (b.item_flags.empty()) g0_bytes = 4.0 * kTilePx * ((double)b.n_items * b.qpl + b.n_wide);  // no flags: every half
     stats = b.stats;
     view = TiledLut{meta.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
                     b.qpl};

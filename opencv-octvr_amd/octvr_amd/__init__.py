@@ -80,6 +80,7 @@ _lib.octvr_mapper_kernel_busy.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(
 _lib.octvr_rig_lut_recomputed.argtypes = [_VP, C.c_int, C.POINTER(C.c_uint64)]
 _lib.octvr_debug_project_f64.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP, _VP]
 _lib.octvr_interval_union.argtypes = [_VP, _VP, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+_lib.octvr_fastmapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
 _lib.octvr_mapper_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
 _lib.octvr_mapper_destroy.argtypes = [_VP]
 _lib.octvr_mapper_destroy.restype = None
@@ -366,6 +367,12 @@ class FastMapper:
         self._h = hd
         self.n = n
         self.out_size = mt.out_size
+
+    def traffic_bytes(self):
+        """Algorithmic bytes of one stitch_nv12 (octvr_fastmapper_traffic)."""
+        b = C.c_double()
+        _check(_lib.octvr_fastmapper_traffic(self._h, C.byref(b)))
+        return b.value
 
     def stitch_nv12(self, inputs, output, stream=None):
         """inputs: uint8 cuda tensors (1.5H x W NV12); output: 1.5H x W (chroma rows V,U)."""

@@ -36,8 +36,16 @@ CONFIGS = {
 }
 
 
+# F2: the C2 rig through vr::FastMapper::stitch_nv12 (feather-weighted NV12, template without ROI as
+# octvr_dump -n writes it; mapper_fast.cpp:27-195) — the second drop-in entry point, not a BASELINE config
+CONFIGS["F2"] = CONFIGS["C2"]
+
 # Mapper blend mode per configuration (mapper.cpp:171-184: 0 copy chain, > 0 multi-band)
-BLEND = {"C1": 0, "C2": 0, "C3": 16, "C4": 0}
+BLEND = {"C1": 0, "C2": 0, "C3": 16, "C4": 0, "F2": 0}
+
+# Gain compensation per configuration: C1 is the reference's CPU plumbing case (BASELINE configs[0]:
+# cv::remap + the seam-mask copy, no gain; SURVEY.md §6 measured it at 192-204 MP/s on 8 threads)
+GAIN = {"C1": False, "C2": True, "C3": True, "C4": True, "F2": False}
 
 
 def splitmix_bytes(seed, n):

@@ -2,6 +2,7 @@
 (BASELINE.json configs[1..3]): the rig built by the GPU LUT build, three frames in
 flight on three streams (the lean gain feed), gains estimated per frame — every output byte and the
 gains against the oracle, which builds its own LUT (threads) and stitches each frame independently.
+  C1: 2 x 1920x1080 fullframe_fisheye (yaw 0 / pi) -> 4096x2048, no blend (the reference's CPU plumbing case)
   C2: 6 x 3840x2160 fullframe_fisheye -> 7680x3840, no blend (copy chain)
   C3: C2 + multi-band blend = 16 (3 bands), seams from create_masks
   C4: 12 x 3840x2160 (pitch +-35 deg, hfov 150 deg) -> 15360x7680, no blend
@@ -33,7 +34,7 @@ def _frames(sizes, seed):
     return out
 
 
-@pytest.mark.parametrize("cfg", ["C2", "C3", "C4"])
+@pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4"])
 def test_gpu_fullsize_bit_exact(product_lib, cfg):
     import torch
     from octvr_amd import synthetic
@@ -93,10 +94,13 @@ def test_gpu_fullsize_bit_exact(product_lib, cfg):
         np.testing.assert_array_equal(np.array(m.gains()), np.array(g_orc))
 
 
-def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch):
-    """C3 at full size: the deep tiles' R = G shortcut (multiband_host.cpp) against the same mapper with it
-    off (OCTVR_MB_NO_DEEP, every owned tile through both pyrUps), on noise frames (every level's
-    Laplacian non-zero): bit-identical output."""
+@pytest.mark.parametrize("scale", [None, (3840, 1920)])
+def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch, scale):
+    """C3 at full size, on noise frames (every level's Laplacian non-zero), three builds of the same
+    mapper, bit-identical: the default (deep tiles' R = G, the deep level-0 tiles' result written by the
+    remap itself: kItemResult / owned 4, multiband_host.cpp), the result left to the level-0 blend
+    (OCTVR_MB_NO_REMAP_RESULT), and no deep shortcut at all (OCTVR_MB_NO_DEEP: every owned tile through
+    both pyrUps).  With a scaled output the remap writes the RGBA result image instead of YUV420P."""
     import torch
     from octvr_amd import synthetic
     ox = product_lib
@@ -105,19 +109,26 @@ def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch):
     mt.create_masks(0)
     rng = np.random.default_rng(11)
     frames = [torch.from_numpy(rng.integers(0, 256, size=(h * 3 // 2, w), dtype=np.uint8)).cuda() for w, h in sizes]
-    outs = []
-    deep = []
-    for off in (False, True):
-        if off:
-            monkeypatch.setenv("OCTVR_MB_NO_DEEP", "1")
-        m = ox.Mapper(mt, sizes, blend=synthetic.BLEND["C3"], enable_gain=True)
-        deep.append([t["deep_tiles"] for t in m.info()["level_tiles"]])
-        out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    OW, OH = scale or (W, H)
+    outs, deep, res = [], [], []
+    for knob in (None, "OCTVR_MB_NO_REMAP_RESULT", "OCTVR_MB_NO_DEEP"):
+        if knob:
+            monkeypatch.setenv(knob, "1")
+        m = ox.Mapper(mt, sizes, blend=synthetic.BLEND["C3"], enable_gain=True, scale_output=scale)
+        info = m.info()
+        deep.append([t["deep_tiles"] for t in info["level_tiles"]])
+        res.append(info["remap_result_tiles"])
+        out = torch.zeros((OH * 3 // 2, OW), dtype=torch.uint8, device="cuda")
         m.stitch(frames, out, gains=[1.0] * len(sizes))
         torch.cuda.synchronize()
         outs.append(out.cpu().numpy())
         del m
-    print(deep)
-    assert deep[0][0] > 0 and sum(deep[1]) == 0
-    d = outs[0] != outs[1]
-    assert not d.any(), (int(d.sum()), np.argwhere(d)[:4].tolist())
+        if knob:
+            monkeypatch.delenv(knob)
+    print(deep, res)
+    assert deep[0][0] > 0 and res[0] > 0.7 * 28800  # C3: 23,040 deep level-0 tiles of 28,800
+    assert res[1] == 0 and deep[1][0] == deep[0][0]
+    assert sum(deep[2]) == 0 and res[2] == 0
+    for k in (1, 2):
+        d = outs[0] != outs[k]
+        assert not d.any(), (k, int(d.sum()), np.argwhere(d)[:4].tolist())
