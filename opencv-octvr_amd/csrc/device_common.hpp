@@ -137,6 +137,33 @@ __device__ __forceinline__ void bilerp_rgba_f(uint32_t c00, uint32_t c01, uint32
     }
 }
 
+// bilerp_rgba_f's weight pairs of fraction code fxy = fx | fy << 5: w.x = {W00, W01}, w.y = {W10, W11}
+// at scale 2^16 (code 0's W00 saturated to 65,535).  The composite keeps all 1,024 in an LDS table.
+__device__ __forceinline__ uint2 bilerp_weights(uint32_t fxy) {
+    const uint32_t fx = fxy & 31u, fy = fxy >> 5;
+    const uint32_t X = __umul24(fx, 0x3FFFC0u) + 2048u;
+    const u16x2_t Xv = __builtin_bit_cast(u16x2_t, X);
+    const unsigned short gy = (unsigned short)(31u - fy);
+    const u16x2_t w0 = __builtin_elementwise_add_sat(Xv * u16x2_t{gy, gy}, Xv);
+    const u16x2_t w1 = Xv * u16x2_t{(unsigned short)fy, (unsigned short)fy};
+    return uint2{__builtin_bit_cast(uint32_t, w0), __builtin_bit_cast(uint32_t, w1)};
+}
+
+// bilerp_rgba_f with the weight pairs given (from the LDS table): perm, perm, dot2, dot2, cvt per channel
+__device__ __forceinline__ void bilerp_rgba_w(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint2 w,
+                                              float (&rgb)[3]) {
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const uint32_t sel = 0x0C000C00u | ((4u + ch) << 16) | (uint32_t)ch;  // {lo.ch, 0, hi.ch, 0}
+        const u16x2_t top = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c01, c00, sel));
+        const u16x2_t bot = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c11, c10, sel));
+        const uint32_t S = __builtin_amdgcn_udot2(
+            bot, __builtin_bit_cast(u16x2_t, w.y),
+            __builtin_amdgcn_udot2(top, __builtin_bit_cast(u16x2_t, w.x), 32768u, false), false);
+        rgb[ch] = (float)((S >> 16) & 255u);
+    }
+}
+
 // Direct (global-memory) bilinear sample of one camera at an 8-byte composite entry — the gain feed
 // samples and "wide" tiles.  Every load is issued unconditionally from a clamped in-image address;
 // taps outside the image and invalid entries are zeroed afterwards.

@@ -943,6 +943,11 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #ifndef OCTVR_STITCH_SGPRS
 #define OCTVR_STITCH_SGPRS (kStitchRegBlocks >= 8 ? 80 : kStitchRegBlocks == 7 ? 96 : 102)
 #endif
+// The VGPR budget of that many waves per SIMD, set explicitly: with the weight table the compiler's
+// LDS occupancy model (24 KiB per workgroup) would otherwise relax it to 5 waves' 102 VGPRs
+#ifndef OCTVR_STITCH_VGPRS
+#define OCTVR_STITCH_VGPRS (kStitchRegBlocks >= 8 ? 64 : kStitchRegBlocks == 7 ? 72 : kStitchRegBlocks == 6 ? 80 : 96)
+#endif
 #ifndef OCTVR_STAGE_REGS
 #define OCTVR_STAGE_REGS 1
 #endif
@@ -1203,21 +1208,57 @@ __device__ __forceinline__ void store_item_wide(const OutFrame& o, const uint32_
     __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, o.rsrc, off, 0, OCTVR_OUT_POLICY);
 }
 
+// The composite's static LDS, one variable (so its size, a multiple of 16, is what the dynamic
+// region's base follows).  OCTVR_WTAB's weight table is the dynamic region (kWtabBytes at launch):
+// kept out of the static size, the compiler's LDS occupancy model still allows 7 workgroups per CU
+// and keeps the 7-wave register budget (72 VGPRs: the lean feed's wave fits beside 6 composite
+// waves per SIMD); the table's base is one add per pixel.
+template <int MODE, int QPL>
+struct alignas(16) StitchLds {
+    uint32_t rgb[kTileLdsBytes / 4];  // the item's staged RGBA boxes (LDS address 0)
+    float gain[kMaxCams];
+    f32x2_t slot_gain[OCTVR_LDS_DB ? 2 : 1][kTileSlots];
+    uint32_t claim[2];
+    uint32_t out[MODE == 2 ? QPL * kTileOutBytes / 4 : 2];
+};
+static_assert(sizeof(StitchLds<0, 2>) % 16 == 0 && sizeof(StitchLds<2, 1>) % 16 == 0, "dynamic LDS base alignment");
+static_assert(!OCTVR_WTAB || (sizeof(StitchLds<0, 2>) == 0x4000 && sizeof(StitchLds<1, 2>) == 0x4000),
+              "the weight table at LDS 0x4000 (tiled_wtab_addr)");
+
+// LDS byte address of a tiled entry's weight pairs.  With the table at 0x4000 (the kernel's static LDS
+// is exactly 16 KiB: launch_stitch checks the compiled size) one v_and_or_b32 forms it; an address
+// built from an integer, so the compiler does not split off a base it cannot fold into the offset.
+template <int MODE, int QPL>
+__device__ __forceinline__ uint2 wtab_read(const uint2* s_wtab, uint32_t e) {
+    typedef __attribute__((address_space(3))) const uint64_t lds_u64;
+    if constexpr (sizeof(StitchLds<MODE, QPL>) == 0x4000) {
+        const uint64_t w = *(const lds_u64*)(uintptr_t)((e & 0x1FF8u) | 0x4000u);
+        return uint2{(uint32_t)w, (uint32_t)(w >> 32)};
+    } else
+        return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(s_wtab) + (e & 0x1FF8u));
+}
+
+// LDS byte offset of a tiled entry's tap (x, y) (kernels.hpp, entry layout): one v_bfe_u32 / v_and_b32
+__device__ __forceinline__ uint32_t tap_off(uint32_t e) { return OCTVR_WTAB ? (e >> 13) & 0x3FFFu : e & 0x7FFFu; }
+
 // Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
 template <bool DWORD_STAGE, int MODE, bool VIG, int QPL>
-__global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
+__global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS)))
+__attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                               const double* gains, int use_gain, uint8_t* out,
                                                               int64_t out_pitch, RgbaOut rgba) {
-    __shared__ __attribute__((aligned(16))) uint32_t s_rgb[kTileLdsBytes / 4];
-    __shared__ float s_gain[kMaxCams];
-    // per iteration parity: written before an item's staging barrier, read after it (the next write
-    // to the same entry is two items later, behind the next barrier)
+    __shared__ __attribute__((aligned(16))) StitchLds<MODE, QPL> L;
+    extern __shared__ __attribute__((aligned(16))) uint2 s_wtab[];  // OCTVR_WTAB: 1,024 weight pairs
+    uint32_t* const s_rgb = L.rgb;
+    float* const s_gain = L.gain;
     // {g, g} per slot (finish_quad2f).  Written after an item's first barrier and read after its
     // second; the next write comes after the next item's first barrier, i.e. after every wave's last
     // read, so one table suffices (two, by iteration parity, when OCTVR_LDS_DB may skip that barrier).
-    __shared__ f32x2_t s_slot_gain[kGainTables][kTileSlots];
-    __shared__ uint32_t s_claim[2];
+    auto& s_slot_gain = L.slot_gain;
+    // per iteration parity: written before an item's staging barrier, read after it (the next write
+    // to the same entry is two items later, behind the next barrier)
+    uint32_t* const s_claim = L.claim;
     // MODE 2: the previous item's YUV420P output, staged in LDS and written with one 16-byte store
     // per lane (store_item_wide) instead of four 1-2-byte stores per quad
     constexpr bool kWideOut = MODE == 2;
@@ -1225,7 +1266,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
     // loads (so waiting for those loads need not drain the stores); else at the next iteration's top
     constexpr bool kStoreLate = OCTVR_STORE_LATE != 0;
     constexpr int SM = MODE == 1 ? 1 : 0;  // sink: YUV (finish_quad) or RGBA
-    __shared__ __attribute__((aligned(16))) uint32_t s_out[kWideOut ? QPL * kTileOutBytes / 4 : 1];
+    uint32_t* const s_out = L.out;
     constexpr int R = QPL == 1 ? kStageRegs : OCTVR_STAGE_REGS2;  // staging chunks prefetched per wave
     static_assert(QPL == 1 || QPL == 2 || QPL == 4, "items of 1, 2 or 4 halves");
     constexpr int kItemH = kTileH * QPL;
@@ -1258,6 +1299,10 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 
     if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
     if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
+    if constexpr (OCTVR_WTAB) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) s_wtab[tid + 256 * k] = bilerp_weights((uint32_t)(tid + 256 * k));
+    }
     // Item sequence of this workgroup: its first three items are static (t0, t0 + step, t0 + 2 step,
     // i.e. the band's first 3 * step items dealt round-robin), every later one is claimed from the
     // band's work counter (one returning atomic per item, issued one iteration before the item's
@@ -1463,7 +1508,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
         uint32_t t00[4], t01[4], t10[4], t11[4];
 #pragma unroll
         for (int p = 0; p < 4; p++) {
-            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + (ent[p] & 0x7FFFu);
+            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + tap_off(ent[p]);
             const uint8_t* r1 = r0 + 4u * S;
             t00[p] = reinterpret_cast<const uint32_t*>(r0)[0];
             t01[p] = reinterpret_cast<const uint32_t*>(r0)[1];
@@ -1478,7 +1523,7 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
             const uint32_t c00 = t00[p], c01 = t01[p], c10 = t10[p], c11 = t11[p];
 #else
             // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
-            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + (e & 0x7FFFu);
+            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + tap_off(e);
             const uint8_t* r1 = r0 + 4u * S;
             const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
             const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
@@ -1488,6 +1533,9 @@ __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_n
 #if OCTVR_DIAG_NOTAPS
             (void)c00; (void)c01; (void)c10; (void)c11;
             rgb[p][0] = (float)(e & 255u); rgb[p][1] = (float)((e >> 8) & 255u); rgb[p][2] = (float)((e >> 16) & 255u);
+#elif OCTVR_WTAB
+            bilerp_rgba_w(c00, c01, c10, c11,
+                          wtab_read<MODE, QPL>(s_wtab, e), rgb[p]);
 #else
             bilerp_rgba_f(c00, c01, c10, c11, e, rgb[p]);
 #endif
@@ -1674,6 +1722,16 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
     store_half<MODE>(of, ro, rgba.res_rgba != 0, finish_any<MODE>(rgbf, gain), camb & 31u, fl, 0, x, y, x < W && y < H);
 }
 
+// The weight table's address (wtab_read) assumes the dynamic LDS starts right after StitchLds: checked
+// once per kernel instance against the compiled static LDS size.
+template <bool DW, int MODE, bool V, int Q>
+static hipError_t stitch_lds_check() {
+    hipFuncAttributes a;
+    const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V, Q>));
+    if (e != hipSuccess) return e;
+    return a.sharedSizeBytes == sizeof(StitchLds<MODE, Q>) ? hipSuccess : hipErrorInvalidKernelFile;
+}
+
 template <int MODE>
 static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                                    int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
@@ -1705,34 +1763,42 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
 #define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
     do {                                                                                                       \
         if (lut.qpl == 2 && wide_out)                                                                          \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, W, \
-                               H, gains, use_gain, out, out_pitch, rgba);                                      \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, 2, V, 2>(); if (lds_ok_) return lds_ok_; \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W, \
+                               H, gains, use_gain, out, out_pitch, rgba); }                                      \
         else if (lut.qpl == 2)                                                                                 \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 2>(); if (lds_ok_) return lds_ok_; \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
         else if (wide_out)                                                                                     \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 1>), dim3(blocks), dim3(256), 0, s, frames, lut, W, \
-                               H, gains, use_gain, out, out_pitch, rgba);                                      \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, 2, V, 1>(); if (lds_ok_) return lds_ok_; \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 1>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W, \
+                               H, gains, use_gain, out, out_pitch, rgba); }                                      \
         else                                                                                                   \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), 0, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 1>(); if (lds_ok_) return lds_ok_; \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
     } while (0)
 #else
 #define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
     do {                                                                                                       \
         (void)wide_out;                                                                                        \
         if (OCTVR_QPL == 4 && lut.qpl == 4)                                                                    \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, OCTVR_QPL == 4 ? 4 : 1>(); if (lds_ok_) return lds_ok_; \
             hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, OCTVR_QPL == 4 ? 4 : 1>), dim3(blocks), dim3(256), \
-                               0, s, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);                \
+                               kWtabBytes, s, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba); }                \
         else if (lut.qpl == 2 && ext_ev)                                                                       \
-            hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, ev0, ev1, \
-                                  0, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);                \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 2>(); if (lds_ok_) return lds_ok_; \
+            hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, ev0, ev1, \
+                                  0, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba); }                \
         else if (lut.qpl == 2)                                                                                 \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), 0, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 2>(); if (lds_ok_) return lds_ok_; \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
         else                                                                                                   \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), 0, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba);                                   \
+            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 1>(); if (lds_ok_) return lds_ok_; \
+            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
+                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
     } while (0)
 #endif
         if (dw && !vig)

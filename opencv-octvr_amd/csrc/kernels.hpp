@@ -73,18 +73,28 @@ __host__ __device__ inline TapCell tap_cell(uint32_t xy, int w, int h) {
 // Each slot's box reaches one column / row past its taps (x0 + 1, y0 + 1), including taps outside
 // the source image: staging writes RGBA 0 for box pixels outside the image (BORDER_CONSTANT), so
 // every tap is read from LDS at off, off + 4, off + 4 S, off + 4 S + 4 (S = row stride) unmasked.
-// The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel:
-//   bits 0-14 LDS byte offset of tap (x, y); 15-19 fx; 20-24 fy; 25 "no gain" (RGBA mode); 26-29
-//   zero; 30-31 slot (so the slot's gain sits at byte offset e >> 27 of a 4-slot table of f32 pairs:
-//   one shift per pixel, kernels.hip).
+// The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel.  OCTVR_WTAB = 1 (default):
+//   bit 0 "no gain" (RGBA mode); bits 1-2 zero; 3-12 the fraction code fx | fy << 5, so e & 0x1FF8 is
+//   the byte offset of the code's two packed weight pairs in the workgroup's 8 KiB LDS weight table;
+//   13-26 LDS byte offset of tap (x, y) (one v_bfe_u32); 27-29 zero; 30-31 slot (the slot's gain
+//   sits at byte offset e >> 27 of a 4-slot table of f32 pairs).  Three VALU decode a pixel's
+//   entry, against ten for the weights computed from fx, fy (OCTVR_WTAB = 0: bits 0-14 offset,
+//   15-19 fx, 20-24 fy, 25 no gain, 30-31 slot).
 // A pixel with no camera, or with every tap outside, is entry 0 and comes out black.
+#ifndef OCTVR_WTAB
+#define OCTVR_WTAB 1
+#endif
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
 #ifndef OCTVR_TILE_LDS_BYTES
-#define OCTVR_TILE_LDS_BYTES (20 * 1024)  // 20 KiB: 7 workgroups fit by LDS, so the composite can take a 7-wave register budget
+// WTAB: 16 KiB less the composite's 176 bytes of other LDS, so its static LDS is exactly 16 KiB and the
+// 8 KiB weight table starts at LDS address 0x4000 (every C2 / C4 item stages < 16 KiB; 6 workgroups
+// per CU by LDS); else 20 KiB: 7 workgroups fit by LDS
+#define OCTVR_TILE_LDS_BYTES (OCTVR_WTAB ? 16 * 1024 - 176 : 20 * 1024)
 #endif
 constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
-static_assert(kTileLdsBytes <= (1 << 15), "the tiled entry holds the LDS byte offset in bits 0-14");
+static_assert(kTileLdsBytes <= (OCTVR_WTAB ? (1 << 14) : (1 << 15)), "the tiled entry's LDS byte offset field");
+constexpr uint32_t kWtabBytes = OCTVR_WTAB ? 1024u * 8u : 0u;
 constexpr int kTileZeroDwords = 4;
 // Staging stores: 2 x 16 bytes per 8-pixel group (row stride a multiple of 4 dwords), or with
 // OCTVR_STAGE_B64 4 x 8 bytes (stride even), so the tiler may pad rows to 2 mod 4 dwords.
@@ -207,9 +217,17 @@ constexpr int kStitchBands = 8;
 // 4-byte tiled entries: bit 25 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
 // in-image map value; mul_scalar_with_mask, exposure_compensate.cu:15-30).  8-byte CompositeEntry
 // records carry the same flag in code bit 16.  TileHdr.nslots bits 16-20: output camera (RGBA mode).
-constexpr uint32_t kEntryNoGain = 1u << 25;
+constexpr uint32_t kEntryNoGain = OCTVR_WTAB ? 1u : 1u << 25;
 constexpr int kEntrySlotShift = 30;
 constexpr uint32_t kCodeNoGain = 1u << 16;
+
+// One staged pixel's 4-byte entry (layout above): off = LDS byte offset of tap (x, y) in the item's
+// staging area, fxy = fx | fy << 5.
+__host__ __device__ constexpr uint32_t tiled_entry(uint32_t off, uint32_t fxy, uint32_t slot, bool nogain) {
+    return OCTVR_WTAB ? (nogain ? kEntryNoGain : 0u) | (fxy & 1023u) << 3 | off << 13 | slot << kEntrySlotShift
+                      : off | (fxy & 31u) << 15 | (fxy >> 5) << 20 | slot << kEntrySlotShift |
+                            (nogain ? kEntryNoGain : 0u);
+}
 
 // Quads per lane of the blend = 0 composite's items (OCTVR_QPL, default 2: 128 x 16 items).
 int composite_qpl();

@@ -147,8 +147,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 if (!px[k].mask) continue;  // black
                 const TileSlot& sl = ts[px[k].slot];
                 const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
-                out[k] = off * 4u | ((uint32_t)(px[k].fxy & 31) << 15) | ((uint32_t)(px[k].fxy >> 5) << 20) |
-                         ((uint32_t)px[k].slot << kEntrySlotShift) | (px[k].nogain ? kEntryNoGain : 0u);
+                out[k] = tiled_entry(off * 4u, (uint32_t)px[k].fxy, (uint32_t)px[k].slot, px[k].nogain != 0);
             }
         }
     };
