@@ -957,6 +957,9 @@ constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_
 #ifndef OCTVR_STORE_LATE
 #define OCTVR_STORE_LATE 0
 #endif
+#ifndef OCTVR_STORE_LATE_M1  // the same for the MODE-1 remap of the multi-band blend
+#define OCTVR_STORE_LATE_M1 0
+#endif
 #ifndef OCTVR_DYN  // 0: static round-robin dealing of a band's items (no work counters)
 #define OCTVR_DYN 1
 #endif
@@ -1129,14 +1132,21 @@ __device__ __forceinline__ void store_result(const OutFrame& o, bool rgba, const
 }
 
 __device__ __forceinline__ void store_rgba(const RgbaSink& o, const QuadOut& q, uint32_t cam, int x, int y, bool in) {
-    const MbCamLevel* c = o.cams + cam;
-    const int xl = x - c->ox, yl = y - c->oy;
-    const bool ok = in && xl >= 0 && yl >= 0 && xl < c->w && yl < c->h;  // w, h even: whole quads
-    const uint32_t off = ok ? c->g_off + (uint32_t)yl * c->g_pitch + (uint32_t)xl * 4u : kDropOffset;
+    // the camera descriptor through the constant address space: scalar loads.  (As a plain global
+    // pointer the compiler cannot rule out the kernel's own stores aliasing it and emitted per-lane
+    // loads, each followed by a vmcnt(0) that drained the next item's prefetches: 34 us of C3's 94 us
+    // remap.)  cam is uniform (the item's camera).
+    typedef __attribute__((address_space(4))) const MbCamLevel kMbCamLevel;
+    const kMbCamLevel* c = (const kMbCamLevel*)o.cams + uniform((int)cam);
+    const int ox = c->ox, oy = c->oy, cw = c->w, chh = c->h;
+    const uint32_t goff = c->g_off, gp = c->g_pitch;
+    const int xl = x - ox, yl = y - oy;
+    const bool ok = in && xl >= 0 && yl >= 0 && xl < cw && yl < chh;  // w, h even: whole quads
+    const uint32_t off = ok ? goff + (uint32_t)yl * gp + (uint32_t)xl * 4u : kDropOffset;
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     const u32x2 r0 = {q.y01, q.y23}, r1 = {q.u, q.v};
     __builtin_amdgcn_raw_buffer_store_b64(r0, o.rsrc, off, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b64(r1, o.rsrc, ok ? off + c->g_pitch : kDropOffset, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(r1, o.rsrc, ok ? off + gp : kDropOffset, 0, 0);
 }
 
 template <int MODE>
@@ -1157,8 +1167,12 @@ __device__ __forceinline__ void store_half(const OutFrame& of, const RgbaSink& r
     if constexpr (MODE == 0) {
         store_quad(of, q, x, y, in);
     } else {
+#if !OCTVR_DIAG_NOG0  // diagnostic (wrong output, timing only)
         if (!((flags >> h) & kItemNoG0)) store_rgba(ro, q, cam, x, y, in);
+#endif
+#if !OCTVR_DIAG_NORES  // diagnostic (wrong output, timing only)
         if ((flags >> h) & kItemResult) store_result(of, res_rgba, q, x, y, in);
+#endif
     }
 }
 
@@ -1264,7 +1278,8 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
     constexpr bool kWideOut = MODE == 2;
     // kStoreLate: an item's output is stored right after its computation, behind the next item's
     // loads (so waiting for those loads need not drain the stores); else at the next iteration's top
-    constexpr bool kStoreLate = OCTVR_STORE_LATE != 0;
+    // (MODE 1 measured 7 % slower with late stores on C3: 111k vs 120k MP/s, so off there too)
+    constexpr bool kStoreLate = (MODE == 1 ? OCTVR_STORE_LATE_M1 : OCTVR_STORE_LATE) != 0;
     constexpr int SM = MODE == 1 ? 1 : 0;  // sink: YUV (finish_quad) or RGBA
     uint32_t* const s_out = L.out;
     constexpr int R = QPL == 1 ? kStageRegs : OCTVR_STAGE_REGS2;  // staging chunks prefetched per wave
@@ -1630,7 +1645,7 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
         if constexpr (kStoreLate && !kWideOut) {  // youngest ops of the iteration (see kStoreLate)
 #pragma unroll
             for (int h = 0; h < QPL; h++)
-                store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+                store_half<SM>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
 #endif
         prev_big = big;

@@ -349,6 +349,8 @@ struct MbBlendArgs {
     int tiles_x;
     const uint32_t* tile_cams;      // bit n: camera n has a non-zero weight in the tile
     const uint8_t* owned;           // multi-band (or NULL): the tile's one camera has weight 1 on every tile pixel
+    const uint32_t* work;           // multi-band (or NULL): the tiles to launch (block b takes tile work[b])
+    int n_work;                     // their count (when work is set)
     const MbCamLevel* cams;         // this level
     const MbCamLevel* cams_next;    // level + 1 (NULL at the top)
     const uint8_t* g;               // this level's pyramid allocation

@@ -307,7 +307,10 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     __shared__ uint32_t s_g[kPatchN];  // the current camera's coarser Gaussian level (u8x4)
 #endif
     const int tid = threadIdx.x;
-    const int tile = blockIdx.x;
+    // work list entry: tile | owned << 24 (a scalar load through the constant address space)
+    typedef __attribute__((address_space(4))) const uint32_t kU32;
+    const uint32_t wk = a.work ? ((const kU32*)a.work)[blockIdx.x] : 0u;
+    const int tile = a.work ? (int)(wk & 0xFFFFFFu) : (int)blockIdx.x;
     const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
     const int wv = uniform(tid >> 6);                                         // quad row of the wave
     const int x = tx * kTileW + 2 * (tid & 63), y = ty * kTileH + 2 * wv;  // quad origin (even)
@@ -358,7 +361,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     // Deep tiles (owned = 2, multiband_host.cpp): R = G on every pixel, by induction over the levels
     // above (one camera of weight 1 on all the pyrUp taps, with the camera's and the collapse's taps
     // identical), so neither pyrUp is taken.
-    const int own = a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
+    const int own = a.work ? (int)(wk >> 24) : a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
     if (own == 3) return;  // no collapse reads this tile (levels >= 1)
     const bool deep = own == 2;
     if (own == 4) return;  // level 0: a deep tile whose result the remap wrote (kItemResult)
@@ -711,7 +714,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s) {
     const int tiles_y = (a.H + kTileH - 1) / kTileH;
-    const int n = a.tiles_x * tiles_y;
+    const int n = a.work ? a.n_work : a.tiles_x * tiles_y;
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(mb_blend_kernel, dim3(n), dim3(256), 0, s, a);
     return hipGetLastError();

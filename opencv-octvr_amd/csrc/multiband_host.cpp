@@ -59,6 +59,9 @@ class MultiBand {
         int n_owned = 0;
         int n_deep = 0;                 // owned tiles with R = G at this level (owned = 2)
         int n_skip = 0;                 // tiles no collapse reads (owned = 3)
+        DevBuf<uint32_t> work;          // multi-band: the tiles mb_blend computes (owned not 3 or 4), in
+                                        // order, as tile | owned << 24
+        int n_work = -1;                // their count (-1: every tile, no list)
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
         int rup_rows = 0;
@@ -647,6 +650,21 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         M.deep_in_remap = M.n_result > 0;
         L0.owned.upload(owned_h[0].data(), owned_h[0].size());
     }
+    // ---- per level, the tiles mb_blend has work on: it is launched over this list only, so the tiles that
+    // return at once (unread: owned 3, written by the remap: owned 4) cost no workgroup dispatch (C3 level
+    // 0: 23,040 of 28,800 tiles)
+    if (!M.feather) {
+        for (int l = 0; l <= B; l++) {
+            auto& L = M.lv[l];
+            if (owned_h[l].empty()) continue;
+            REQUIRE(owned_h[l].size() < (1u << 24), "multi-band: level grid too large");
+            std::vector<uint32_t> work;
+            for (size_t t = 0; t < owned_h[l].size(); t++)
+                if (owned_h[l][t] != 3 && owned_h[l][t] != 4) work.push_back((uint32_t)t | (uint32_t)owned_h[l][t] << 24);
+            L.n_work = (int)work.size();
+            if (!work.empty()) L.work.upload(work.data(), work.size());
+        }
+    }
     // ---- required 8x8 blocks per camera and level, then tiles ------------------------------------
     // need(l) = weight blocks(l) + pyrUp support of weight blocks(l-1) + pyrDown support of need(l+1)
     // (level 0 with deep tiles written by the remap: their weight blocks need no G0)
@@ -863,6 +881,8 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
         a.tiles_x = L.tx_n;
         a.tile_cams = L.tile_cams.p;
         a.owned = L.owned.p;
+        a.work = L.n_work >= 0 ? L.work.p : nullptr;
+        a.n_work = L.n_work;
         a.cams = L.cams.p;
         a.g = G(l);
         if (l < M.B) {
