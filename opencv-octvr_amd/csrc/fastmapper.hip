@@ -26,24 +26,6 @@ __device__ __forceinline__ uint32_t sat_u16_rte(float v) {
     return (uint32_t)__builtin_amdgcn_fmed3f(__builtin_rintf(v), 0.f, 65535.f);  // v >= 0 here
 }
 
-// remap_weighted.cl:46-75 for one pixel of one camera: taps outside the source are 0.
-__device__ __forceinline__ uint32_t weighted_tap(const uint8_t* plane, int sw, int sh, int64_t pitch, int step,
-                                                 uint2 e) {
-    const int sx = (int)(int16_t)(e.x & 0xFFFFu), sy = (int)(int16_t)(e.x >> 16);
-    const uint32_t code = e.y & 1023u, w = e.y >> 16;
-    const float ux = (float)(code & 31u) / 32.f, uy = (float)(code >> 5) / 32.f;
-    float t[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int x = sx + (k & 1), y = sy + (k >> 1);
-        const bool out = x >= sw || y >= sh || x < 0 || y < 0;
-        t[k] = out ? 0.f : (float)plane[(int64_t)y * pitch + (int64_t)x * step];
-    }
-    float v = t[0] * (1 - ux) * (1 - uy) + t[1] * (ux) * (1 - uy) + t[2] * (1 - ux) * (uy) + t[3] * (ux) * (uy);
-    v *= (float)w;
-    return sat_u16_rte(v);
-}
-
 __device__ __forceinline__ uint8_t convert_out(uint32_t acc) {  // convertTo(CV_8U, 1/255.) (convert.cl:77)
     return (uint8_t)__builtin_amdgcn_fmed3f(__builtin_rintf(__builtin_fmaf((float)(acc & 0xFFFFu), (float)(1.0 / 255.0), 0.f)),
                                             0.f, 255.f);
@@ -51,55 +33,125 @@ __device__ __forceinline__ uint8_t convert_out(uint32_t acc) {  // convertTo(CV_
 
 }  // namespace
 
+// remap_weighted.cl:46-75 for one pixel of one camera from its four taps (0 outside the source)
+__device__ __forceinline__ uint32_t weighted_sum(const float (&t)[4], uint2 e) {
+    const uint32_t code = e.y & 1023u, w = e.y >> 16;
+    const float ux = (float)(code & 31u) / 32.f, uy = (float)(code >> 5) / 32.f;
+    float v = t[0] * (1 - ux) * (1 - uy) + t[1] * (ux) * (1 - uy) + t[2] * (1 - ux) * (uy) + t[3] * (ux) * (uy);
+    v *= (float)w;
+    return sat_u16_rte(v);
+}
+
+// A run's cameras in groups of kFastGroup: every entry load of the group, then every tap gather, then
+// the arithmetic, so a pixel costs two memory round trips per group instead of two per camera (the
+// plain per-camera loop, 920 us for a C2 frame, was a chain of dependent loads).  A tap row is one
+// 8-byte load through the camera's frame as a buffer resource (32-bit offsets; addresses clamped into
+// the image, taps outside it zeroed by mask, as BORDER_CONSTANT), instead of 2 (Y) or 4 (chroma) byte
+// loads.  PLANE 0: Y; 1: the interleaved
+// NV12 chroma, V and U (merge order c1, c2: V first, mapper_fast.cpp:181-187).
+constexpr int kFastGroup = 4;
+
+template <int PLANE>
+__device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* __restrict__ ent, const uint2* __restrict__ runs,
+                                           int W, int H, uint8_t* out, int64_t out_pitch) {
+    const int pw = PLANE ? W / 2 : W, ph = PLANE ? H / 2 : H;
+    const int64_t npx = (int64_t)pw * ph;
+    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint2 rr = runs[blockIdx.x];
+    uint32_t m = (uint32_t)uniform((int)rr.x);
+    uint32_t blk = (uint32_t)uniform((int)rr.y);
+    uint32_t acc0 = 0, acc1 = 0;  // Y (or V), U
+    while (m) {
+        uint2 e[kFastGroup];
+        int cam[kFastGroup];
+        bool live[kFastGroup];
+#pragma unroll
+        for (int k = 0; k < kFastGroup; k++) {  // uniform: the group's cameras and their entry blocks
+            live[k] = m != 0u;
+            cam[k] = live[k] ? __builtin_ctz(m) : 0;
+            m &= m - 1u;
+            e[k] = ent[(int64_t)(live[k] ? blk + k : blk) * 256 + threadIdx.x];
+        }
+        blk += live[3] ? 4u : live[2] ? 3u : live[1] ? 2u : 1u;
+        // per camera and tap row one 8-byte load from the 4-byte aligned start at or below the row's
+        // first in-image tap byte: it holds both taps' bytes (Y: x, x + 1; chroma: the V, U pairs of x, x + 1)
+        uint2 rw[kFastGroup][2];
+        uint32_t sel[kFastGroup];
+#pragma unroll
+        for (int k = 0; k < kFastGroup; k++) {
+            const SourceFrame f = frames.f[cam[k]];
+            const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
+            const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint8_t*>(f.yuv), 0, (int)((uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2)), 0x00020000);
+            const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
+            const int xa = min(max(sx, 0), sw - 1);
+            const uint32_t bx = (uint32_t)xa * (PLANE ? 2u : 1u) & ~3u;  // 4-byte aligned row start
+            // byte index of taps x = sx, sx + 1 in the 8 loaded bytes (exact for taps inside the image,
+            // any byte for the ones outside, which are masked below); chroma: even, so i + 1 <= 7
+            const uint32_t i0 = (uint32_t)(sx * (PLANE ? 2 : 1) - (int)bx) & 7u;
+            const uint32_t i1 = (uint32_t)((sx + 1) * (PLANE ? 2 : 1) - (int)bx) & 7u;
+            sel[k] = PLANE ? (i0 | (i0 + 1u) << 8 | i1 << 16 | (i1 + 1u) << 24) : (i0 | i1 << 8 | 0x0C0C0000u);
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const int y = min(max(sy + r, 0), sh - 1);
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, base + (uint32_t)y * (uint32_t)f.pitch + bx, 0, 0);
+                rw[k][r] = make_uint2(v.x, v.y);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kFastGroup; k++) {
+            if (!live[k] || (e[k].y >> 16) == 0) continue;
+            const SourceFrame f = frames.f[cam[k]];
+            const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
+            const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
+            float t0[4], t1[4];
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                // row r's taps: Y bytes {x, x + 1}, or chroma bytes {U x, V x, U x+1, V x+1}
+                const uint32_t b = __builtin_amdgcn_perm(rw[k][r].y, rw[k][r].x, sel[k]);
+                const int y = sy + r;
+#pragma unroll
+                for (int c = 0; c < 2; c++) {
+                    const int x = sx + c;
+                    const bool in = x >= 0 && y >= 0 && x < sw && y < sh;
+                    const int j = 2 * r + c;
+                    if (PLANE) {
+                        t0[j] = in ? (float)((b >> (16 * c + 8)) & 255u) : 0.f;  // V
+                        t1[j] = in ? (float)((b >> (16 * c)) & 255u) : 0.f;      // U
+                    } else {
+                        t0[j] = in ? (float)((b >> (8 * c)) & 255u) : 0.f;
+                    }
+                }
+            }
+            acc0 += weighted_sum(t0, e[k]);
+            if (PLANE) acc1 += weighted_sum(t1, e[k]);
+        }
+    }
+    if (idx >= npx) return;
+    const int y = (int)(idx / pw), x = (int)(idx - (int64_t)y * pw);
+    if (PLANE) {
+        uint8_t* o = out + (int64_t)(H + y) * out_pitch + 2 * x;  // merge(c1c2): V first, then U
+        o[0] = convert_out(acc0);
+        o[1] = convert_out(acc1);
+    } else {
+        out[(int64_t)y * out_pitch + x] = convert_out(acc0);
+    }
+}
+
 // runs[r] = {camera mask, first block}: run r's cameras (ascending) own blocks first, first + 1, ... of
 // 256 entries (fastmapper.cpp)
 __global__ void __launch_bounds__(256) fast_y_kernel(FrameSet frames, const uint2* __restrict__ ent,
                                                      const uint2* __restrict__ runs, int W, int H, uint8_t* out,
                                                      int64_t out_pitch) {
-    const int64_t npx = (int64_t)W * H;
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint2 rr = runs[blockIdx.x];
-    uint32_t m = (uint32_t)uniform((int)rr.x);
-    uint32_t blk = (uint32_t)uniform((int)rr.y);
-    if (idx >= npx) return;
-    uint32_t acc = 0;
-    while (m) {
-        const int c = __builtin_ctz(m);
-        m &= m - 1;
-        const uint2 e = ent[(int64_t)(blk++) * 256 + threadIdx.x];
-        if ((e.y >> 16) == 0) continue;
-        const SourceFrame& f = frames.f[c];
-        acc += weighted_tap(f.yuv, f.w, f.h, f.pitch, 1, e);
-    }
-    const int y = (int)(idx / W), x = (int)(idx - (int64_t)y * W);
-    out[(int64_t)y * out_pitch + x] = convert_out(acc);
+    fast_plane<0>(frames, ent, runs, W, H, out, out_pitch);
 }
 
 __global__ void __launch_bounds__(256) fast_uv_kernel(FrameSet frames, const uint2* __restrict__ ent,
                                                       const uint2* __restrict__ runs, int W, int H, uint8_t* out,
                                                       int64_t out_pitch) {
-    const int hw = W / 2, hh = H / 2;
-    const int64_t npx = (int64_t)hw * hh;
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint2 rr = runs[blockIdx.x];
-    uint32_t m = (uint32_t)uniform((int)rr.x);
-    uint32_t blk = (uint32_t)uniform((int)rr.y);
-    if (idx >= npx) return;
-    uint32_t accV = 0, accU = 0;
-    while (m) {
-        const int c = __builtin_ctz(m);
-        m &= m - 1;
-        const uint2 e = ent[(int64_t)(blk++) * 256 + threadIdx.x];
-        if ((e.y >> 16) == 0) continue;
-        const SourceFrame& f = frames.f[c];
-        const uint8_t* uv = f.yuv + (int64_t)f.h * f.pitch;  // interleaved U, V rows (NV12)
-        accV += weighted_tap(uv + 1, f.w / 2, f.h / 2, f.pitch, 2, e);
-        accU += weighted_tap(uv, f.w / 2, f.h / 2, f.pitch, 2, e);
-    }
-    const int y = (int)(idx / hw), x = (int)(idx - (int64_t)y * hw);
-    uint8_t* o = out + (int64_t)(H + y) * out_pitch + 2 * x;  // merge(c1c2): V first, then U
-    o[0] = convert_out(accV);
-    o[1] = convert_out(accU);
+    fast_plane<1>(frames, ent, runs, W, H, out, out_pitch);
 }
 
 hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint2* runs_y,

@@ -54,3 +54,30 @@ def test_gpu_fastmapper_needs_full_frame_templates(product_lib):
     sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
     with pytest.raises(ox.OctvrError):
         ox.FastMapper(mt, sizes)
+
+
+def test_gpu_fastmapper_edge_taps(product_lib):
+    """Maps scattered over [-0.06, 1.06] of small frames: taps at x / y = -1, 0, w - 1, w and beyond on
+    both planes, where the kernel's 8-byte row loads start at the clamped column and the taps outside
+    the image read 0 (remap_weighted BORDER_CONSTANT); bit-exact vs the oracle, full-frame masks."""
+    import torch
+    ox = product_lib
+    W, H = 96, 48
+    sizes = [(40, 24), (56, 30)]
+    rng = np.random.default_rng(7)
+    m1 = [rng.uniform(-0.06, 1.06, (H, W)).astype(np.float32) for _ in sizes]
+    m2 = [rng.uniform(-0.06, 1.06, (H, W)).astype(np.float32) for _ in sizes]
+    mk = [np.full((H, W), 255, np.uint8) for _ in sizes]
+    mk[1][:, : W // 3] = 0
+    mt = ox.MapperTemplate.from_arrays(W, H, [[0, 0, W, H]] * 2, m1, m2, mk)
+    fm = ox.FastMapper(mt, sizes)
+    for seed in (3, 4):
+        frames = [O.rand_img(w, h * 3 // 2, 1, 50 * seed + i) for i, (w, h) in enumerate(sizes)]
+        out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+        fm.stitch_nv12([torch.from_numpy(f).cuda() for f in frames], out)
+        torch.cuda.synchronize()
+        want = O.fastmapper_nv12(frames, sizes, m1, m2, mk, W, H)
+        got = out.cpu().numpy()
+        d = got != want
+        assert not d.any(), (seed, int(d.sum()), np.argwhere(d)[:5].tolist())
+        assert want.any()
