@@ -234,6 +234,9 @@ int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_
         memset(&fs, 0, sizeof fs);
         for (int i = 0; i < fm->n; i++) {
             REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)fm->in_w[i], "bad input frame");
+            REQUIRE(in_pitch[i] * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) >= 8 &&
+                        in_pitch[i] * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) < 0x7FFFFFFFull,
+                    "input frame of fewer than 8 or more than 2^31 bytes");
             fs.f[i] = SourceFrame{in_dev[i], fm->in_w[i], fm->in_h[i], (int64_t)in_pitch[i], nullptr};
         }
         HIP_CHECK(launch_fastmapper_nv12(fs, fm->ent_y.p, fm->runs_y.p, fm->ent_uv.p, fm->runs_uv.p, fm->W, fm->H, out_dev,

@@ -76,27 +76,32 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
         // per camera and tap row one 8-byte load from the 4-byte aligned start at or below the row's
         // first in-image tap byte: it holds both taps' bytes (Y: x, x + 1; chroma: the V, U pairs of x, x + 1)
         uint2 rw[kFastGroup][2];
-        uint32_t sel[kFastGroup];
+        uint32_t sel[kFastGroup][2];
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) {
             const SourceFrame f = frames.f[cam[k]];
             const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
             const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                const_cast<uint8_t*>(f.yuv), 0, (int)((uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2)), 0x00020000);
+            const uint32_t size = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2);  // >= 8 (host check)
+            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(f.yuv), 0, (int)size, 0x00020000);
             const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
             const int xa = min(max(sx, 0), sw - 1);
             const uint32_t bx = (uint32_t)xa * (PLANE ? 2u : 1u) & ~3u;  // 4-byte aligned row start
-            // byte index of taps x = sx, sx + 1 in the 8 loaded bytes (exact for taps inside the image,
-            // any byte for the ones outside, which are masked below); chroma: even, so i + 1 <= 7
-            const uint32_t i0 = (uint32_t)(sx * (PLANE ? 2 : 1) - (int)bx) & 7u;
-            const uint32_t i1 = (uint32_t)((sx + 1) * (PLANE ? 2 : 1) - (int)bx) & 7u;
-            sel[k] = PLANE ? (i0 | (i0 + 1u) << 8 | i1 << 16 | (i1 + 1u) << 24) : (i0 | i1 << 8 | 0x0C0C0000u);
-            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
             for (int r = 0; r < 2; r++) {
                 const int y = min(max(sy + r, 0), sh - 1);
-                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, base + (uint32_t)y * (uint32_t)f.pitch + bx, 0, 0);
+                const uint32_t row = base + (uint32_t)y * (uint32_t)f.pitch;
+                // the buffer range-checks whole dwords: a start within 8 bytes of the frame's end (its last
+                // chroma row, a pitch not a multiple of 4) is clamped to size - 8 and the taps taken from there
+                const uint32_t st = min(row + bx, size - 8u);
+                // byte index of taps x = sx, sx + 1 in the 8 loaded bytes (exact for taps inside the image,
+                // any byte for the ones outside, which are masked below); an in-image chroma pair starts
+                // at most at byte 6, so its second byte is i + 1 <= 7
+                const uint32_t i0 = (row + (uint32_t)(sx * (PLANE ? 2 : 1)) - st) & 7u;
+                const uint32_t i1 = (row + (uint32_t)((sx + 1) * (PLANE ? 2 : 1)) - st) & 7u;
+                sel[k][r] = PLANE ? (i0 | (i0 + 1u) << 8 | i1 << 16 | (i1 + 1u) << 24) : (i0 | i1 << 8 | 0x0C0C0000u);
+                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, st, 0, 0);
                 rw[k][r] = make_uint2(v.x, v.y);
             }
         }
@@ -110,7 +115,7 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
 #pragma unroll
             for (int r = 0; r < 2; r++) {
                 // row r's taps: Y bytes {x, x + 1}, or chroma bytes {U x, V x, U x+1, V x+1}
-                const uint32_t b = __builtin_amdgcn_perm(rw[k][r].y, rw[k][r].x, sel[k]);
+                const uint32_t b = __builtin_amdgcn_perm(rw[k][r].y, rw[k][r].x, sel[k][r]);
                 const int y = sy + r;
 #pragma unroll
                 for (int c = 0; c < 2; c++) {

@@ -58,12 +58,13 @@ def test_gpu_fastmapper_needs_full_frame_templates(product_lib):
 
 def test_gpu_fastmapper_edge_taps(product_lib):
     """Maps scattered over [-0.06, 1.06] of small frames: taps at x / y = -1, 0, w - 1, w and beyond on
-    both planes, where the kernel's 8-byte row loads start at the clamped column and the taps outside
-    the image read 0 (remap_weighted BORDER_CONSTANT); bit-exact vs the oracle, full-frame masks."""
+    both planes, where the kernel's 8-byte row loads start at the clamped column (and within 8 bytes of
+    a frame that ends mid-dword, at size - 8) and the taps outside the image read 0 (remap_weighted
+    BORDER_CONSTANT); bit-exact vs the oracle, full-frame masks."""
     import torch
     ox = product_lib
     W, H = 96, 48
-    sizes = [(40, 24), (56, 30)]
+    sizes = [(40, 24), (42, 26)]  # 42 x 39 = 1638 bytes: the frame ends mid-dword
     rng = np.random.default_rng(7)
     m1 = [rng.uniform(-0.06, 1.06, (H, W)).astype(np.float32) for _ in sizes]
     m2 = [rng.uniform(-0.06, 1.06, (H, W)).astype(np.float32) for _ in sizes]
