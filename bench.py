@@ -122,6 +122,25 @@ def pmc_traffic(config, blend):
     return None, "no PMC summary of this liboctvr_hip.so (sha256 %s...)" % sha[:12]
 
 
+def pmc_valu_busy(config):
+    """The composite's VALU issue share from the PMC summary of this binary: SQ_ACTIVE_INST_VALU (quad-cycles
+    summed over every SIMD) x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), i.e. the fraction of the kernel's
+    SIMD cycles spent issuing VALU (MI355X_MICROARCH.md, SQ counters).  None without such a summary."""
+    import glob
+    sha = lib_sha256()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % config))):
+        d = json.load(open(path))
+        if d.get("so_sha256") != sha:
+            continue
+        for k, cs in d.get("counters", {}).items():
+            if "stitch_tiled_kernel" in k and "SQ_ACTIVE_INST_VALU" in cs and "GRBM_GUI_ACTIVE" in cs:
+                a, g = cs["SQ_ACTIVE_INST_VALU"]["median"], cs["GRBM_GUI_ACTIVE"]["median"]
+                return {"frac": round(a * 4.0 / (g / 8.0 * 1024.0), 3), "source": os.path.basename(path),
+                        "note": "one launch alone under rocprofv3 (PMC serialises dispatches): SIMD cycles issuing VALU / "
+                                "kernel cycles; the composite is VALU-issue-bound (DESIGN.md §4)"}
+    return None
+
+
 def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
     """AsyncMultiMapper end to end (async.cpp:32-193): host YUV420P planes pushed, copied into pinned
     staging, uploaded, stitched, downloaded and copied out, 3 frames in flight (the reference's
@@ -458,7 +477,8 @@ def gpu_rank(args, world, rank, local_rank, dist):
                      "frac_at_step_time": round(bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
                      # the counter-based fraction: PMC HBM bytes of the same binary over the same kernel time
                      "frac_traffic": round(traffic / avg_kernel_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None,
-                     "traffic_over_bytes": round(traffic / bytes_per_launch, 3) if traffic else None},
+                     "traffic_over_bytes": round(traffic / bytes_per_launch, 3) if traffic else None,
+                     **({"valu_busy": pmc_valu_busy(args.config)} if blend == 0 else {})},
         "survey_b_alg": {"bytes": survey_b_alg,
                          "gbps_at_step_time": round(survey_b_alg / (elapsed / args.steps) / 1e9, 1),
                          "note": "SURVEY.md §8(d) B_alg (per-camera maps re-read for every valid (camera, pixel)); "

@@ -12,7 +12,7 @@ STEPS=${STEPS:-6}
 INFLIGHT=${INFLIGHT:-3}
 PASSES=${PASSES:-FETCH WRITE}
 if [ -z "$RE" ]; then
-  case $CFG in C3) RE="stitch_tiled|mb_down|mb_blend|gain_feed" ;; *) RE="stitch_tiled|gain_feed" ;; esac
+  case $CFG in C3) RE="stitch_tiled|mb_down|mb_blend|gain_feed" ;; F2) RE="fast_y|fast_uv" ;; *) RE="stitch_tiled|gain_feed" ;; esac
 fi
 declare -A P
 P[FETCH]="FETCH_SIZE"

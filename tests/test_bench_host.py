@@ -51,7 +51,9 @@ def test_committed_pmc_summaries_are_well_formed():
         d = json.load(open(p))
         assert len(d["so_sha256"]) == 64, p
         assert d["traffic_per_frame_bytes"] > 0, p
-        assert any("stitch_tiled_kernel" in k for k in d["traffic_bytes"]), p
+        # the composite (C1-C4) or the FastMapper's two plane kernels (F2)
+        want_k = ("fast_y_kernel", "fast_uv_kernel") if d.get("config") == "F2" else ("stitch_tiled_kernel",)
+        assert all(any(w in k for k in d["traffic_bytes"]) for w in want_k), p
         # per launch: 2 x FETCH_SIZE + WRITE_SIZE, the medians over the profiled launches, KiB -> bytes
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             for k, t in d["traffic_bytes"].items():
