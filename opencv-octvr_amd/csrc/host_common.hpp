@@ -155,7 +155,9 @@ void mapper_out_size(const octvr_mapper* m, int* w, int* h);
 struct TileJob {
     int tx, ty;  // 128 x (8 qpl) item of the output (or level-0) grid
     int cam;     // RGBA mode: the camera whose pyramid image the tile is written to
-    uint32_t flags = 0;  // RGBA mode: per half kItemResult / kItemNoG0 (kernels.hpp)
+    // RGBA mode: item_result_bit / item_g0_bit per half and quarter (kernels.hpp); by default every
+    // sub-tile's G0 (the scaled output's result image) and no result
+    uint32_t flags = kItemAllG0;
 };
 // entry(job, x, y): the 8-byte CompositeEntry of grid pixel (x, y) for that job ({0,0} = black)
 using EntryFn = std::function<CompositeEntry(int job, int x, int y)>;
@@ -165,8 +167,8 @@ struct TiledLutBuild {
     std::vector<uint32_t> entries;
     std::vector<CompositeEntry> wide;
     std::vector<uint32_t> wide_tiles;
-    std::vector<uint8_t> wide_cams;  // camera | result << 5 | no-G0 << 6 (RGBA mode)
-    std::vector<uint8_t> item_flags;  // per staged item: its job's flags (RGBA mode)
+    std::vector<uint16_t> wide_cams;  // camera | the half's flags (quarters' result bits, G0 bits << 4) << 8
+    std::vector<uint16_t> item_flags;  // per staged item: its job's flags (RGBA mode)
     std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
     int qpl = 1;  // 128x8 halves per item (kernels.hpp TiledLut::qpl)
@@ -181,7 +183,7 @@ struct TiledLutDev {
     DevBuf<uint32_t> entries;
     DevBuf<CompositeEntry> wide;
     DevBuf<uint32_t> wide_tiles;
-    DevBuf<uint8_t> wide_cams;
+    DevBuf<uint16_t> wide_cams;
     DevBuf<int32_t> bands;
     DevBuf<uint32_t> queue;
     double staged_bytes = 0;

@@ -1158,20 +1158,21 @@ __device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro
         store_rgba(ro, q, cam, x, y, in);
 }
 
-// One half of an item: MODE 0 the YUV quad into `of`; MODE 1 the G0 quad unless the item's flags
-// (uniform, kItemNoG0) say nothing reads it, and the final result into `of` (the result frame) where they
-// say the tile is deep (kItemResult)
+// One half of an item: MODE 0 the YUV quad into `of`; MODE 1 the G0 quad where the item's flags say some
+// pyrDown or blend reads the lane's sub-tile (item_g0_bit), and the final result into `of` (the result frame)
+// where they say the sub-tile is deep (item_result_bit).  The lane's sub-tile: quarter (lane & 63) >> 4.
 template <int MODE>
 __device__ __forceinline__ void store_half(const OutFrame& of, const RgbaSink& ro, bool res_rgba, const QuadOut& q,
                                            uint32_t cam, uint32_t flags, int h, int x, int y, bool in) {
     if constexpr (MODE == 0) {
         store_quad(of, q, x, y, in);
     } else {
+        const int q4 = (int)((threadIdx.x & 63u) >> 4);
 #if !OCTVR_DIAG_NOG0  // diagnostic (wrong output, timing only)
-        if (!((flags >> h) & kItemNoG0)) store_rgba(ro, q, cam, x, y, in);
+        if (flags & item_g0_bit(h, q4)) store_rgba(ro, q, cam, x, y, in);
 #endif
 #if !OCTVR_DIAG_NORES  // diagnostic (wrong output, timing only)
-        if ((flags >> h) & kItemResult) store_result(of, res_rgba, q, x, y, in);
+        if (flags & item_result_bit(h, q4)) store_result(of, res_rgba, q, x, y, in);
 #endif
     }
 }
@@ -1365,7 +1366,7 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
     const uint32_t lane_y = (uint32_t)(2 * qy) * of.pitch + (uint32_t)(2 * qx), lane_c = (uint32_t)qy * of.pitch + (uint32_t)qx;
     int pox = 0, poy = 0;  // the previous item's origin (uniform)
     bool pfull = false;    // the previous item lies wholly inside W x H (uniform)
-    uint32_t pcam = 0, pfl = 0;  // the previous item's RGBA-mode camera and flags (kItemResult / kItemNoG0)
+    uint32_t pcam = 0, pfl = 0;  // the previous item's RGBA-mode camera and flags (item_result_bit / item_g0_bit)
     bool pin = false;
     uint32_t par = 0, half = 0;  // iteration parity; LDS half of the next small item
     bool prev_big = true;
@@ -1639,7 +1640,7 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
         poy = (int)(cur.tile >> 16) * kItemH;
         pfull = pox + kTileW <= W && poy + kItemH <= H;
         pcam = (cur.nslots >> 16) & 31u;
-        pfl = SM == 1 ? (cur.map >> 8) & 0xFFu : 0u;
+        pfl = SM == 1 ? (cur.map >> 8) & 0xFFFFu : 0u;
         pin = x < W && y < H;
 #if !OCTVR_DIAG_NOSTORE
         if constexpr (kStoreLate && !kWideOut) {  // youngest ops of the iteration (see kStoreLate)
@@ -1732,8 +1733,9 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
     for (int p = 0; p < 4; p++)
 #pragma unroll
         for (int ch = 0; ch < 3; ch++) rgbf[p][ch] = (float)rgb[p][ch];
-    // camera byte: camera | result << 5 | no-G0 << 6 (tiling.cpp), i.e. the item flags of half 0
-    const uint32_t fl = ((camb >> 5) & 1u ? kItemResult : 0u) | ((camb >> 6) & 1u ? kItemNoG0 : 0u);
+    // camera word: camera | the half's quarters' result bits << 8 | G0 bits << 12 (tiling.cpp), i.e. the
+    // item flags of a half 0
+    const uint32_t fl = ((camb >> 8) & 15u) | ((camb >> 12) & 15u) << 8;
     store_half<MODE>(of, ro, rgba.res_rgba != 0, finish_any<MODE>(rgbf, gain), camb & 31u, fl, 0, x, y, x < W && y < H);
 }
 

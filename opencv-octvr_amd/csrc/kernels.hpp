@@ -197,7 +197,7 @@ struct TiledLut {
     const uint32_t* wide_tiles;   // tile column | row << 16 of each wide tile
     const CompositeEntry* wide;   // kTilePx per wide tile
     int n_wide;
-    const uint8_t* wide_cams;     // RGBA mode: output camera of each wide tile
+    const uint16_t* wide_cams;    // RGBA mode: output camera of each wide tile | its half's item flags << 8
     const int32_t* bands;         // kStitchBands + 1 staged-item boundaries (one band per XCD)
     uint32_t* queue;              // per band a work counter, then a done ticket, kQueueStride apart;
                                   // zero before a launch, left zero by its last workgroup
@@ -331,9 +331,17 @@ struct RgbaOut {
     uint32_t res_pitch, res_u_off, res_v_off;
     int res_rgba;
 };
-// Per-item flags of the MODE-1 remap (bits 8-15 of the item header's device word 2, see TiledLutDev::upload;
-// bits 5 / 6 of a wide tile's camera byte): half h writes its result (1 << h), half h writes no G0 (16 << h).
-constexpr uint32_t kItemResult = 1u, kItemNoG0 = 16u;
+// Sub-tiles: 32 x 8 quarters of a 128 x 8 tile (one mb_blend wave each; lane = quad).  The multi-band
+// classification (owned / deep / unread / result, multiband_host.cpp) is per sub-tile, so a seam that
+// crosses a tile leaves its other quarters on the cheap paths.
+constexpr int kSubW = 32, kSubs = kTileW / kSubW;
+// Per-item flags of the MODE-1 remap (bits 8-23 of the item header's device word 2, see
+// TiledLutDev::upload; bits 8-15 of a wide tile's camera word, for its one half): for half h and quarter q,
+// bit 4h + q: that sub-tile's final result is written by the remap (its one deep camera's G0 converted),
+// bit 8 + 4h + q: its G0 is written (some pyrDown or blend reads it).  Items of <= 2 halves.
+__host__ __device__ constexpr uint32_t item_result_bit(int h, int q) { return 1u << (4 * h + q); }
+__host__ __device__ constexpr uint32_t item_g0_bit(int h, int q) { return 1u << (8 + 4 * h + q); }
+constexpr uint32_t kItemAllG0 = 0xFF00u;
 
 hipError_t launch_mb_remap(const FrameSet& frames, const TiledLut& lut, const double* gains, int use_gain,
                            const RgbaOut& out, hipStream_t s);
@@ -349,8 +357,10 @@ struct MbBlendArgs {
     int tiles_x;
     const uint32_t* tile_cams;      // bit n: camera n has a non-zero weight in the tile
     const uint8_t* owned;           // multi-band (or NULL): the tile's one camera has weight 1 on every tile pixel
-    const uint32_t* work;           // multi-band (or NULL): the tiles to launch (block b takes tile work[b])
-    int n_work;                     // their count (when work is set)
+    const uint2* work;              // multi-band (or NULL): the sub-tiles to blend, 4 per workgroup (wave w of
+                                    // block b takes work[4 b + w]): x = tile | quarter << 24 | owned << 27,
+                                    // y = the sub-tile's cameras; padded with owned = 3 (nothing to do)
+    int n_work;                     // their count (a multiple of 4, when work is set)
     const MbCamLevel* cams;         // this level
     const MbCamLevel* cams_next;    // level + 1 (NULL at the top)
     const uint8_t* g;               // this level's pyramid allocation

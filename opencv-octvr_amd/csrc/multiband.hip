@@ -38,7 +38,7 @@ constexpr int kDnRows = 2 * kTileH + 4, kDnCols = 2 * kTileW + 4;
 __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ items, const MbCamLevel* cams_l,
                                                       const MbCamLevel* cams_prev, const uint8_t* __restrict__ g_prev,
                                                       uint8_t* __restrict__ g_l) {
-    __shared__ uint2 s_v[kTileH * kDnCols];             // 16.3 KiB: (c0 | c1 << 16, c2)
+    __shared__ uint2 s_v[kTileH * kDnCols];             // 16.3 KiB: (R | B << 16, G | A << 16) column sums
     const uint2 it = items[blockIdx.x];
     const int cam = uniform((int)it.x);
     const int tx = uniform((int)(it.y & 0xFFFFu)), ty = uniform((int)(it.y >> 16));
@@ -49,32 +49,46 @@ __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ 
     const int xo = tx * kTileW - c.ox, yo = ty * kTileH - c.oy;
     const int sx0 = 2 * xo - 2, sy0 = 2 * yo - 2;
     const uint8_t* src = g_prev + p.g_off;
-    // lane t holds column t of the 20 source rows in registers (lanes 0-3 also columns 256-259), all
-    // loads in flight before the first use; the vertical pass runs on them directly
-    const uint32_t w5[5] = {1u, 4u, 6u, 4u, 1u};
-    {
-        const int sxa = min(max(sx0 + tid, 0), p.w - 1), sxb = min(max(sx0 + kDnCols - 4 + (tid & 3), 0), p.w - 1);
-        uint32_t va[kDnRows], vb[kDnRows];
+    // Channel sums in packed 16-bit halves: R and B of a pixel as (v & 0x00FF00FF), G and A as
+    // (v >> 8) & 0x00FF00FF, so one packed multiply-add serves two channels.  Every sum stays exact in
+    // 16 bits: a 5-tap column sum <= 16 * 255 = 4,080, the 5 x 5 sum <= 256 * 255 = 65,280.
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    constexpr unsigned short kW5[5] = {1, 4, 6, 4, 1};
+    auto colsum = [&](const uint32_t (&col)[kDnRows], int tgt) {
+        u16x2 rb[kDnRows], ga[kDnRows];
 #pragma unroll
-        for (int r = 0; r < kDnRows; r++) {
-            const uint8_t* row = src + (int64_t)min(max(sy0 + r, 0), p.h - 1) * p.g_pitch;
-            va[r] = *reinterpret_cast<const uint32_t*>(row + (int64_t)sxa * 4);
-            vb[r] = *reinterpret_cast<const uint32_t*>(row + (int64_t)sxb * 4);
+        for (int k = 0; k < kDnRows; k++) {
+            rb[k] = __builtin_bit_cast(u16x2, col[k] & 0x00FF00FFu);
+            ga[k] = __builtin_bit_cast(u16x2, (col[k] >> 8) & 0x00FF00FFu);
         }
 #pragma unroll
         for (int r = 0; r < kTileH; r++) {
+            u16x2 srb = rb[2 * r] * kW5[0], sga = ga[2 * r] * kW5[0];
 #pragma unroll
-            for (int half = 0; half < 2; half++) {
-                if (half && tid >= 4) continue;
-                const uint32_t* col = half ? vb : va;
-                uint32_t acc[3] = {0u, 0u, 0u};
-#pragma unroll
-                for (int j = 0; j < 5; j++)
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++) acc[ch] += w5[j] * ch_of(col[2 * r + j], ch);
-                s_v[r * kDnCols + (half ? kDnCols - 4 + tid : tid)] = make_uint2(acc[0] | (acc[1] << 16), acc[2]);
+            for (int j = 1; j < 5; j++) {
+                srb += rb[2 * r + j] * kW5[j];
+                sga += ga[2 * r + j] * kW5[j];
             }
+            s_v[r * kDnCols + tgt] = make_uint2(__builtin_bit_cast(uint32_t, srb), __builtin_bit_cast(uint32_t, sga));
         }
+    };
+    // lane t holds column t of the 20 source rows in registers (lanes 0-3 of wave 0 also columns
+    // 256-259), all loads in flight before the first use; the vertical pass runs on them directly
+    {
+        const int sxa = min(max(sx0 + tid, 0), p.w - 1);
+        uint32_t va[kDnRows];
+#pragma unroll
+        for (int r = 0; r < kDnRows; r++)
+            va[r] = *reinterpret_cast<const uint32_t*>(src + (int64_t)min(max(sy0 + r, 0), p.h - 1) * p.g_pitch + (int64_t)sxa * 4);
+        if (tid < 4) {
+            const int sxb = min(max(sx0 + kDnCols - 4 + tid, 0), p.w - 1);
+            uint32_t vb[kDnRows];
+#pragma unroll
+            for (int r = 0; r < kDnRows; r++)
+                vb[r] = *reinterpret_cast<const uint32_t*>(src + (int64_t)min(max(sy0 + r, 0), p.h - 1) * p.g_pitch + (int64_t)sxb * 4);
+            colsum(vb, kDnCols - 4 + tid);
+        }
+        colsum(va, tid);
     }
     __syncthreads();
     const int qx = tid & 63, qy = tid >> 6;
@@ -85,16 +99,17 @@ __global__ void __launch_bounds__(256) mb_down_kernel(const uint2* __restrict__ 
     for (int p4 = 0; p4 < 4; p4++) {
         const int r = 2 * qy + (p4 >> 1), cx = 2 * (2 * qx + (p4 & 1));  // source column 2x-2 -> index 2x
         const uint2* v = s_v + r * kDnCols + cx;
-        const uint32_t w[5] = {1u, 4u, 6u, 4u, 1u};
-        uint32_t a0 = 0, a1 = 0, a2 = 0;
+        u16x2 hrb = __builtin_bit_cast(u16x2, v[0].x) * kW5[0], hga = __builtin_bit_cast(u16x2, v[0].y) * kW5[0];
 #pragma unroll
-        for (int k = 0; k < 5; k++) {
-            a0 += w[k] * (v[k].x & 0xFFFFu);
-            a1 += w[k] * (v[k].x >> 16);
-            a2 += w[k] * v[k].y;
+        for (int k = 1; k < 5; k++) {
+            hrb += __builtin_bit_cast(u16x2, v[k].x) * kW5[k];
+            hga += __builtin_bit_cast(u16x2, v[k].y) * kW5[k];
         }
-        px[p4] = (uint32_t)min(rne_shr<8>((int)a0), 255) | ((uint32_t)min(rne_shr<8>((int)a1), 255) << 8) |
-                 ((uint32_t)min(rne_shr<8>((int)a2), 255) << 16);
+        // sat(rne(S / 256)) per channel: (S + 127 + bit8(S)) >> 8 <= 255 (S <= 65,280: no carry, no clamp)
+        const u16x2 one = {1, 1}, c127 = {127, 127};
+        const u16x2 orb = (hrb + c127 + ((hrb >> 8) & one)) >> 8, oga = (hga + c127 + ((hga >> 8) & one)) >> 8;
+        // R | G << 8 | B << 16 (A = 0): bytes 0 and 2 of orb, byte 0 of oga
+        px[p4] = __builtin_amdgcn_perm(__builtin_bit_cast(uint32_t, oga), __builtin_bit_cast(uint32_t, orb), 0x0C020400u);
     }
 #pragma unroll
     for (int p4 = 0; p4 < 4; p4++) {  // per pixel: odd-sized top levels end mid-quad
@@ -307,13 +322,19 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     __shared__ uint32_t s_g[kPatchN];  // the current camera's coarser Gaussian level (u8x4)
 #endif
     const int tid = threadIdx.x;
-    // work list entry: tile | owned << 24 (a scalar load through the constant address space)
-    typedef __attribute__((address_space(4))) const uint32_t kU32;
-    const uint32_t wk = a.work ? ((const kU32*)a.work)[blockIdx.x] : 0u;
-    const int tile = a.work ? (int)(wk & 0xFFFFFFu) : (int)blockIdx.x;
+    const int wv = uniform(tid >> 6), lane = tid & 63;
+    // Multi-band: wave w of block b blends sub-tile work[4 b + w] (32 x 8: lane = quad, 16 per quad row;
+    // a scalar load through the constant address space): tile | quarter << 24 | kind << 27, its cameras.
+    // Waves share nothing (no LDS, no barriers in the direct-taps build), so a workgroup's four sub-tiles
+    // may lie anywhere.  Feather (no list): one tile per workgroup, wave = quad row, lane = quad.
+    static_assert(MB_DIRECT_TAPS, "per-wave sub-tiles need the barrier-free direct-taps blend");
+    typedef __attribute__((address_space(4))) const uint64_t kU64;
+    const uint64_t wk64 = a.work ? ((const kU64*)a.work)[blockIdx.x * 4 + wv] : 0ull;
+    const uint2 wk = make_uint2((uint32_t)wk64, (uint32_t)(wk64 >> 32));
+    const int tile = a.work ? (int)(wk.x & 0xFFFFFFu) : (int)blockIdx.x;
     const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-    const int wv = uniform(tid >> 6);                                         // quad row of the wave
-    const int x = tx * kTileW + 2 * (tid & 63), y = ty * kTileH + 2 * wv;  // quad origin (even)
+    const int x = a.work ? tx * kTileW + (int)((wk.x >> 24) & 3u) * kSubW + 2 * (lane & 15) : tx * kTileW + 2 * lane;
+    const int y = a.work ? ty * kTileH + 2 * (lane >> 4) : ty * kTileH + 2 * wv;  // quad origin (even)
     const bool top = a.level == a.bands;
     bool valid[4];
 #pragma unroll
@@ -353,7 +374,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     }
 #endif
     int R[4][3];
-    uint32_t m = (uint32_t)uniform((int)a.tile_cams[tile]);
+    uint32_t m = a.work ? (uint32_t)uniform((int)wk.y) : (uint32_t)uniform((int)a.tile_cams[tile]);
     // Tiles owned by one camera (its weight is exactly 1.0f on every tile pixel: seam 255 at level 0,
     // the f32 pyramid's 1.0f above; tile_owned): D = G - pyrUp(G_next) (G at the top level) exactly,
     // the weight sum is kWsumOwned and rint(D * kRcpOwned) = D (|D| <= 255), so the Laplacian is taken
@@ -361,7 +382,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     // Deep tiles (owned = 2, multiband_host.cpp): R = G on every pixel, by induction over the levels
     // above (one camera of weight 1 on all the pyrUp taps, with the camera's and the collapse's taps
     // identical), so neither pyrUp is taken.
-    const int own = a.work ? (int)(wk >> 24) : a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
+    const int own = a.work ? (int)(wk.x >> 27) : a.owned != nullptr ? uniform((int)a.owned[tile]) : 0;
     if (own == 3) return;  // no collapse reads this tile (levels >= 1)
     const bool deep = own == 2;
     if (own == 4) return;  // level 0: a deep tile whose result the remap wrote (kItemResult)
@@ -714,7 +735,7 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 
 hipError_t launch_mb_blend(const MbBlendArgs& a, hipStream_t s) {
     const int tiles_y = (a.H + kTileH - 1) / kTileH;
-    const int n = a.work ? a.n_work : a.tiles_x * tiles_y;
+    const int n = a.work ? a.n_work / 4 : a.tiles_x * tiles_y;  // (the list: 4 sub-tiles per workgroup)
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(mb_blend_kernel, dim3(n), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -54,14 +54,16 @@ class MultiBand {
         DevBuf<float> wts;              // level > 0: f32 weights over each align_roi >> l
         DevBuf<uint32_t> tile_cams;
         std::vector<uint32_t> tile_cams_h;
-        DevBuf<uint8_t> owned;          // multi-band: per tile, one camera of weight exactly 1 throughout
-                                        // (1), and R = G on every tile pixel (2, the deep pass); 3: read by no collapse
+        // multi-band, per 32 x 8 sub-tile (tile * kSubs + quarter): the cameras with a non-zero weight there,
+        // and its kind: 1 owned (one camera of weight exactly 1 throughout), 2 deep (R = G on every pixel,
+        // the deep pass), 3 read by no collapse, 4 (level 0) deep with its result written by the remap
+        std::vector<uint32_t> sub_cams_h;
+        std::vector<uint8_t> sub_own_h;
         int n_owned = 0;
-        int n_deep = 0;                 // owned tiles with R = G at this level (owned = 2)
-        int n_skip = 0;                 // tiles no collapse reads (owned = 3)
-        DevBuf<uint32_t> work;          // multi-band: the tiles mb_blend computes (owned not 3 or 4), in
-                                        // order, as tile | owned << 24
-        int n_work = -1;                // their count (-1: every tile, no list)
+        int n_deep = 0;                 // sub-tiles with R = G at this level (owned = 2 or 4)
+        int n_skip = 0;                 // sub-tiles no collapse reads (owned = 3)
+        DevBuf<uint2> work;             // multi-band: the sub-tiles mb_blend computes (kinds 0-2), MbBlendArgs::work
+        int n_work = -1;                // their count, padded to a multiple of 4 (-1: every tile, no list)
         DevBuf<UpQuad> up;              // per camera: rows then cols (level < B)
         DevBuf<UpQuad> rup;             // collapse: rows then cols (level < B)
         int rup_rows = 0;
@@ -114,6 +116,13 @@ int up_taps(int o, bool rows, int* u, int* w) {
     u[1] = (rows && (o & 7) == 7) ? ((o + 1) >> 1) + 1 : (o + 1) >> 1;
     w[0] = 4, w[1] = 4;
     return 2;
+}
+
+// The sub-tile (tile * kSubs + quarter) holding 8 x 8 block (bx, by) of a level grid tx_n tiles wide.
+constexpr int kBlkPx = 8;
+static_assert(kBlkPx == kTileH && kSubW % kBlkPx == 0, "blocks tile the sub-tiles");
+size_t sub_of_block(int tx_n, int bx, int by) {
+    return ((size_t)by * tx_n + (size_t)(bx * kBlkPx / kTileW)) * kSubs + (size_t)((bx * kBlkPx % kTileW) / kSubW);
 }
 
 // Tap table over the level grid's quad rows (cols): grid index g -> local index g - off, valid in
@@ -432,28 +441,37 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                 }
             }
             for (int8_t& o : om) o = o < 0 ? (int8_t)-1 : o;
-            std::vector<uint8_t> owned((size_t)L.tx_n * L.ty_n, 0);
+            // per sub-tile: its cameras (8 x 8 blocks lie in one sub-tile each) and whether it is owned
+            L.sub_cams_h.assign((size_t)L.tx_n * L.ty_n * kSubs, 0u);
+            for (int i = 0; i < n; i++)
+                for (int by = 0; by < by_n; by++)
+                    for (int bx = 0; bx < bx_n; bx++)
+                        if (act[l][i][(size_t)by * bx_n + bx]) L.sub_cams_h[sub_of_block(L.tx_n, bx, by)] |= 1u << i;
+            std::vector<uint8_t> owned(L.sub_cams_h.size(), 0);
             for (int ty = 0; ty < L.ty_n; ty++)
-                for (int tx = 0; tx < L.tx_n; tx++) {
-                    const uint32_t msk = L.tile_cams_h[(size_t)ty * L.tx_n + tx];
-                    if (__builtin_popcount(msk) != 1) continue;
-                    const int i = __builtin_ctz(msk);
-                    const auto& c = L.cams_h[i];
-                    const size_t woff = l == 0 ? seam_off[i] : (size_t)(static_cast<const float*>(c.weight) - L.wts.p);
-                    bool all = c.w >= 2;  // the fast path reads pixel pairs
-                    for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
-                        for (int x = tx * kTileW; x < std::min((tx + 1) * kTileW, L.W); x++) {
-                            const int xl = x - c.ox, yl = y - c.oy;
-                            const size_t k = woff + (size_t)yl * c.w + xl;
-                            if (xl < 0 || yl < 0 || xl >= c.w || yl >= c.h ||
-                                (l == 0 ? seam_h[k] != 255 : wl[k] != 1.0f)) {
-                                all = false;
-                                break;
+                for (int tx = 0; tx < L.tx_n; tx++)
+                    for (int q = 0; q < kSubs; q++) {
+                        const size_t sidx = ((size_t)ty * L.tx_n + tx) * kSubs + q;
+                        const uint32_t msk = L.sub_cams_h[sidx];
+                        if (__builtin_popcount(msk) != 1) continue;
+                        const int i = __builtin_ctz(msk);
+                        const auto& c = L.cams_h[i];
+                        const size_t woff = l == 0 ? seam_off[i] : (size_t)(static_cast<const float*>(c.weight) - L.wts.p);
+                        bool all = c.w >= 2;  // the fast path reads pixel pairs
+                        const int x0 = tx * kTileW + q * kSubW;
+                        for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
+                            for (int x = x0; x < std::min(x0 + kSubW, L.W); x++) {
+                                const int xl = x - c.ox, yl = y - c.oy;
+                                const size_t k = woff + (size_t)yl * c.w + xl;
+                                if (xl < 0 || yl < 0 || xl >= c.w || yl >= c.h ||
+                                    (l == 0 ? seam_h[k] != 255 : wl[k] != 1.0f)) {
+                                    all = false;
+                                    break;
+                                }
                             }
-                        }
-                    owned[(size_t)ty * L.tx_n + tx] = all ? 1 : 0;
-                    L.n_owned += all ? 1 : 0;
-                }
+                        owned[sidx] = all ? 1 : 0;
+                        L.n_owned += all ? 1 : 0;
+                    }
             owned_h[l] = std::move(owned);
         }
     }
@@ -579,44 +597,50 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                         if (deep_px(x, y)) deep[(size_t)y * L.W + x] = own_map[l][(size_t)y * L.W + x];
             }
             for (int ty = 0; ty < L.ty_n; ty++)
-                for (int tx = 0; tx < L.tx_n; tx++) {
-                    uint8_t& t = owned_h[l][(size_t)ty * L.tx_n + tx];
-                    if (!t) continue;
-                    bool all = true;
-                    for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
-                        for (int x = tx * kTileW; x < std::min((tx + 1) * kTileW, L.W); x++)
-                            if (l > 0 ? deep[(size_t)y * L.W + x] < 0 : !deep_px(x, y)) {
-                                all = false;
-                                break;
-                            }
-                    if (all && deep_on) t = 2, L.n_deep++;
-                }
+                for (int tx = 0; tx < L.tx_n; tx++)
+                    for (int q = 0; q < kSubs; q++) {
+                        uint8_t& t = owned_h[l][((size_t)ty * L.tx_n + tx) * kSubs + q];
+                        if (!t) continue;
+                        bool all = true;
+                        const int x0 = tx * kTileW + q * kSubW;
+                        for (int y = ty * kTileH; all && y < std::min((ty + 1) * kTileH, L.H); y++)
+                            for (int x = x0; x < std::min(x0 + kSubW, L.W); x++)
+                                if (l > 0 ? deep[(size_t)y * L.W + x] < 0 : !deep_px(x, y)) {
+                                    all = false;
+                                    break;
+                                }
+                        if (all && deep_on) t = 2, L.n_deep++;
+                    }
             deep_next = std::move(deep);
         }
-        // Tiles of level l >= 1 that no collapse reads (every level-(l-1) tile whose pyrUp taps reach them
-        // is deep or itself unread): owned = 3, mb_blend returns at once there, and their Gaussian blocks
-        // are not required for them (below).
+        // Sub-tiles of level l >= 1 that no collapse reads (every level-(l-1) sub-tile whose pyrUp taps reach
+        // them is deep or itself unread): owned = 3, mb_blend skips them, and their Gaussian blocks are not
+        // required for them (below).
         for (int l = 1; deep_on && l <= B; l++) {
             auto& L = M.lv[l];
             const auto& Lf = M.lv[l - 1];
-            std::vector<uint8_t> read((size_t)L.tx_n * L.ty_n, 0);
+            std::vector<uint8_t> read(owned_h[l].size(), 0);
             for (int ty = 0; ty < Lf.ty_n; ty++)
-                for (int tx = 0; tx < Lf.tx_n; tx++) {
-                    const uint8_t t = owned_h[l - 1][(size_t)ty * Lf.tx_n + tx];
-                    if (t >= 2) continue;  // deep (2, 4) or unread (3): no collapse reads level l there
-                    int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
-                    for (int q = ty * kTileH / 2; q < (ty + 1) * kTileH / 2; q++)
-                        for (int j = 0; j < 3; j++)
-                            if (rup_r[l - 1][q].w0[j] | rup_r[l - 1][q].w1[j])
-                                r0 = std::min(r0, (int)rup_r[l - 1][q].idx[j]), r1 = std::max(r1, (int)rup_r[l - 1][q].idx[j]);
-                    for (int q = tx * kTileW / 2; q < (tx + 1) * kTileW / 2; q++)
-                        for (int j = 0; j < 3; j++)
-                            if (rup_c[l - 1][q].w0[j] | rup_c[l - 1][q].w1[j])
-                                c0 = std::min(c0, (int)rup_c[l - 1][q].idx[j]), c1 = std::max(c1, (int)rup_c[l - 1][q].idx[j]);
-                    if (r1 < 0 || c1 < 0) continue;
-                    for (int y = r0 / kTileH; y <= std::min(r1 / kTileH, L.ty_n - 1); y++)
-                        for (int x = c0 / kTileW; x <= std::min(c1 / kTileW, L.tx_n - 1); x++) read[(size_t)y * L.tx_n + x] = 1;
-                }
+                for (int tx = 0; tx < Lf.tx_n; tx++)
+                    for (int sq = 0; sq < kSubs; sq++) {
+                        const uint8_t t = owned_h[l - 1][((size_t)ty * Lf.tx_n + tx) * kSubs + sq];
+                        if (t >= 2) continue;  // deep (2, 4) or unread (3): no collapse reads level l there
+                        int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
+                        for (int q = ty * kTileH / 2; q < (ty + 1) * kTileH / 2; q++)
+                            for (int j = 0; j < 3; j++)
+                                if (rup_r[l - 1][q].w0[j] | rup_r[l - 1][q].w1[j])
+                                    r0 = std::min(r0, (int)rup_r[l - 1][q].idx[j]), r1 = std::max(r1, (int)rup_r[l - 1][q].idx[j]);
+                        const int qc = (tx * kTileW + sq * kSubW) / 2;
+                        for (int q = qc; q < qc + kSubW / 2; q++)
+                            for (int j = 0; j < 3; j++)
+                                if (rup_c[l - 1][q].w0[j] | rup_c[l - 1][q].w1[j])
+                                    c0 = std::min(c0, (int)rup_c[l - 1][q].idx[j]), c1 = std::max(c1, (int)rup_c[l - 1][q].idx[j]);
+                        if (r1 < 0 || c1 < 0) continue;
+                        const int cmax = L.tx_n * kTileW - 1;
+                        for (int y = r0 / kTileH; y <= std::min(r1 / kTileH, L.ty_n - 1); y++)
+                            for (int x = c0 / kSubW; x <= std::min(c1, cmax) / kSubW; x++)
+                                read[(size_t)y * L.tx_n * kSubs + x] = 1;  // a tile row's sub-tiles are consecutive
+                    }
             for (size_t t = 0; t < read.size(); t++)
                 if (!read[t]) {
                     L.n_deep -= owned_h[l][t] == 2 ? 1 : 0;
@@ -624,43 +648,45 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                     L.n_skip++;
                 }
         }
-        for (int l = 0; l <= B; l++) M.lv[l].owned.upload(owned_h[l].data(), owned_h[l].size());
     }
-    // ---- deep level-0 tiles: the remap writes their result (kItemResult) ----------------------------
-    // A deep level-0 tile's result is its one camera's G0 (R = G, above), so the MODE-1 remap item of that
-    // camera converts it to YUV420P (or the RGBA result) right away and mb_blend skips the tile (owned 4):
-    // its G0 is then needed only where a level-1 pyrDown reads it.  Only tiles wholly inside the crop and
-    // the output frame qualify (the remap's result stores take no bounds).  (OCTVR_MB_NO_REMAP_RESULT=1:
-    // measurement / cross-check knob, the level-0 blend writes every tile.)
-    std::vector<int8_t> deep0_owner;  // per level-0 tile: the camera of a remap-result tile, else -1
+    // ---- deep level-0 sub-tiles: the remap writes their result (item_result_bit) --------------------
+    // A deep level-0 sub-tile's result is its one camera's G0 (R = G, above), so the MODE-1 remap item of that
+    // camera converts it to YUV420P (or the RGBA result) right away and mb_blend skips it (owned 4): its
+    // G0 is then needed only where a level-1 pyrDown reads it.  Only sub-tiles wholly inside the crop and the
+    // output frame qualify (the remap's result stores take no bounds).  (OCTVR_MB_NO_REMAP_RESULT=1:
+    // measurement / cross-check knob, the level-0 blend writes every sub-tile.)
+    std::vector<int8_t> deep0_owner;  // per level-0 sub-tile: the camera of a remap-result sub-tile, else -1
     if (!M.feather && deep_on && std::getenv("OCTVR_MB_NO_REMAP_RESULT") == nullptr) {
         auto& L0 = M.lv[0];
-        deep0_owner.assign((size_t)L0.tx_n * L0.ty_n, (int8_t)-1);
+        deep0_owner.assign(owned_h[0].size(), (int8_t)-1);
         for (int ty = 0; ty < L0.ty_n; ty++)
-            for (int tx = 0; tx < L0.tx_n; tx++) {
-                const size_t t = (size_t)ty * L0.tx_n + tx;
-                const int x1 = (tx + 1) * kTileW, y1 = (ty + 1) * kTileH;
-                if (owned_h[0][t] != 2 || x1 > M.crop_w || y1 > M.crop_h || M.arr.x + x1 > rig.out_w ||
-                    M.arr.y + y1 > rig.out_h)
-                    continue;
-                deep0_owner[t] = (int8_t)__builtin_ctz(L0.tile_cams_h[t]);
-                owned_h[0][t] = 4;
-                M.n_result++;
-            }
+            for (int tx = 0; tx < L0.tx_n; tx++)
+                for (int q = 0; q < kSubs; q++) {
+                    const size_t t = ((size_t)ty * L0.tx_n + tx) * kSubs + q;
+                    const int x1 = tx * kTileW + (q + 1) * kSubW, y1 = (ty + 1) * kTileH;
+                    if (owned_h[0][t] != 2 || x1 > M.crop_w || y1 > M.crop_h || M.arr.x + x1 > rig.out_w ||
+                        M.arr.y + y1 > rig.out_h)
+                        continue;
+                    deep0_owner[t] = (int8_t)__builtin_ctz(L0.sub_cams_h[t]);
+                    owned_h[0][t] = 4;
+                    M.n_result++;
+                }
         M.deep_in_remap = M.n_result > 0;
-        L0.owned.upload(owned_h[0].data(), owned_h[0].size());
     }
-    // ---- per level, the tiles mb_blend has work on: it is launched over this list only, so the tiles that
-    // return at once (unread: owned 3, written by the remap: owned 4) cost no workgroup dispatch (C3 level
-    // 0: 23,040 of 28,800 tiles)
+    // ---- per level, the sub-tiles mb_blend has work on (kinds 0-2), 4 per workgroup: it is launched over
+    // this list only, so sub-tiles that need nothing (unread: 3, written by the remap: 4) cost no dispatch
     if (!M.feather) {
         for (int l = 0; l <= B; l++) {
             auto& L = M.lv[l];
-            if (owned_h[l].empty()) continue;
-            REQUIRE(owned_h[l].size() < (1u << 24), "multi-band: level grid too large");
-            std::vector<uint32_t> work;
+            L.sub_own_h = owned_h[l];
+            REQUIRE((size_t)L.tx_n * L.ty_n < (1u << 24), "multi-band: level grid too large");
+            std::vector<uint2> work;
             for (size_t t = 0; t < owned_h[l].size(); t++)
-                if (owned_h[l][t] != 3 && owned_h[l][t] != 4) work.push_back((uint32_t)t | (uint32_t)owned_h[l][t] << 24);
+                if (owned_h[l][t] < 3)
+                    work.push_back(make_uint2((uint32_t)(t / kSubs) | (uint32_t)(t % kSubs) << 24 |
+                                                  (uint32_t)owned_h[l][t] << 27,
+                                              L.sub_cams_h[t]));
+            while (work.size() % 4) work.push_back(make_uint2(3u << 27, 0u));
             L.n_work = (int)work.size();
             if (!work.empty()) L.work.upload(work.data(), work.size());
         }
@@ -670,17 +696,17 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     // (level 0 with deep tiles written by the remap: their weight blocks need no G0)
     std::vector<std::vector<Bitmap>> req(B + 1, std::vector<Bitmap>(n));  // tiles
     std::vector<std::vector<uint8_t>> need_next(n);                       // blocks of level l + 1
+    std::vector<std::vector<uint8_t>> req0_sub(n);                        // level 0, per sub-tile
     for (int l = B; l >= 0; l--) {
         auto& L = M.lv[l];
         const int bx_n = (L.W + kBlk - 1) / kBlk, by_n = (L.H + kBlk - 1) / kBlk;
         for (int i = 0; i < n; i++) {
             const auto& c = L.cams_h[i];
             std::vector<uint8_t> need = act[l][i];
-            auto tile_of = [&](int lv_, int bx, int by) {  // owned flag of the tile holding block (bx, by)
-                const auto& Lt = M.lv[lv_];
-                return owned_h[lv_].empty() ? 0 : (int)owned_h[lv_][(size_t)(by * kBlk / kTileH) * Lt.tx_n + bx * kBlk / kTileW];
+            auto tile_of = [&](int lv_, int bx, int by) {  // kind of the sub-tile holding block (bx, by)
+                return owned_h[lv_].empty() ? 0 : (int)owned_h[lv_][sub_of_block(M.lv[lv_].tx_n, bx, by)];
             };
-            for (int by = 0; by < by_n; by++)  // blocks of unread tiles: no blend reads G there
+            for (int by = 0; by < by_n; by++)  // blocks of unread / remap-result sub-tiles: no blend reads G there
                 for (int bx = 0; bx < bx_n; bx++)
                     if (tile_of(l, bx, by) == 3 || tile_of(l, bx, by) == 4) need[(size_t)by * bx_n + bx] = 0;
             auto mark = [&](int x0, int y0, int x1, int y1) {  // level-grid pixel rectangle, inclusive
@@ -695,7 +721,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                 for (int by = 0; by < fby; by++)
                     for (int bx = 0; bx < fbx; bx++) {
                         if (!act[l - 1][i][(size_t)by * fbx + bx]) continue;
-                        if (tile_of(l - 1, bx, by) >= 2) continue;  // deep / unread: no pyrUp of G_l there
+                        if (tile_of(l - 1, bx, by) >= 2) continue;  // deep / unread / result: no pyrUp of G_l there
                         int r0 = INT32_MAX, r1 = -1, c0 = INT32_MAX, c1 = -1;
                         for (int q = by * kBlk / 2; q < (by + 1) * kBlk / 2; q++) {
                             const UpQuad& u = ur[l - 1][i][q];
@@ -733,6 +759,12 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
                                (by + 1) * kBlk > c.oy))
                         v = 0;
                 }
+            if (l == 0) {  // the remap writes G0 per sub-tile (item_g0_bit)
+                req0_sub[i].assign((size_t)L.tx_n * L.ty_n * kSubs, 0);
+                for (int by = 0; by < by_n; by++)
+                    for (int bx = 0; bx < bx_n; bx++)
+                        if (need[(size_t)by * bx_n + bx]) req0_sub[i][sub_of_block(L.tx_n, bx, by)] = 1;
+            }
             Bitmap& R = req[l][i];
             R.init(L.tx_n, L.ty_n);
             for (int by = 0; by < by_n; by++)
@@ -763,23 +795,23 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         auto& L0 = M.lv[0];
         // items of qpl vertically adjacent tiles (128 x 8 qpl), kept when any of them is required
         const int qpl = composite_qpl();
-        // per half: G0 written where required (else kItemNoG0), the result where the tile is deep and
-        // this camera owns it (kItemResult)
+        REQUIRE(qpl <= 2, "multi-band remap: items of at most 2 tiles (item flags)");
+        // per half and sub-tile: G0 written where required (item_g0_bit), the result where the sub-tile is
+        // deep and this camera owns it (item_result_bit)
         std::vector<TileJob> jobs;
         for (int i = 0; i < n; i++)
             for (int ty = 0; ty < (L0.ty_n + qpl - 1) / qpl; ty++)
                 for (int tx = 0; tx < L0.tx_n; tx++) {
-                    bool any = false;
                     uint32_t fl = 0;
                     for (int h = 0; h < qpl; h++) {
-                        const size_t t = (size_t)(ty * qpl + h) * L0.tx_n + tx;
-                        const bool in = ty * qpl + h < L0.ty_n;
-                        const bool g0 = in && req[0][i].b[t] != 0;
-                        const bool res = in && !deep0_owner.empty() && deep0_owner[t] == i;
-                        any |= g0 || res;
-                        fl |= (g0 ? 0u : kItemNoG0 << h) | (res ? kItemResult << h : 0u);
+                        if (ty * qpl + h >= L0.ty_n) continue;
+                        for (int q = 0; q < kSubs; q++) {
+                            const size_t t = ((size_t)(ty * qpl + h) * L0.tx_n + tx) * kSubs + q;
+                            if (req0_sub[i][t]) fl |= item_g0_bit(h, q);
+                            if (!deep0_owner.empty() && deep0_owner[t] == i) fl |= item_result_bit(h, q);
+                        }
                     }
-                    if (any) jobs.push_back(TileJob{tx, ty, i, fl});
+                    if (fl) jobs.push_back(TileJob{tx, ty, i, fl});
                 }
         const Rect arr = M.arr;
         auto entry = [&](int job, int x, int y) -> CompositeEntry {
@@ -880,7 +912,7 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
         a.H = L.H;
         a.tiles_x = L.tx_n;
         a.tile_cams = L.tile_cams.p;
-        a.owned = L.owned.p;
+        a.owned = nullptr;  // (the tile kinds travel in the work list)
         a.work = L.n_work >= 0 ? L.work.p : nullptr;
         a.n_work = L.n_work;
         a.cams = L.cams.p;
@@ -920,7 +952,7 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
 //   remap:   4 B tiled entry per item pixel (8 B wide), the G0 halves it writes (4 B / px), the deep
 //            tiles' results (1.5 B / px YUV420P), the unique source bytes of its staged boxes, metadata;
 //   down l:  4 B written per level-l item pixel, its 2 x 2 level-(l-1) source (16 B / px);
-//   blend l: per tile by kind — unread (owned 3): nothing; deep (2): G 4 B + R 8 B (level 0: nothing
+//   blend l: per sub-tile by kind — unread (owned 3): nothing; deep (2): G 4 B + R 8 B (level 0: nothing
 //            when the remap wrote it, else 1.5 B out); owned (1): G 4 B + coarser G taps 1 B + collapsed
 //            coarser level 2 B + R 8 B / out 1.5 B; general: per weighted camera G 4 B + weight (1 B u8
 //            seam at level 0, else 4 B f32) + coarser G 1 B, then coarser R 2 B + R 8 B / out 1.5 B.
@@ -936,15 +968,14 @@ std::vector<std::pair<std::string, double>> multiband_traffic_parts(const MultiB
         const auto& L = M.lv[l];
         const bool up = l < M.B;
         const double out_b = l ? 8.0 : 1.5;
-        std::vector<uint8_t> own;
-        if (L.owned.p) {
-            own.resize(L.owned.n);
-            HIP_CHECK(hipMemcpy(own.data(), L.owned.p, own.size(), hipMemcpyDeviceToHost));
-        }
+        // per sub-tile (multi-band) or per tile (feather: every tile general)
+        const bool sub = !L.sub_own_h.empty();
+        const std::vector<uint32_t>& cams = sub ? L.sub_cams_h : L.tile_cams_h;
+        const double unit_px = sub ? (double)kSubW * kTileH : (double)kTilePx;
         double b = 0;
-        for (size_t k = 0; k < L.tile_cams_h.size(); k++) {
-            const uint32_t m = L.tile_cams_h[k];
-            const int o = own.empty() ? 0 : own[k];
+        for (size_t k = 0; k < cams.size(); k++) {
+            const uint32_t m = cams[k];
+            const int o = sub ? L.sub_own_h[k] : 0;
             double px_b = 0;
             if (o == 3) {
                 px_b = 0;
@@ -960,7 +991,7 @@ std::vector<std::pair<std::string, double>> multiband_traffic_parts(const MultiB
             } else {
                 px_b = (up ? 2.0 : 0.0) + out_b;  // no camera: the collapse alone
             }
-            b += px_b * kTilePx;
+            b += px_b * unit_px;
         }
         parts.emplace_back("blend" + std::to_string(l), b);
     }
@@ -978,7 +1009,7 @@ std::string multiband_info(const MultiBand& M) {
                     std::to_string(M.arr.y) + ", " + std::to_string(M.arr.w) + ", " + std::to_string(M.arr.h) +
                     "], \"remap_items\": " + std::to_string(M.remap.view.n_items) +
                     ", \"remap_wide\": " + std::to_string(M.remap.view.n_wide) +
-                    ", \"remap_result_tiles\": " + std::to_string(M.n_result) + ", \"traffic_parts\": {";
+                    ", \"remap_result_subtiles\": " + std::to_string(M.n_result) + ", \"traffic_parts\": {";
     {
         bool first = true;
         for (const auto& p : multiband_traffic_parts(M)) {
@@ -993,11 +1024,12 @@ std::string multiband_info(const MultiBand& M) {
         const auto& L = M.lv[l];
         size_t cam_tiles = 0;
         for (uint32_t m : L.tile_cams_h) cam_tiles += (size_t)__builtin_popcount(m);
-        char buf[288];
+        char buf[512];
         snprintf(buf, sizeof buf, "%s{\"tiles\": %d, \"required\": %zu, \"weight_cam_tiles\": %zu, \"down_items\": %d%s}",
                  l ? ", " : "", L.tx_n * L.ty_n, L.req_tiles, cam_tiles, L.n_down,
-                 L.owned.p ? (", \"owned_tiles\": " + std::to_string(L.n_owned) + ", \"deep_tiles\": " +
-                              std::to_string(L.n_deep) + ", \"unread_tiles\": " + std::to_string(L.n_skip)).c_str() : "");
+                 !L.sub_own_h.empty() ? (", \"blend_subtiles\": " + std::to_string(L.n_work) + ", \"owned_subtiles\": " +
+                              std::to_string(L.n_owned) + ", \"deep_subtiles\": " + std::to_string(L.n_deep) +
+                              ", \"unread_subtiles\": " + std::to_string(L.n_skip)).c_str() : "");
         s += buf;
     }
     return s + "]";

@@ -161,8 +161,9 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             const TileJob& J = jobs[t];
             for (int h = 0; h < qpl; h++) {
                 b.wide_tiles.push_back((uint32_t)J.tx | ((uint32_t)(J.ty * qpl + h) << 16));
-                b.wide_cams.push_back((uint8_t)(J.cam | ((J.flags >> h) & kItemResult ? 32 : 0) |
-                                                 ((J.flags >> h) & kItemNoG0 ? 64 : 0)));
+                // the half's quarters as half 0's bits: results at bits 8-11, G0 at bits 12-15
+                const uint32_t rq = (J.flags >> (4 * h)) & 15u, gq = (J.flags >> (8 + 4 * h)) & 15u;
+                b.wide_cams.push_back((uint16_t)(J.cam | rq << 8 | gq << 12));
                 b.wide.insert(b.wide.end(), wide_raw[t].begin() + (size_t)h * kTilePx,
                               wide_raw[t].begin() + (size_t)(h + 1) * kTilePx);
             }
@@ -176,7 +177,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                       b.entries.begin() + (size_t)n_items * item_px);
         }
         b.staged_bytes += 8.0 * b.hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes per 4-pixel group
-        b.item_flags.push_back((uint8_t)jobs[t].flags);
+        b.item_flags.push_back((uint16_t)jobs[t].flags);
         n_items++;
     }
     b.n_items = n_items;
@@ -281,7 +282,7 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
             for (int j = 1; j < kTileSlots; j++) q += (j < ns && c >= (int)b.slots[t * kTileSlots + j].chunk0) ? 1 : 0;
             map |= (uint32_t)q << (2 * c);
         }
-        if (t < b.item_flags.size()) map |= (uint32_t)b.item_flags[t] << 8;  // RGBA mode: kItemResult / kItemNoG0
+        if (t < b.item_flags.size()) map |= (uint32_t)b.item_flags[t] << 8;  // RGBA mode: item_result_bit / item_g0_bit
         m[t * kMetaWords].stage_groups = map;
         std::memcpy(&m[t * kMetaWords + 1], &b.slots[t * kTileSlots], kTileSlots * sizeof(TileSlot));
     }
@@ -299,16 +300,17 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     source_bytes = b.source_bytes;
     result_bytes = 0;
     g0_bytes = 0;
-    for (size_t t = 0; t < b.item_flags.size(); t++)
-        for (int h = 0; h < b.qpl; h++) {
-            const uint32_t f = (uint32_t)b.item_flags[t] >> h;
-            g0_bytes += (f & kItemNoG0) ? 0.0 : 4.0 * kTilePx;
-            result_bytes += (f & kItemResult) ? 1.0 * kTilePx : 0.0;  // result pixels (bytes: x 1.5 or 4)
-        }
-    for (uint8_t c : b.wide_cams) {
-        g0_bytes += (c & 64) ? 0.0 : 4.0 * kTilePx;
-        result_bytes += (c & 32) ? 1.0 * kTilePx : 0.0;
+    constexpr double kSubPx = (double)kSubW * kTileH;
+    for (size_t t = 0; t < b.item_flags.size(); t++) {
+        const uint32_t f = b.item_flags[t];
+        g0_bytes += 4.0 * kSubPx * __builtin_popcount(f & 0xFF00u);
+        result_bytes += kSubPx * __builtin_popcount(f & 0xFFu);  // result pixels (bytes: x 1.5 or 4)
     }
+    if (!b.item_flags.empty())
+        for (uint16_t c : b.wide_cams) {
+            g0_bytes += 4.0 * kSubPx * __builtin_popcount((uint32_t)c >> 12);
+            result_bytes += kSubPx * __builtin_popcount(((uint32_t)c >> 8) & 15u);
+        }
     if (b.item_flags.empty()) g0_bytes = 4.0 * kTilePx * ((double)b.n_items * b.qpl + b.n_wide);  // no flags: every half
     stats = b.stats;
     view = TiledLut{meta.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,

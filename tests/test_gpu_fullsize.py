@@ -116,8 +116,8 @@ def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch, scale):
             monkeypatch.setenv(knob, "1")
         m = ox.Mapper(mt, sizes, blend=synthetic.BLEND["C3"], enable_gain=True, scale_output=scale)
         info = m.info()
-        deep.append([t["deep_tiles"] for t in info["level_tiles"]])
-        res.append(info["remap_result_tiles"])
+        deep.append([t["deep_subtiles"] for t in info["level_tiles"]])
+        res.append(info["remap_result_subtiles"])
         out = torch.zeros((OH * 3 // 2, OW), dtype=torch.uint8, device="cuda")
         m.stitch(frames, out, gains=[1.0] * len(sizes))
         torch.cuda.synchronize()
@@ -126,7 +126,7 @@ def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch, scale):
         if knob:
             monkeypatch.delenv(knob)
     print(deep, res)
-    assert deep[0][0] > 0 and res[0] > 0.7 * 28800  # C3: 23,040 deep level-0 tiles of 28,800
+    assert deep[0][0] > 0 and res[0] > 0.7 * 4 * 28800  # C3: 28,800 level-0 tiles of 4 sub-tiles each
     assert res[1] == 0 and deep[1][0] == deep[0][0]
     assert sum(deep[2]) == 0 and res[2] == 0
     for k in (1, 2):

@@ -417,8 +417,8 @@ def test_gpu_multiband_deep_tiles(ox):
             info = []
             got, want, _, _ = _stitch_case(ox, name, synthetic.smooth_yuv_frame, None, blend=blend, info=info)
             lv = info[0]["level_tiles"]
-            deep[(name, blend)] = [t.get("deep_tiles", 0) for t in lv]
-            assert all(t["deep_tiles"] <= t["owned_tiles"] for t in lv)
+            deep[(name, blend)] = [t.get("deep_subtiles", 0) for t in lv]
+            assert all(t["deep_subtiles"] <= t["owned_subtiles"] for t in lv)
             d = got != want
             assert not d.any(), (name, blend, int(d.sum()), np.argwhere(d)[:5].tolist())
     print(deep)
