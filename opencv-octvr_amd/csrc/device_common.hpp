@@ -54,6 +54,20 @@ __device__ __forceinline__ void yuv2_to_rgba(uint32_t y0, uint32_t y1, uint32_t 
     p1 = pack_u8(B.y, 2, pack_u8(G.y, 1, pack_u8(R.y, 0, 0u)));
 }
 
+// yuv_to_rgba of two pixels with their own chroma: bytes 0 and 1 of y, u, v; each fma issued for both
+// as one v_pk_fma_f32 (every element rounded as yuv_to_rgba's)
+__device__ __forceinline__ void yuv_pair_to_rgba(uint32_t y, uint32_t u, uint32_t v, uint32_t& p0, uint32_t& p1) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const f2 Y = {(float)(y & 255u), (float)((y >> 8) & 255u)};
+    const f2 U = f2{(float)(u & 255u), (float)((u >> 8) & 255u)} - f2{128.f, 128.f};
+    const f2 V = f2{(float)(v & 255u), (float)((v >> 8) & 255u)} - f2{128.f, 128.f};
+    const f2 R = __builtin_elementwise_fma(f2{1.140f, 1.140f}, V, Y);
+    const f2 G = __builtin_elementwise_fma(f2{-0.581f, -0.581f}, V, __builtin_elementwise_fma(f2{-0.394f, -0.394f}, U, Y));
+    const f2 B = __builtin_elementwise_fma(f2{2.032f, 2.032f}, U, Y);
+    p0 = pack_u8(B.x, 2, pack_u8(G.x, 1, pack_u8(R.x, 0, 0u)));
+    p1 = pack_u8(B.y, 2, pack_u8(G.y, 1, pack_u8(R.y, 0, 0u)));
+}
+
 // yuv2_to_rgba with the chroma already as the floats u - 128, v - 128
 __device__ __forceinline__ void yuv2_to_rgba_c(uint32_t y0, uint32_t y1, float Uf, float Vf, uint32_t& p0,
                                                uint32_t& p1) {

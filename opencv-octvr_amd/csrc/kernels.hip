@@ -396,90 +396,72 @@ __device__ __forceinline__ void gain_system_row(const double* I, const int32_t* 
     b[i] = bi;
 }
 
-// Gain-feed gathers: per sample the 2 luma and 2 chroma rows of its 2x2 taps as 8-byte buffer loads
-// from 4-byte aligned starts (6 loads instead of 12 byte loads).  The frame-sized buffer resource
-// range-checks whole dwords, so a load may not reach past the frame's last byte (the last chroma row
-// of a tight-pitch frame whose V row ends mid-dword): every start is clamped to size - 8 and the tap
-// bytes are taken relative to the clamped start.  The taps are extracted and converted in
-// feed_taps_finish, after every sample's loads are in flight.
+// Gain-feed gathers: per sample the 2 luma, 2 U and 2 V row segments of its 2x2 taps as 8-byte buffer
+// loads from 4-byte aligned starts (6 loads instead of 12 byte loads).  The frame-sized buffer resource
+// range-checks whole dwords, so a load may not reach past the frame's last byte: only a V row segment of
+// the last chroma row can (Y rows are followed by the chroma rows, U halves by V halves), and its start
+// is clamped to size - 8, the bytes taken relative to the clamped start.  Everything the extraction
+// needs — the tap bytes' positions in the 8 loaded bytes as v_perm selectors, the taps' in-image flags,
+// the fractions — is derived once at issue and carried to feed_taps_finish, after every sample's loads
+// are in flight.
 struct FeedRaw {
     uint2 y0, y1, u0, u1, v0, v1;
-    uint32_t xy, code;
+    uint32_t sel;   // bytes of taps x0, x1: luma (bits 0-15), chroma (16-31), as v_perm selectors
+    uint32_t meta;  // code bits 0-15 (fx, fy, valid), in-image ix0 ix1 iy0 iy1 at 16-19, V row shifts at 20-22 / 23-25
 };
-
-// The six row segments of a sample's taps: row base offsets in the frame (Y row y0, y1; U and V rows
-// y0/2, y1/2) and the clamped 8-byte load starts.
-struct FeedRows {
-    uint32_t by0, by1, bu0, bu1, bv0, bv1;  // offsets of the rows' first bytes
-    uint32_t sy0, sy1, su0, su1, sv0, sv1;  // load starts
-};
-__device__ __forceinline__ FeedRows feed_rows(const SourceFrame& f, const TapCell& tc) {
-    const uint32_t p = (uint32_t)f.pitch;
-    const uint32_t lim = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2) - 8u;  // frames >= 8 B (host check)
-    const uint32_t uo = (uint32_t)f.h * p, vo = uo + (uint32_t)(f.w >> 1);
-    const uint32_t xa = (uint32_t)tc.x0 & ~3u, ca = ((uint32_t)tc.x0 >> 1) & ~3u;
-    FeedRows r;
-    r.by0 = (uint32_t)tc.y0 * p;
-    r.by1 = (uint32_t)tc.y1 * p;
-    r.bu0 = uo + (uint32_t)(tc.y0 >> 1) * p;
-    r.bu1 = uo + (uint32_t)(tc.y1 >> 1) * p;
-    r.bv0 = vo + (uint32_t)(tc.y0 >> 1) * p;
-    r.bv1 = vo + (uint32_t)(tc.y1 >> 1) * p;
-    r.sy0 = min(r.by0 + xa, lim);
-    r.sy1 = min(r.by1 + xa, lim);
-    r.su0 = min(r.bu0 + ca, lim);
-    r.su1 = min(r.bu1 + ca, lim);
-    r.sv0 = min(r.bv0 + ca, lim);
-    r.sv1 = min(r.bv1 + ca, lim);
-    return r;
-}
 
 __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
                                                 uint32_t code, FeedRaw& r) {
-    const FeedRows w = feed_rows(f, tap_cell(xy, f.w, f.h));
+    const TapCell tc = tap_cell(xy, f.w, f.h);
+    const uint32_t p = (uint32_t)f.pitch;
+    const uint32_t lim = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2) - 8u;  // frames >= 8 B (host check)
+    const uint32_t uo = (uint32_t)f.h * p, vo = uo + (uint32_t)(f.w >> 1);
+    const uint32_t x0 = (uint32_t)tc.x0, x1 = (uint32_t)tc.x1, c0 = x0 >> 1, c1 = x1 >> 1;
+    const uint32_t xa = x0 & ~3u, ca = c0 & ~3u;
+    const uint32_t ry0 = (uint32_t)tc.y0 * p, ry1 = (uint32_t)tc.y1 * p;
+    const uint32_t rc0 = (uint32_t)(tc.y0 >> 1) * p, rc1 = (uint32_t)(tc.y1 >> 1) * p;
+    const uint32_t sv0 = vo + rc0 + ca, sv1 = vo + rc1 + ca;
+    const uint32_t lv0 = min(sv0, lim), lv1 = min(sv1, lim);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 t;
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sy0, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, ry0 + xa, 0, 0);
     r.y0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sy1, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, ry1 + xa, 0, 0);
     r.y1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.su0, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + rc0 + ca, 0, 0);
     r.u0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.su1, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + rc1 + ca, 0, 0);
     r.u1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sv0, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv0, 0, 0);
     r.v0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, w.sv1, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv1, 0, 0);
     r.v1 = make_uint2(t.x, t.y);
-    r.xy = xy;
-    r.code = code;
-}
-
-// byte k (0-7) of an 8-byte row segment
-__device__ __forceinline__ uint32_t seg_byte(const uint2& v, uint32_t k) {
-    return (uint32_t)(((((uint64_t)v.y) << 32) | v.x) >> (8u * k)) & 255u;
+    const uint32_t iy = x0 & 3u, ic = c0 & 3u;  // x1 - x0, c1 - c0 in {0, 1}
+    r.sel = iy | (iy + (x1 - x0)) << 8 | ic << 16 | (ic + (c1 - c0)) << 24;
+    r.meta = (code & 0xFFFFu) | (tc.ix0 ? 1u << 16 : 0u) | (tc.ix1 ? 1u << 17 : 0u) | (tc.iy0 ? 1u << 18 : 0u) |
+             (tc.iy1 ? 1u << 19 : 0u) | (sv0 - lv0) << 20 | (sv1 - lv1) << 23;
 }
 
 // Same taps, validity and conversions as gather_taps_frame (device_common.hpp), without vignette.
-__device__ __forceinline__ void feed_taps_finish(const SourceFrame& f, const FeedRaw& r, Taps& t) {
-    const bool valid = (r.code & 0x8000u) != 0;
-    const TapCell tc = tap_cell(r.xy, f.w, f.h);
-    const FeedRows w = feed_rows(f, tc);
-    const uint32_t x0 = (uint32_t)tc.x0, x1 = (uint32_t)tc.x1, c0 = x0 >> 1, c1 = x1 >> 1;
-    const uint32_t ca = yuv_to_rgba(seg_byte(r.y0, w.by0 + x0 - w.sy0), seg_byte(r.u0, w.bu0 + c0 - w.su0),
-                                    seg_byte(r.v0, w.bv0 + c0 - w.sv0));
-    const uint32_t cb = yuv_to_rgba(seg_byte(r.y0, w.by0 + x1 - w.sy0), seg_byte(r.u0, w.bu0 + c1 - w.su0),
-                                    seg_byte(r.v0, w.bv0 + c1 - w.sv0));
-    const uint32_t cc = yuv_to_rgba(seg_byte(r.y1, w.by1 + x0 - w.sy1), seg_byte(r.u1, w.bu1 + c0 - w.su1),
-                                    seg_byte(r.v1, w.bv1 + c0 - w.sv1));
-    const uint32_t cd = yuv_to_rgba(seg_byte(r.y1, w.by1 + x1 - w.sy1), seg_byte(r.u1, w.bu1 + c1 - w.su1),
-                                    seg_byte(r.v1, w.bv1 + c1 - w.sv1));
-    t.c[0] = (valid && tc.ix0 && tc.iy0) ? ca : 0u;
-    t.c[1] = (valid && tc.ix1 && tc.iy0) ? cb : 0u;
-    t.c[2] = (valid && tc.ix0 && tc.iy1) ? cc : 0u;
-    t.c[3] = (valid && tc.ix1 && tc.iy1) ? cd : 0u;
-    t.fx = r.code & 31u;
-    t.fy = (r.code >> 5) & 31u;
+__device__ __forceinline__ void feed_taps_finish(const FeedRaw& r, Taps& t) {
+    const uint32_t m = r.meta;
+    const uint32_t sy = (r.sel & 0xFFFFu) | 0x0C0C0000u, sc = (r.sel >> 16) | 0x0C0C0000u;
+    const uint32_t sv0 = sc + ((m >> 20) & 7u) * 0x0101u, sv1 = sc + ((m >> 23) & 7u) * 0x0101u;
+    // two tap bytes of each row segment in bytes 0, 1
+    const uint32_t Y0 = __builtin_amdgcn_perm(r.y0.y, r.y0.x, sy), Y1 = __builtin_amdgcn_perm(r.y1.y, r.y1.x, sy);
+    const uint32_t U0 = __builtin_amdgcn_perm(r.u0.y, r.u0.x, sc), U1 = __builtin_amdgcn_perm(r.u1.y, r.u1.x, sc);
+    const uint32_t V0 = __builtin_amdgcn_perm(r.v0.y, r.v0.x, sv0), V1 = __builtin_amdgcn_perm(r.v1.y, r.v1.x, sv1);
+    uint32_t ca, cb, cc, cd;
+    yuv_pair_to_rgba(Y0, U0, V0, ca, cb);
+    yuv_pair_to_rgba(Y1, U1, V1, cc, cd);
+    const bool valid = (m & 0x8000u) != 0;
+    const bool ix0 = (m >> 16) & 1u, ix1 = (m >> 17) & 1u, iy0 = (m >> 18) & 1u, iy1 = (m >> 19) & 1u;
+    t.c[0] = (valid && ix0 && iy0) ? ca : 0u;
+    t.c[1] = (valid && ix1 && iy0) ? cb : 0u;
+    t.c[2] = (valid && ix0 && iy1) ? cc : 0u;
+    t.c[3] = (valid && ix1 && iy1) ? cd : 0u;
+    t.fx = m & 31u;
+    t.fy = (m >> 5) & 31u;
 }
 
 // LEAN = false: every sample's gathers in flight at once (kGainPer samples per lane) and the register
@@ -539,7 +521,7 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
 #pragma unroll
                 for (int u = 0; u < kLeanBatch; u++) feed_taps_issue(rs, fr, e[u].xy, e[u].code, raw[u]);
 #pragma unroll
-                for (int u = 0; u < kLeanBatch; u++) feed_taps_finish(fr, raw[u], t[u]);
+                for (int u = 0; u < kLeanBatch; u++) feed_taps_finish(raw[u], t[u]);
             }
             double nv[kLeanBatch];
             uint32_t pm_any = 0u;
@@ -585,7 +567,7 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
 #pragma unroll
             for (int u = 0; u < kPer; u++) feed_taps_issue(rs, fr, es[u].xy, es[u].code, raw[u]);
 #pragma unroll
-            for (int u = 0; u < kPer; u++) feed_taps_finish(fr, raw[u], t[u]);
+            for (int u = 0; u < kPer; u++) feed_taps_finish(raw[u], t[u]);
         }
 #pragma unroll
         for (int u = 0; u < kPer; u++) {

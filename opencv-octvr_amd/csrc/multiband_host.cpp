@@ -951,7 +951,8 @@ void multiband_run(MultiBand& M, int slot, const FrameSet& frames, const double*
 // counted once per launch that needs it (re-reads of a neighbour's halo from L2 are not counted).
 //   remap:   4 B tiled entry per item pixel (8 B wide), the G0 halves it writes (4 B / px), the deep
 //            tiles' results (1.5 B / px YUV420P), the unique source bytes of its staged boxes, metadata;
-//   down l:  4 B written per level-l item pixel, its 2 x 2 level-(l-1) source (16 B / px);
+//   down l:  4 B written per level-l item pixel, its level-(l-1) source window with the 5 x 5 halo
+//            (20 x 260 pixels of 4 B per 128 x 8 item);
 //   blend l: per sub-tile by kind — unread (owned 3): nothing; deep (2): G 4 B + R 8 B (level 0: nothing
 //            when the remap wrote it, else 1.5 B out); owned (1): G 4 B + coarser G taps 1 B + collapsed
 //            coarser level 2 B + R 8 B / out 1.5 B; general: per weighted camera G 4 B + weight (1 B u8
@@ -963,7 +964,11 @@ std::vector<std::pair<std::string, double>> multiband_traffic_parts(const MultiB
     parts.emplace_back("remap", 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + r.g0_bytes +
                                     1.5 * r.result_bytes + r.source_bytes +
                                     (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)));
-    for (int l = 1; l <= M.B; l++) parts.emplace_back("down" + std::to_string(l), (double)M.lv[l].n_down * kTilePx * (16.0 + 4.0));
+    // down l: per item its (2 kTileH + 4) x (2 kTileW + 4) source window (the 5 x 5 support's halo) and the
+    // tile it writes
+    for (int l = 1; l <= M.B; l++)
+        parts.emplace_back("down" + std::to_string(l),
+                           (double)M.lv[l].n_down * (4.0 * (2 * kTileH + 4) * (2 * kTileW + 4) + 4.0 * kTilePx));
     for (int l = M.B; l >= 0; l--) {
         const auto& L = M.lv[l];
         const bool up = l < M.B;
