@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -21,16 +22,25 @@
 using namespace octvr;
 
 namespace octvr {
-hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint2* runs_y,
-                                  const uint2* ent_uv, const uint2* runs_uv, int W, int H, uint8_t* out,
-                                  int64_t out_pitch, hipStream_t s);
+hipError_t launch_fastmapper_nv12(const FrameSet& frames, const FastMapperPlane& y, const FastMapperPlane& uv, int W,
+                                  int H, uint8_t* out, int64_t out_pitch, hipStream_t s);
 }
+
+// one plane's entries on the device: per (run, camera with weight in the run) a block of 256
+struct FastPlaneDev {
+    bool compact = true;
+    DevBuf<uint2> ent;    // wide entries
+    DevBuf<uint32_t> off; // compact: dx | dy << 11 | code << 22
+    DevBuf<uint8_t> wgt;  // compact: feather weight
+    DevBuf<uint2> hdr;    // compact: per block {bsx | bsy << 16, 0}
+    DevBuf<uint2> runs;   // per run: camera mask, first block
+    FastMapperPlane view() const { return FastMapperPlane{compact, ent.p, off.p, wgt.p, hdr.p, runs.p}; }
+};
 
 struct octvr_fastmapper {
     int device = 0, n = 0, W = 0, H = 0;
     std::vector<int> in_w, in_h;
-    DevBuf<uint2> ent_y, ent_uv;     // per (run, camera with weight in the run): 256 entries
-    DevBuf<uint2> runs_y, runs_uv;   // per run: camera mask, first block
+    FastPlaneDev y, uv;
     double bytes = 0;                // algorithmic bytes per stitch (octvr_fastmapper_traffic)
     size_t blocks = 0;               // 256-entry (camera, run) blocks, Y + UV
 };
@@ -55,6 +65,41 @@ uint2 make_entry(float m1, float m2, float sx, float sy, uint8_t w) {
     e.x = sat_s16(ix >> 5) | (sat_s16(iy >> 5) << 16);
     e.y = (uint32_t)((iy & 31) * 32 + (ix & 31)) | ((uint32_t)w << 16);
     return e;
+}
+
+// The compact form of a plane's wide entries: per block the smallest in-use tap (entries of weight 0
+// are never used) as the header, per entry the 11-bit offsets from it, the fractions and the weight.
+// Returns false (nothing written) when some block's in-use taps span 2048 pixels or more.
+bool compact_entries(const std::vector<uint2>& e, size_t nblk, std::vector<uint32_t>& off, std::vector<uint8_t>& wgt,
+                     std::vector<uint2>& hdr) {
+    off.assign(e.size(), 0u);
+    wgt.assign(e.size(), 0u);
+    hdr.assign(std::max<size_t>(nblk, 1), make_uint2(0u, 0u));
+    std::vector<uint8_t> fits(std::max<size_t>(nblk, 1), 1);
+    parallel_for(nblk, [&](size_t b) {
+        int x0 = 32767, y0 = 32767, x1 = -32768, y1 = -32768;
+        for (size_t k = b * 256; k < b * 256 + 256; k++) {
+            if (!(e[k].y >> 16)) continue;
+            const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
+            x0 = std::min(x0, sx), x1 = std::max(x1, sx), y0 = std::min(y0, sy), y1 = std::max(y1, sy);
+        }
+        if (x1 < x0) x0 = x1 = y0 = y1 = 0;
+        if (x1 - x0 >= 2048 || y1 - y0 >= 2048) {
+            fits[b] = 0;
+            return;
+        }
+        hdr[b] = make_uint2((uint32_t)(uint16_t)x0 | (uint32_t)(uint16_t)y0 << 16, 0u);
+        for (size_t k = b * 256; k < b * 256 + 256; k++) {
+            const uint32_t w = e[k].y >> 16;
+            wgt[k] = (uint8_t)w;
+            if (!w) continue;
+            const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
+            off[k] = (uint32_t)(sx - x0) | (uint32_t)(sy - y0) << 11 | (e[k].y & 1023u) << 22;
+        }
+    });
+    for (size_t b = 0; b < nblk; b++)
+        if (!fits[b]) return false;
+    return true;
 }
 
 // cv::resize(f32 map, half size): resizeAreaFast with the SSE grouping (imgwarp.cpp:2284-2337, 2441-2454).
@@ -177,9 +222,19 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
                     euv[blk * 256 + (k - r * 256)] = make_entry(h1[k], h2[k], hx, hy, hm_i[k]);
             });
         }
-        // per stitch: 8 B per entry read, 1.5 B per output pixel written, and the source bytes the
-        // weighted taps reach (each once: luma pixels 1 B, interleaved chroma pairs 2 B)
-        fm->bytes = 8.0 * (double)(by + buv) * 256 + 1.5 * (double)npx;
+        // OCTVR_FAST_WIDE=1 keeps the 8-byte entries (tests of the wide kernels)
+        const char* wide_env = getenv("OCTVR_FAST_WIDE");
+        const bool force_wide = wide_env && wide_env[0] == '1';
+        std::vector<uint32_t> oy, ouv;
+        std::vector<uint8_t> wy, wuv;
+        std::vector<uint2> hy, huv;
+        fm->y.compact = !force_wide && compact_entries(ey, by, oy, wy, hy);
+        fm->uv.compact = !force_wide && compact_entries(euv, buv, ouv, wuv, huv);
+        // per stitch: the entries read (compact: 5 B per entry and 8 B per block header; wide: 8 B per
+        // entry), 1.5 B per output pixel written, and the source bytes the weighted taps reach (each once:
+        // luma pixels 1 B, interleaved chroma pairs 2 B)
+        auto ent_bytes = [](bool compact, size_t blocks) { return compact ? (5.0 * 256 + 8.0) * blocks : 8.0 * 256 * blocks; };
+        fm->bytes = ent_bytes(fm->y.compact, by) + ent_bytes(fm->uv.compact, buv) + 1.5 * (double)npx;
         for (int i = 0; i < n; i++) {
             const int w = in_w[i], h = in_h[i];
             std::vector<uint8_t> ty((size_t)w * h, 0), tuv((size_t)(w / 2) * (h / 2), 0);
@@ -209,10 +264,19 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
         }
         fm->blocks = by + buv;
         DeviceGuard dg(device);
-        fm->ent_y.upload(ey.data(), ey.size());
-        fm->ent_uv.upload(euv.data(), euv.size());
-        fm->runs_y.upload(ry.data(), ry.size());
-        fm->runs_uv.upload(ruv.data(), ruv.size());
+        auto upload = [](FastPlaneDev& d, const std::vector<uint2>& e, const std::vector<uint32_t>& o,
+                         const std::vector<uint8_t>& w, const std::vector<uint2>& h, const std::vector<uint2>& runs) {
+            if (d.compact) {
+                d.off.upload(o.data(), o.size());
+                d.wgt.upload(w.data(), w.size());
+                d.hdr.upload(h.data(), h.size());
+            } else {
+                d.ent.upload(e.data(), e.size());
+            }
+            d.runs.upload(runs.data(), runs.size());
+        };
+        upload(fm->y, ey, oy, wy, hy, ry);
+        upload(fm->uv, euv, ouv, wuv, huv, ruv);
         *out = fm.release();
         return OCTVR_OK;
     } catch (const OctvrError& e) {
@@ -239,8 +303,8 @@ int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_
                     "input frame of fewer than 8 or more than 2^31 bytes");
             fs.f[i] = SourceFrame{in_dev[i], fm->in_w[i], fm->in_h[i], (int64_t)in_pitch[i], nullptr};
         }
-        HIP_CHECK(launch_fastmapper_nv12(fs, fm->ent_y.p, fm->runs_y.p, fm->ent_uv.p, fm->runs_uv.p, fm->W, fm->H, out_dev,
-                                         (int64_t)out_pitch, (hipStream_t)stream));
+        HIP_CHECK(launch_fastmapper_nv12(fs, fm->y.view(), fm->uv.view(), fm->W, fm->H, out_dev, (int64_t)out_pitch,
+                                         (hipStream_t)stream));
         return OCTVR_OK;
     } catch (const OctvrError& e) {
         set_last_error(e.what());

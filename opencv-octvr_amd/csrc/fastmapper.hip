@@ -8,9 +8,12 @@
 // a register (u16 adds wrap, so the camera order does not matter) and writes the final u8 directly:
 // no u16 accumulator planes in HBM, no separate convert pass.
 //
-// Per (camera, pixel) entry (uint2, built on the host from convertMaps + the feather weights; stored only
-// for the (camera, 256-pixel run) pairs where the camera has a non-zero weight somewhere in the run):
-//   x = sx | sy << 16 (s16 each, convertMaps' integer tap), y = code (10-bit fractions) | weight << 16.
+// Per (camera, pixel) entry, built on the host from convertMaps + the feather weights and stored only
+// for the (camera, 256-pixel run) pairs where the camera has a non-zero weight somewhere in the run.
+// Compact format (5 B per entry, the default): per 256-entry block a header {bsx | bsy << 16 (s16)},
+// per entry a u32 dx | dy << 11 | code << 22 (tap = (bsx + dx, bsy + dy), 11-bit offsets, 10-bit
+// fractions) and a u8 feather weight in a plane of its own.  Wide format (8 B, used for a plane when
+// one of its blocks spans 2048 source pixels or more): uint2 {sx | sy << 16 (s16), code | weight << 16}.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -34,8 +37,7 @@ __device__ __forceinline__ uint8_t convert_out(uint32_t acc) {  // convertTo(CV_
 }  // namespace
 
 // remap_weighted.cl:46-75 for one pixel of one camera from its four taps (0 outside the source)
-__device__ __forceinline__ uint32_t weighted_sum(const float (&t)[4], uint2 e) {
-    const uint32_t code = e.y & 1023u, w = e.y >> 16;
+__device__ __forceinline__ uint32_t weighted_sum(const float (&t)[4], uint32_t code, uint32_t w) {
     const float ux = (float)(code & 31u) / 32.f, uy = (float)(code >> 5) / 32.f;
     float v = t[0] * (1 - ux) * (1 - uy) + t[1] * (ux) * (1 - uy) + t[2] * (1 - ux) * (uy) + t[3] * (ux) * (uy);
     v *= (float)w;
@@ -51,18 +53,28 @@ __device__ __forceinline__ uint32_t weighted_sum(const float (&t)[4], uint2 e) {
 // NV12 chroma, V and U (merge order c1, c2: V first, mapper_fast.cpp:181-187).
 constexpr int kFastGroup = 4;
 
-template <int PLANE>
-__device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* __restrict__ ent, const uint2* __restrict__ runs,
-                                           int W, int H, uint8_t* out, int64_t out_pitch) {
+struct FastPlane {
+    const uint2* ent;     // wide entries
+    const uint32_t* off;  // compact entries
+    const uint8_t* wgt;   // compact weights
+    const uint2* hdr;     // compact block headers
+    const uint2* runs;    // per run: camera mask, first block
+};
+
+template <int PLANE, bool COMPACT>
+__device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPlane& fp, int W, int H, uint8_t* out,
+                                           int64_t out_pitch) {
+    typedef __attribute__((address_space(4))) const uint64_t kU64;
     const int pw = PLANE ? W / 2 : W, ph = PLANE ? H / 2 : H;
     const int64_t npx = (int64_t)pw * ph;
     const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const uint2 rr = runs[blockIdx.x];
+    const uint2 rr = fp.runs[blockIdx.x];
     uint32_t m = (uint32_t)uniform((int)rr.x);
     uint32_t blk = (uint32_t)uniform((int)rr.y);
     uint32_t acc0 = 0, acc1 = 0;  // Y (or V), U
     while (m) {
-        uint2 e[kFastGroup];
+        int sxk[kFastGroup], syk[kFastGroup];
+        uint32_t code[kFastGroup], wk[kFastGroup];
         int cam[kFastGroup];
         bool live[kFastGroup];
 #pragma unroll
@@ -70,7 +82,21 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
             live[k] = m != 0u;
             cam[k] = live[k] ? __builtin_ctz(m) : 0;
             m &= m - 1u;
-            e[k] = ent[(int64_t)(live[k] ? blk + k : blk) * 256 + threadIdx.x];
+            const uint32_t b = live[k] ? blk + k : blk;  // dead slots reload the group's first block
+            if (COMPACT) {
+                const uint64_t h = *(kU64*)(uintptr_t)(fp.hdr + b);
+                const uint32_t c = fp.off[(int64_t)b * 256 + threadIdx.x];
+                wk[k] = fp.wgt[(int64_t)b * 256 + threadIdx.x];
+                sxk[k] = (int)(int16_t)(uint32_t)h + (int)(c & 2047u);
+                syk[k] = (int)(int16_t)(uint32_t)(h >> 16) + (int)((c >> 11) & 2047u);
+                code[k] = c >> 22;
+            } else {
+                const uint2 e = fp.ent[(int64_t)b * 256 + threadIdx.x];
+                sxk[k] = (int)(int16_t)(e.x & 0xFFFFu);
+                syk[k] = (int)(int16_t)(e.x >> 16);
+                code[k] = e.y & 1023u;
+                wk[k] = e.y >> 16;
+            }
         }
         blk += live[3] ? 4u : live[2] ? 3u : live[1] ? 2u : 1u;
         // per camera and tap row one 8-byte load from the 4-byte aligned start at or below the row's
@@ -84,7 +110,7 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
             const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
             const uint32_t size = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2);  // >= 8 (host check)
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(f.yuv), 0, (int)size, 0x00020000);
-            const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
+            const int sx = sxk[k], sy = syk[k];
             const int xa = min(max(sx, 0), sw - 1);
             const uint32_t bx = (uint32_t)xa * (PLANE ? 2u : 1u) & ~3u;  // 4-byte aligned row start
 #pragma unroll
@@ -107,10 +133,10 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
         }
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) {
-            if (!live[k] || (e[k].y >> 16) == 0) continue;
+            if (!live[k] || wk[k] == 0) continue;
             const SourceFrame f = frames.f[cam[k]];
             const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
-            const int sx = (int)(int16_t)(e[k].x & 0xFFFFu), sy = (int)(int16_t)(e[k].x >> 16);
+            const int sx = sxk[k], sy = syk[k];
             float t0[4], t1[4];
 #pragma unroll
             for (int r = 0; r < 2; r++) {
@@ -130,8 +156,8 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
                     }
                 }
             }
-            acc0 += weighted_sum(t0, e[k]);
-            if (PLANE) acc1 += weighted_sum(t1, e[k]);
+            acc0 += weighted_sum(t0, code[k], wk[k]);
+            if (PLANE) acc1 += weighted_sum(t1, code[k], wk[k]);
         }
     }
     if (idx >= npx) return;
@@ -147,29 +173,45 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const uint2* 
 
 // runs[r] = {camera mask, first block}: run r's cameras (ascending) own blocks first, first + 1, ... of
 // 256 entries (fastmapper.cpp)
-__global__ void __launch_bounds__(256) fast_y_kernel(FrameSet frames, const uint2* __restrict__ ent,
-                                                     const uint2* __restrict__ runs, int W, int H, uint8_t* out,
+template <bool COMPACT>
+__global__ void __launch_bounds__(256) fast_y_kernel(FrameSet frames, FastPlane fp, int W, int H, uint8_t* out,
                                                      int64_t out_pitch) {
-    fast_plane<0>(frames, ent, runs, W, H, out, out_pitch);
+    fast_plane<0, COMPACT>(frames, fp, W, H, out, out_pitch);
 }
 
-__global__ void __launch_bounds__(256) fast_uv_kernel(FrameSet frames, const uint2* __restrict__ ent,
-                                                      const uint2* __restrict__ runs, int W, int H, uint8_t* out,
+template <bool COMPACT>
+__global__ void __launch_bounds__(256) fast_uv_kernel(FrameSet frames, FastPlane fp, int W, int H, uint8_t* out,
                                                       int64_t out_pitch) {
-    fast_plane<1>(frames, ent, runs, W, H, out, out_pitch);
+    fast_plane<1, COMPACT>(frames, fp, W, H, out, out_pitch);
 }
 
-hipError_t launch_fastmapper_nv12(const FrameSet& frames, const uint2* ent_y, const uint2* runs_y,
-                                  const uint2* ent_uv, const uint2* runs_uv, int W, int H, uint8_t* out,
-                                  int64_t out_pitch, hipStream_t s) {
-    const int64_t ny = (int64_t)W * H, nuv = (int64_t)(W / 2) * (H / 2);
-    hipLaunchKernelGGL(fast_y_kernel, dim3((unsigned)((ny + 255) / 256)), dim3(256), 0, s, frames, ent_y, runs_y, W, H,
-                       out, out_pitch);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(fast_uv_kernel, dim3((unsigned)((nuv + 255) / 256)), dim3(256), 0, s, frames, ent_uv, runs_uv, W,
-                       H, out, out_pitch);
+template <int PLANE, bool COMPACT>
+static void launch_plane_kernel(dim3 grid, const FrameSet& frames, const FastPlane& fp, int W, int H, uint8_t* out,
+                                int64_t out_pitch, hipStream_t s) {
+    if (PLANE)
+        hipLaunchKernelGGL((fast_uv_kernel<COMPACT>), grid, dim3(256), 0, s, frames, fp, W, H, out, out_pitch);
+    else
+        hipLaunchKernelGGL((fast_y_kernel<COMPACT>), grid, dim3(256), 0, s, frames, fp, W, H, out, out_pitch);
+}
+
+template <int PLANE>
+static hipError_t launch_plane(const FrameSet& frames, const FastMapperPlane& p, int W, int H, uint8_t* out,
+                               int64_t out_pitch, hipStream_t s) {
+    const int64_t n = PLANE ? (int64_t)(W / 2) * (H / 2) : (int64_t)W * H;
+    const dim3 grid((unsigned)((n + 255) / 256));
+    const FastPlane fp{p.ent, p.off, p.wgt, p.hdr, p.runs};
+    if (p.compact)
+        launch_plane_kernel<PLANE, true>(grid, frames, fp, W, H, out, out_pitch, s);
+    else
+        launch_plane_kernel<PLANE, false>(grid, frames, fp, W, H, out, out_pitch, s);
     return hipGetLastError();
+}
+
+hipError_t launch_fastmapper_nv12(const FrameSet& frames, const FastMapperPlane& y, const FastMapperPlane& uv, int W,
+                                  int H, uint8_t* out, int64_t out_pitch, hipStream_t s) {
+    const hipError_t e = launch_plane<0>(frames, y, W, H, out, out_pitch, s);
+    if (e != hipSuccess) return e;
+    return launch_plane<1>(frames, uv, W, H, out, out_pitch, s);
 }
 
 }  // namespace octvr

@@ -141,6 +141,18 @@ struct FrameSet {
     SourceFrame f[kMaxCams];
 };
 
+// One NV12 plane of a FastMapper (fastmapper.cpp / fastmapper.hip): per run {camera mask, first block},
+// and per (camera, run) block either the compact entries (header + u32 offsets/fractions + u8 weights)
+// or the wide uint2 entries.
+struct FastMapperPlane {
+    bool compact;
+    const uint2* ent;
+    const uint32_t* off;
+    const uint8_t* wgt;
+    const uint2* hdr;
+    const uint2* runs;
+};
+
 // ROI-sized per-camera template data resident on the device.
 struct CamTemplate {
     const float* map1;

@@ -12,10 +12,13 @@ import oracle_py as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("wide", [False, True], ids=["compact", "wide"])
 @pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
-def test_gpu_fastmapper_nv12_bit_exact(product_lib, name):
+def test_gpu_fastmapper_nv12_bit_exact(product_lib, name, wide, monkeypatch):
+    """Both entry formats: the compact 5-byte entries (default) and the 8-byte ones (OCTVR_FAST_WIDE=1)."""
     import torch
     ox = product_lib
+    monkeypatch.setenv("OCTVR_FAST_WIDE", "1" if wide else "0")
     rig, z = O.load_rig(name)
     W, H = (int(v) for v in z["out_size"])
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=False)  # octvr_dump without ROI
@@ -82,3 +85,29 @@ def test_gpu_fastmapper_edge_taps(product_lib):
         d = got != want
         assert not d.any(), (seed, int(d.sum()), np.argwhere(d)[:5].tolist())
         assert want.any()
+
+
+def test_gpu_fastmapper_wide_blocks(product_lib):
+    """A 4000-pixel-wide source sampled at random over a 96-pixel output: a luma block's taps span more
+    than 2048 pixels, so the Y plane falls back to the 8-byte entries, while the half-size chroma plane
+    (spans < 2000) stays compact; both bit-exact vs the oracle."""
+    import torch
+    ox = product_lib
+    W, H = 96, 32
+    sizes = [(4000, 24), (64, 20)]
+    rng = np.random.default_rng(9)
+    m1 = [rng.uniform(0.0, 1.0, (H, W)).astype(np.float32) for _ in sizes]
+    m2 = [rng.uniform(0.0, 1.0, (H, W)).astype(np.float32) for _ in sizes]
+    mk = [np.full((H, W), 255, np.uint8) for _ in sizes]
+    mk[1][:, W // 2:] = 0
+    mt = ox.MapperTemplate.from_arrays(W, H, [[0, 0, W, H]] * 2, m1, m2, mk)
+    fm = ox.FastMapper(mt, sizes)
+    frames = [O.rand_img(w, h * 3 // 2, 1, 70 + i) for i, (w, h) in enumerate(sizes)]
+    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    fm.stitch_nv12([torch.from_numpy(f).cuda() for f in frames], out)
+    torch.cuda.synchronize()
+    want = O.fastmapper_nv12(frames, sizes, m1, m2, mk, W, H)
+    got = out.cpu().numpy()
+    d = got != want
+    assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
+    assert want.any()
