@@ -331,8 +331,9 @@ def fast_rank(args, world, rank, local_rank, dist):
                      "kernel": "fast_y_kernel + fast_uv_kernel", "kernel_us": round(kern_s * 1e6, 2),
                      "kernel_us_basis": "torch events around 16 back-to-back stitch_nv12 on the launch stream",
                      "bytes_per_launch": b,
-                     "bytes_basis": "8 B per (camera, 256-px run) entry block pixel, 1.5 B out per px, source bytes the "
-                                    "weighted taps reach (octvr_fastmapper_traffic)",
+                     "bytes_basis": "per (camera, 256-px run) entry block pixel 5 B (compact entry + weight; 8 B per "
+                                    "block header) or 8 B (wide planes), 1.5 B out per px, source bytes the weighted "
+                                    "taps reach (octvr_fastmapper_traffic)",
                      "frac_at_step_time": round(b / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
                      "frac_traffic": round(traffic / kern_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None},
     }
