@@ -122,6 +122,7 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
         REQUIRE(n_inputs == n && n > 0 && n <= kMaxCams && n <= 32, "in_sizes must cover the inputs (<= 32)");
         const int W = rig->out_w, H = rig->out_h;
         REQUIRE(W % 2 == 0 && H % 2 == 0, "NV12 output needs even width/height");
+        REQUIRE((int64_t)W * H < ((int64_t)1 << 31), "output of 2^31 pixels or more");
         for (int i = 0; i < n; i++) {
             const RigInput& in = rig->inputs[i];
             // "does not support ROI yet" (mapper_fast.cpp:50-51): every map covers the whole output
@@ -297,7 +298,7 @@ int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_
         FrameSet fs;
         memset(&fs, 0, sizeof fs);
         for (int i = 0; i < fm->n; i++) {
-            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)fm->in_w[i], "bad input frame");
+            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)fm->in_w[i] && in_pitch[i] < ((size_t)1 << 24), "bad input frame");
             REQUIRE(in_pitch[i] * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) >= 8 &&
                         in_pitch[i] * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) < 0x7FFFFFFFull,
                     "input frame of fewer than 8 or more than 2^31 bytes");

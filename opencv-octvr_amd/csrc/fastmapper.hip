@@ -36,12 +36,31 @@ __device__ __forceinline__ uint8_t convert_out(uint32_t acc) {  // convertTo(CV_
 
 }  // namespace
 
-// remap_weighted.cl:46-75 for one pixel of one camera from its four taps (0 outside the source)
-__device__ __forceinline__ uint32_t weighted_sum(const float (&t)[4], uint32_t code, uint32_t w) {
-    const float ux = (float)(code & 31u) / 32.f, uy = (float)(code >> 5) / 32.f;
-    float v = t[0] * (1 - ux) * (1 - uy) + t[1] * (ux) * (1 - uy) + t[2] * (1 - ux) * (uy) + t[3] * (ux) * (uy);
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// remap_weighted.cl:46-75 for one pixel of one camera from its four taps (0 outside the source):
+// ((t0 (1 - ux)) (1 - uy) + (t1 ux) (1 - uy)) + (t2 (1 - ux)) uy + (t3 ux) uy, every product and sum
+// rounded as written (-ffp-contract=off), two channels at a time in packed f32 (lane .x / .y of t01,
+// t23: {t0, t1} / {t2, t3} for one channel, or {V, U} of one tap pair when CH2)
+__device__ __forceinline__ f32x2 uxy(uint32_t code) {
+    return f32x2{(float)(code & 31u) / 32.f, (float)(code >> 5) / 32.f};
+}
+__device__ __forceinline__ uint32_t weighted_sum(f32x2 t01, f32x2 t23, uint32_t code, uint32_t w) {
+    const f32x2 u = uxy(code);
+    const f32x2 q = (t01 * f32x2{1 - u.x, u.x}) * f32x2{1 - u.y, 1 - u.y};
+    const f32x2 r = (t23 * f32x2{1 - u.x, u.x}) * f32x2{u.y, u.y};
+    float v = ((q.x + q.y) + r.x) + r.y;
     v *= (float)w;
     return sat_u16_rte(v);
+}
+// the same for two channels c = .x, .y: taps t[j] = {c0 tap j, c1 tap j}
+__device__ __forceinline__ void weighted_sum2(const f32x2 (&t)[4], uint32_t code, uint32_t w, uint32_t& a0, uint32_t& a1) {
+    const f32x2 u = uxy(code);
+    const f32x2 nx = {1 - u.x, 1 - u.x}, px = {u.x, u.x}, ny = {1 - u.y, 1 - u.y}, py = {u.y, u.y};
+    f32x2 v = (((t[0] * nx) * ny + (t[1] * px) * ny) + (t[2] * nx) * py) + (t[3] * px) * py;
+    v *= f32x2{(float)w, (float)w};
+    a0 += sat_u16_rte(v.x);
+    a1 += sat_u16_rte(v.y);
 }
 
 // A run's cameras in groups of kFastGroup: every entry load of the group, then every tap gather, then
@@ -49,8 +68,10 @@ __device__ __forceinline__ uint32_t weighted_sum(const float (&t)[4], uint32_t c
 // plain per-camera loop, 920 us for a C2 frame, was a chain of dependent loads).  A tap row is one
 // 8-byte load through the camera's frame as a buffer resource (32-bit offsets; addresses clamped into
 // the image, taps outside it zeroed by mask, as BORDER_CONSTANT), instead of 2 (Y) or 4 (chroma) byte
-// loads.  PLANE 0: Y; 1: the interleaved
-// NV12 chroma, V and U (merge order c1, c2: V first, mapper_fast.cpp:181-187).
+// loads.  Slots past the run's cameras are skipped by uniform branches (a C2 run has 1.3 cameras: the
+// kernels issue VALU in every SIMD cycle and keep the texture data path 94 % busy, so work done for
+// empty slots cost its full share).  PLANE 0: Y; 1: the interleaved NV12 chroma, V and U (merge order
+// c1, c2: V first, mapper_fast.cpp:181-187).
 constexpr int kFastGroup = 4;
 
 struct FastPlane {
@@ -65,9 +86,9 @@ template <int PLANE, bool COMPACT>
 __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPlane& fp, int W, int H, uint8_t* out,
                                            int64_t out_pitch) {
     typedef __attribute__((address_space(4))) const uint64_t kU64;
+    constexpr uint32_t bpp = PLANE ? 2u : 1u;  // bytes per source pixel of the plane
     const int pw = PLANE ? W / 2 : W, ph = PLANE ? H / 2 : H;
-    const int64_t npx = (int64_t)pw * ph;
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint32_t npx = (uint32_t)pw * (uint32_t)ph;  // < 2^31 (host check)
     const uint2 rr = fp.runs[blockIdx.x];
     uint32_t m = (uint32_t)uniform((int)rr.x);
     uint32_t blk = (uint32_t)uniform((int)rr.y);
@@ -77,25 +98,36 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
         uint32_t code[kFastGroup], wk[kFastGroup];
         int cam[kFastGroup];
         bool live[kFastGroup];
+        uint2 en[kFastGroup];  // compact: {offsets, weight}; wide: the entry
+        uint64_t hd[kFastGroup];
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) {  // uniform: the group's cameras and their entry blocks
             live[k] = m != 0u;
             cam[k] = live[k] ? __builtin_ctz(m) : 0;
             m &= m - 1u;
-            const uint32_t b = live[k] ? blk + k : blk;  // dead slots reload the group's first block
+            // every slot loads (dead ones the group's first block) so that no load waits on a branch
+            const uint32_t b = live[k] ? blk + k : blk;
+            const uint32_t e = b * 256u + threadIdx.x;  // < 2^32 (host check)
             if (COMPACT) {
-                const uint64_t h = *(kU64*)(uintptr_t)(fp.hdr + b);
-                const uint32_t c = fp.off[(int64_t)b * 256 + threadIdx.x];
-                wk[k] = fp.wgt[(int64_t)b * 256 + threadIdx.x];
-                sxk[k] = (int)(int16_t)(uint32_t)h + (int)(c & 2047u);
-                syk[k] = (int)(int16_t)(uint32_t)(h >> 16) + (int)((c >> 11) & 2047u);
-                code[k] = c >> 22;
+                hd[k] = *(kU64*)(uintptr_t)(fp.hdr + b);
+                en[k] = make_uint2(fp.off[e], fp.wgt[e]);
             } else {
-                const uint2 e = fp.ent[(int64_t)b * 256 + threadIdx.x];
-                sxk[k] = (int)(int16_t)(e.x & 0xFFFFu);
-                syk[k] = (int)(int16_t)(e.x >> 16);
-                code[k] = e.y & 1023u;
-                wk[k] = e.y >> 16;
+                hd[k] = 0;
+                en[k] = fp.ent[e];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kFastGroup; k++) {
+            if (COMPACT) {
+                sxk[k] = (int)(int16_t)(uint32_t)hd[k] + (int)(en[k].x & 2047u);
+                syk[k] = (int)(int16_t)(uint32_t)(hd[k] >> 16) + (int)((en[k].x >> 11) & 2047u);
+                code[k] = en[k].x >> 22;
+                wk[k] = en[k].y;
+            } else {
+                sxk[k] = (int)(int16_t)(en[k].x & 0xFFFFu);
+                syk[k] = (int)(int16_t)(en[k].x >> 16);
+                code[k] = en[k].y & 1023u;
+                wk[k] = en[k].y >> 16;
             }
         }
         blk += live[3] ? 4u : live[2] ? 3u : live[1] ? 2u : 1u;
@@ -105,6 +137,9 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
         uint32_t sel[kFastGroup][2];
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) {
+            rw[k][0] = rw[k][1] = make_uint2(0u, 0u);
+            sel[k][0] = sel[k][1] = 0u;
+            if (!live[k]) continue;
             const SourceFrame f = frames.f[cam[k]];
             const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
             const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
@@ -112,19 +147,20 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
             const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(f.yuv), 0, (int)size, 0x00020000);
             const int sx = sxk[k], sy = syk[k];
             const int xa = min(max(sx, 0), sw - 1);
-            const uint32_t bx = (uint32_t)xa * (PLANE ? 2u : 1u) & ~3u;  // 4-byte aligned row start
+            const uint32_t bx = (uint32_t)xa * bpp & ~3u;  // 4-byte aligned row start
 #pragma unroll
             for (int r = 0; r < 2; r++) {
                 const int y = min(max(sy + r, 0), sh - 1);
-                const uint32_t row = base + (uint32_t)y * (uint32_t)f.pitch;
+                // y < 2^15, pitch < 2^24 (host check): a 24-bit multiply
+                const uint32_t row = base + __umul24((uint32_t)y, (uint32_t)f.pitch);
                 // the buffer range-checks whole dwords: a start within 8 bytes of the frame's end (its last
                 // chroma row, a pitch not a multiple of 4) is clamped to size - 8 and the taps taken from there
                 const uint32_t st = min(row + bx, size - 8u);
                 // byte index of taps x = sx, sx + 1 in the 8 loaded bytes (exact for taps inside the image,
                 // any byte for the ones outside, which are masked below); an in-image chroma pair starts
                 // at most at byte 6, so its second byte is i + 1 <= 7
-                const uint32_t i0 = (row + (uint32_t)(sx * (PLANE ? 2 : 1)) - st) & 7u;
-                const uint32_t i1 = (row + (uint32_t)((sx + 1) * (PLANE ? 2 : 1)) - st) & 7u;
+                const uint32_t d = row + (uint32_t)sx * bpp - st;
+                const uint32_t i0 = d & 7u, i1 = (d + bpp) & 7u;
                 sel[k][r] = PLANE ? (i0 | (i0 + 1u) << 8 | i1 << 16 | (i1 + 1u) << 24) : (i0 | i1 << 8 | 0x0C0C0000u);
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, st, 0, 0);
@@ -133,37 +169,40 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
         }
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) {
-            if (!live[k] || wk[k] == 0) continue;
+            if (!live[k]) continue;
+            if (wk[k] == 0) continue;
             const SourceFrame f = frames.f[cam[k]];
-            const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
+            const uint32_t sw = (uint32_t)(PLANE ? f.w / 2 : f.w), sh = (uint32_t)(PLANE ? f.h / 2 : f.h);
             const int sx = sxk[k], sy = syk[k];
-            float t0[4], t1[4];
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                // row r's taps: Y bytes {x, x + 1}, or chroma bytes {U x, V x, U x+1, V x+1}
-                const uint32_t b = __builtin_amdgcn_perm(rw[k][r].y, rw[k][r].x, sel[k][r]);
-                const int y = sy + r;
-#pragma unroll
-                for (int c = 0; c < 2; c++) {
-                    const int x = sx + c;
-                    const bool in = x >= 0 && y >= 0 && x < sw && y < sh;
-                    const int j = 2 * r + c;
-                    if (PLANE) {
-                        t0[j] = in ? (float)((b >> (16 * c + 8)) & 255u) : 0.f;  // V
-                        t1[j] = in ? (float)((b >> (16 * c)) & 255u) : 0.f;      // U
-                    } else {
-                        t0[j] = in ? (float)((b >> (8 * c)) & 255u) : 0.f;
-                    }
-                }
+            const bool ix0 = (uint32_t)sx < sw, ix1 = (uint32_t)(sx + 1) < sw;
+            const bool iy0 = (uint32_t)sy < sh, iy1 = (uint32_t)(sy + 1) < sh;
+            // row r's taps: Y bytes {x, x + 1}, or chroma bytes {U x, V x, U x+1, V x+1}
+            const uint32_t b0 = __builtin_amdgcn_perm(rw[k][0].y, rw[k][0].x, sel[k][0]);
+            const uint32_t b1 = __builtin_amdgcn_perm(rw[k][1].y, rw[k][1].x, sel[k][1]);
+            auto byte = [](uint32_t b, int i, bool in) { return in ? (float)((b >> (8 * i)) & 255u) : 0.f; };
+            if (PLANE) {
+                const f32x2 t[4] = {{byte(b0, 1, ix0 && iy0), byte(b0, 0, ix0 && iy0)},
+                                    {byte(b0, 3, ix1 && iy0), byte(b0, 2, ix1 && iy0)},
+                                    {byte(b1, 1, ix0 && iy1), byte(b1, 0, ix0 && iy1)},
+                                    {byte(b1, 3, ix1 && iy1), byte(b1, 2, ix1 && iy1)}};
+                weighted_sum2(t, code[k], wk[k], acc0, acc1);
+            } else {
+                acc0 += weighted_sum(f32x2{byte(b0, 0, ix0 && iy0), byte(b0, 1, ix1 && iy0)},
+                                     f32x2{byte(b1, 0, ix0 && iy1), byte(b1, 1, ix1 && iy1)}, code[k], wk[k]);
             }
-            acc0 += weighted_sum(t0, code[k], wk[k]);
-            if (PLANE) acc1 += weighted_sum(t1, code[k], wk[k]);
         }
     }
-    if (idx >= npx) return;
-    const int y = (int)(idx / pw), x = (int)(idx - (int64_t)y * pw);
+    // pixel index -> (x, y): the run's first row by one scalar division, then at most 256 / pw row steps
+    const uint32_t idx0 = blockIdx.x * 256u;
+    uint32_t y = (uint32_t)uniform((int)(idx0 / (uint32_t)pw));
+    uint32_t x = idx0 - y * (uint32_t)pw + threadIdx.x;
+    if (idx0 + threadIdx.x >= npx) return;
+    while (x >= (uint32_t)pw) {
+        x -= (uint32_t)pw;
+        y++;
+    }
     if (PLANE) {
-        uint8_t* o = out + (int64_t)(H + y) * out_pitch + 2 * x;  // merge(c1c2): V first, then U
+        uint8_t* o = out + (int64_t)(H + (int)y) * out_pitch + 2 * x;  // merge(c1c2): V first, then U
         o[0] = convert_out(acc0);
         o[1] = convert_out(acc1);
     } else {
