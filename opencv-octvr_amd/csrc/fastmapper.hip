@@ -63,16 +63,38 @@ __device__ __forceinline__ void weighted_sum2(const f32x2 (&t)[4], uint32_t code
     a1 += sat_u16_rte(v.y);
 }
 
+// The same sum in integers (OCTVR_FAST_INT = 1).  With ux = fx / 32, uy = fy / 32 and integer taps t <= 255
+// every product and partial sum above is exact in f32 (t (32 - fx) (32 - fy) <= 255 * 1024 < 2^24, and the
+// four terms add up to at most 255 * 1024 / 1024): v = N / 1024 with
+//   N = (32 - fy) (t0 (32 - fx) + t1 fx) + fy (t2 (32 - fx) + t3 fx),
+// two v_dot2_u32_u16 for the rows and one for the column.  The only rounding is v * w: fl(N / 1024 * w) =
+// fl(N * (w / 1024)), w / 1024 exact; then round half to even (<= 65,025, no saturation).  Taps outside
+// the image are zeroed through the weights: column c's weight is 0 when x + c is outside, row r's when
+// y + r is (tap (c, r) is inside exactly when both are).
+#ifndef OCTVR_FAST_INT
+#define OCTVR_FAST_INT 1
+#endif
+typedef unsigned short fast_u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t weighted_sum_int(uint32_t row0, uint32_t row1, uint32_t wx, uint32_t wy, float wf) {
+    const uint32_t h0 = __builtin_amdgcn_udot2(__builtin_bit_cast(fast_u16x2, row0), __builtin_bit_cast(fast_u16x2, wx), 0u, false);
+    const uint32_t h1 = __builtin_amdgcn_udot2(__builtin_bit_cast(fast_u16x2, row1), __builtin_bit_cast(fast_u16x2, wx), 0u, false);
+    const uint32_t n = __builtin_amdgcn_udot2(__builtin_bit_cast(fast_u16x2, h0 | h1 << 16), __builtin_bit_cast(fast_u16x2, wy), 0u, false);
+    return (uint32_t)__builtin_rintf((float)n * wf);
+}
+
 // A run's cameras in groups of kFastGroup: every entry load of the group, then every tap gather, then
 // the arithmetic, so a pixel costs two memory round trips per group instead of two per camera (the
 // plain per-camera loop, 920 us for a C2 frame, was a chain of dependent loads).  A tap row is one
 // 8-byte load through the camera's frame as a buffer resource (32-bit offsets; addresses clamped into
 // the image, taps outside it zeroed by mask, as BORDER_CONSTANT), instead of 2 (Y) or 4 (chroma) byte
-// loads.  Slots past the run's cameras are skipped by uniform branches (a C2 run has 1.3 cameras: the
-// kernels issue VALU in every SIMD cycle and keep the texture data path 94 % busy, so work done for
-// empty slots cost its full share).  PLANE 0: Y; 1: the interleaved NV12 chroma, V and U (merge order
+// loads.  Slots past the run's cameras are skipped by uniform branches (a C2 run has about 4 cameras,
+// i.e. a second group of 4 is mostly empty; the kernels issue VALU in every SIMD cycle and keep the
+// texture data path 94 % busy, so work done for empty slots cost its full share).  PLANE 0: Y; 1: the interleaved NV12 chroma, V and U (merge order
 // c1, c2: V first, mapper_fast.cpp:181-187).
-constexpr int kFastGroup = 4;
+#ifndef OCTVR_FAST_GROUP
+#define OCTVR_FAST_GROUP 4
+#endif
+constexpr int kFastGroup = OCTVR_FAST_GROUP;
 
 struct FastPlane {
     const uint2* ent;     // wide entries
@@ -130,7 +152,8 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
                 wk[k] = en[k].y >> 16;
             }
         }
-        blk += live[3] ? 4u : live[2] ? 3u : live[1] ? 2u : 1u;
+#pragma unroll
+        for (int k = 0; k < kFastGroup; k++) blk += live[k] ? 1u : 0u;
         // per camera and tap row one 8-byte load from the 4-byte aligned start at or below the row's
         // first in-image tap byte: it holds both taps' bytes (Y: x, x + 1; chroma: the V, U pairs of x, x + 1)
         uint2 rw[kFastGroup][2];
@@ -161,7 +184,11 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
                 // at most at byte 6, so its second byte is i + 1 <= 7
                 const uint32_t d = row + (uint32_t)sx * bpp - st;
                 const uint32_t i0 = d & 7u, i1 = (d + bpp) & 7u;
+#if OCTVR_FAST_INT  // u16 pairs {tap x, tap x + 1} (chroma: of U; V is the next byte of each)
+                sel[k][r] = i0 | i1 << 16 | 0x0C000C00u;
+#else
                 sel[k][r] = PLANE ? (i0 | (i0 + 1u) << 8 | i1 << 16 | (i1 + 1u) << 24) : (i0 | i1 << 8 | 0x0C0C0000u);
+#endif
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, st, 0, 0);
                 rw[k][r] = make_uint2(v.x, v.y);
@@ -176,6 +203,20 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
             const int sx = sxk[k], sy = syk[k];
             const bool ix0 = (uint32_t)sx < sw, ix1 = (uint32_t)(sx + 1) < sw;
             const bool iy0 = (uint32_t)sy < sh, iy1 = (uint32_t)(sy + 1) < sh;
+#if OCTVR_FAST_INT
+            const uint32_t fx = code[k] & 31u, fy = code[k] >> 5;
+            // {32 - f, f} as u16 pairs: 32 + f * 0xFFFF, masked per column / row
+            const uint32_t wx = (32u + fx * 0xFFFFu) & ((ix0 ? 0xFFFFu : 0u) | (ix1 ? 0xFFFF0000u : 0u));
+            const uint32_t wy = (32u + fy * 0xFFFFu) & ((iy0 ? 0xFFFFu : 0u) | (iy1 ? 0xFFFF0000u : 0u));
+            const float wf = (float)wk[k] * (1.f / 1024.f);
+            const uint2 q0 = rw[k][0], q1 = rw[k][1];
+            acc0 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0] + (PLANE ? 0x00010001u : 0u)),
+                                     __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1] + (PLANE ? 0x00010001u : 0u)), wx, wy, wf);
+            if (PLANE)
+                acc1 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0]), __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1]),
+                                         wx, wy, wf);
+            continue;
+#endif
             // row r's taps: Y bytes {x, x + 1}, or chroma bytes {U x, V x, U x+1, V x+1}
             const uint32_t b0 = __builtin_amdgcn_perm(rw[k][0].y, rw[k][0].x, sel[k][0]);
             const uint32_t b1 = __builtin_amdgcn_perm(rw[k][1].y, rw[k][1].x, sel[k][1]);
