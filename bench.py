@@ -35,9 +35,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: independent frame sets stitched round-robin on this many streams "
-                         "(octvr_mapper_set_frames_in_flight)")
+                         "(octvr_mapper_set_frames_in_flight); default per config, DEFAULT_INFLIGHT")
     ap.add_argument("--no-async-e2e", action="store_true",
                     help="skip the AsyncMultiMapper end-to-end (PCIe-inclusive) measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -171,6 +171,9 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
                     "D2H, copy-out, 3 frames in flight; PCIe- and host-copy-inclusive, not the roofline basis"}
 
 
+# frames in flight per config, from interleaved sweeps on one box (scripts/r4_inflight_sweep.sh): C2 2 / 3 / 4 =
+# 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k
+DEFAULT_INFLIGHT = {"C3": 4}
 CPU_BASELINE_S = float(os.environ.get("OCTVR_CPU_BASELINE_S", "10"))
 
 
@@ -370,7 +373,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
     m = ox.Mapper(mt, sizes, blend=blend, enable_gain=use_gain, device=dev)
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
-    inflight = max(1, args.inflight)
+    inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 3))
     m.set_frames_in_flight(inflight)
     # each rank stitches an independent rig instance: frames seeded by (rank, in-flight slot, camera)
     frames_np = [synthetic.yuv_frame(w, h, frame_seed(rank, 0, i)) for i, (w, h) in enumerate(sizes)]
