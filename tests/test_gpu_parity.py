@@ -182,7 +182,8 @@ def test_gpu_stitch_is_deterministic_and_stream_ordered(ox):
     assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
-@pytest.mark.parametrize("k,blend,n", [(2, 0, 6), (3, 0, 6), (2, 0, 3), (2, 0, 12), (2, 16, 6), (3, -10, 6)])
+@pytest.mark.parametrize("k,blend,n", [(2, 0, 6), (3, 0, 6), (2, 0, 3), (2, 0, 12), (2, 16, 6), (3, -10, 6),
+                                         (4, 0, 6), (4, 16, 6)])
 def test_gpu_frames_in_flight_vs_oracle(ox, k, blend, n):
     """octvr_mapper_set_frames_in_flight(k): 2k frames with their own inputs and outputs issued
     round-robin on k streams (no host sync in between) -> every output and the last frame's gains
