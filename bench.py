@@ -172,8 +172,9 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
 
 
 # frames in flight per config, from interleaved sweeps on one box (scripts/r4_inflight_sweep.sh): C2 2 / 3 / 4 =
-# 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k
-DEFAULT_INFLIGHT = {"C3": 4}
+# 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k, F2 (stitch_nv12 on 1 / 2 / 3
+# streams) 85k / 91k / 93k
+DEFAULT_INFLIGHT = {"C3": 4, "F2": 3}
 CPU_BASELINE_S = float(os.environ.get("OCTVR_CPU_BASELINE_S", "10"))
 
 
@@ -303,26 +304,31 @@ def fast_rank(args, world, rank, local_rank, dist):
     fm = ox.FastMapper(mt, sizes, device=dev)
     frames_np = [nv12_of(synthetic.yuv_frame(w, h, frame_seed(rank, 0, i))) for i, (w, h) in enumerate(sizes)]
     frames = [torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]
-    out = torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}")
-    stream = torch.cuda.current_stream(dev)
+    # stitch_nv12 keeps no per-call device state, so a caller may run several at once on their own
+    # streams and outputs (frames in flight, as the Mapper configs do through set_frames_in_flight)
+    inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 1))
+    outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    stream, out = streams[0], outs[0]
 
     def step(k):
-        fm.stitch_nv12(frames, out, stream=stream)
+        fm.stitch_nv12(frames, outs[k % inflight], stream=streams[k % inflight])
 
     if args.pmc_child:
         for k in range(max(args.steps, 1)):
             step(k)
         torch.cuda.synchronize(dev)
         sys.exit(0)
-    for k in range(max(args.warmup, 1)):
+    for k in range(max(args.warmup, inflight)):  # every stream's first launch outside the timed region
         step(k)
     torch.cuda.synchronize(dev)
     elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
-    # kernel time: events around 16 back-to-back stitches (both plane launches) after the timed region
+    # kernel time: events around 16 back-to-back stitches (both plane launches) on one stream, after the
+    # timed region
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for k in range(16):
-        step(k)
+        fm.stitch_nv12(frames, out, stream=stream)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     kern_s = e0.elapsed_time(e1) / 1e3 / 16
@@ -336,11 +342,11 @@ def fast_rank(args, world, rank, local_rank, dist):
         "data": "synthetic (splitmix64 frames as NV12, SURVEY.md §8d rig)",
         "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
                                "template without ROI), NV12 in/out" % (len(sizes), sizes[0][0], sizes[0][1], W, H),
-                   "rigs_per_gpu": 1, "frames_in_flight": 1, "parallelism": "independent rig per GPU"},
+                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "fast_y_kernel + fast_uv_kernel", "kernel_us": round(kern_s * 1e6, 2),
-                     "kernel_us_basis": "torch events around 16 back-to-back stitch_nv12 on the launch stream",
+                     "kernel_us_basis": "torch events around 16 back-to-back stitch_nv12 on one stream",
                      "bytes_per_launch": b,
                      "bytes_basis": "per (camera, 256-px run) entry block pixel 5 B (compact entry + weight; 8 B per "
                                     "block header) or 8 B (wide planes), 1.5 B out per px, source bytes the weighted "
