@@ -172,8 +172,8 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
 
 
 # frames in flight per config, from interleaved sweeps on one box (scripts/r4_inflight_sweep.sh): C2 2 / 3 / 4 =
-# 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k, F2 (stitch_nv12 on 1 / 2 / 3
-# streams) 85k / 91k / 93k
+# 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k, C1 371k / 483k / 485k (3 kept: the
+# two 4s were 511k and 459k), F2 (stitch_nv12 on 1 / 2 / 3 streams) 85k / 91k / 93k
 DEFAULT_INFLIGHT = {"C3": 4, "F2": 3}
 CPU_BASELINE_S = float(os.environ.get("OCTVR_CPU_BASELINE_S", "10"))
 
