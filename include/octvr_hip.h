@@ -222,8 +222,9 @@ typedef struct octvr_fastmapper octvr_fastmapper;
 int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h,
                             octvr_fastmapper** fastmapper);
 /* FastMapper::stitch_nv12 (mapper_fast.cpp:153-195) on device NV12 frames (H rows of Y, then H/2 rows
- * of interleaved U,V; pitch >= W).  Output: W x 3H/2, chroma rows interleaved V,U — the reference's
- * channel order (merge of the V-then-U accumulators).  Stream-ordered. */
+ * of interleaved U,V; W <= pitch < 2^24).  Output: W x 3H/2, chroma rows interleaved V,U — the reference's
+ * channel order (merge of the V-then-U accumulators).  Stream-ordered; the FastMapper keeps no per-call
+ * device state, so calls with their own outputs may run concurrently on different streams. */
 int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fastmapper, const uint8_t* const* in_dev, const size_t* in_pitch,
                                  uint8_t* out_dev, size_t out_pitch, void* stream);
 /* Algorithmic bytes one stitch_nv12 moves (entries read, output written, source bytes its weighted taps
