@@ -38,6 +38,10 @@ def parse():
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: independent frame sets stitched round-robin on this many streams "
                          "(octvr_mapper_set_frames_in_flight); default per config, DEFAULT_INFLIGHT")
+    ap.add_argument("--frame-sets", type=int, default=None,
+                    help="distinct source frame sets rotated through the timed region (default 8, at least the "
+                         "frames in flight): 8 C2 sets are 600 MB, more than the 256 MB Infinity Cache, so every "
+                         "step reads its sources from HBM as a live pipeline's fresh frames would be")
     ap.add_argument("--no-async-e2e", action="store_true",
                     help="skip the AsyncMultiMapper end-to-end (PCIe-inclusive) measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
@@ -69,6 +73,21 @@ def frame_seed(rank, slot, cam):
     """Seed of camera `cam`'s synthetic frame for in-flight slot `slot` on rank `rank`: every rank
     stitches its own independent rig instance."""
     return 1000 * (rank + 1) + 100 * slot + cam
+
+
+def derive_set(base, seeds):
+    """Frame set from a base set on the device: camera i's frame XOR synthetic.frame_key(seeds[i]) repeated
+    over its bytes (synthetic.derived_frame, byte for byte) — distinct uniform-random content in milliseconds
+    instead of a host splitmix pass per 4K frame."""
+    import torch
+    from octvr_amd import synthetic
+    out = []
+    for t, sd in zip(base, seeds):
+        key = torch.from_numpy(synthetic.frame_key(sd)).to(t.device)
+        flat = t.reshape(-1)
+        reps = (flat.numel() + key.numel() - 1) // key.numel()
+        out.append(torch.bitwise_xor(flat, key.repeat(reps)[:flat.numel()]).reshape(t.shape))
+    return out
 
 
 def timed_region(step, steps, sync, dist=None):
@@ -123,9 +142,13 @@ def pmc_traffic(config, blend):
 
 
 def pmc_valu_busy(config):
-    """The composite's VALU issue share from the PMC summary of this binary: SQ_ACTIVE_INST_VALU (quad-cycles
-    summed over every SIMD) x 4 / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024 SIMDs), i.e. the fraction of the kernel's
-    SIMD cycles spent issuing VALU (MI355X_MICROARCH.md, SQ counters).  None without such a summary."""
+    """Bounds on the composite's VALU issue share from the PMC summary of this binary (one launch alone
+    under rocprofv3, which serialises dispatches).  SIMD cycles of the launch = GRBM_GUI_ACTIVE / 8 XCDs x
+    1,024 SIMDs.  Upper bound: SQ_ACTIVE_INST_VALU (quad-cycles) x 4 — the counter charges about one
+    quad-cycle per VALU instruction, the issue cost of one wave alone; lower bound: SQ_INSTS_VALU x 2, the
+    SIMD-32's cost of a wave64 instruction when two or more waves share the SIMD (MI355X_MICROARCH.md,
+    Execution model and the per-instruction table).  Slow opcodes of this loop (v_perm, v_dot2, the packed
+    forms) sit between the two.  None without such a summary."""
     import glob
     sha = lib_sha256()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % config))):
@@ -135,9 +158,14 @@ def pmc_valu_busy(config):
         for k, cs in d.get("counters", {}).items():
             if "stitch_tiled_kernel" in k and "SQ_ACTIVE_INST_VALU" in cs and "GRBM_GUI_ACTIVE" in cs:
                 a, g = cs["SQ_ACTIVE_INST_VALU"]["median"], cs["GRBM_GUI_ACTIVE"]["median"]
-                return {"frac": round(a * 4.0 / (g / 8.0 * 1024.0), 3), "source": os.path.basename(path),
-                        "note": "one launch alone under rocprofv3 (PMC serialises dispatches): SIMD cycles issuing VALU / "
-                                "kernel cycles; the composite is VALU-issue-bound (DESIGN.md §4)"}
+                simd_cycles = g / 8.0 * 1024.0
+                r = {"upper": round(a * 4.0 / simd_cycles, 3), "source": os.path.basename(path),
+                     "note": "share of the launch's SIMD cycles spent issuing VALU, bounded: upper = "
+                             "SQ_ACTIVE_INST_VALU quad-cycles x 4 (4 cycles per instruction), lower = SQ_INSTS_VALU x 2 "
+                             "(2 cycles per wave64 instruction on a shared SIMD-32)"}
+                if "SQ_INSTS_VALU" in cs:
+                    r["lower"] = round(cs["SQ_INSTS_VALU"]["median"] * 2.0 / simd_cycles, 3)
+                return r
     return None
 
 
@@ -176,6 +204,13 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
 # two 4s were 511k and 459k), F2 (stitch_nv12 on 1 / 2 / 3 streams) 85k / 91k / 93k
 DEFAULT_INFLIGHT = {"C3": 4, "F2": 3}
 CPU_BASELINE_S = float(os.environ.get("OCTVR_CPU_BASELINE_S", "10"))
+DEFAULT_FRAME_SETS = 8
+
+
+def frame_sets_of(args, inflight):
+    """Distinct source frame sets the timed steps rotate through: --frame-sets, default 8, never fewer
+    than the frames in flight (a set is in use by one in-flight stitch at a time)."""
+    return max(inflight, args.frame_sets if args.frame_sets is not None else DEFAULT_FRAME_SETS)
 
 
 def cpu_baseline(mt, frames_np, sizes, W, H, blend=0, gain=True):
@@ -208,11 +243,32 @@ def cpu_baseline(mt, frames_np, sizes, W, H, blend=0, gain=True):
     return r
 
 
-def visible_gpus():
-    """Number of GPUs this process may use, counted without initialising HIP (the parent of a
-    multi-rank launch must not touch the GPU before it starts its ranks)."""
-    import torch
-    return torch.cuda.device_count()
+def visible_gpus(kfd_nodes="/sys/class/kfd/kfd/topology/nodes", env=None):
+    """Number of GPUs this process may use, counted without any HIP call: the parent of a multi-rank
+    launch must not touch the GPU before it starts its ranks (torch.cuda.device_count() falls back to
+    hipGetDeviceCount when amdsmi cannot enumerate).  GPU agents are the KFD topology nodes with SIMDs
+    (simd_count > 0), narrowed by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES as
+    the runtime narrows them.  Raises RuntimeError when the topology is unreadable."""
+    env = os.environ if env is None else env
+    try:
+        names = sorted(os.listdir(kfd_nodes), key=lambda x: int(x) if x.isdigit() else -1)
+    except OSError as e:
+        raise RuntimeError("bench.py: cannot count GPUs without HIP: %s unreadable (%s)" % (kfd_nodes, e))
+    n = 0
+    for name in names:
+        try:
+            with open(os.path.join(kfd_nodes, name, "properties")) as f:
+                props = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:  # each narrows the list the previous one left
+            ids = [x for x in v.split(",") if x.strip() != ""]
+            n = min(n, len(ids)) if v.strip() else 0
+    return n
 
 
 def launch_ranks(n, argv, check_devices=True):
@@ -222,7 +278,11 @@ def launch_ranks(n, argv, check_devices=True):
     one JSON line.  Runs before anything touches the GPU; returns the worst child exit status."""
     import socket
     if check_devices:
-        have = visible_gpus()
+        try:
+            have = visible_gpus()
+        except RuntimeError as e:
+            sys.stderr.write("%s\n" % e)
+            return 2
         if n > have:
             sys.stderr.write("bench.py: --gpus %d but only %d GPU(s) visible\n" % (n, have))
             return 2
@@ -302,17 +362,22 @@ def fast_rank(args, world, rank, local_rank, dist):
     rig, W, H, sizes = synthetic.CONFIGS[args.config]()
     mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=False, device=dev)
     fm = ox.FastMapper(mt, sizes, device=dev)
-    frames_np = [nv12_of(synthetic.yuv_frame(w, h, frame_seed(rank, 0, i))) for i, (w, h) in enumerate(sizes)]
-    frames = [torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]
     # stitch_nv12 keeps no per-call device state, so a caller may run several at once on their own
     # streams and outputs (frames in flight, as the Mapper configs do through set_frames_in_flight)
     inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 1))
+    nsets = frame_sets_of(args, inflight)
+    # distinct frame sets (seeded by rank, set, camera), rotated through the steps as the Mapper configs do
+    frame_sets = [[torch.from_numpy(nv12_of(synthetic.yuv_frame(w, h, frame_seed(rank, 0, i)))).to(f"cuda:{dev}")
+                   for i, (w, h) in enumerate(sizes)]]
+    for j in range(1, nsets):
+        frame_sets.append(derive_set(frame_sets[0], [frame_seed(rank, j, i) for i in range(len(sizes))]))
+    frames = frame_sets[0]
     outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     stream, out = streams[0], outs[0]
 
     def step(k):
-        fm.stitch_nv12(frames, outs[k % inflight], stream=streams[k % inflight])
+        fm.stitch_nv12(frame_sets[k % nsets], outs[k % inflight], stream=streams[k % inflight])
 
     if args.pmc_child:
         for k in range(max(args.steps, 1)):
@@ -339,10 +404,11 @@ def fast_rank(args, world, rank, local_rank, dist):
         "value": round(aggregate_mps(world, args.steps, W * H, elapsed), 1), "unit": "MP/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-        "data": "synthetic (splitmix64 frames as NV12, SURVEY.md §8d rig)",
+        "data": "synthetic (splitmix64 frames as NV12, further sets derived by a splitmix64 key, SURVEY.md §8d rig)",
         "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
                                "template without ROI), NV12 in/out" % (len(sizes), sizes[0][0], sizes[0][1], W, H),
-                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "parallelism": "independent rig per GPU"},
+                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
+                   "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "fast_y_kernel + fast_uv_kernel", "kernel_us": round(kern_s * 1e6, 2),
@@ -381,18 +447,20 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
     inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 3))
     m.set_frames_in_flight(inflight)
-    # each rank stitches an independent rig instance: frames seeded by (rank, in-flight slot, camera)
+    # each rank stitches an independent rig instance: frames seeded by (rank, frame set, camera); the
+    # steps rotate through nsets distinct sets (> 256 MB of sources for C2 / C4 at the default 8, so the
+    # Infinity Cache cannot keep them between steps)
+    nsets = frame_sets_of(args, inflight)
     frames_np = [synthetic.yuv_frame(w, h, frame_seed(rank, 0, i)) for i, (w, h) in enumerate(sizes)]
     frame_sets = [[torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]]
-    for j in range(1, inflight):
-        frame_sets.append([torch.from_numpy(synthetic.yuv_frame(w, h, frame_seed(rank, j, i))).to(f"cuda:{dev}")
-                           for i, (w, h) in enumerate(sizes)])
+    for j in range(1, nsets):
+        frame_sets.append(derive_set(frame_sets[0], [frame_seed(rank, j, i) for i in range(len(sizes))]))
     outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
 
     def step(k):
         j = k % inflight
-        m.stitch(frame_sets[j], outs[j], stream=streams[j])
+        m.stitch(frame_sets[k % nsets], outs[j], stream=streams[j])
 
     if args.pmc_child:  # a few launches for rocprofv3 --pmc passes
         for k in range(max(args.steps, 1)):
@@ -474,13 +542,14 @@ def gpu_rank(args, world, rank, local_rank, dist):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (splitmix64 YUV420P frames, SURVEY.md §8d rig)",
+        "data": "synthetic (splitmix64 YUV420P frames, further sets derived by a splitmix64 key, SURVEY.md §8d rig)",
         "config": {"workload": "%s: %d x %dx%d fullframe_fisheye -> %dx%d equirect, remap + %s + %s, YUV420P in/out" % (
                                    args.config, len(sizes), sizes[0][0], sizes[0][1], W, H,
                                    "gain (estimated per frame)" if use_gain else "no gain",
                                    "multi-band blend=%d (%d bands)" % (blend, int(math.ceil(math.log(blend) / math.log(2.)) - 1))
                                    if blend > 0 else "no-blend composite"),
-                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "parallelism": "independent rig per GPU"},
+                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
+                   "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "multiband sequence (remap, pyrDown, blend levels)" if blend > 0 else "stitch_kernel",

@@ -27,7 +27,13 @@
 #ifndef OCTVR_HPP
 #define OCTVR_HPP
 
+// std::to_chars(double) for the rapidjson overloads where the standard library has it (C++17 and
+// libstdc++ 11+ / libc++ 14+); without it write_double falls back to a locale-safe snprintf
+#if defined(OCTVR_HAVE_RAPIDJSON) && defined(__has_include) && __cplusplus >= 201703L
+#if __has_include(<charconv>)
 #include <charconv>
+#endif
+#endif
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -132,10 +138,27 @@ inline cv::Mat mat_copy(const T* src, int rows, int cols, int type) {
 inline cv::Mat packed(const cv::Mat& m) { return m.isContinuous() ? m : m.clone(); }
 
 #ifdef OCTVR_HAVE_RAPIDJSON
-// a rapidjson value as JSON text with every number in its shortest round-trip form (std::to_chars),
-// parsed back with correct rounding (OCTVR_JSON_EXACT, std::from_chars): the doubles the caller's
-// rapidjson holds, unchanged.  Both conversions are locale-independent (a Qt caller has called
-// setlocale(LC_ALL, ""); printf / strtod would write and read "1,5" under a comma locale).
+// one double as JSON text that reads back as the same double, whatever the C library's LC_NUMERIC: the
+// shortest round-trip form with std::to_chars where the standard library has the floating-point overload
+// (C++17, libstdc++ 11+), else 17 significant digits with the locale's radix character put back to '.'
+inline void write_double(double d, std::string& out) {
+    char buf[64];
+#if defined(__cpp_lib_to_chars) && __cpp_lib_to_chars >= 201611L
+    const std::to_chars_result r = std::to_chars(buf, buf + sizeof buf, d);
+    out.append(buf, r.ptr);
+#else
+    const int k = snprintf(buf, sizeof buf, "%.17g", d);
+    for (int i = 0; i < k; i++)
+        if (!((buf[i] >= '0' && buf[i] <= '9') || buf[i] == '-' || buf[i] == '+' || buf[i] == 'e' || buf[i] == 'E' ||
+              buf[i] == 'i' || buf[i] == 'n' || buf[i] == 'f' || buf[i] == 'a'))
+            buf[i] = '.';
+    out.append(buf, buf + k);
+#endif
+}
+// a rapidjson value as JSON text with every number in a round-trip form (write_double), parsed back with
+// correct rounding (OCTVR_JSON_EXACT, std::from_chars): the doubles the caller's rapidjson holds,
+// unchanged.  Both conversions are locale-independent (a Qt caller has called setlocale(LC_ALL, "");
+// printf / strtod would write and read "1,5" under a comma locale).
 inline void write_exact(const rapidjson::Value& v, std::string& out) {
     char buf[64];
     if (v.IsObject()) {
@@ -172,8 +195,7 @@ inline void write_exact(const rapidjson::Value& v, std::string& out) {
         snprintf(buf, sizeof buf, "%llu", (unsigned long long)v.GetUint64());
         out += buf;
     } else {
-        const std::to_chars_result r = std::to_chars(buf, buf + sizeof buf, v.GetDouble());
-        out.append(buf, r.ptr);
+        write_double(v.GetDouble(), out);
     }
 }
 inline std::string json_exact(const rapidjson::Value& v) {

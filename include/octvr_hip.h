@@ -259,6 +259,18 @@ int octvr_rig_lut_recomputed(const octvr_rig* rig, int i, uint64_t* n);
  * fragile unused).  x, y, fragile: host arrays of out_w * out_h.  Include masks are not evaluated. */
 int octvr_debug_project_f64(const char* json, int out_w, int out_h, int input, int device, int where, double* x,
                             double* y, uint8_t* fragile);
+/* FastMapper index audit (host only, no GPU): builds the FastMapper plan of `rig` for these input sizes
+ * (8-byte entries when force_wide) exactly as octvr_fastmapper_create does, and replays on the host every
+ * index fast_y_kernel / fast_uv_kernel derive for every run, camera group, slot and lane — block, entry,
+ * weight and header indices against the uploaded arrays, camera against the frame set, each 8-byte tap-row
+ * load against an NV12 frame of pitch w + pitch_pad, the in-image taps' bytes inside the loaded 8, the
+ * output bytes.  Writes per-plane counts as JSON; returns OCTVR_E_INVALID if any access is out of range. */
+int octvr_debug_fastmapper_audit(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, int force_wide,
+                                 int pitch_pad, char* json, size_t len);
+/* The rig-config JSON reader on one document: the first number of `json` (a number, or the first element
+ * of an array), parsed with rapidjson's rules (flags 0, as the reference reads its configs) or correctly
+ * rounded (OCTVR_JSON_EXACT; out-of-range literals give +-HUGE_VAL / the subnormal / 0 as strtod). */
+int octvr_debug_json_number(const char* json, int flags, double* value);
 /* Saturating float -> u8 conversion as the kernels implement it (method 0: rint + clamp in VALU,
  * method 1: v_cvt_pk_u8_f32), for a known-answer test of round-half-even and clamping on device. */
 int octvr_selftest_sat_u8(const float* in_dev, uint8_t* out_dev, int n, int method, void* stream);

@@ -121,38 +121,13 @@ __device__ __forceinline__ void bilerp_rgba(uint32_t c00, uint32_t c01, uint32_t
     }
 }
 
-// bilerp_rgba at weight scale 2^16, straight from a tiled entry (fx bits 15-19, fy 20-24), channel
-// values returned as floats.  X = {64 (32 - fx), 64 fx} (one 24-bit multiply-add), w0 = X (32 - fy) and
-// w1 = X fy per 16-bit half, so (sum + 2^15) >> 16 is bilerp_rgba's (sum' + 2^9) >> 10 exactly
-// (w = 64 w').  Every half stays <= 63,488 except code 0's (fx = fy = 0) 65,536: w0 is formed as
-// X (31 - fy) + X with a saturating packed add (v_pk_add_u16 clamp; gfx950 ignores the clamp bit of
-// v_pk_mul_lo_u16, scripts/clamp_probe.hip), so that half becomes 65,535 and
-// (65535 c00 + 2^15) >> 16 = c00 for c00 <= 255 — the table's own {32767, 0, 0, 1} result.  The sum
-// stays below 2^24, so the result is byte 2 of it: v_cvt_f32_ubyte2, no shift (5 VALU per channel
-// instead of 6: perm, perm, dot2, dot2, cvt).
-__device__ __forceinline__ void bilerp_rgba_f(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint32_t e,
-                                              float (&rgb)[3]) {
-    const uint32_t fx = (e >> 15) & 31u, fy = (e >> 20) & 31u;
-    const uint32_t X = __umul24(fx, 0x3FFFC0u) + 2048u;  // (2048 - 64 fx) | (64 fx) << 16
-    // (X is 28 bits wide, beyond __umul24's operands: packed 16-bit multiplies)
-    const u16x2_t Xv = __builtin_bit_cast(u16x2_t, X);
-    const unsigned short gy = (unsigned short)(31u - fy);
-    const u16x2_t w0v = __builtin_elementwise_add_sat(Xv * u16x2_t{gy, gy}, Xv);
-    const uint32_t w0 = __builtin_bit_cast(uint32_t, w0v);
-    const u16x2_t w1 = Xv * u16x2_t{(unsigned short)fy, (unsigned short)fy};
-#pragma unroll
-    for (int ch = 0; ch < 3; ch++) {
-        const uint32_t sel = 0x0C000C00u | ((4u + ch) << 16) | (uint32_t)ch;  // {lo.ch, 0, hi.ch, 0}
-        const u16x2_t top = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c01, c00, sel));
-        const u16x2_t bot = __builtin_bit_cast(u16x2_t, __builtin_amdgcn_perm(c11, c10, sel));
-        const uint32_t S = __builtin_amdgcn_udot2(
-            bot, w1, __builtin_amdgcn_udot2(top, __builtin_bit_cast(u16x2_t, w0), 32768u, false), false);
-        rgb[ch] = (float)((S >> 16) & 255u);
-    }
-}
-
-// bilerp_rgba_f's weight pairs of fraction code fxy = fx | fy << 5: w.x = {W00, W01}, w.y = {W10, W11}
-// at scale 2^16 (code 0's W00 saturated to 65,535).  The composite keeps all 1,024 in an LDS table.
+// bilerp_rgba's weights at scale 2^16 for fraction code fxy = fx | fy << 5, as two packed 16-bit pairs
+// w.x = {W00, W01}, w.y = {W10, W11}: X = {64 (32 - fx), 64 fx} (one 24-bit multiply-add), W0 = X (32 - fy)
+// and W1 = X fy per half, so (sum + 2^15) >> 16 is bilerp_rgba's (sum' + 2^9) >> 10 exactly (w = 64 w').
+// Every half stays <= 63,488 except code 0's (fx = fy = 0) 65,536: w0 is formed as X (31 - fy) + X with
+// a saturating packed add (gfx950 ignores the clamp bit of v_pk_mul_lo_u16, scripts/clamp_probe.hip), so
+// that half becomes 65,535 and (65535 c00 + 2^15) >> 16 = c00 for c00 <= 255 — the 15-bit table's own
+// {32767, 0, 0, 1} result.  The composite keeps all 1,024 in an LDS table.
 __device__ __forceinline__ uint2 bilerp_weights(uint32_t fxy) {
     const uint32_t fx = fxy & 31u, fy = fxy >> 5;
     const uint32_t X = __umul24(fx, 0x3FFFC0u) + 2048u;
@@ -163,7 +138,8 @@ __device__ __forceinline__ uint2 bilerp_weights(uint32_t fxy) {
     return uint2{__builtin_bit_cast(uint32_t, w0), __builtin_bit_cast(uint32_t, w1)};
 }
 
-// bilerp_rgba_f with the weight pairs given (from the LDS table): perm, perm, dot2, dot2, cvt per channel
+// The bilinear sum with the weight pairs given (from the LDS table): the sum stays below 2^24, so the
+// channel is byte 2 of it — perm, perm, dot2, dot2, v_cvt_f32_ubyte2 per channel, values as floats
 __device__ __forceinline__ void bilerp_rgba_w(uint32_t c00, uint32_t c01, uint32_t c10, uint32_t c11, uint2 w,
                                               float (&rgb)[3]) {
 #pragma unroll
@@ -316,20 +292,15 @@ struct OutFrame {
 constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host: frame < 2^31 - 64 B)
 // Cache-policy bits of the output-frame stores (gfx950: 1 sc0, 2 nt, 16 sc1).  sc1 writes the frame
 // through (nothing of it left dirty in the XCD L2s when the kernel ends): C2 stitch -1.5 %.
-#ifndef OCTVR_OUT_POLICY
-#define OCTVR_OUT_POLICY 16
-#endif
+constexpr int kOutPolicy = 16;
 
 __device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
-#if OCTVR_DIAG_HOTOUT  // diagnostic: every tile row writes rows 0-7 (the same 64 KB): no DRAM writes
-    y &= 7;
-#endif
     const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
     const uint32_t oc = in ? (uint32_t)(y >> 1) * o.pitch + (uint32_t)(x >> 1) : kDropOffset;
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, OCTVR_OUT_POLICY);
-    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, OCTVR_OUT_POLICY);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, OCTVR_OUT_POLICY);
-    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, OCTVR_OUT_POLICY);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y01, o.rsrc, oy, 0, kOutPolicy);
+    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)q.y23, o.rsrc, in ? oy + o.pitch : kDropOffset, 0, kOutPolicy);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.u, o.rsrc, in ? oc + o.u_off : kDropOffset, 0, kOutPolicy);
+    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)q.v, o.rsrc, in ? oc + o.v_off : kDropOffset, 0, kOutPolicy);
 }
 
 

@@ -36,44 +36,16 @@ __device__ __forceinline__ uint8_t convert_out(uint32_t acc) {  // convertTo(CV_
 
 }  // namespace
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-// remap_weighted.cl:46-75 for one pixel of one camera from its four taps (0 outside the source):
-// ((t0 (1 - ux)) (1 - uy) + (t1 ux) (1 - uy)) + (t2 (1 - ux)) uy + (t3 ux) uy, every product and sum
-// rounded as written (-ffp-contract=off), two channels at a time in packed f32 (lane .x / .y of t01,
-// t23: {t0, t1} / {t2, t3} for one channel, or {V, U} of one tap pair when CH2)
-__device__ __forceinline__ f32x2 uxy(uint32_t code) {
-    return f32x2{(float)(code & 31u) / 32.f, (float)(code >> 5) / 32.f};
-}
-__device__ __forceinline__ uint32_t weighted_sum(f32x2 t01, f32x2 t23, uint32_t code, uint32_t w) {
-    const f32x2 u = uxy(code);
-    const f32x2 q = (t01 * f32x2{1 - u.x, u.x}) * f32x2{1 - u.y, 1 - u.y};
-    const f32x2 r = (t23 * f32x2{1 - u.x, u.x}) * f32x2{u.y, u.y};
-    float v = ((q.x + q.y) + r.x) + r.y;
-    v *= (float)w;
-    return sat_u16_rte(v);
-}
-// the same for two channels c = .x, .y: taps t[j] = {c0 tap j, c1 tap j}
-__device__ __forceinline__ void weighted_sum2(const f32x2 (&t)[4], uint32_t code, uint32_t w, uint32_t& a0, uint32_t& a1) {
-    const f32x2 u = uxy(code);
-    const f32x2 nx = {1 - u.x, 1 - u.x}, px = {u.x, u.x}, ny = {1 - u.y, 1 - u.y}, py = {u.y, u.y};
-    f32x2 v = (((t[0] * nx) * ny + (t[1] * px) * ny) + (t[2] * nx) * py) + (t[3] * px) * py;
-    v *= f32x2{(float)w, (float)w};
-    a0 += sat_u16_rte(v.x);
-    a1 += sat_u16_rte(v.y);
-}
-
-// The same sum in integers (OCTVR_FAST_INT = 1).  With ux = fx / 32, uy = fy / 32 and integer taps t <= 255
-// every product and partial sum above is exact in f32 (t (32 - fx) (32 - fy) <= 255 * 1024 < 2^24, and the
-// four terms add up to at most 255 * 1024 / 1024): v = N / 1024 with
+// remap_weighted.cl:46-75 for one pixel of one camera, ((t0 (1 - ux)) (1 - uy) + (t1 ux) (1 - uy)) +
+// (t2 (1 - ux)) uy + (t3 ux) uy in f32 with every product and sum rounded as written, computed in
+// integers: with ux = fx / 32, uy = fy / 32 and integer taps t <= 255 every product and partial sum is
+// exact in f32 (t (32 - fx) (32 - fy) <= 255 * 1024 < 2^24, and the four terms add up to at most
+// 255 * 1024 / 1024): v = N / 1024 with
 //   N = (32 - fy) (t0 (32 - fx) + t1 fx) + fy (t2 (32 - fx) + t3 fx),
 // two v_dot2_u32_u16 for the rows and one for the column.  The only rounding is v * w: fl(N / 1024 * w) =
 // fl(N * (w / 1024)), w / 1024 exact; then round half to even (<= 65,025, no saturation).  Taps outside
 // the image are zeroed through the weights: column c's weight is 0 when x + c is outside, row r's when
 // y + r is (tap (c, r) is inside exactly when both are).
-#ifndef OCTVR_FAST_INT
-#define OCTVR_FAST_INT 1
-#endif
 typedef unsigned short fast_u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t weighted_sum_int(uint32_t row0, uint32_t row1, uint32_t wx, uint32_t wy, float wf) {
     const uint32_t h0 = __builtin_amdgcn_udot2(__builtin_bit_cast(fast_u16x2, row0), __builtin_bit_cast(fast_u16x2, wx), 0u, false);
@@ -89,12 +61,9 @@ __device__ __forceinline__ uint32_t weighted_sum_int(uint32_t row0, uint32_t row
 // the image, taps outside it zeroed by mask, as BORDER_CONSTANT), instead of 2 (Y) or 4 (chroma) byte
 // loads.  Slots past the run's cameras are skipped by uniform branches (a C2 run has about 4 cameras,
 // i.e. a second group of 4 is mostly empty; the kernels issue VALU in every SIMD cycle and keep the
-// texture data path 94 % busy, so work done for empty slots cost its full share).  PLANE 0: Y; 1: the interleaved NV12 chroma, V and U (merge order
-// c1, c2: V first, mapper_fast.cpp:181-187).
-#ifndef OCTVR_FAST_GROUP
-#define OCTVR_FAST_GROUP 4
-#endif
-constexpr int kFastGroup = OCTVR_FAST_GROUP;
+// texture data path 94 % busy, so work done for empty slots cost its full share).  PLANE 0: Y; 1: the
+// interleaved NV12 chroma, V and U (merge order c1, c2: V first, mapper_fast.cpp:181-187).
+constexpr int kFastGroup = 4;  // (groups of 2, 3 or 6 measured 1-6 % slower)
 
 struct FastPlane {
     const uint2* ent;     // wide entries
@@ -102,6 +71,7 @@ struct FastPlane {
     const uint8_t* wgt;   // compact weights
     const uint2* hdr;     // compact block headers
     const uint2* runs;    // per run: camera mask, first block
+    uint32_t nblk;        // blocks allocated (>= 1)
 };
 
 template <int PLANE, bool COMPACT>
@@ -127,8 +97,11 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
             live[k] = m != 0u;
             cam[k] = live[k] ? __builtin_ctz(m) : 0;
             m &= m - 1u;
-            // every slot loads (dead ones the group's first block) so that no load waits on a branch
-            const uint32_t b = live[k] ? blk + k : blk;
+            // every slot loads (dead ones the group's first block) so that no load waits on a branch.  The
+            // block is clamped into the plane's allocation (one scalar min): the host's index replay
+            // (octvr_debug_fastmapper_audit) shows it never engages, but no entry, weight or header
+            // address can then leave the buffers whatever the run table holds.
+            const uint32_t b = min(live[k] ? blk + k : blk, fp.nblk - 1u);
             const uint32_t e = b * 256u + threadIdx.x;  // < 2^32 (host check)
             if (COMPACT) {
                 hd[k] = *(kU64*)(uintptr_t)(fp.hdr + b);
@@ -184,11 +157,8 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
                 // at most at byte 6, so its second byte is i + 1 <= 7
                 const uint32_t d = row + (uint32_t)sx * bpp - st;
                 const uint32_t i0 = d & 7u, i1 = (d + bpp) & 7u;
-#if OCTVR_FAST_INT  // u16 pairs {tap x, tap x + 1} (chroma: of U; V is the next byte of each)
+                // u16 pairs {tap x, tap x + 1} (chroma: of U; V is the next byte of each)
                 sel[k][r] = i0 | i1 << 16 | 0x0C000C00u;
-#else
-                sel[k][r] = PLANE ? (i0 | (i0 + 1u) << 8 | i1 << 16 | (i1 + 1u) << 24) : (i0 | i1 << 8 | 0x0C0C0000u);
-#endif
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                 const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, st, 0, 0);
                 rw[k][r] = make_uint2(v.x, v.y);
@@ -203,7 +173,6 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
             const int sx = sxk[k], sy = syk[k];
             const bool ix0 = (uint32_t)sx < sw, ix1 = (uint32_t)(sx + 1) < sw;
             const bool iy0 = (uint32_t)sy < sh, iy1 = (uint32_t)(sy + 1) < sh;
-#if OCTVR_FAST_INT
             const uint32_t fx = code[k] & 31u, fy = code[k] >> 5;
             // {32 - f, f} as u16 pairs: 32 + f * 0xFFFF, masked per column / row
             const uint32_t wx = (32u + fx * 0xFFFFu) & ((ix0 ? 0xFFFFu : 0u) | (ix1 ? 0xFFFF0000u : 0u));
@@ -215,22 +184,6 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
             if (PLANE)
                 acc1 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0]), __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1]),
                                          wx, wy, wf);
-            continue;
-#endif
-            // row r's taps: Y bytes {x, x + 1}, or chroma bytes {U x, V x, U x+1, V x+1}
-            const uint32_t b0 = __builtin_amdgcn_perm(rw[k][0].y, rw[k][0].x, sel[k][0]);
-            const uint32_t b1 = __builtin_amdgcn_perm(rw[k][1].y, rw[k][1].x, sel[k][1]);
-            auto byte = [](uint32_t b, int i, bool in) { return in ? (float)((b >> (8 * i)) & 255u) : 0.f; };
-            if (PLANE) {
-                const f32x2 t[4] = {{byte(b0, 1, ix0 && iy0), byte(b0, 0, ix0 && iy0)},
-                                    {byte(b0, 3, ix1 && iy0), byte(b0, 2, ix1 && iy0)},
-                                    {byte(b1, 1, ix0 && iy1), byte(b1, 0, ix0 && iy1)},
-                                    {byte(b1, 3, ix1 && iy1), byte(b1, 2, ix1 && iy1)}};
-                weighted_sum2(t, code[k], wk[k], acc0, acc1);
-            } else {
-                acc0 += weighted_sum(f32x2{byte(b0, 0, ix0 && iy0), byte(b0, 1, ix1 && iy0)},
-                                     f32x2{byte(b1, 0, ix0 && iy1), byte(b1, 1, ix1 && iy1)}, code[k], wk[k]);
-            }
         }
     }
     // pixel index -> (x, y): the run's first row by one scalar division, then at most 256 / pw row steps
@@ -279,7 +232,7 @@ static hipError_t launch_plane(const FrameSet& frames, const FastMapperPlane& p,
                                int64_t out_pitch, hipStream_t s) {
     const int64_t n = PLANE ? (int64_t)(W / 2) * (H / 2) : (int64_t)W * H;
     const dim3 grid((unsigned)((n + 255) / 256));
-    const FastPlane fp{p.ent, p.off, p.wgt, p.hdr, p.runs};
+    const FastPlane fp{p.ent, p.off, p.wgt, p.hdr, p.runs, p.nblk};
     if (p.compact)
         launch_plane_kernel<PLANE, true>(grid, frames, fp, W, H, out, out_pitch, s);
     else

@@ -3,6 +3,9 @@
 // rig schema needs: objects, arrays, numbers, strings, true/false/null.  Throws std::runtime_error.
 #pragma once
 
+#include <locale.h>
+
+#include <cerrno>
 #include <charconv>
 #include <cstdint>
 #include <cstdlib>
@@ -143,7 +146,14 @@ private:
                 if (b < e && !(*b == '-' || (*b >= '0' && *b <= '9'))) fail("bad number");
                 double x = 0.0;
                 const std::from_chars_result r = std::from_chars(b, e, x, std::chars_format::general);
-                if (r.ec != std::errc() || r.ptr == b) fail("bad number");
+                if (r.ptr == b || (r.ec != std::errc() && r.ec != std::errc::result_out_of_range)) fail("bad number");
+                if (r.ec == std::errc::result_out_of_range) {
+                    // overflow (1e400) or underflow (subnormals on some libstdc++ versions): the value the
+                    // previous strtod path gave — +-HUGE_VAL, the subnormal, or 0 — read in the C locale
+                    static const locale_t c_loc = newlocale(LC_NUMERIC_MASK, "C", (locale_t)0);
+                    const std::string tok(b, r.ptr);
+                    x = c_loc ? strtod_l(tok.c_str(), nullptr, c_loc) : 0.0;
+                }
                 v.num = x;
                 i_ += (size_t)(r.ptr - b);
             } else {

@@ -13,26 +13,10 @@
 
 #include "device_common.hpp"
 #include "kernels.hpp"
-#ifndef OCTVR_LU_BLOCK_MIN  // smallest n solved by the workgroup-parallel LU (below: one lane, registers)
-#define OCTVR_LU_BLOCK_MIN 9
-#endif
-#ifndef OCTVR_FEED_VARIANT
-#define OCTVR_FEED_VARIANT 0
-#endif
 
 namespace octvr {
 
-#if OCTVR_PHASES && !OCTVR_STAMPS
-#define OCTVR_STAMPS 2  // the phase rows share the stamp buffer (no per-workgroup stamps then)
-#endif
-#if OCTVR_STAMPS
-// Diagnostic builds only (scripts/build_variant.sh NAME -DOCTVR_STAMPS=1): per-workgroup start / end
-// wall-clock stamps (s_memrealtime, 100 MHz) of the stitch and gain-feed kernels, read back with
-// octvr_debug_stamps().  Rows of 4 u64: start, end, items processed, staging chunks processed.
-constexpr int kStampRows = 8192;
-constexpr size_t kFeedStampBase = 4 * (size_t)kStampRows;  // gain-feed rows of 8 u64 after the stitch rows
-__device__ unsigned long long g_octvr_stamps[2 * kStampRows * 4];
-#endif
+constexpr int kLuBlockMin = 9;  // smallest n solved by the workgroup-parallel LU (below: one lane, registers)
 
 // ---------------------------------------------------------------------------------------------
 // LUT build: MapperTemplate::add_input (template.cpp:46-133), one thread per output pixel, FP64.
@@ -469,10 +453,7 @@ __device__ __forceinline__ void feed_taps_finish(const FeedRaw& r, Taps& t) {
 // round, partner sums in LDS, the workgroup LU above n = 3 (<= 80 VGPRs), so the feed of frame k+1
 // fits beside frame k's composite (6 workgroups per CU at 72 VGPRs / 96 SGPRs / 20.7 KiB LDS) and runs
 // under it.  Both sum the same exact values: identical gains.
-#ifndef OCTVR_LEAN_BATCH  // lean feed: samples per lane in flight per round
-#define OCTVR_LEAN_BATCH 3
-#endif
-constexpr int kLeanBatch = OCTVR_LEAN_BATCH;
+constexpr int kLeanBatch = 3;  // lean feed: samples per lane in flight per round
 template <bool LEAN>
 __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const CompositeEntry* samples,
                                                const uint16_t* partners, int n_chunks, const int32_t* N, int n,
@@ -483,9 +464,6 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
     __shared__ double s_b[kGainMaxCams];
     __shared__ double s_x[kGainMaxCams];
     const int tid = threadIdx.x, lane = tid & 63;
-#if OCTVR_STAMPS == 1
-    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
-#endif
     // Wave w of workgroup b takes the kGainWaveRun contiguous samples from (4 b + w) kGainWaveRun: one
     // camera's (runs padded on the host with invalid samples, partner mask 0), named in every entry's
     // code.  Every norm is 0 or a multiple of 2^-23 in [1, 2^9), so the f64 sums below are exact in any order.
@@ -587,19 +565,9 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
             }
         }
     }
-#if OCTVR_STAMPS == 1
-    unsigned long long st1 = 0, st2 = 0, st3 = 0;
-    if (tid == 0) {  // after the gathers and the f32 norms (the loop above consumed every load)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        st1 = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
     // then per (camera, partner) over the workgroup's waves, then one u64 atomic per pair
     if (lane == 0) s_wcam[wave] = cam;
     __syncthreads();
-#if OCTVR_STAMPS == 1
-    if (tid == 0) st2 = __builtin_amdgcn_s_memrealtime();
-#endif
     if (tid < 4 * n) {  // (wave w, partner j); the first wave of each camera adds for all its waves
         const int w = tid / n, j = tid - w * n, c = s_wcam[w];
         bool first = true;
@@ -616,9 +584,6 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
     // every wave's adds have completed before the workgroup takes its ticket
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-#if OCTVR_STAMPS == 1
-    if (tid == 0) st3 = __builtin_amdgcn_s_memrealtime();
-#endif
     if (tid == 0) {
         const int xcd = blockIdx.x & 7;
         const uint32_t in_xcd = (uint32_t)((n_chunks - xcd + 7) >> 3);
@@ -628,20 +593,6 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
             last = __hip_atomic_fetch_add(&tickets[8], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == groups - 1;
         }
         s_last = last;
-#if OCTVR_STAMPS == 1
-        if (blockIdx.x < 2048) {  // rows of 8: start, gathered, reduced, adds done, ticket, last, ...
-            unsigned long long* r = g_octvr_stamps + kFeedStampBase + (size_t)blockIdx.x * 8;
-            r[0] = st0;
-            r[1] = st1;
-            r[2] = st2;
-            r[3] = st3;
-            r[4] = __builtin_amdgcn_s_memrealtime();
-            r[5] = (unsigned long long)last;
-            r[6] = 0;
-            r[7] = 0;
-            (void)cam;
-        }
-#endif
     }
     __syncthreads();
     if (!s_last) return;
@@ -657,37 +608,21 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
     }
     if (tid < 9) __hip_atomic_exchange(&tickets[tid], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-#if OCTVR_STAMPS == 1
-    if (tid == 0) g_octvr_stamps[kFeedStampBase + (size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime();
-#endif
-#if OCTVR_FEED_VARIANT == 1
-    if (tid < n) gains[tid] = s_I[tid];
-    return;
-#endif
     if (tid < n) gain_system_row(s_I, s_N, n, tid, s_A, s_b);
     __syncthreads();
-#if OCTVR_STAMPS == 1
-    if (tid == 0) g_octvr_stamps[kFeedStampBase + 2048 * 8] = __builtin_amdgcn_s_memrealtime();
-#endif
     // cv::solve (lapack.cpp:1050-1275): one lane with the matrix in registers for n <= 8 (closed forms
     // n <= 3); the LU across the workgroup for 9..16
     bool ok;
     if (LEAN && n > 3) {  // the register LU would set the lean kernel's VGPR budget
         ok = lu_solve_block(s_A, s_b, n, s_x);
-    } else if (LEAN || n < OCTVR_LU_BLOCK_MIN || n <= 3) {
+    } else if (LEAN || n < kLuBlockMin || n <= 3) {
         if (tid == 0) s_last = (LEAN ? solve_small(s_A, s_b, n, s_x) : solve_dispatch(s_A, s_b, n, s_x)) ? 1 : 0;
         __syncthreads();
         ok = s_last != 0;
     } else {
         ok = lu_solve_block(s_A, s_b, n, s_x);
     }
-#if OCTVR_STAMPS == 1
-    if (tid == 0) g_octvr_stamps[kFeedStampBase + 2048 * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
     if (tid < n) gains[tid] = ok ? s_x[tid] : 1.0;  // cv::solve failure leaves gains_ unspecified; 1 as the oracle
-#if OCTVR_STAMPS == 1
-    if (tid == 0) g_octvr_stamps[kFeedStampBase + (size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
-#endif
 }
 
 __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
@@ -897,92 +832,27 @@ __device__ __forceinline__ void stage_store(const StageGroup& sg, uint32_t* s_rg
         b.z = vig_mul(b.z, sg.g1.z);
         b.w = vig_mul(b.w, sg.g1.w);
     }
-#if OCTVR_STAGE_B64
-    *reinterpret_cast<uint2*>(s_rgb + sg.dst) = make_uint2(a.x, a.y);
-    *reinterpret_cast<uint2*>(s_rgb + sg.dst + 2) = make_uint2(a.z, a.w);
-    *reinterpret_cast<uint2*>(s_rgb + sg.dst + 4) = make_uint2(b.x, b.y);
-    *reinterpret_cast<uint2*>(s_rgb + sg.dst + 6) = make_uint2(b.z, b.w);
-#else
     *reinterpret_cast<uint4*>(s_rgb + sg.dst) = a;
     *reinterpret_cast<uint4*>(s_rgb + sg.dst + 4) = b;
-#endif
 }
 
-#ifndef OCTVR_STITCH_BLOCKS_PER_CU
-#define OCTVR_STITCH_BLOCKS_PER_CU 6
-#endif
-constexpr int kStitchBlocksPerCU = OCTVR_STITCH_BLOCKS_PER_CU;
-// Residency of 256-thread workgroups is also capped by scalar registers: min(8, 800 / (sgpr16 + 16))
-// (MI355X_MICROARCH.md, Residency), i.e. <= 80 SGPRs for 8 per CU, <= 96 for 7 (the compiler's own
-// occupancy model allows more, so the budget is set explicitly).
-// The register budget is that of one workgroup more than the grid places per CU: the VGPRs / SGPRs
-// left on each SIMD (80 / 96 with 6 composite waves at <= 72 / 96) hold one wave of the lean gain
-// feed, so the next frame's feed runs beside this frame's composite (frames in flight).
-#ifndef OCTVR_STITCH_REG_BLOCKS
-#define OCTVR_STITCH_REG_BLOCKS (kStitchBlocksPerCU + 1)
-#endif
-constexpr int kStitchRegBlocks = OCTVR_STITCH_REG_BLOCKS > 8 ? 8 : OCTVR_STITCH_REG_BLOCKS;
-#ifndef OCTVR_STITCH_SGPRS
-#define OCTVR_STITCH_SGPRS (kStitchRegBlocks >= 8 ? 80 : kStitchRegBlocks == 7 ? 96 : 102)
-#endif
-// The VGPR budget of that many waves per SIMD, set explicitly: with the weight table the compiler's
-// LDS occupancy model (24 KiB per workgroup) would otherwise relax it to 5 waves' 102 VGPRs
-#ifndef OCTVR_STITCH_VGPRS
-#define OCTVR_STITCH_VGPRS (kStitchRegBlocks >= 8 ? 64 : kStitchRegBlocks == 7 ? 72 : kStitchRegBlocks == 6 ? 80 : 96)
-#endif
-#ifndef OCTVR_STAGE_REGS
-#define OCTVR_STAGE_REGS 1
-#endif
-#ifndef OCTVR_STAGE_SKIP
-#define OCTVR_STAGE_SKIP 1
-#endif
-#ifndef OCTVR_STORE_LATE
-#define OCTVR_STORE_LATE 0
-#endif
-#ifndef OCTVR_STORE_LATE_M1  // the same for the MODE-1 remap of the multi-band blend
-#define OCTVR_STORE_LATE_M1 0
-#endif
-#ifndef OCTVR_DYN  // 0: static round-robin dealing of a band's items (no work counters)
-#define OCTVR_DYN 1
-#endif
-#ifndef OCTVR_LDS_DB  // 1: small items alternate between two LDS halves (one barrier per item; C2 measured
-                      // 65.5 vs 63.7 us: the barrier is not what the item loop waits on), 0: off
-#define OCTVR_LDS_DB 0
-#endif
-#ifndef OCTVR_ISSUE_EARLY  // 1: the next item's loads issued before this item's second barrier
-#define OCTVR_ISSUE_EARLY 0
-#endif
-constexpr int kGainTables = OCTVR_LDS_DB ? 2 : 1;
-#ifndef OCTVR_ENT_LATE  // 1: the next item's entries loaded after this item's computation (not after its barrier)
-#define OCTVR_ENT_LATE 0
-#endif
-#ifndef OCTVR_SLN_LATE  // 1: the next item's staging slots resolved after the second barrier, right before
-                        // its loads (27 -> 5 SGPR spills, 30 -> 15 v_readlane per iteration; C2 +3 %)
-#define OCTVR_SLN_LATE 1
-#endif
-#ifndef OCTVR_FAST_STORE  // 1: scalar-offset output stores for items wholly inside the frame (MODE 0)
-#define OCTVR_FAST_STORE 1
-#endif
-#ifndef OCTVR_PRIO_STAGE  // > 0: s_setprio for the staging phase (the waves its barrier waits for)
-#define OCTVR_PRIO_STAGE 0
-#endif
-#ifndef OCTVR_WIDE_OUT  // 1: LDS-staged 16-byte output stores (measured no faster on C2; off)
-#define OCTVR_WIDE_OUT 0
-#endif
-// staging groups per lane loaded one item ahead (256 per reg) for items of 1 / 2 halves
-constexpr int kStageRegs = OCTVR_STAGE_REGS;
-#ifndef OCTVR_STAGE_REGS2
-#define OCTVR_STAGE_REGS2 1
-#endif
-#ifndef OCTVR_QPL  // quads per lane (128 x 8 halves per item) of the blend = 0 composite
-#define OCTVR_QPL 2
-#endif
+// Residency and register budget of the composite: 6 workgroups per CU (the grid is one resident wave
+// of them), compiled with the registers of 7 (72 VGPRs, 96 SGPRs; residency of 256-thread workgroups is
+// also capped by scalar registers, min(8, 800 / (sgpr16 + 16)), MI355X_MICROARCH.md, Residency), so each
+// SIMD keeps 80 VGPRs / 96 SGPRs and a wave slot for one wave of the lean gain feed beside 6 composite
+// waves: the next frame's feed runs under this frame's composite (frames in flight).  Set explicitly:
+// with the weight table the compiler's LDS occupancy model (24 KiB per workgroup) would otherwise relax
+// the budget to 5 waves' 102 VGPRs.
+constexpr int kStitchBlocksPerCU = 6;
+constexpr int kStitchRegBlocks = kStitchBlocksPerCU + 1;
+constexpr int kStitchSgprs = 96, kStitchVgprs = 72;
 
-// Software pipeline over a block's tiles (t, t + step, ...):
-//   iteration of tile t:  stage tile t's YUV (loaded during the previous iteration) into LDS,
-//                         read tile t+step's metadata (loaded one iteration earlier) into SGPRs,
-//                         issue tile t+step's entries + YUV loads and tile t+2*step's metadata load,
-//                         then compute tile t from LDS while all of those are in flight.
+// Software pipeline over a workgroup's items (t, then the items it claims):
+//   iteration of item t:  stage item t's YUV (loaded during the previous iteration) into LDS,
+//                         read the next item's metadata (loaded one iteration earlier),
+//                         store the previous item's output, issue the next item's entries + YUV loads and
+//                         the metadata load of the item after it,
+//                         then compute item t from LDS while all of those are in flight.
 // No global load is waited on in the iteration that issues it, and every iteration issues the
 // same vector-memory operations in the same order (clamped addresses instead of branches), so the
 // compiler's wait counts stay exact across the loop.
@@ -1014,52 +884,35 @@ __device__ __forceinline__ TileMeta meta_read(const uint4& v, int t) {
 }
 
 // An item's in-flight loads: its entries (one uint4 = one quad per lane and half) and the staging
-// groups of R chunks per wave.
-template <int Q, int R>
+// group of the wave's first chunk.
 struct TileData {
-    uint4 e4[Q];
-    StageGroup sg[R];
+    uint4 e4[kItemHalves];
+    StageGroup sg;
 };
 
-// Issue an item's entry loads and the staging loads of its first R chunks per wave (sl[r]: the
-// slots of chunks r * 4 + wave, from stage_slot).
+// Issue an item's entry loads and the staging loads of its first chunk per wave (sl: the slot of
+// chunk `wave`, from stage_slot<true>).
 // er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
 // scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
 // that the entries fit 32-bit offsets)
-template <bool DWORD_STAGE, bool VIG, int Q, int R, bool ENTRIES = true>
-__device__ __forceinline__ void data_issue(const TiledLut& lut, const __amdgpu_buffer_rsrc_t& er, const TileMeta& m,
-                                           int t_end, const StageSlot (&sl)[R], TileData<Q, R>& d) {
+template <bool DWORD_STAGE, bool VIG>
+__device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, const TileMeta& m, int t_end,
+                                           const StageSlot& sl, TileData& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
     const int wave = uniform(tid >> 6);
 #pragma unroll
-    for (int h = 0; h < Q; h++) {
-        if constexpr (!ENTRIES) break;
-#if OCTVR_DIAG_HOTENT  // diagnostic: every item reads item 0's entries (L2-resident)
-        d.e4[h] = reinterpret_cast<const uint4*>(lut.entries + (int64_t)h * kTilePx)[tid];
-#elif OCTVR_ENT_NT  // entries stream once: non-temporal loads (keep the source boxes in L2)
-        typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-        const u32x4_t v = __builtin_nontemporal_load(
-            reinterpret_cast<const u32x4_t*>(lut.entries + ((int64_t)(live ? m.t : 0) * Q + h) * kTilePx) + tid);
-        d.e4[h] = uint4{v.x, v.y, v.z, v.w};
-#else
+    for (int h = 0; h < kItemHalves; h++) {
         typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
-        const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * Q + h) * (uint32_t)(kTilePx * 4);
+        const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
         const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
         d.e4[h] = uint4{v.x, v.y, v.z, v.w};
-        (void)lut;
-#endif
     }
-#pragma unroll
-    for (int r = 0; r < R; r++) {
-#if OCTVR_STAGE_SKIP
-        if (!sl[r].live) {  // wave-uniform: no loads for a chunk the item lacks
-            d.sg[r].dst = -1;
-            continue;
-        }
-#endif
-        stage_load<DWORD_STAGE, VIG>(sl[r], m.stride, r * 4 + wave, d.sg[r]);
+    if (!sl.live) {  // wave-uniform: no loads for a chunk the item lacks
+        d.sg.dst = -1;
+        return;
     }
+    stage_load<DWORD_STAGE, VIG>(sl, m.stride, wave, d.sg);
 }
 
 // The composite's two sinks.  MODE 0: gain + RGB -> YUV420P into the output frame (blend = 0).
@@ -1131,15 +984,6 @@ __device__ __forceinline__ void store_rgba(const RgbaSink& o, const QuadOut& q, 
     __builtin_amdgcn_raw_buffer_store_b64(r1, o.rsrc, ok ? off + gp : kDropOffset, 0, 0);
 }
 
-template <int MODE>
-__device__ __forceinline__ void store_any(const OutFrame& of, const RgbaSink& ro, const QuadOut& q, uint32_t cam,
-                                          int x, int y, bool in) {
-    if constexpr (MODE == 0)
-        store_quad(of, q, x, y, in);
-    else
-        store_rgba(ro, q, cam, x, y, in);
-}
-
 // One half of an item: MODE 0 the YUV quad into `of`; MODE 1 the G0 quad where the item's flags say some
 // pyrDown or blend reads the lane's sub-tile (item_g0_bit), and the final result into `of` (the result frame)
 // where they say the sub-tile is deep (item_result_bit).  The lane's sub-tile: quarter (lane & 63) >> 4.
@@ -1150,124 +994,56 @@ __device__ __forceinline__ void store_half(const OutFrame& of, const RgbaSink& r
         store_quad(of, q, x, y, in);
     } else {
         const int q4 = (int)((threadIdx.x & 63u) >> 4);
-#if !OCTVR_DIAG_NOG0  // diagnostic (wrong output, timing only)
         if (flags & item_g0_bit(h, q4)) store_rgba(ro, q, cam, x, y, in);
-#endif
-#if !OCTVR_DIAG_NORES  // diagnostic (wrong output, timing only)
         if (flags & item_result_bit(h, q4)) store_result(of, res_rgba, q, x, y, in);
-#endif
     }
 }
 
-// MODE 2 output staging: one item's YUV420P output (Q halves of 128 x 8) in LDS as Y rows 0..8Q-1
-// (128 B each), then U rows 0..4Q-1 and V rows 0..4Q-1 (64 B each).  Each lane writes its quad's
-// 2 + 2 Y bytes and U, V bytes; after the next barrier lanes 0..96Q-1 store it with one 16-byte
-// store each (Y: 8 lanes per row, U / V: 4) instead of four 1-2-byte stores per quad.
-template <int Q>
-__device__ __forceinline__ void stage_out_quad(uint32_t* s_out, const QuadOut& q, int h, int qx, int qy) {
-    uint8_t* b = reinterpret_cast<uint8_t*>(s_out);
-    constexpr int kU = kTileW * kTileH * Q, kV = kU + (kTileH / 2) * (kTileW / 2) * Q;
-    const int yr = h * kTileH + 2 * qy, cr = h * (kTileH / 2) + qy;
-    *reinterpret_cast<uint16_t*>(b + yr * kTileW + 2 * qx) = (uint16_t)q.y01;
-    *reinterpret_cast<uint16_t*>(b + (yr + 1) * kTileW + 2 * qx) = (uint16_t)q.y23;
-    b[kU + cr * (kTileW / 2) + qx] = (uint8_t)q.u;
-    b[kV + cr * (kTileW / 2) + qx] = (uint8_t)q.v;
-}
-
-// Needs W % 32 == 0 and a 16-byte aligned frame and pitch (checked on the host); rows at or past H
-// (luma) / H/2 (chroma) are dropped.  (x0, y0): the item's top-left output pixel.
-template <int Q>
-__device__ __forceinline__ void store_item_wide(const OutFrame& o, const uint32_t* s_out, int x0, int y0, bool in, int H) {
-    const int l = threadIdx.x;
-    constexpr int kYl = 8 * kTileH * Q, kCl = 4 * (kTileH / 2) * Q;  // lanes of Y / of U (and V)
-    constexpr int kU = kTileW * kTileH * Q, kV = kU + (kTileH / 2) * (kTileW / 2) * Q;
-    int lds, row, col;
-    uint32_t plane;
-    bool ok;
-    if (l < kYl) {
-        row = y0 + (l >> 3);
-        col = x0 + 16 * (l & 7);
-        lds = (l >> 3) * kTileW + 16 * (l & 7);
-        plane = 0u;
-        ok = row < H;
-    } else {
-        const int k = l - kYl, isv = k >= kCl ? 1 : 0, kk = k - isv * kCl;
-        row = (y0 >> 1) + (kk >> 2);
-        col = (x0 >> 1) + 16 * (kk & 3);
-        lds = (isv ? kV : kU) + (kk >> 2) * (kTileW / 2) + 16 * (kk & 3);
-        plane = isv ? o.v_off : o.u_off;
-        ok = k < 2 * kCl && row < (H >> 1);
-    }
-    ok = ok && in;
-    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s_out) + (ok ? lds : 0));
-    const uint32_t off = ok ? plane + (uint32_t)row * o.pitch + (uint32_t)col : kDropOffset;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, o.rsrc, off, 0, OCTVR_OUT_POLICY);
-}
-
-// The composite's static LDS, one variable (so its size, a multiple of 16, is what the dynamic
-// region's base follows).  OCTVR_WTAB's weight table is the dynamic region (kWtabBytes at launch):
-// kept out of the static size, the compiler's LDS occupancy model still allows 7 workgroups per CU
-// and keeps the 7-wave register budget (72 VGPRs: the lean feed's wave fits beside 6 composite
-// waves per SIMD); the table's base is one add per pixel.
-template <int MODE, int QPL>
+// The composite's static LDS, one variable (so its size, exactly 16 KiB, is where the dynamic region
+// starts).  The weight table is the dynamic region (kWtabBytes at launch): kept out of the static size,
+// the compiler's LDS occupancy model still allows 7 workgroups per CU and keeps the 7-wave register
+// budget (72 VGPRs: the lean feed's wave fits beside 6 composite waves per SIMD); the table's base is
+// then the constant 0x4000 (wtab_read).
 struct alignas(16) StitchLds {
     uint32_t rgb[kTileLdsBytes / 4];  // the item's staged RGBA boxes (LDS address 0)
     float gain[kMaxCams];
-    f32x2_t slot_gain[OCTVR_LDS_DB ? 2 : 1][kTileSlots];
+    f32x2_t slot_gain[kTileSlots];
     uint32_t claim[2];
-    uint32_t out[MODE == 2 ? QPL * kTileOutBytes / 4 : 2];
+    uint32_t pad[2];
 };
-static_assert(sizeof(StitchLds<0, 2>) % 16 == 0 && sizeof(StitchLds<2, 1>) % 16 == 0, "dynamic LDS base alignment");
-static_assert(!OCTVR_WTAB || (sizeof(StitchLds<0, 2>) == 0x4000 && sizeof(StitchLds<1, 2>) == 0x4000),
-              "the weight table at LDS 0x4000 (tiled_wtab_addr)");
+static_assert(sizeof(StitchLds) == 0x4000, "the weight table at LDS 0x4000 (wtab_read)");
 
-// LDS byte address of a tiled entry's weight pairs.  With the table at 0x4000 (the kernel's static LDS
-// is exactly 16 KiB: launch_stitch checks the compiled size) one v_and_or_b32 forms it; an address
-// built from an integer, so the compiler does not split off a base it cannot fold into the offset.
-template <int MODE, int QPL>
-__device__ __forceinline__ uint2 wtab_read(const uint2* s_wtab, uint32_t e) {
+// LDS byte address of a tiled entry's weight pairs: the table sits at 0x4000 (the kernel's static LDS
+// is exactly 16 KiB: launch_composite checks the compiled size), so one v_and_or_b32 forms it; an
+// address built from an integer, so the compiler does not split off a base it cannot fold into the offset.
+__device__ __forceinline__ uint2 wtab_read(uint32_t e) {
     typedef __attribute__((address_space(3))) const uint64_t lds_u64;
-    if constexpr (sizeof(StitchLds<MODE, QPL>) == 0x4000) {
-        const uint64_t w = *(const lds_u64*)(uintptr_t)((e & 0x1FF8u) | 0x4000u);
-        return uint2{(uint32_t)w, (uint32_t)(w >> 32)};
-    } else
-        return *reinterpret_cast<const uint2*>(reinterpret_cast<const uint8_t*>(s_wtab) + (e & 0x1FF8u));
+    const uint64_t w = *(const lds_u64*)(uintptr_t)((e & 0x1FF8u) | 0x4000u);
+    return uint2{(uint32_t)w, (uint32_t)(w >> 32)};
 }
 
-// LDS byte offset of a tiled entry's tap (x, y) (kernels.hpp, entry layout): one v_bfe_u32 / v_and_b32
-__device__ __forceinline__ uint32_t tap_off(uint32_t e) { return OCTVR_WTAB ? (e >> 13) & 0x3FFFu : e & 0x7FFFu; }
+// LDS byte offset of a tiled entry's tap (x, y) (kernels.hpp, entry layout): one v_bfe_u32
+__device__ __forceinline__ uint32_t tap_off(uint32_t e) { return (e >> 13) & 0x3FFFu; }
 
-// Staged tiles.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
-// dispatch (blocks b, b+8, ...), so neighbouring tiles' source boxes share that XCD's L2.
-template <bool DWORD_STAGE, int MODE, bool VIG, int QPL>
-__global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(OCTVR_STITCH_SGPRS)))
-__attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
-                                                              const double* gains, int use_gain, uint8_t* out,
-                                                              int64_t out_pitch, RgbaOut rgba) {
-    __shared__ __attribute__((aligned(16))) StitchLds<MODE, QPL> L;
-    extern __shared__ __attribute__((aligned(16))) uint2 s_wtab[];  // OCTVR_WTAB: 1,024 weight pairs
+// Staged items.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
+// dispatch (blocks b, b+8, ...), so neighbouring items' source boxes share that XCD's L2.
+template <bool DWORD_STAGE, int MODE, bool VIG>
+__global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
+__attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
+                                                                   const double* gains, int use_gain, uint8_t* out,
+                                                                   int64_t out_pitch, RgbaOut rgba) {
+    __shared__ StitchLds L;
+    extern __shared__ __attribute__((aligned(16))) uint2 s_wtab[];  // 1,024 weight pairs at LDS 0x4000
     uint32_t* const s_rgb = L.rgb;
     float* const s_gain = L.gain;
     // {g, g} per slot (finish_quad2f).  Written after an item's first barrier and read after its
     // second; the next write comes after the next item's first barrier, i.e. after every wave's last
-    // read, so one table suffices (two, by iteration parity, when OCTVR_LDS_DB may skip that barrier).
-    auto& s_slot_gain = L.slot_gain;
+    // read, so one table suffices.
+    f32x2_t* const s_slot_gain = L.slot_gain;
     // per iteration parity: written before an item's staging barrier, read after it (the next write
     // to the same entry is two items later, behind the next barrier)
     uint32_t* const s_claim = L.claim;
-    // MODE 2: the previous item's YUV420P output, staged in LDS and written with one 16-byte store
-    // per lane (store_item_wide) instead of four 1-2-byte stores per quad
-    constexpr bool kWideOut = MODE == 2;
-    // kStoreLate: an item's output is stored right after its computation, behind the next item's
-    // loads (so waiting for those loads need not drain the stores); else at the next iteration's top
-    // (MODE 1 measured 7 % slower with late stores on C3: 111k vs 120k MP/s, so off there too)
-    constexpr bool kStoreLate = (MODE == 1 ? OCTVR_STORE_LATE_M1 : OCTVR_STORE_LATE) != 0;
-    constexpr int SM = MODE == 1 ? 1 : 0;  // sink: YUV (finish_quad) or RGBA
-    uint32_t* const s_out = L.out;
-    constexpr int R = QPL == 1 ? kStageRegs : OCTVR_STAGE_REGS2;  // staging chunks prefetched per wave
-    static_assert(QPL == 1 || QPL == 2 || QPL == 4, "items of 1, 2 or 4 halves");
-    constexpr int kItemH = kTileH * QPL;
+    constexpr int kItemH = kTileH * kItemHalves;
 
     const int groups = kStitchBands;
     const int g = blockIdx.x % groups;
@@ -1275,13 +1051,13 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
     const int t_begin = lut.bands[g];
     const int t_end = lut.bands[g + 1];
     const __amdgpu_buffer_rsrc_t ersrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(QPL * kTilePx * 4)), 0x00020000);
+        const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kItemHalves * kTilePx * 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<TileHdr*>(lut.meta), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kMetaWords * 16)), 0x00020000);
     OutFrame of{};
     RgbaSink ro{};
     bool res_rgba = false;
-    if constexpr (SM == 0) {
+    if constexpr (MODE == 0) {
         of = make_out_frame(out, W, H, out_pitch);
     } else {
         ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
@@ -1290,36 +1066,25 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
     }
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
-#if OCTVR_STAMPS == 1
-    const unsigned long long st0 = __builtin_amdgcn_s_memrealtime();
-    unsigned long long st_items = 0, st_chunks = 0;
-#endif
 
     if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
     if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
-    if constexpr (OCTVR_WTAB) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) s_wtab[tid + 256 * k] = bilerp_weights((uint32_t)(tid + 256 * k));
-    }
+    for (int k = 0; k < 4; k++) s_wtab[tid + 256 * k] = bilerp_weights((uint32_t)(tid + 256 * k));
     // Item sequence of this workgroup: its first three items are static (t0, t0 + step, t0 + 2 step,
     // i.e. the band's first 3 * step items dealt round-robin), every later one is claimed from the
     // band's work counter (one returning atomic per item, issued one iteration before the item's
     // metadata load and handed to the other waves through LDS), so workgroups that drew cheap items
     // keep pulling work while expensive ones finish (static dealing left the band's workgroups
-    // finishing between 31 and 80 us on C2, scripts/stamps.py).
+    // finishing between 31 and 80 us on C2).
     const int t0 = t_begin + (int)(blockIdx.x / groups);
     const int dyn0 = t_begin + 3 * step;  // item of claim value 0
     uint32_t* const q = lut.queue + g * kQueueStride;
     const int wave = uniform(tid >> 6);
     TileMeta cur = meta_read(meta_issue(mrsrc, t0, t_end), t0);
     __syncthreads();
-    TileData<QPL, R> d;
-    {
-        StageSlot sl[R];
-#pragma unroll
-        for (int r = 0; r < R; r++) sl[r] = r == 0 ? stage_slot<true>(cur, t_end, wave) : stage_slot(cur, t_end, r * 4 + wave);
-        data_issue<DWORD_STAGE, VIG>(lut, ersrc, cur, t_end, sl, d);
-    }
+    TileData d;
+    data_issue<DWORD_STAGE, VIG>(ersrc, cur, t_end, stage_slot<true>(cur, t_end, wave), d);
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
     uint4 mv = meta_issue(mrsrc, t_mv, t_end);
@@ -1330,116 +1095,55 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
     // so the compiler cannot fold them into one load at the header (waited on right there)
     asm volatile("" : "+v"(mv.x), "+v"(mv.y), "+v"(mv.z), "+v"(mv.w));
 #pragma unroll
-    for (int h = 0; h < QPL; h++) asm volatile("" : "+v"(d.e4[h].x), "+v"(d.e4[h].y), "+v"(d.e4[h].z), "+v"(d.e4[h].w));
-#pragma unroll
-    for (int r = 0; r < R; r++)
-        asm volatile("" : "+v"(d.sg[r].y0), "+v"(d.sg[r].y1), "+v"(d.sg[r].uq), "+v"(d.sg[r].vq));
+    for (int h = 0; h < kItemHalves; h++) asm volatile("" : "+v"(d.e4[h].x), "+v"(d.e4[h].y), "+v"(d.e4[h].z), "+v"(d.e4[h].w));
+    asm volatile("" : "+v"(d.sg.y0), "+v"(d.sg.y1), "+v"(d.sg.uq), "+v"(d.sg.vq));
 
-    // the previous tile's output, stored at the top of the next iteration: every store is then
-    // older than the loads it shares the iteration with (vmcnt waits on a load that is older than
-    // a store must drain everything, as loads and stores complete out of order)
-    QuadOut prev[QPL];
+    // the previous item's output, stored in the next iteration: every store is then older than the
+    // loads it shares the iteration with (vmcnt waits on a load that is older than a store must drain
+    // everything, as loads and stores complete out of order)
+    QuadOut prev[kItemHalves];
 #pragma unroll
-    for (int h = 0; h < QPL; h++) prev[h] = QuadOut{0u, 0u, 0u, 0u};
+    for (int h = 0; h < kItemHalves; h++) prev[h] = QuadOut{0u, 0u, 0u, 0u};
     int px = 0, py = 0;  // the previous item's quad of this lane in its first half
     // MODE 0 stores of items wholly inside the frame: the lane's part of the byte offsets is
     // loop-invariant (voffset), the item's part a scalar (soffset) — no per-lane address arithmetic
-    constexpr bool kFastStore = OCTVR_FAST_STORE && SM == 0 && !kWideOut && !kStoreLate;
     const uint32_t lane_y = (uint32_t)(2 * qy) * of.pitch + (uint32_t)(2 * qx), lane_c = (uint32_t)qy * of.pitch + (uint32_t)qx;
     int pox = 0, poy = 0;  // the previous item's origin (uniform)
     bool pfull = false;    // the previous item lies wholly inside W x H (uniform)
     uint32_t pcam = 0, pfl = 0;  // the previous item's RGBA-mode camera and flags (item_result_bit / item_g0_bit)
     bool pin = false;
-    uint32_t par = 0, half = 0;  // iteration parity; LDS half of the next small item
-    bool prev_big = true;
-#if OCTVR_PHASES
-    // diagnostic: per-wave shader cycles spent in each phase of the item loop (s_memtime)
-    unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
-    unsigned long long pt = __builtin_amdgcn_s_memtime();
-#define OCTVR_PHASE(k)                                             \
-    do {                                                           \
-        const unsigned long long tn_ = __builtin_amdgcn_s_memtime(); \
-        ph[k] += tn_ - pt;                                         \
-        pt = tn_;                                                  \
-    } while (0)
-#else
-#define OCTVR_PHASE(k) \
-    do {               \
-    } while (0)
-#endif
+    uint32_t par = 0;  // iteration parity
     while (cur.t < t_end) {
         const int x = (int)(cur.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.tile >> 16) * kItemH + qy * 2;
         const uint32_t S = cur.stride;
-        uint4 e4[QPL];
+        uint4 e4[kItemHalves];
 #pragma unroll
-        for (int h = 0; h < QPL; h++) e4[h] = d.e4[h];
-        OCTVR_PHASE(5);   // back edge: waits for the loads of this item
-        // (diagnostic ablations below: wrong output, timing only.  The barriers are never ablated: the
-        // claim hand-over through LDS then desynchronises the waves, and a barrier-free build faulted)
-        // Staging region: a small item takes the LDS half the previous item does not read; a big item
-        // (or one after a big item) overlaps it and first waits for its readers.
-        const bool big = !OCTVR_LDS_DB || (cur.nslots & kHdrBigItem) != 0u;
-#if OCTVR_DIAG_NOBAR  // diagnostic (wrong output, timing only): no item barriers, static dealing only
-        static_assert(!OCTVR_DYN, "the claim hand-over through LDS needs the barriers");
-#else
-        if (big || prev_big) __syncthreads();
-#endif
-#if OCTVR_PRIO_STAGE  // the staging phase (between the item's two barriers) at raised wave priority
-        __builtin_amdgcn_s_setprio(OCTVR_PRIO_STAGE);
-#endif
-        uint32_t* const s_stage = s_rgb + (big ? 0u : half * (uint32_t)(kTileHalfBytes / 4));
-        if (tid < kTileZeroDwords) s_stage[tid] = 0u;  // black pixels read offset 0 of the region
-        OCTVR_PHASE(0);
+        for (int h = 0; h < kItemHalves; h++) e4[h] = d.e4[h];
+        // every wave has read the previous item's staging area
+        __syncthreads();
+        if (tid < kTileZeroDwords) s_rgb[tid] = 0u;  // black pixels read offset 0 of the region
         const TileMeta nxt = meta_read(mv, t_mv);
-        // the next item's staging slots (+ their frames' kernarg loads), used after the barrier below
-        StageSlot sln[R];
-#if !OCTVR_SLN_LATE
-#pragma unroll
-        for (int r = 0; r < R; r++) sln[r] = r == 0 ? stage_slot<true>(nxt, t_end, wave) : stage_slot(nxt, t_end, r * 4 + wave);
-#endif
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
             // clamped to [0, FLT_MAX] (NaN -> 0) in MODE 0; no result depends on it (finish_quad2f
             // saturates with v_cvt_pk_u8_f32, which maps negative and NaN products to 0 either way)
             const float gs = s_gain[cw & 31u];
-            const float gc = SM == 0 ? __builtin_fminf(__builtin_fmaxf(gs, 0.f), FLT_MAX) : gs;
-            if (tid < kTileSlots) s_slot_gain[kGainTables > 1 ? par : 0][tid] = f32x2_t{gc, gc};
+            const float gc = MODE == 0 ? __builtin_fminf(__builtin_fmaxf(gs, 0.f), FLT_MAX) : gs;
+            if (tid < kTileSlots) s_slot_gain[tid] = f32x2_t{gc, gc};
         }
         if (claimed && tid == 0) s_claim[par] = claim;  // issued one iteration ago
-#if !OCTVR_DIAG_NOSTAGE
-#pragma unroll
-        for (int r = 0; r < R; r++) stage_store<VIG>(d.sg[r], s_stage);
+        stage_store<VIG>(d.sg, s_rgb);
         const uint32_t nch = (cur.nslots >> 8) & 0xFFu;
-#else
-        const uint32_t nch = 0;
-#endif
-#if OCTVR_STAMPS == 1
-        st_items++;
-        st_chunks += nch;
-#endif
-        if (nch > (uint32_t)(R * 4)) {  // large boxes only: the other chunks now
-            for (int c = R * 4 + wave; c < (int)nch; c += 4) {
+        if (nch > 4u) {  // large boxes only: the other chunks now
+            for (int c = 4 + wave; c < (int)nch; c += 4) {
                 StageGroup sg;
                 stage_load<DWORD_STAGE, VIG>(stage_slot(cur, t_end, c), S, c, sg);
-                stage_store<VIG>(sg, s_stage);
+                stage_store<VIG>(sg, s_rgb);
             }
         }
-#if OCTVR_ISSUE_EARLY
-        // the next item's entry and staging loads before the barrier (their registers are free once
-        // staged): their latency then also covers the barrier wait, not only this item's compute
-        data_issue<DWORD_STAGE, VIG>(lut, ersrc, nxt, t_end, sln, d);
-#endif
-        OCTVR_PHASE(1);
-#if !OCTVR_DIAG_NOBAR
         __syncthreads();
-#endif
-#if OCTVR_PRIO_STAGE
-        __builtin_amdgcn_s_setprio(0);
-#endif
-        OCTVR_PHASE(2);
-        // the item two ahead: static on the first iteration, else the claim handed over above
+        // the item two ahead: static on the first iteration, else the claim handed over above.
         if (!first) {
-#if OCTVR_DYN
             // Global addresses derive from this LDS-handed claim (the item's header, slots and entries,
             // and through its slots the camera frames), so it is range-checked as unsigned: a value that
             // is not a claim of this band (the r02 barrier-free ablation read s_claim before wave 0 wrote
@@ -1448,47 +1152,29 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
             // (one scalar min: dyn0 + cv then cannot wrap negative, and t_n2 below stays in [0, t_end])
             const uint32_t cv = min((uint32_t)uniform((int)s_claim[par]), 0x3FFFFFFFu);
             const int v = claimed ? dyn0 + (int)cv : t_end;
-#else  // static dealing (round-robin over the band's workgroups)
-            const int v = t_n2 < t_end ? t_n2 + step : t_end;
-#endif
             t_n2 = v < t_end ? v : t_end;
         }
         first = false;
-#if !OCTVR_DIAG_NOSTORE
-        if constexpr (kWideOut) {
-            store_item_wide<QPL>(of, s_out, px - 2 * qx, py - 2 * qy, pin, H);
-        } else if constexpr (kFastStore) {
-            if (pfull) {
+        if (MODE == 0 && pfull) {
 #pragma unroll
-                for (int h = 0; h < QPL; h++) {
-                    const uint32_t sy = (uint32_t)uniform((poy + h * kTileH) * (int)of.pitch + pox);
-                    const uint32_t sc = (uint32_t)uniform(((poy + h * kTileH) >> 1) * (int)of.pitch + (pox >> 1));
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)prev[h].y01, of.rsrc, lane_y, sy, OCTVR_OUT_POLICY);
-                    __builtin_amdgcn_raw_buffer_store_b16((uint16_t)prev[h].y23, of.rsrc, lane_y, sy + of.pitch, OCTVR_OUT_POLICY);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)prev[h].u, of.rsrc, lane_c, sc + of.u_off, OCTVR_OUT_POLICY);
-                    __builtin_amdgcn_raw_buffer_store_b8((uint8_t)prev[h].v, of.rsrc, lane_c, sc + of.v_off, OCTVR_OUT_POLICY);
-                }
-            } else {
-#pragma unroll
-                for (int h = 0; h < QPL; h++)
-                    store_any<SM>(of, ro, prev[h], pcam, px, py + h * kTileH, pin && py + h * kTileH < H);
+            for (int h = 0; h < kItemHalves; h++) {
+                const uint32_t sy = (uint32_t)uniform((poy + h * kTileH) * (int)of.pitch + pox);
+                const uint32_t sc = (uint32_t)uniform(((poy + h * kTileH) >> 1) * (int)of.pitch + (pox >> 1));
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)prev[h].y01, of.rsrc, lane_y, sy, kOutPolicy);
+                __builtin_amdgcn_raw_buffer_store_b16((uint16_t)prev[h].y23, of.rsrc, lane_y, sy + of.pitch, kOutPolicy);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)prev[h].u, of.rsrc, lane_c, sc + of.u_off, kOutPolicy);
+                __builtin_amdgcn_raw_buffer_store_b8((uint8_t)prev[h].v, of.rsrc, lane_c, sc + of.v_off, kOutPolicy);
             }
-        } else if constexpr (!kStoreLate) {
+        } else {
 #pragma unroll
-            for (int h = 0; h < QPL; h++)
-                store_half<SM>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
+            for (int h = 0; h < kItemHalves; h++)
+                store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
-#endif
-#if !OCTVR_ISSUE_EARLY
-#if OCTVR_SLN_LATE  // the next item's slots resolved only now (shorter scalar live ranges, exposed kernarg loads)
-#pragma unroll
-        for (int r = 0; r < R; r++) sln[r] = r == 0 ? stage_slot<true>(nxt, t_end, wave) : stage_slot(nxt, t_end, r * 4 + wave);
-#endif
-        data_issue<DWORD_STAGE, VIG, QPL, R, !OCTVR_ENT_LATE>(lut, ersrc, nxt, t_end, sln, d);
-#endif
+        // the next item's first staging slot resolved only now (short scalar live ranges), then its loads
+        data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, stage_slot<true>(nxt, t_end, wave), d);
         mv = meta_issue(mrsrc, t_n2, t_end);
         t_mv = t_n2;
-        claimed = OCTVR_DYN && t_n2 < t_end;  // claim the item after it (only while the sequence is live)
+        claimed = t_n2 < t_end;  // claim the item after it (only while the sequence is live)
         if (claimed && tid == 0) {
             // an opaque (per-lane looking) address: the atomic optimizer would otherwise rewrite the
             // single-lane claim into a wave-level one whose result it broadcasts (and waits for) at once
@@ -1496,157 +1182,41 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
             asm volatile("" : "+v"(zero));
             claim = __hip_atomic_fetch_add(q + zero, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        OCTVR_PHASE(3);
 #pragma unroll
-        for (int h = 0; h < QPL; h++) {
-        const uint32_t ent[4] = {e4[h].x, e4[h].y, e4[h].z, e4[h].w};
-        float rgb[4][3];
-        f32x2_t gain[4];
-#if OCTVR_TAPS_FIRST  // the quad's 8 LDS reads issued before any of its arithmetic
-        uint32_t t00[4], t01[4], t10[4], t11[4];
+        for (int h = 0; h < kItemHalves; h++) {
+            const uint32_t ent[4] = {e4[h].x, e4[h].y, e4[h].z, e4[h].w};
+            float rgb[4][3];
+            f32x2_t gain[4];
 #pragma unroll
-        for (int p = 0; p < 4; p++) {
-            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + tap_off(ent[p]);
-            const uint8_t* r1 = r0 + 4u * S;
-            t00[p] = reinterpret_cast<const uint32_t*>(r0)[0];
-            t01[p] = reinterpret_cast<const uint32_t*>(r0)[1];
-            t10[p] = reinterpret_cast<const uint32_t*>(r1)[0];
-            t11[p] = reinterpret_cast<const uint32_t*>(r1)[1];
-        }
-#endif
-#pragma unroll
-        for (int p = 0; p < 4; p++) {
-            const uint32_t e = ent[p];
-#if OCTVR_TAPS_FIRST
-            const uint32_t c00 = t00[p], c01 = t01[p], c10 = t10[p], c11 = t11[p];
-#else
-            // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
-            const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_stage) + tap_off(e);
-            const uint8_t* r1 = r0 + 4u * S;
-            const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
-            const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
-            const uint32_t c10 = reinterpret_cast<const uint32_t*>(r1)[0];
-            const uint32_t c11 = reinterpret_cast<const uint32_t*>(r1)[1];
-#endif
-#if OCTVR_DIAG_NOTAPS
-            (void)c00; (void)c01; (void)c10; (void)c11;
-            rgb[p][0] = (float)(e & 255u); rgb[p][1] = (float)((e >> 8) & 255u); rgb[p][2] = (float)((e >> 16) & 255u);
-#elif OCTVR_WTAB
-            bilerp_rgba_w(c00, c01, c10, c11,
-                          wtab_read<MODE, QPL>(s_wtab, e), rgb[p]);
-#else
-            bilerp_rgba_f(c00, c01, c10, c11, e, rgb[p]);
-#endif
-            // slot << 3 = e >> 27 (bits 25-29 of a composite entry are zero; kernels.hpp)
-            gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain[kGainTables > 1 ? par : 0]) +
-                                                        (e >> 27));
-            if (SM == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
-        }
-#if OCTVR_DIAG_NOCOMPUTE
-        prev[h] = QuadOut{(uint32_t)rgb[0][0] ^ (uint32_t)rgb[1][1], (uint32_t)rgb[2][2] ^ (uint32_t)rgb[3][0], (uint32_t)gain[0].x, (uint32_t)gain[3].y};
-#else
-#if OCTVR_DIAG_XOP  // diagnostic: 16 extra independent instructions of one opcode per quad (4 per pixel), to
-                    // price an opcode inside this loop (scripts/r3_diag4.sh); the results feed nothing
-#if OCTVR_DIAG_XOP == 1
-#define OCTVR_XOP_ASM "v_xor_b32 %0, %0, %1"
-#elif OCTVR_DIAG_XOP == 2
-#define OCTVR_XOP_ASM "v_pk_mul_lo_u16 %0, %0, %1"
-#elif OCTVR_DIAG_XOP == 3
-#define OCTVR_XOP_ASM "v_perm_b32 %0, %0, %1, %1"
-#elif OCTVR_DIAG_XOP == 4
-#define OCTVR_XOP_ASM "v_mul_u32_u24 %0, %0, %1"
-#elif OCTVR_DIAG_XOP == 5
-#define OCTVR_XOP_ASM "v_dot2_u32_u16 %0, %1, %1, %0"
-#elif OCTVR_DIAG_XOP == 6
-#define OCTVR_XOP_ASM "v_pk_add_u16 %0, %0, %1"
-#elif OCTVR_DIAG_XOP == 7
-#define OCTVR_XOP_ASM "v_cvt_pk_u8_f32 %0, %1, 1, %0"
-#elif OCTVR_DIAG_XOP == 8
-#define OCTVR_XOP_ASM "v_fmac_f32 %0, %1, %1"
-#elif OCTVR_DIAG_XOP == 9
-#define OCTVR_XOP_ASM "v_rndne_f32 %0, %0"
-#elif OCTVR_DIAG_XOP == 10
-#define OCTVR_XOP_ASM "v_med3_f32 %0, %0, %1, %1"
-#elif OCTVR_DIAG_XOP == 11
-#define OCTVR_XOP_ASM "v_min_f32 %0, %0, %1"
-#elif OCTVR_DIAG_XOP == 12
-#define OCTVR_XOP_ASM "v_bfe_u32 %0, %0, 3, 5"
-#elif OCTVR_DIAG_XOP == 13
-#define OCTVR_XOP_ASM "v_cvt_f32_ubyte1 %0, %0"
-#elif OCTVR_DIAG_XOP == 14
-#define OCTVR_XOP_ASM "v_mul_f32 %0, %0, %1"
-#elif OCTVR_DIAG_XOP == 16
-#define OCTVR_XOP_ASM "v_mul_lo_u32 %0, %0, %1"
-#else
-#define OCTVR_XOP_ASM "v_mov_b32 %0, %1"
-#endif
-        {
-            uint32_t z0 = ent[0], z1 = ent[1], z2 = ent[2], z3 = ent[3];
-            const uint32_t k = ent[0] ^ ent[3];
-#pragma unroll
-            for (int r = 0; r < 4; r++) {
-                asm volatile(OCTVR_XOP_ASM : "+v"(z0) : "v"(k));
-                asm volatile(OCTVR_XOP_ASM : "+v"(z1) : "v"(k));
-                asm volatile(OCTVR_XOP_ASM : "+v"(z2) : "v"(k));
-                asm volatile(OCTVR_XOP_ASM : "+v"(z3) : "v"(k));
+            for (int p = 0; p < 4; p++) {
+                const uint32_t e = ent[p];
+                // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
+                const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) + tap_off(e);
+                const uint8_t* r1 = r0 + 4u * S;
+                const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
+                const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
+                const uint32_t c10 = reinterpret_cast<const uint32_t*>(r1)[0];
+                const uint32_t c11 = reinterpret_cast<const uint32_t*>(r1)[1];
+                bilerp_rgba_w(c00, c01, c10, c11, wtab_read(e), rgb[p]);
+                // slot << 3 = e >> 27 (bits 27-29 of a tiled entry are zero; kernels.hpp)
+                gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + (e >> 27));
+                if (MODE == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
             }
-            asm volatile("" ::"v"(z0), "v"(z1), "v"(z2), "v"(z3));
+            prev[h] = finish_any<MODE>(rgb, gain);
         }
-#endif
-        prev[h] = finish_any<SM>(rgb, gain);
-#endif
-        // MODE 2: staged for the wide stores after the next barrier
-        if constexpr (kWideOut) stage_out_quad<QPL>(s_out, prev[h], h, qx, qy);
-#if OCTVR_PHASES
-        asm volatile("" : "+v"(prev[h].y01), "+v"(prev[h].y23), "+v"(prev[h].u), "+v"(prev[h].v));
-#endif
-        }
-#if OCTVR_ENT_LATE
-        // the next item's entries only now, after this item's last use of its own: no copy of the
-        // in-flight entries is held across the computation (they land during the staging phase)
-        {
-            const bool nlive = nxt.t < t_end;
-#pragma unroll
-            for (int h = 0; h < QPL; h++) {
-                typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
-                const uint32_t so = (uint32_t)uniform((nlive ? nxt.t : 0) * QPL + h) * (uint32_t)(kTilePx * 4);
-                const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(ersrc, (uint32_t)tid * 16u, so, 0);
-                d.e4[h] = uint4{v.x, v.y, v.z, v.w};
-            }
-        }
-#endif
-        OCTVR_PHASE(4);
         px = x;
         py = y;
         pox = (int)(cur.tile & 0xFFFFu) * kTileW;
         poy = (int)(cur.tile >> 16) * kItemH;
         pfull = pox + kTileW <= W && poy + kItemH <= H;
         pcam = (cur.nslots >> 16) & 31u;
-        pfl = SM == 1 ? (cur.map >> 8) & 0xFFFFu : 0u;
+        pfl = MODE == 1 ? (cur.map >> 8) & 0xFFFFu : 0u;
         pin = x < W && y < H;
-#if !OCTVR_DIAG_NOSTORE
-        if constexpr (kStoreLate && !kWideOut) {  // youngest ops of the iteration (see kStoreLate)
-#pragma unroll
-            for (int h = 0; h < QPL; h++)
-                store_half<SM>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
-        }
-#endif
-        prev_big = big;
-        half ^= big ? 0u : 1u;
         par ^= 1u;
         cur = nxt;
     }
     // the last workgroup to finish resets the work counters for the next launch (stream order makes
     // the reset visible to it); every claim of this workgroup has returned before its ticket
-#if OCTVR_PHASES
-    if ((tid & 63) == 0 && MODE != 1 && blockIdx.x * 4 + (tid >> 6) < 2 * kStampRows * 4 / 8) {
-        unsigned long long* r = g_octvr_stamps + (size_t)(blockIdx.x * 4 + (tid >> 6)) * 8;
-        for (int k = 0; k < 6; k++) r[k] = ph[k];
-        r[6] = (unsigned long long)g;
-        r[7] = 1;
-    }
-#endif
-#undef OCTVR_PHASE
     if (tid == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         (void)claim;
@@ -1656,23 +1226,9 @@ __attribute__((amdgpu_num_vgpr(OCTVR_STITCH_VGPRS))) stitch_tiled_kernel(FrameSe
                 __hip_atomic_exchange(lut.queue + k * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if constexpr (kWideOut) {
-        __syncthreads();
-        store_item_wide<QPL>(of, s_out, px - 2 * qx, py - 2 * qy, pin, H);
-    } else if constexpr (!kStoreLate) {
 #pragma unroll
-        for (int h = 0; h < QPL; h++)
-            store_half<SM>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
-    }
-#if OCTVR_STAMPS == 1
-    if (MODE != 1 && tid == 0 && blockIdx.x < kStampRows) {
-        unsigned long long* r = g_octvr_stamps + (size_t)blockIdx.x * 4;
-        r[0] = st0;
-        r[1] = __builtin_amdgcn_s_memrealtime();
-        r[2] = st_items;
-        r[3] = st_chunks;
-    }
-#endif
+    for (int h = 0; h < kItemHalves; h++)
+        store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
 }
 
 // Wide tiles: one workgroup per tile, 8-byte absolute entries, direct global gathers.
@@ -1723,28 +1279,43 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 
 // The weight table's address (wtab_read) assumes the dynamic LDS starts right after StitchLds: checked
 // once per kernel instance against the compiled static LDS size.
-template <bool DW, int MODE, bool V, int Q>
+template <bool DW, int MODE, bool V>
 static hipError_t stitch_lds_check() {
     hipFuncAttributes a;
-    const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V, Q>));
+    const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V>));
     if (e != hipSuccess) return e;
-    return a.sharedSizeBytes == sizeof(StitchLds<MODE, Q>) ? hipSuccess : hipErrorInvalidKernelFile;
+    return a.sharedSizeBytes == sizeof(StitchLds) ? hipSuccess : hipErrorInvalidKernelFile;
+}
+
+template <bool DW, int MODE, bool V>
+static hipError_t launch_tiled(int blocks, const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
+                               int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
+                               hipEvent_t ev0, hipEvent_t ev1) {
+    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V>();
+    if (lds_ok != hipSuccess) return lds_ok;
+    if (ev0)  // the timing events carried by the dispatch packet itself
+        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, ev0, ev1, 0,
+                              frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);
+    else
+        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W, H,
+                           gains, use_gain, out, out_pitch, rgba);
+    return hipGetLastError();
 }
 
 template <int MODE>
 static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                                    int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
                                    hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
-    // timing events: carried by the dispatch packet itself when the tiled kernel is the only launch
-    // (no marker packets between the launches of the timed loop), else recorded around the launches
-    const bool ext_ev = ev0 && lut.n_items > 0 && lut.n_wide == 0 && lut.qpl == 2 && !OCTVR_WIDE_OUT;
+    if (lut.n_items > 0 && lut.qpl != kItemHalves) return hipErrorInvalidValue;
+    // timing events: carried by the dispatch packet when the tiled kernel is the only launch (no marker
+    // packets between the launches of the timed loop), else recorded around the launches
+    const bool ext_ev = ev0 && lut.n_items > 0 && lut.n_wide == 0;
     if (ev0 && !ext_ev) {
         const hipError_t e = hipEventRecord(ev0, s);
         if (e != hipSuccess) return e;
     }
     if (lut.n_items > 0) {
-        // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU: 25 KiB LDS each), each
-        // walking its XCD band's items
+        // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU), each walking its XCD band's items
         int blocks = std::min(lut.n_items, 256 * kStitchBlocksPerCU);
         blocks = std::max(8, (blocks + 7) / 8 * 8);
         // wide staging loads need 8-byte aligned Y rows (then U / V rows are 4-byte aligned)
@@ -1755,61 +1326,16 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
             if ((reinterpret_cast<uintptr_t>(f.yuv) & 7u) || (f.pitch & 7) || (f.w & 7)) dw = false;
             vig |= f.vig != nullptr;
         }
-        // YUV output with 16-byte row segments: the LDS-staged wide stores (MODE 2)
-        const bool wide_out = MODE == 0 && OCTVR_WIDE_OUT && W % 32 == 0 && out_pitch % 16 == 0 &&
-                              (reinterpret_cast<uintptr_t>(out) & 15u) == 0;
-#if OCTVR_WIDE_OUT
-#define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
-    do {                                                                                                       \
-        if (lut.qpl == 2 && wide_out)                                                                          \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, 2, V, 2>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W, \
-                               H, gains, use_gain, out, out_pitch, rgba); }                                      \
-        else if (lut.qpl == 2)                                                                                 \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 2>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
-        else if (wide_out)                                                                                     \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, 2, V, 1>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, 2, V, 1>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W, \
-                               H, gains, use_gain, out, out_pitch, rgba); }                                      \
-        else                                                                                                   \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 1>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
-    } while (0)
-#else
-#define OCTVR_LAUNCH_TILED(DW, V)                                                                              \
-    do {                                                                                                       \
-        (void)wide_out;                                                                                        \
-        if (OCTVR_QPL == 4 && lut.qpl == 4)                                                                    \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, OCTVR_QPL == 4 ? 4 : 1>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, OCTVR_QPL == 4 ? 4 : 1>), dim3(blocks), dim3(256), \
-                               kWtabBytes, s, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba); }                \
-        else if (lut.qpl == 2 && ext_ev)                                                                       \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 2>(); if (lds_ok_) return lds_ok_; \
-            hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, ev0, ev1, \
-                                  0, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba); }                \
-        else if (lut.qpl == 2)                                                                                 \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 2>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 2>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
-        else                                                                                                   \
-            { static const hipError_t lds_ok_ = stitch_lds_check<DW, MODE, V, 1>(); if (lds_ok_) return lds_ok_; \
-            hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, 1>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, \
-                               W, H, gains, use_gain, out, out_pitch, rgba); }                                   \
-    } while (0)
-#endif
+        hipEvent_t e0 = ext_ev ? ev0 : nullptr, e1 = ext_ev ? ev1 : nullptr;
+        hipError_t e;
         if (dw && !vig)
-            OCTVR_LAUNCH_TILED(true, false);
+            e = launch_tiled<true, MODE, false>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
         else if (dw)
-            OCTVR_LAUNCH_TILED(true, true);
+            e = launch_tiled<true, MODE, true>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
         else if (!vig)
-            OCTVR_LAUNCH_TILED(false, false);
+            e = launch_tiled<false, MODE, false>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
         else
-            OCTVR_LAUNCH_TILED(false, true);
-#undef OCTVR_LAUNCH_TILED
-        const hipError_t e = hipGetLastError();
+            e = launch_tiled<false, MODE, true>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
         if (e != hipSuccess) return e;
     }
     if (lut.n_wide > 0)
@@ -1822,16 +1348,7 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
     return hipGetLastError();
 }
 
-#if OCTVR_STAMPS
-extern "C" int octvr_debug_stamps(unsigned long long* out, int rows) {
-    if (rows > 2 * kStampRows) rows = 2 * kStampRows;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_octvr_stamps), (size_t)rows * 4 * 8, 0, hipMemcpyDeviceToHost) ==
-                   hipSuccess ? rows : -1;
-}
-#endif
-
-int composite_qpl() { return OCTVR_QPL; }
+int composite_qpl() { return kItemHalves; }
 
 hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                          int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {

@@ -73,44 +73,25 @@ __host__ __device__ inline TapCell tap_cell(uint32_t xy, int w, int h) {
 // Each slot's box reaches one column / row past its taps (x0 + 1, y0 + 1), including taps outside
 // the source image: staging writes RGBA 0 for box pixels outside the image (BORDER_CONSTANT), so
 // every tap is read from LDS at off, off + 4, off + 4 S, off + 4 S + 4 (S = row stride) unmasked.
-// The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel.  OCTVR_WTAB = 1 (default):
+// The LUT is tile-major (quad-major inside the tile), 4 bytes per pixel:
 //   bit 0 "no gain" (RGBA mode); bits 1-2 zero; 3-12 the fraction code fx | fy << 5, so e & 0x1FF8 is
 //   the byte offset of the code's two packed weight pairs in the workgroup's 8 KiB LDS weight table;
 //   13-26 LDS byte offset of tap (x, y) (one v_bfe_u32); 27-29 zero; 30-31 slot (the slot's gain
-//   sits at byte offset e >> 27 of a 4-slot table of f32 pairs).  Three VALU decode a pixel's
-//   entry, against ten for the weights computed from fx, fy (OCTVR_WTAB = 0: bits 0-14 offset,
-//   15-19 fx, 20-24 fy, 25 no gain, 30-31 slot).
+//   sits at byte offset e >> 27 of a 4-slot table of f32 pairs).  Three VALU decode a pixel's entry.
 // A pixel with no camera, or with every tap outside, is entry 0 and comes out black.
-#ifndef OCTVR_WTAB
-#define OCTVR_WTAB 1
-#endif
 constexpr int kTileW = 128, kTileH = 8, kTilePx = kTileW * kTileH;
 constexpr int kTileSlots = 4;
-#ifndef OCTVR_TILE_LDS_BYTES
-// WTAB: 16 KiB less the composite's 176 bytes of other LDS, so its static LDS is exactly 16 KiB and the
-// 8 KiB weight table starts at LDS address 0x4000 (every C2 / C4 item stages < 16 KiB; 6 workgroups
-// per CU by LDS); else 20 KiB: 7 workgroups fit by LDS
-#define OCTVR_TILE_LDS_BYTES (OCTVR_WTAB ? 16 * 1024 - 176 : 20 * 1024)
-#endif
-constexpr int kTileLdsBytes = OCTVR_TILE_LDS_BYTES;
-static_assert(kTileLdsBytes <= (OCTVR_WTAB ? (1 << 14) : (1 << 15)), "the tiled entry's LDS byte offset field");
-constexpr uint32_t kWtabBytes = OCTVR_WTAB ? 1024u * 8u : 0u;
+// Items of the tiled composite: two vertically adjacent 128 x 8 tiles (128 x 16 pixels, 8 quads per lane).
+constexpr int kItemHalves = 2;
+// Staging LDS: 16 KiB less the composite's 176 bytes of other LDS, so its static LDS is exactly 16 KiB
+// and the 8 KiB weight table starts at LDS address 0x4000 (every C2 / C4 item stages < 16 KiB; 6
+// workgroups per CU by LDS)
+constexpr int kTileLdsBytes = 16 * 1024 - 176;
+static_assert(kTileLdsBytes <= (1 << 14), "the tiled entry's LDS byte offset field");
+constexpr uint32_t kWtabBytes = 1024u * 8u;
 constexpr int kTileZeroDwords = 4;
-// Staging stores: 2 x 16 bytes per 8-pixel group (row stride a multiple of 4 dwords), or with
-// OCTVR_STAGE_B64 4 x 8 bytes (stride even), so the tiler may pad rows to 2 mod 4 dwords.
-#ifndef OCTVR_STAGE_B64
-#define OCTVR_STAGE_B64 0
-#endif
-constexpr int kStageAlignDwords = OCTVR_STAGE_B64 ? 2 : 4;
-#ifndef OCTVR_LDS_PAD_DEFAULT
-#define OCTVR_LDS_PAD_DEFAULT 0
-#endif
-// Items whose staged boxes fit half the staging LDS alternate between the two halves, so an item is
-// staged while the previous one is still being read (one barrier per item); larger items carry
-// kHdrBigItem in TileHdr::nslots and take the whole buffer behind an extra barrier.
-constexpr int kTileHalfBytes = kTileLdsBytes / 2;
-constexpr uint32_t kHdrBigItem = 1u << 24;
-constexpr int kTileOutBytes = kTileW * kTileH * 3 / 2;  // one tile's YUV420P output (LDS-staged stores)
+// Staging stores: 2 x 16 bytes per 8-pixel group, so a row stride is a multiple of 4 dwords.
+constexpr int kStageAlignDwords = 4;
 
 struct TileSlot {
     uint16_t cam;
@@ -143,7 +124,7 @@ struct FrameSet {
 
 // One NV12 plane of a FastMapper (fastmapper.cpp / fastmapper.hip): per run {camera mask, first block},
 // and per (camera, run) block either the compact entries (header + u32 offsets/fractions + u8 weights)
-// or the wide uint2 entries.
+// or the wide uint2 entries; nblk: the blocks allocated (>= 1).
 struct FastMapperPlane {
     bool compact;
     const uint2* ent;
@@ -151,6 +132,7 @@ struct FastMapperPlane {
     const uint8_t* wgt;
     const uint2* hdr;
     const uint2* runs;
+    uint32_t nblk;
 };
 
 // ROI-sized per-camera template data resident on the device.
@@ -170,10 +152,7 @@ struct CamTemplate {
 // wave each, so a wave's frame is uniform), the whole array to chunks of kGainChunk (one workgroup,
 // about one workgroup per CU on C2).
 constexpr int kGainMaxCams = 16;
-#ifndef OCTVR_GAIN_PER  // samples per lane of the gain feed
-#define OCTVR_GAIN_PER 3
-#endif
-constexpr int kGainPer = OCTVR_GAIN_PER;
+constexpr int kGainPer = 3;  // samples per lane of the gain feed
 constexpr int kGainWaveRun = 64 * kGainPer;  // one wave's samples: contiguous, one camera
 constexpr int kGainChunk = 4 * kGainWaveRun;  // one workgroup's samples (4 waves)
 constexpr int kGainTotalStride = 32;  // u64 words between pair totals: one 256-B line each
@@ -218,30 +197,25 @@ struct TiledLut {
 constexpr int kMetaWords = 1 + kTileSlots;
 constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter
 // The staged items are cut into one contiguous band per XCD (locality: neighbouring tiles share
-// source boxes in that XCD's L2), balanced by cost = base + chunk weight x staging chunks.  Measured
-// on the C2 rig (r01 v10): equal item counts (chunk weight 0) beat every chunk-weighted split tried
-// (base 16 / 8 / 4 / 2 per chunk: +2 % / +4 % / +10 % / +19 % stitch time) — the large pole boxes
-// are re-read from L2 by many tiles, so staging chunks do not predict a tile's cost.
+// source boxes in that XCD's L2) of equal item counts.  Measured on the C2 rig (r01 v10): equal counts
+// beat every split weighted by staging chunks tried (base 16 / 8 / 4 / 2 per chunk: +2 % / +4 % / +10 % /
+// +19 % stitch time) — the large pole boxes are re-read from L2 by many tiles, so staging chunks do not
+// predict a tile's cost.
 constexpr int kStitchBands = 8;
-#ifndef OCTVR_BAND_CHUNK_WEIGHT
-#define OCTVR_BAND_CHUNK_WEIGHT 0
-#endif
-// 4-byte tiled entries: bit 25 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
+// 4-byte tiled entries: bit 0 = "no gain" (a pixel the gain does not touch: LUT mask 0 with an
 // in-image map value; mul_scalar_with_mask, exposure_compensate.cu:15-30).  8-byte CompositeEntry
 // records carry the same flag in code bit 16.  TileHdr.nslots bits 16-20: output camera (RGBA mode).
-constexpr uint32_t kEntryNoGain = OCTVR_WTAB ? 1u : 1u << 25;
+constexpr uint32_t kEntryNoGain = 1u;
 constexpr int kEntrySlotShift = 30;
 constexpr uint32_t kCodeNoGain = 1u << 16;
 
 // One staged pixel's 4-byte entry (layout above): off = LDS byte offset of tap (x, y) in the item's
 // staging area, fxy = fx | fy << 5.
 __host__ __device__ constexpr uint32_t tiled_entry(uint32_t off, uint32_t fxy, uint32_t slot, bool nogain) {
-    return OCTVR_WTAB ? (nogain ? kEntryNoGain : 0u) | (fxy & 1023u) << 3 | off << 13 | slot << kEntrySlotShift
-                      : off | (fxy & 31u) << 15 | (fxy >> 5) << 20 | slot << kEntrySlotShift |
-                            (nogain ? kEntryNoGain : 0u);
+    return (nogain ? kEntryNoGain : 0u) | (fxy & 1023u) << 3 | off << 13 | slot << kEntrySlotShift;
 }
 
-// Quads per lane of the blend = 0 composite's items (OCTVR_QPL, default 2: 128 x 16 items).
+// 128 x 8 halves per item of the tiled composite (kItemHalves): the tiler's qpl.
 int composite_qpl();
 
 // ev0 / ev1 (optional): timing events around the composite (carried by the dispatch packet when it

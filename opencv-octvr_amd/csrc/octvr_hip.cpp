@@ -893,7 +893,6 @@ struct octvr_mapper {
         uint32_t* tickets = nullptr;
         uint32_t* queue = nullptr;
         hipEvent_t done = nullptr;  // recorded after the slot's last stitch (its stream may since be gone)
-        hipEvent_t feed_in = nullptr, feed_done = nullptr;  // hand-over to / from the feed stream
     };
     struct SlotBufs {
         DevBuf<double> gains;
@@ -903,15 +902,12 @@ struct octvr_mapper {
     std::vector<FrameSlot> slots;
     std::vector<std::unique_ptr<SlotBufs>> slot_bufs;  // owners of slots 1..k-1
     int cur_slot = 0;                                  // slot of the last stitch
-    hipStream_t feed_stream = nullptr;  // high-priority stream of the gain feed (frames in flight)
     int timing = 0;             // event-timing period in stitches (0 = off)
     uint64_t timed_calls = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events, free_events;  // recorded / reusable
     ~octvr_mapper() {
         for (auto& sl : slots)
-            for (hipEvent_t e : {sl.done, sl.feed_in, sl.feed_done})
-                if (e) (void)hipEventDestroy(e);
-        if (feed_stream) (void)hipStreamDestroy(feed_stream);
+            if (sl.done) (void)hipEventDestroy(sl.done);
         for (auto* v : {&events, &free_events})
             for (auto& e : *v) {
                 (void)hipEventDestroy(e.first);
@@ -1083,24 +1079,6 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
 // =================================================================================================
 namespace octvr {
 
-// OCTVR_LEAN_FEED=0 keeps the wide-prefetch gain feed with frames in flight (measurement knob)
-// OCTVR_FEED_PRIO=1: the lean feed on a high-priority stream (measurement knob)
-static bool feed_prio() {
-    static const bool v = [] {
-        const char* e = getenv("OCTVR_FEED_PRIO");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
-static bool lean_feed() {
-    static const bool v = [] {
-        const char* e = getenv("OCTVR_LEAN_FEED");
-        return !(e && e[0] == '0');
-    }();
-    return v;
-}
-
 // The RGB(A) result frame of the scaled-output and preview paths (allocated on first use).
 void ensure_result(octvr_mapper& m) {
     if (m.result.p) return;
@@ -1167,27 +1145,9 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             } else {
                 // with frames in flight the feed runs beside the previous frame's composite: the lean
                 // variant fits next to it (the wide-prefetch one waits for its workgroups to drain)
-                const bool lean = m->slots.size() > 1 && lean_feed();
-                if (lean && feed_prio()) {
-                    // on a high-priority stream (stream-ordered after everything before this call on
-                    // s): its workgroups are dispatched ahead of the composites that occupy the CUs
-                    if (!m->feed_stream) {
-                        int least = 0, greatest = 0;
-                        HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-                        HIP_CHECK(hipStreamCreateWithPriority(&m->feed_stream, hipStreamNonBlocking, greatest));
-                    }
-                    if (!sl.feed_in) HIP_CHECK(hipEventCreateWithFlags(&sl.feed_in, hipEventDisableTiming));
-                    if (!sl.feed_done) HIP_CHECK(hipEventCreateWithFlags(&sl.feed_done, hipEventDisableTiming));
-                    HIP_CHECK(hipEventRecord(sl.feed_in, s));
-                    HIP_CHECK(hipStreamWaitEvent(m->feed_stream, sl.feed_in, 0));
-                    HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n, sl.totals,
-                                               sl.tickets, sl.gains, m->feed_stream, true));
-                    HIP_CHECK(hipEventRecord(sl.feed_done, m->feed_stream));
-                    HIP_CHECK(hipStreamWaitEvent(s, sl.feed_done, 0));
-                } else {
-                    HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n,
-                                               sl.totals, sl.tickets, sl.gains, s, lean));
-                }
+                const bool lean = m->slots.size() > 1;
+                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n, sl.totals,
+                                           sl.tickets, sl.gains, s, lean));
             }
         }
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -1704,8 +1664,7 @@ int octvr_mapper_set_frames_in_flight(octvr_mapper* m, int k) {
             m->cur_slot = 0;
         }
         for (size_t i = 1; i < m->slots.size(); i++)
-            for (hipEvent_t e : {m->slots[i].done, m->slots[i].feed_in, m->slots[i].feed_done})
-                if (e) (void)hipEventDestroy(e);
+            if (m->slots[i].done) (void)hipEventDestroy(m->slots[i].done);
         m->slots.resize(1);
         m->slot_bufs.clear();
         std::vector<double> ones(kMaxCams, 1.0);
@@ -1875,6 +1834,15 @@ int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, co
         if (mw == 0 || mh == 0) return;
         HIP_CHECK(launch_remap_u8(src, sw, sh, (int64_t)spitch, cn, map1, map2, mw, mh, (int64_t)mpitch, scale_x,
                                   scale_y, dst, (int64_t)dpitch, (hipStream_t)stream));
+    });
+}
+
+int octvr_debug_json_number(const char* json, int flags, double* value) {
+    return guarded([&] {
+        REQUIRE(json && value, "NULL argument");
+        const JsonValue v = json_parse(json, (flags & OCTVR_JSON_EXACT) != 0);
+        const JsonValue& n = v.kind == JsonValue::Array ? v[0] : v;
+        *value = n.as_double();
     });
 }
 

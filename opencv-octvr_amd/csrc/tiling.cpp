@@ -18,16 +18,6 @@
 
 namespace octvr {
 
-// Dwords added to every staged row (LDS bank spread): a box whose rows are a multiple of 16 dwords
-// apart puts the taps of vertically adjacent source pixels on 2 of the 32 banks.  OCTVR_LDS_PAD
-// overrides it (experiments); rounded up to the staging stores' alignment.
-static uint32_t tile_lds_pad() {
-    int pad = OCTVR_LDS_PAD_DEFAULT;
-    if (const char* e = getenv("OCTVR_LDS_PAD")) pad = atoi(e);
-    pad = std::max(0, std::min(pad, 64));
-    return (uint32_t)((pad + kStageAlignDwords - 1) / kStageAlignDwords * kStageAlignDwords);
-}
-
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
                               const std::vector<int>& in_h, int qpl) {
     const int n_jobs = (int)jobs.size();
@@ -40,7 +30,6 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     std::vector<uint8_t> is_wide(n_jobs, 0);
     std::vector<std::vector<CompositeEntry>> wide_raw(n_jobs);
     const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    const uint32_t pad = tile_lds_pad();
     auto work = [&](int tid) {
         struct Px {
             int slot, x0, y0, fxy, mask, nogain;
@@ -121,7 +110,6 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
                 groups += (uint32_t)(bws[j] * bhs[j] / 4);
             }
-            if (ns > 0) stride += pad;
             uint32_t lds = kTileZeroDwords, chunks = 0;
             for (int j = 0; j < ns && !wide; j++) {
                 ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
@@ -138,8 +126,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 continue;
             }
             b.hdr[t] = TileHdr{(uint32_t)J.tx | ((uint32_t)J.ty << 16),
-                               (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16) |
-                                   (lds * 4 > (uint32_t)kTileHalfBytes ? kHdrBigItem : 0u),
+                               (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16),
                                groups, stride};
             for (int j = 0; j < kTileSlots; j++) b.slots[(size_t)t * kTileSlots + j] = ts[j];
             uint32_t* out = b.entries.data() + (size_t)t * item_px;
@@ -212,12 +199,9 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             for (uint8_t x : v) cells += x;
         b.source_bytes = cells * 16 * 1.5;
     }
-    {  // cost-balanced XCD bands over the staged items
+    {  // XCD bands of equal item counts over the staged items (kernels.hpp kStitchBands)
         std::vector<double> cum(n_items + 1, 0.0);
-        for (int t = 0; t < n_items; t++) {
-            const int ch = (int)((b.hdr[t].nslots >> 8) & 0xFFu);
-            cum[t + 1] = cum[t] + 1.0 + OCTVR_BAND_CHUNK_WEIGHT * ch;
-        }
+        for (int t = 0; t < n_items; t++) cum[t + 1] = cum[t] + 1.0;
         b.bands.assign(kStitchBands + 1, n_items);
         b.bands[0] = 0;
         int t = 0;

@@ -98,6 +98,9 @@ _lib.octvr_fastmapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_in
 _lib.octvr_fastmapper_stitch_nv12.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP]
 _lib.octvr_fastmapper_destroy.argtypes = [_VP]
 _lib.octvr_fastmapper_destroy.restype = None
+_lib.octvr_debug_json_number.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double)]
+_lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
+                                              C.c_char_p, C.c_size_t]
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
                                 C.c_float, C.c_float, _VP, C.c_size_t, _VP]
 
@@ -122,6 +125,29 @@ def debug_project_f64(rig_json, out_w, out_h, input, device=0, where=0):
                                         int(input), int(device), int(where), x.ctypes.data_as(_VP),
                                         y.ctypes.data_as(_VP), f.ctypes.data_as(_VP)))
     return x, y, (f if where == 0 else None)
+
+
+def debug_json_number(text, exact=True):
+    """The first number of a JSON document as the rig-config reader parses it (octvr_debug_json_number):
+    exact=True correctly rounded (OCTVR_JSON_EXACT), False with rapidjson's rules."""
+    v = C.c_double()
+    _check(_lib.octvr_debug_json_number(text.encode(), 1 if exact else 0, C.byref(v)))
+    return v.value
+
+
+def debug_fastmapper_audit(mt, in_sizes, wide=False, pitch_pad=0):
+    """(ok, report): the host replay of every index the FastMapper kernels derive for this template and
+    these input sizes, in the compact or (wide=True) 8-byte entry format (octvr_debug_fastmapper_audit;
+    no GPU).  report: per plane ("y", "uv") the counts and the first violation."""
+    n = len(in_sizes)
+    w = (C.c_int * n)(*[s[0] for s in in_sizes])
+    h = (C.c_int * n)(*[s[1] for s in in_sizes])
+    buf = C.create_string_buffer(4096)
+    rc = _lib.octvr_debug_fastmapper_audit(mt._h, n, w, h, int(bool(wide)), int(pitch_pad), buf, len(buf))
+    import json as _json
+    if not buf.value:  # the plan itself failed (bad arguments): no report
+        _check(rc)
+    return rc == 0, _json.loads(buf.value.decode())
 
 
 def interval_union(starts, ends):

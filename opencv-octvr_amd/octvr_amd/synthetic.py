@@ -63,6 +63,23 @@ def yuv_frame(w, h, seed):
     return splitmix_bytes(seed, w * h * 3 // 2).reshape(h * 3 // 2, w)
 
 
+FRAME_KEY_BYTES = 1 << 16
+
+
+def frame_key(seed):
+    """The 64 KiB byte key of a derived frame set (derived_frame)."""
+    return splitmix_bytes(seed, FRAME_KEY_BYTES)
+
+
+def derived_frame(base, seed):
+    """Another frame of the same shape: base XOR frame_key(seed) repeated over its bytes (still uniform
+    random bytes, distinct content).  The bench derives its extra frame sets this way on the device
+    (bench.py derive_set), the same bytes as this."""
+    flat = base.reshape(-1)
+    key = np.resize(frame_key(seed), flat.size)
+    return (flat ^ key).reshape(base.shape)
+
+
 def smooth_yuv_frame(w, h, seed):
     """A frame with image-like structure (gradients + texture) — exercises gain estimation with
     realistic overlaps rather than white noise."""

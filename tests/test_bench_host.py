@@ -61,3 +61,57 @@ def test_committed_pmc_summaries_are_well_formed():
                 if f and w:
                     want = (2 * f["kib_median"] + w["kib_median"]) * 1024
                     assert t == pytest.approx(want, rel=1e-6), (p, k)
+
+
+def _kfd_tree(root, simds):
+    for i, s in enumerate(simds):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text("cpu_cores_count %d\nsimd_count %d\nmax_waves_per_simd 8\n" % (0 if s else 64, s))
+
+
+def test_visible_gpus_without_hip(tmp_path, monkeypatch):
+    """The launcher parent counts GPUs from the KFD topology only: any HIP device query (which would
+    initialise the runtime before the rank processes start) fails the test."""
+    import torch
+    import bench
+
+    def no_hip(*a, **k):
+        raise AssertionError("HIP queried by the launcher parent")
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", no_hip, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", no_hip)
+    monkeypatch.setattr(torch.cuda, "is_available", no_hip)
+    nodes = tmp_path / "nodes"
+    _kfd_tree(nodes, [0, 1024, 1024, 0, 1024])  # two CPU agents, three GPUs
+    assert bench.visible_gpus(str(nodes), env={}) == 3
+    assert bench.visible_gpus(str(nodes), env={"HIP_VISIBLE_DEVICES": "0,2"}) == 2
+    assert bench.visible_gpus(str(nodes), env={"ROCR_VISIBLE_DEVICES": "1", "HIP_VISIBLE_DEVICES": "0,1"}) == 1
+    assert bench.visible_gpus(str(nodes), env={"CUDA_VISIBLE_DEVICES": ""}) == 0
+    with pytest.raises(RuntimeError):
+        bench.visible_gpus(str(tmp_path / "absent"), env={})
+
+
+def test_frame_sets_default_and_floor():
+    """The timed steps rotate through at least 8 distinct source frame sets (more than the Infinity Cache
+    holds for C2 / C4), never fewer than the frames in flight."""
+    import argparse
+    import bench
+    a = argparse.Namespace(frame_sets=None)
+    assert bench.frame_sets_of(a, 3) == 8 and bench.frame_sets_of(a, 12) == 12
+    a.frame_sets = 2
+    assert bench.frame_sets_of(a, 3) == 3
+
+
+def test_derived_frame_sets_match_on_device_and_host():
+    """bench.derive_set (torch, on the device in the bench) == synthetic.derived_frame (numpy, the tests'
+    oracle inputs) byte for byte, and a derived set differs from its base."""
+    import numpy as np
+    import torch
+    import bench
+    from octvr_amd import synthetic
+    base = [torch.from_numpy(synthetic.yuv_frame(w, h, 5 + i)) for i, (w, h) in enumerate([(64, 36), (300, 20)])]
+    got = bench.derive_set(base, [1107, 1108])
+    for i, t in enumerate(base):
+        want = synthetic.derived_frame(t.numpy(), 1107 + i)
+        assert np.array_equal(got[i].numpy(), want)
+        assert (want != t.numpy()).mean() > 0.9

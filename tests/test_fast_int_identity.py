@@ -1,4 +1,4 @@
-"""The FastMapper kernels (opencv-octvr_amd/csrc/fastmapper.hip, OCTVR_FAST_INT) evaluate remap_weighted's
+"""The FastMapper kernels (opencv-octvr_amd/csrc/fastmapper.hip, weighted_sum_int) evaluate remap_weighted's
 per-camera sum (imgproc/src/opencl/remap_weighted.cl:46-75)
 
     v = t0 (1 - ux) (1 - uy) + t1 ux (1 - uy) + t2 (1 - ux) uy + t3 ux uy;  v *= w;  convert_ushort_sat_rte(v)

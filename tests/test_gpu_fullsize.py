@@ -132,3 +132,66 @@ def test_gpu_c3_deep_tiles_equal_pyrup_path(product_lib, monkeypatch, scale):
     for k in (1, 2):
         d = outs[0] != outs[k]
         assert not d.any(), (k, int(d.sum()), np.argwhere(d)[:4].tolist())
+
+
+_F2_ORACLE = {}
+
+
+def _nv12(yuv420p):
+    """bench.py nv12_of: the same frame with interleaved U, V chroma rows, as FastMapper takes it."""
+    h, w = yuv420p.shape[0] * 2 // 3, yuv420p.shape[1]
+    m = np.empty_like(yuv420p)
+    m[:h] = yuv420p[:h]
+    m[h:, 0::2] = yuv420p[h:, : w // 2]
+    m[h:, 1::2] = yuv420p[h:, w // 2:]
+    return m
+
+
+@pytest.mark.parametrize("wide", [False, True], ids=["compact", "wide"])
+def test_gpu_fullsize_f2_fastmapper(product_lib, monkeypatch, wide):
+    """F2 at the size it is benched: the C2 rig built by the GPU LUT build without ROI (octvr_dump -n), a
+    vr::FastMapper in the compact (default) or the 8-byte entry format (OCTVR_FAST_WIDE=1), three
+    stitch_nv12 calls in flight on three streams with their own outputs and the bench's splitmix frame
+    sets (bench.py fast_rank) — every output byte against the oracle's FastMapper
+    (mapper_fast.cpp:27-195, remap_weighted.cl:20-78)."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    rig, W, H, sizes = synthetic.CONFIGS["F2"]()
+    text = json.dumps(rig)
+    monkeypatch.setenv("OCTVR_FAST_WIDE", "1" if wide else "0")
+    mt = ox.MapperTemplate.from_json(text, W, H, use_roi=False)
+    k = 3
+    if "sets" not in _F2_ORACLE:
+        want = O.lut_build(O.json_loads_rj(text), W, H, use_roi=False, threads=THREADS)
+        _F2_ORACLE["luts"] = [(r[1], r[2], r[3]) for r in want]
+        # bench.py fast_rank's sets: frame_seed(rank 0, set j, camera i) = 1000 + 100 j + i, set 0 splitmix64
+        # frames, the others derived from it (bench.derive_set = synthetic.derived_frame)
+        base = [_nv12(synthetic.yuv_frame(w, h, 1000 + i)) for i, (w, h) in enumerate(sizes)]
+        _F2_ORACLE["sets"] = [base] + [[synthetic.derived_frame(f, 1000 + 100 * j + i) for i, f in enumerate(base)]
+                                       for j in range(1, k)]
+        _F2_ORACLE["want"] = [O.fastmapper_nv12(s, sizes, [l[0] for l in _F2_ORACLE["luts"]],
+                                                [l[1] for l in _F2_ORACLE["luts"]], [l[2] for l in _F2_ORACLE["luts"]],
+                                                W, H) for s in _F2_ORACLE["sets"]]
+    for i, (m1, m2, mk) in enumerate(_F2_ORACLE["luts"]):
+        roi, g1, g2, gm, _ = mt.input(i)
+        assert roi == (0, 0, W, H)
+        assert np.array_equal(gm, mk) and np.array_equal(g1.view(np.int32), m1.view(np.int32)) and \
+            np.array_equal(g2.view(np.int32), m2.view(np.int32)), i
+    fm = ox.FastMapper(mt, sizes)
+    ok, rep = ox.debug_fastmapper_audit(mt, sizes, wide=wide)  # the same plan, replayed on the host
+    assert ok, rep
+    assert rep["y"]["compact"] == (0 if wide else 1)
+    dev = [[torch.from_numpy(f).cuda() for f in s] for s in _F2_ORACLE["sets"]]
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(k)]
+    streams = [torch.cuda.Stream() for _ in range(k)]
+    torch.cuda.synchronize()
+    for rep_ in range(2):  # twice round the streams: each stream's second call overlaps the others' first
+        for j in range(k):
+            fm.stitch_nv12(dev[j], outs[j], stream=streams[j])
+    torch.cuda.synchronize()
+    for j in range(k):
+        got = outs[j].cpu().numpy()
+        d = got != _F2_ORACLE["want"][j]
+        assert not d.any(), (wide, j, int(d.sum()), np.argwhere(d)[:4].tolist())
+        assert got[:H].std() > 10

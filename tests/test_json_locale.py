@@ -73,3 +73,20 @@ def test_rapidjson_overloads_exact_doubles(tmp_path):
         w, h, _ = _size(cfg, {"LC_ALL": "C"})
         lo_rj, hi_rj = (O.json_loads_rj(repr(v)) for v in (lo, hi))  # the doubles the caller's rapidjson holds
         assert int(h) == int(1000.0 / (2.0 / ((hi_rj - lo_rj) / math.pi))), (lo, hi)
+
+
+@pytest.mark.parametrize("text,want", [
+    ("4.9e-324", 5e-324),                 # the smallest subnormal
+    ("2.2250738585072011e-308", 2.2250738585072011e-308),  # below DBL_MIN: subnormal
+    ("1e-400", 0.0),                      # underflow to 0, as strtod
+    ("-1e-400", -0.0),
+    ("1e400", math.inf),                  # overflow to HUGE_VAL, as strtod
+    ("[-1.7976931348623159e308]", -math.inf),
+    ("0.30000000000000004", 0.30000000000000004),
+])
+def test_exact_numbers_out_of_range_as_strtod(product_lib, text, want):
+    """OCTVR_JSON_EXACT parsing (std::from_chars) keeps strtod's answer for literals outside the normal
+    double range: overflow gives +-HUGE_VAL, underflow the subnormal or 0, instead of a
+    parse error (some libstdc++ versions report result_out_of_range for subnormals)."""
+    got = product_lib.debug_json_number(text, exact=True)
+    assert got == want and math.copysign(1.0, got) == math.copysign(1.0, want)
