@@ -169,11 +169,12 @@ struct TiledLutBuild {
     std::vector<uint32_t> wide_tiles;
     std::vector<uint16_t> wide_cams;  // camera | the half's flags (quarters' result bits, G0 bits << 4) << 8
     std::vector<uint16_t> item_flags;  // per staged item: its job's flags (RGBA mode)
+    std::vector<uint16_t> grp0, grp1;  // staging groups (kernels.hpp TiledLut::grp0 / grp1)
     std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
     int qpl = 1;  // 128x8 halves per item (kernels.hpp TiledLut::qpl)
-    double staged_bytes = 0;  // YUV bytes staged, summed over items (boxes of neighbouring items overlap)
-    double source_bytes = 0;  // unique source bytes: the union of the staged boxes (+ wide tiles' taps)
+    double staged_bytes = 0;  // YUV bytes staged, summed over items (groups of neighbouring items overlap)
+    double source_bytes = 0;  // unique source bytes: the union of the staged groups (+ wide tiles' taps)
     std::string stats;  // JSON fragment: staged items by staging chunks / LDS bytes, per-band chunk sums
 };
 TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& entry, const std::vector<int>& in_w,
@@ -186,6 +187,7 @@ struct TiledLutDev {
     DevBuf<uint16_t> wide_cams;
     DevBuf<int32_t> bands;
     DevBuf<uint32_t> queue;
+    DevBuf<uint16_t> grp0, grp1;
     double staged_bytes = 0;
     double source_bytes = 0;
     double g0_bytes = 0;      // RGBA mode: G0 bytes the items write (halves without kItemNoG0)

@@ -756,22 +756,15 @@ __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, in
     return s;
 }
 
-// Loads of staging chunk c of a tile: 64 groups of 8 luma pixels inside one slot.  A lane's group k
-// within the slot is row k / (bw/8), column k % (bw/8) of the slot's box.  Lanes past the slot's
-// groups (and chunks past the item's) read the box origin and are marked dst = -1.  With box columns
-// 8-aligned, the Y load is 8-byte and the U / V loads 4-byte aligned (DWORD_STAGE).
-// Offsets use 24-bit multiplies: rows < 256, pitch < 2^24 (checked on the host).
+// Loads of one staging group of 8 luma pixels of a slot: g is the lane's u16 group (kernels.hpp: valid,
+// column and row in the slot's box, from the item's group table), so a chunk of 64 lanes covers only the
+// box rows' tap spans.  Invalid groups (a slot's last chunk, chunks past the item's) read the box origin
+// and are marked dst = -1.  With box columns 8-aligned, the Y load is 8-byte and the U / V loads 4-byte
+// aligned (DWORD_STAGE).  Offsets use 24-bit multiplies: rows < 256, pitch < 2^24 (checked on the host).
 template <bool DWORD_STAGE, bool VIG>
-__device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, int c, StageGroup& sg) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t rowg = max(1u, s.bw >> 3);
-    const uint32_t groups = s.bw * s.bh >> 3;
-    const uint32_t k = (uint32_t)(c - (int)s.chunk0) * 64u + (uint32_t)lane;
-    const bool ok = s.live && k < groups;
-    // k < 2^14, rowg <= 32: (k + 0.5) / rowg is >= 1/64 away from an integer, far above f32 error
-    const float inv = __builtin_amdgcn_rcpf((float)rowg);
-    const uint32_t row_f = (uint32_t)(((float)k + 0.5f) * inv);
-    const uint32_t row_k = ok ? row_f : 0u, col_k = ok ? k - __umul24(row_f, rowg) : 0u;
+__device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, uint32_t g, StageGroup& sg) {
+    const bool ok = s.live && (g & kGroupValid) != 0u;
+    const uint32_t row_k = ok ? (g & 255u) : 0u, col_k = ok ? (g >> 8) & 31u : 0u;
     const SourceFrame& f = s.f;
     // box groups past the image's right / bottom edge (w % 8 == 0: whole groups) stage RGBA 0:
     // they load from the box origin and are replaced by Y = 0, U = V = 128 (-> R = G = B = 0)
@@ -807,6 +800,15 @@ __device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, 
         sg.g1 = *reinterpret_cast<const float4*>(gv + 4);
         if (!f.vig) sg.flags |= kStageNoVig;
     }
+}
+
+// The lane's group of an item's chunk c < kGroupFirst (c = the wave: each wave's first chunk), addressed
+// by the item index alone (loop-invariant voffset, scalar soffset), so it is loaded one iteration ahead
+// with the item's metadata.
+__device__ __forceinline__ uint32_t group_issue(const __amdgpu_buffer_rsrc_t& gr, int t, int t_end) {
+    const int tt = t < t_end ? t : 0;
+    return __builtin_amdgcn_raw_buffer_load_b16(gr, (uint32_t)threadIdx.x * 2u,
+                                                (uint32_t)uniform(tt) * (uint32_t)(kGroupFirst * 64 * 2), 0);
 }
 
 template <bool VIG>
@@ -891,16 +893,15 @@ struct TileData {
 };
 
 // Issue an item's entry loads and the staging loads of its first chunk per wave (sl: the slot of
-// chunk `wave`, from stage_slot<true>).
+// chunk `wave`, from stage_slot<true>; g: the lane's group of that chunk, from group_issue).
 // er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
 // scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
 // that the entries fit 32-bit offsets)
 template <bool DWORD_STAGE, bool VIG>
 __device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, const TileMeta& m, int t_end,
-                                           const StageSlot& sl, TileData& d) {
+                                           const StageSlot& sl, uint32_t g, TileData& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
-    const int wave = uniform(tid >> 6);
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++) {
         typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
@@ -912,7 +913,7 @@ __device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, con
         d.sg.dst = -1;
         return;
     }
-    stage_load<DWORD_STAGE, VIG>(sl, m.stride, wave, d.sg);
+    stage_load<DWORD_STAGE, VIG>(sl, m.stride & ((1u << kStrideBits) - 1u), g, d.sg);
 }
 
 // The composite's two sinks.  MODE 0: gain + RGB -> YUV420P into the output frame (blend = 0).
@@ -1054,6 +1055,10 @@ __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet fram
         const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kItemHalves * kTilePx * 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<TileHdr*>(lut.meta), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kMetaWords * 16)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t grsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint16_t*>(lut.grp0), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kGroupFirst * 64 * 2)), 0x00020000);
+    const __amdgpu_buffer_rsrc_t g1rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(lut.grp1), 0, (int)(lut.n_grp1 * 2u), 0x00020000);
     OutFrame of{};
     RgbaSink ro{};
     bool res_rgba = false;
@@ -1082,18 +1087,20 @@ __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet fram
     uint32_t* const q = lut.queue + g * kQueueStride;
     const int wave = uniform(tid >> 6);
     TileMeta cur = meta_read(meta_issue(mrsrc, t0, t_end), t0);
+    const uint32_t g0 = group_issue(grsrc, t0, t_end);
     __syncthreads();
     TileData d;
-    data_issue<DWORD_STAGE, VIG>(ersrc, cur, t_end, stage_slot<true>(cur, t_end, wave), d);
+    data_issue<DWORD_STAGE, VIG>(ersrc, cur, t_end, stage_slot<true>(cur, t_end, wave), g0, d);
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
     uint4 mv = meta_issue(mrsrc, t_mv, t_end);
+    uint32_t mg = group_issue(grsrc, t_mv, t_end);  // the lane's first staging group of item t_mv
     uint32_t claim = 0u;  // lane 0 of wave 0: returned value of the claim in flight
     bool claimed = false; // a claim for the item after t_n2 is in flight (uniform)
     bool first = true;
     // opaque copies of the prologue loads: the loop-header phis then merge a load with a non-load,
     // so the compiler cannot fold them into one load at the header (waited on right there)
-    asm volatile("" : "+v"(mv.x), "+v"(mv.y), "+v"(mv.z), "+v"(mv.w));
+    asm volatile("" : "+v"(mv.x), "+v"(mv.y), "+v"(mv.z), "+v"(mv.w), "+v"(mg));
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++) asm volatile("" : "+v"(d.e4[h].x), "+v"(d.e4[h].y), "+v"(d.e4[h].z), "+v"(d.e4[h].w));
     asm volatile("" : "+v"(d.sg.y0), "+v"(d.sg.y1), "+v"(d.sg.uq), "+v"(d.sg.vq));
@@ -1115,7 +1122,7 @@ __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet fram
     uint32_t par = 0;  // iteration parity
     while (cur.t < t_end) {
         const int x = (int)(cur.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.tile >> 16) * kItemH + qy * 2;
-        const uint32_t S = cur.stride;
+        const uint32_t S = cur.stride & ((1u << kStrideBits) - 1u);
         uint4 e4[kItemHalves];
 #pragma unroll
         for (int h = 0; h < kItemHalves; h++) e4[h] = d.e4[h];
@@ -1134,10 +1141,13 @@ __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet fram
         if (claimed && tid == 0) s_claim[par] = claim;  // issued one iteration ago
         stage_store<VIG>(d.sg, s_rgb);
         const uint32_t nch = (cur.nslots >> 8) & 0xFFu;
-        if (nch > 4u) {  // large boxes only: the other chunks now
-            for (int c = 4 + wave; c < (int)nch; c += 4) {
+        if (nch > (uint32_t)kGroupFirst) {  // large items only: the other chunks now, groups from grp1
+            const uint32_t ovf = cur.stride >> kStrideBits;
+            for (int c = kGroupFirst + wave; c < (int)nch; c += 4) {
+                const uint32_t gk = __builtin_amdgcn_raw_buffer_load_b16(
+                    g1rsrc, (uint32_t)(tid & 63) * 2u, (ovf + (uint32_t)(c - kGroupFirst)) * 128u, 0);
                 StageGroup sg;
-                stage_load<DWORD_STAGE, VIG>(stage_slot(cur, t_end, c), S, c, sg);
+                stage_load<DWORD_STAGE, VIG>(stage_slot(cur, t_end, c), S, gk, sg);
                 stage_store<VIG>(sg, s_rgb);
             }
         }
@@ -1171,8 +1181,9 @@ __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet fram
                 store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
         // the next item's first staging slot resolved only now (short scalar live ranges), then its loads
-        data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, stage_slot<true>(nxt, t_end, wave), d);
+        data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, stage_slot<true>(nxt, t_end, wave), mg, d);
         mv = meta_issue(mrsrc, t_n2, t_end);
+        mg = group_issue(grsrc, t_n2, t_end);
         t_mv = t_n2;
         claimed = t_n2 < t_end;  // claim the item after it (only while the sequence is live)
         if (claimed && tid == 0) {

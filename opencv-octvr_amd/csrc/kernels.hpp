@@ -105,9 +105,19 @@ struct TileSlot {
 struct TileHdr {           // one staged item
     uint32_t tile;          // item column | item row << 16 (items of 128 x 8 qpl pixels)
     uint32_t nslots;        // bits 0-7: slots used (0..4); bits 8-15: 64-group staging chunks
-    uint32_t stage_groups;  // 4-pixel groups to convert into LDS
-    uint32_t stride;        // LDS row stride in dwords (max box width of the tile)
+    uint32_t stage_groups;  // 4-pixel groups to convert into LDS (host; the device word: TiledLutDev::upload)
+    uint32_t stride;        // bits 0-8: LDS row stride in dwords (max box width of the item); bits 9-31:
+                            // the item's first chunk in the group overflow table (TiledLut::grp1)
 };
+constexpr int kStrideBits = 9;
+// Staging groups: an item stages, per slot and box row, only the 8-pixel groups between the row's leftmost
+// and rightmost tap (the box layout in LDS is kept: the entries' tap offsets do not change).  One u16 per
+// group: bit 15 valid, bits 8-12 the group's column in the box (x = bx0 + 8 col), bits 0-7 its row.  A
+// slot's groups fill whole 64-group chunks (the last one padded with invalid groups); chunk c of an item:
+// grp0[(t kGroupFirst + c) 64 + lane] for c < kGroupFirst (each wave's first chunk, loaded one iteration
+// ahead by item index alone), grp1[(ovf + c - kGroupFirst) 64 + lane] after (ovf: TileHdr::stride >> 9).
+constexpr int kGroupFirst = 4;
+constexpr uint32_t kGroupValid = 0x8000u;
 
 // One input camera as the per-frame kernels see it: a YUV420P frame in "Y over [U|V]" layout.
 struct SourceFrame {
@@ -193,6 +203,9 @@ struct TiledLut {
     uint32_t* queue;              // per band a work counter, then a done ticket, kQueueStride apart;
                                   // zero before a launch, left zero by its last workgroup
     int qpl;                      // quads per lane: an item is 128 x (8 qpl) pixels, qpl * kTilePx entries
+    const uint16_t* grp0;         // staging groups of each item's first kGroupFirst chunks (kGroupFirst * 64 per item)
+    const uint16_t* grp1;         // the items' further chunks
+    uint32_t n_grp1;              // entries of grp1
 };
 constexpr int kMetaWords = 1 + kTileSlots;
 constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter

@@ -29,6 +29,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     b.entries.assign((size_t)n_jobs * item_px, 0u);
     std::vector<uint8_t> is_wide(n_jobs, 0);
     std::vector<std::vector<CompositeEntry>> wide_raw(n_jobs);
+    std::vector<std::vector<uint16_t>> grp_job(n_jobs);  // per job its staging groups, chunk-padded
     const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     auto work = [&](int tid) {
         struct Px {
@@ -88,7 +89,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             if (ns > kTileSlots) wide = true;
             TileSlot ts[kTileSlots] = {};
             int bws[kTileSlots] = {}, bhs[kTileSlots] = {};
-            uint32_t stride = 0, groups = 0;
+            uint32_t stride = 0;
             for (int j = 0; j < ns && !wide; j++) {
                 if (in_w[cams[j]] % 8) {  // dword staging of boxes needs 8-aligned box columns inside the image
                     wide = true;
@@ -108,14 +109,64 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 ts[j].bx0 = (uint16_t)bx0;
                 ts[j].by0 = (uint16_t)by0;
                 stride = std::max<uint32_t>(stride, (uint32_t)bws[j]);
-                groups += (uint32_t)(bws[j] * bhs[j] / 4);
             }
-            uint32_t lds = kTileZeroDwords, chunks = 0;
+            // Staged groups: per slot and box row, the 8-pixel groups from the row's leftmost to its
+            // rightmost tap (row spans inside the box; the box keeps the LDS layout, so the entries'
+            // tap offsets are unchanged, but the box's corners no tap reads are not staged)
+            std::vector<uint16_t>& G = grp_job[t];
+            G.clear();
+            uint32_t chunks = 0, groups = 0;
+            if (!wide) {
+                std::vector<int> g_lo[kTileSlots], g_hi[kTileSlots];
+                for (int j = 0; j < ns; j++) {
+                    g_lo[j].assign(bhs[j], INT32_MAX);
+                    g_hi[j].assign(bhs[j], -1);
+                }
+                for (int k = 0; k < item_px; k++) {
+                    if (!px[k].mask) continue;
+                    const int j = px[k].slot;
+                    const int r = px[k].y0 - ts[j].by0, ga = (px[k].x0 - ts[j].bx0) >> 3, gb = (px[k].x0 + 1 - ts[j].bx0) >> 3;
+                    for (int rr = r; rr <= r + 1; rr++) {
+                        g_lo[j][rr] = std::min(g_lo[j][rr], ga);
+                        g_hi[j][rr] = std::max(g_hi[j][rr], gb);
+                    }
+                }
+                for (int j = 0; j < ns; j++) {
+                    ts[j].chunk0 = (uint16_t)chunks;
+                    uint32_t n = 0;
+                    for (int r = 0; r < bhs[j]; r++)
+                        for (int g = g_lo[j][r]; g <= g_hi[j][r]; g++, n++)
+                            G.push_back((uint16_t)(kGroupValid | (uint32_t)g << 8 | (uint32_t)r));
+                    const uint32_t c = (n + 63) / 64;
+                    G.resize((size_t)(chunks + c) * 64, 0);  // the slot's last chunk padded with invalid groups
+                    chunks += c;
+                    groups += n;
+                }
+                // every tap of every pixel lies in a staged group of its slot (what the kernel reads from
+                // LDS is exactly what staging wrote): checked here, once per rig
+                std::vector<uint32_t> staged[kTileSlots];
+                for (int j = 0; j < ns; j++) staged[j].assign(bhs[j], 0u);
+                for (int j = 0; j < ns; j++) {
+                    const uint32_t c_end = j + 1 < ns ? ts[j + 1].chunk0 : chunks;
+                    for (uint32_t c = ts[j].chunk0; c < c_end; c++)
+                        for (int i = 0; i < 64; i++) {
+                            const uint16_t g = G[(size_t)c * 64 + i];
+                            if (g & kGroupValid) staged[j][g & 255] |= 1u << ((g >> 8) & 31);
+                        }
+                }
+                for (int k = 0; k < item_px; k++) {
+                    if (!px[k].mask) continue;
+                    const int j = px[k].slot, r = px[k].y0 - ts[j].by0;
+                    const int ga = (px[k].x0 - ts[j].bx0) >> 3, gb = (px[k].x0 + 1 - ts[j].bx0) >> 3;
+                    const uint32_t need = (1u << ga) | (1u << gb);
+                    REQUIRE((staged[j][r] & need) == need && (staged[j][r + 1] & need) == need,
+                            "tiled LUT: a tap outside the staged groups (internal error)");
+                }
+            }
+            uint32_t lds = kTileZeroDwords;
             for (int j = 0; j < ns && !wide; j++) {
                 ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
                 lds += stride * (uint32_t)bhs[j];
-                ts[j].chunk0 = (uint16_t)chunks;
-                chunks += (uint32_t)(bws[j] * bhs[j] / 8 + 63) / 64;
             }
             for (int j = ns; j < kTileSlots; j++) ts[j].chunk0 = (uint16_t)std::min<uint32_t>(chunks, 255u);
             if (chunks > 255) wide = true;
@@ -123,11 +174,12 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             if (wide) {
                 is_wide[t] = 1;
                 wide_raw[t] = raw;
+                G.clear();
                 continue;
             }
             b.hdr[t] = TileHdr{(uint32_t)J.tx | ((uint32_t)J.ty << 16),
                                (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16),
-                               groups, stride};
+                               2 * groups, stride};
             for (int j = 0; j < kTileSlots; j++) b.slots[(size_t)t * kTileSlots + j] = ts[j];
             uint32_t* out = b.entries.data() + (size_t)t * item_px;
             for (int k = 0; k < item_px; k++) {
@@ -165,39 +217,62 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
         }
         b.staged_bytes += 8.0 * b.hdr[n_items].stage_groups;  // 4 Y + 2 U + 2 V bytes per 4-pixel group
         b.item_flags.push_back((uint16_t)jobs[t].flags);
+        // the item's first kGroupFirst chunks in its fixed grp0 block, the rest appended to grp1 (the
+        // item's first overflow chunk in TileHdr::stride bits 9-31)
+        {
+            const std::vector<uint16_t>& G = grp_job[t];
+            b.grp0.resize((size_t)(n_items + 1) * kGroupFirst * 64, 0);
+            const size_t first = std::min<size_t>(G.size(), (size_t)kGroupFirst * 64);
+            std::copy(G.begin(), G.begin() + first, b.grp0.begin() + (size_t)n_items * kGroupFirst * 64);
+            const size_t ovf_chunk = b.grp1.size() / 64;
+            REQUIRE(ovf_chunk < (1u << 23), "tiled LUT: staging group overflow table too large");
+            b.hdr[n_items].stride |= (uint32_t)ovf_chunk << kStrideBits;
+            b.grp1.insert(b.grp1.end(), G.begin() + first, G.end());
+            std::vector<uint16_t>().swap(grp_job[t]);
+        }
         n_items++;
     }
     b.n_items = n_items;
     b.n_wide = (int)b.wide_tiles.size();
-    {  // unique source bytes the launch reads: the union over items of each camera's staged boxes (8 x 2
-       // luma cells, 1.5 B per luma pixel of YUV420P), plus the wide tiles' tap cells
+    {  // unique source bytes the launch reads: the union over items of the staged groups (8 luma bytes per
+       // group row, 4 U + 4 V bytes per group row pair), plus the wide tiles' tap cells
         const int nc = (int)in_w.size();
-        std::vector<std::vector<uint8_t>> cell(nc);
+        std::vector<std::vector<uint8_t>> lum(nc), chr(nc);
         std::vector<int> cw(nc);
         for (int c = 0; c < nc; c++) {
             cw[c] = (in_w[c] + 7) / 8;
-            cell[c].assign((size_t)cw[c] * ((in_h[c] + 1) / 2), 0);
+            lum[c].assign((size_t)cw[c] * in_h[c], 0);
+            chr[c].assign((size_t)cw[c] * ((in_h[c] + 1) / 2), 0);
         }
         auto mark = [&](int c, int x, int y) {
             if (c < 0 || c >= nc || x < 0 || y < 0 || x >= in_w[c] || y >= in_h[c]) return;
-            cell[c][(size_t)(y / 2) * cw[c] + x / 8] = 1;
+            lum[c][(size_t)y * cw[c] + x / 8] = 1;
+            chr[c][(size_t)(y / 2) * cw[c] + x / 8] = 1;
         };
-        for (int t = 0; t < n_items; t++)
-            for (int j = 0; j < (int)(b.hdr[t].nslots & 0xFFu); j++) {
+        for (int t = 0; t < n_items; t++) {
+            const int ns = (int)(b.hdr[t].nslots & 0xFFu), nch = (int)((b.hdr[t].nslots >> 8) & 0xFFu);
+            for (int c = 0; c < nch; c++) {
+                int j = 0;
+                while (j + 1 < ns && c >= (int)b.slots[(size_t)t * kTileSlots + j + 1].chunk0) j++;
                 const TileSlot& sl = b.slots[(size_t)t * kTileSlots + j];
-                for (int y = sl.by0; y < sl.by0 + sl.bh; y += 2)
-                    for (int x = sl.bx0; x < sl.bx0 + sl.bw; x += 8) mark(sl.cam, x, y);
+                const uint16_t* g = c < kGroupFirst ? b.grp0.data() + ((size_t)t * kGroupFirst + c) * 64
+                                                     : b.grp1.data() + ((size_t)(b.hdr[t].stride >> kStrideBits) + c - kGroupFirst) * 64;
+                for (int i = 0; i < 64; i++)
+                    if (g[i] & kGroupValid) mark(sl.cam, sl.bx0 + 8 * ((g[i] >> 8) & 31), sl.by0 + (g[i] & 255));
             }
+        }
         for (const CompositeEntry& e : b.wide) {
             if (!(e.code & 0x8000u)) continue;
             const int c = (int)((e.code >> 10) & 31u);
             const int sx = (int)(int16_t)(e.xy & 0xFFFFu), sy = (int)(int16_t)(e.xy >> 16);
             for (int k = 0; k < 4; k++) mark(c, sx + (k & 1), sy + (k >> 1));
         }
-        double cells = 0;
-        for (auto& v : cell)
-            for (uint8_t x : v) cells += x;
-        b.source_bytes = cells * 16 * 1.5;
+        double groups = 0, pairs = 0;
+        for (int c = 0; c < nc; c++) {
+            for (uint8_t x : lum[c]) groups += x;
+            for (uint8_t x : chr[c]) pairs += x;
+        }
+        b.source_bytes = groups * 8 + pairs * 8;
     }
     {  // XCD bands of equal item counts over the staged items (kernels.hpp kStitchBands)
         std::vector<double> cum(n_items + 1, 0.0);
@@ -223,7 +298,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             hist[k]++;
             uint32_t lds = kTileZeroDwords;
             for (int j = 0; j < (int)(b.hdr[t].nslots & 0xFFu); j++)
-                lds += b.hdr[t].stride * b.slots[(size_t)t * kTileSlots + j].bh;
+                lds += (b.hdr[t].stride & ((1u << kStrideBits) - 1)) * b.slots[(size_t)t * kTileSlots + j].bh;
             const uint32_t kb = lds * 4u / 1024u;  // 0-1, 1-2, 2-4, 4-8, 8-16, 16-24, >24 KiB
             lds_hist[kb < 1 ? 0 : kb < 2 ? 1 : kb < 4 ? 2 : kb < 8 ? 3 : kb < 16 ? 4 : kb < 24 ? 5 : 6]++;
             for (int g = 0; g < kStitchBands; g++)
@@ -240,6 +315,8 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
         b.stats = s;
     }
     b.hdr.resize(std::max(n_items, 1));
+    b.grp0.resize((size_t)std::max(n_items, 1) * kGroupFirst * 64, 0);
+    if (b.grp1.empty()) b.grp1.assign(64, 0);
     b.slots.resize((size_t)std::max(n_items, 1) * kTileSlots);
     b.entries.resize((size_t)std::max(n_items, 1) * item_px);
     if (b.wide.empty()) {
@@ -271,6 +348,9 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
         std::memcpy(&m[t * kMetaWords + 1], &b.slots[t * kTileSlots], kTileSlots * sizeof(TileSlot));
     }
     meta.upload(m.data(), m.size());
+    REQUIRE(b.grp0.size() * 2 < (size_t)1 << 31 && b.grp1.size() * 2 < (size_t)1 << 31, "staging group tables exceed 2 GiB");
+    grp0.upload(b.grp0.data(), b.grp0.size());
+    grp1.upload(b.grp1.data(), b.grp1.size());
     // the composite addresses the entries through a buffer resource with 32-bit offsets
     REQUIRE(b.entries.size() * sizeof(uint32_t) < (size_t)1 << 32, "tiled LUT entries exceed 4 GiB");
     entries.upload(b.entries.data(), b.entries.size());
@@ -298,7 +378,7 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     if (b.item_flags.empty()) g0_bytes = 4.0 * kTilePx * ((double)b.n_items * b.qpl + b.n_wide);  // no flags: every half
     stats = b.stats;
     view = TiledLut{meta.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
-                    b.qpl};
+                    b.qpl, grp0.p, grp1.p, (uint32_t)b.grp1.size()};
 }
 
 }  // namespace octvr

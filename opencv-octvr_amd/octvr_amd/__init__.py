@@ -98,9 +98,12 @@ _lib.octvr_fastmapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_in
 _lib.octvr_fastmapper_stitch_nv12.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP]
 _lib.octvr_fastmapper_destroy.argtypes = [_VP]
 _lib.octvr_fastmapper_destroy.restype = None
-_lib.octvr_debug_json_number.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double)]
-_lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
-                                              C.c_char_p, C.c_size_t]
+# self-test hooks (absent from older builds that OCTVR_HIP_LIB may select for an A/B)
+if hasattr(_lib, "octvr_debug_json_number"):
+    _lib.octvr_debug_json_number.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double)]
+if hasattr(_lib, "octvr_debug_fastmapper_audit"):
+    _lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
+                                                  C.c_int, C.c_char_p, C.c_size_t]
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
                                 C.c_float, C.c_float, _VP, C.c_size_t, _VP]
 
