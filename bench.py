@@ -90,15 +90,21 @@ def derive_set(base, seeds):
     return out
 
 
+ISSUE_S = [0.0]  # host time the last timed_region spent issuing its steps (before the final sync)
+
+
 def timed_region(step, steps, sync, dist=None):
     """Exactly `steps` calls of step(k), bracketed by a barrier + device sync on both sides; returns
-    the MAX over ranks of the elapsed wall time (the job is as slow as its slowest rank)."""
+    the MAX over ranks of the elapsed wall time (the job is as slow as its slowest rank).  The host time
+    spent issuing the steps is left in ISSUE_S[0]: close to the elapsed time means the host, not the
+    GPU, set the pace."""
     if dist:
         dist.barrier()
     sync()
     t0 = time.perf_counter()
     for k in range(steps):
         step(k)
+    ISSUE_S[0] = time.perf_counter() - t0
     sync()
     if dist:
         dist.barrier()
@@ -376,15 +382,19 @@ def fast_rank(args, world, rank, local_rank, dist):
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     stream, out = streams[0], outs[0]
 
+    refs = [ox.Mapper.frame_refs(fs) for fs in frame_sets]
+    import ctypes
+    raw_streams = [ctypes.c_void_p(st.cuda_stream) for st in streams]
+
     def step(k):
-        fm.stitch_nv12(frame_sets[k % nsets], outs[k % inflight], stream=streams[k % inflight])
+        fm.stitch_nv12(refs[k % nsets], outs[k % inflight], stream=raw_streams[k % inflight])
 
     if args.pmc_child:
         for k in range(max(args.steps, 1)):
             step(k)
         torch.cuda.synchronize(dev)
         sys.exit(0)
-    for k in range(max(args.warmup, inflight)):  # every stream's first launch outside the timed region
+    for k in range(max(args.warmup, inflight, nsets)):  # every stream and frame set once outside the timed region
         step(k)
     torch.cuda.synchronize(dev)
     elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
@@ -403,6 +413,7 @@ def fast_rank(args, world, rank, local_rank, dist):
         "metric": "stitched megapixels/sec (6x4K->8K equirect, FastMapper NV12)",
         "value": round(aggregate_mps(world, args.steps, W * H, elapsed), 1), "unit": "MP/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "host_issue_ms_per_step": round(ISSUE_S[0] * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (splitmix64 frames as NV12, further sets derived by a splitmix64 key, SURVEY.md §8d rig)",
         "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
@@ -457,10 +468,14 @@ def gpu_rank(args, world, rank, local_rank, dist):
         frame_sets.append(derive_set(frame_sets[0], [frame_seed(rank, j, i) for i in range(len(sizes))]))
     outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
+    # the frame sets' pointers marshalled once, raw stream handles (a capture ring reuses its buffers)
+    refs = [ox.Mapper.frame_refs(fs) for fs in frame_sets]
+    import ctypes
+    raw_streams = [ctypes.c_void_p(st.cuda_stream) for st in streams]
 
     def step(k):
         j = k % inflight
-        m.stitch(frame_sets[k % nsets], outs[j], stream=streams[j])
+        m.stitch(refs[k % nsets], outs[j], stream=raw_streams[j])
 
     if args.pmc_child:  # a few launches for rocprofv3 --pmc passes
         for k in range(max(args.steps, 1)):
@@ -471,7 +486,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # setup: one stitch per stream first, so every stream's hardware queue exists before the W warmup
     # steps (the first launch on a new stream costs ~8 ms: with W < inflight it used to land inside the
     # timed region — the "four in flight" cliff of round 2, profiles/r03_kt_inflight_cliff.md)
-    for j in range(inflight):
+    for j in range(max(inflight, nsets)):  # (and every frame set once: no first touch in the timed region)
         step(j)
     torch.cuda.synchronize(dev)
     for k in range(args.warmup):
@@ -538,6 +553,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "host_issue_ms_per_step": round(ISSUE_S[0] * 1e3 / args.steps, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,

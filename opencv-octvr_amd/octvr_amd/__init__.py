@@ -165,6 +165,8 @@ def interval_union(starts, ends):
 
 
 def _stream_ptr(stream):
+    if isinstance(stream, C.c_void_p):
+        return stream
     if stream is None:
         stream = torch.cuda.current_stream()
     return C.c_void_p(stream.cuda_stream)
@@ -297,6 +299,18 @@ class MapperTemplate:
             pass
 
 
+class FrameRefs:
+    """A frame set's device pointers and pitches marshalled once (Mapper.frame_refs), for callers that
+    stitch the same buffers repeatedly (a capture ring): stitch() then skips the per-call ctypes work."""
+    __slots__ = ("tensors", "ptrs", "pitches", "n")
+
+    def __init__(self, tensors):
+        self.tensors = list(tensors)  # kept alive while the references are in use
+        self.n = len(self.tensors)
+        self.ptrs = (_VP * self.n)(*[t.data_ptr() for t in self.tensors])
+        self.pitches = (C.c_size_t * self.n)(*[t.stride(0) for t in self.tensors])
+
+
 class Mapper:
     """vr::Mapper on one device: stitch(inputs YUV420P, output YUV420P) with optional gain."""
 
@@ -314,13 +328,21 @@ class Mapper:
         # output frame size: scale_output, or the template's out_size (mapper.cpp:69)
         self.out_size = tuple(scale_output) if scale_output[0] else mt.out_size
 
+    @staticmethod
+    def frame_refs(inputs):
+        """FrameRefs of a list of input tensors, accepted by stitch() in place of the list."""
+        return FrameRefs(inputs)
+
     def stitch(self, inputs, output, gains=None, stream=None, preview=None):
-        """inputs: list of uint8 cuda tensors (1.5H x W "Y over [U|V]"); output likewise.  preview: an
-        optional (h, w, 3) uint8 cuda tensor receiving Mapper::stitch's preview_output (the RGB result
-        resized, mapper.cpp:308-312)."""
-        n = len(inputs)
-        ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
-        pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
+        """inputs: list of uint8 cuda tensors (1.5H x W "Y over [U|V]") or their FrameRefs; output likewise.
+        preview: an optional (h, w, 3) uint8 cuda tensor receiving Mapper::stitch's preview_output (the RGB
+        result resized, mapper.cpp:308-312).  stream: a torch stream or a raw ctypes stream handle."""
+        if isinstance(inputs, FrameRefs):
+            n, ptrs, pitches = inputs.n, inputs.ptrs, inputs.pitches
+        else:
+            n = len(inputs)
+            ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
+            pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
         g = None
         ng = 0
         if gains is not None:
@@ -404,10 +426,13 @@ class FastMapper:
         return b.value
 
     def stitch_nv12(self, inputs, output, stream=None):
-        """inputs: uint8 cuda tensors (1.5H x W NV12); output: 1.5H x W (chroma rows V,U)."""
-        n = len(inputs)
-        ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
-        pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
+        """inputs: uint8 cuda tensors (1.5H x W NV12) or their FrameRefs; output: 1.5H x W (chroma rows V,U)."""
+        if isinstance(inputs, FrameRefs):
+            n, ptrs, pitches = inputs.n, inputs.ptrs, inputs.pitches
+        else:
+            n = len(inputs)
+            ptrs = (_VP * n)(*[t.data_ptr() for t in inputs])
+            pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
         _check(_lib.octvr_fastmapper_stitch_nv12(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()), output.stride(0),
                                                  _stream_ptr(stream)))
 

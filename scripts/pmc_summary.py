@@ -24,7 +24,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def short(name):
     m = re.search(r"octvr(\d+)(\w+?_kernel)", name)
     base = m.group(2) if m else name.split("(")[0][:60]
-    t = re.search(r"_kernelIL(b\d)ELi(\d)ELb(\d)ELi(\d)E", name)  # stitch_tiled_kernel<DW, MODE, VIG, QPL>
+    t = re.search(r"_kernelIL(b\d)ELi(\d)ELb(\d)E", name)  # stitch_tiled_kernel<DW, MODE, VIG(, QPL)>
     if t:
         base += "<mode%s>" % t.group(2)
     return base
