@@ -133,15 +133,17 @@ hipError_t launch_mb_down(const uint2* items, int n_items, const MbCamLevel* cam
 //   L    = sat_s16(rne(D * (1.0f / (1e-5f + sum_n w_n))))                                     [K11]
 //   R    = top ? L : sat_s16(L + pyrUp(R_next))                                                [add]
 //   level 0: out = sat_u8(R) as RGB -> YUV420P; otherwise R is stored (s16x4) for the next level.
-// One workgroup per 128x8 tile of the level grid, one 2x2 quad per lane.  pyrUp taps come from the
-// UpQuad tables: 3 rows x 3 columns of source per quad, per-pixel integer weights over them.
+// Multi-band: one wave per 32x8 sub-tile of a per-level work list (feather: one workgroup per 128x8 tile),
+// one 2x2 quad per lane.  pyrUp taps are computed in registers (up_arith, kernels.hpp; the host proves
+// per rig that they weigh exactly the UpQuad tables' sources, check_up_arith): 3 rows x 3 columns of
+// source per quad, per-pixel integer weights over them, read straight from global memory.
 // ---------------------------------------------------------------------------------------------
 struct Up9 {
     int s[4][3];  // per quad pixel, per channel: the integer tap sum (scale 1/64)
 };
 
-// pyrUp sums of a quad from a staged LDS patch (rows r0.., cols c0.. of the coarser level):
-// 3 x 3 union taps, per-pixel integer weights over them (UpQuad).  The 1-D weights of a quad row /
+// pyrUp sums of a quad from its 3 x 3 union taps and per-pixel integer weights over them (UpArith).
+// The 1-D weights of a quad row /
 // column sum to 8 (1 6 1 or 4 4), so with s16 sources every product and partial sum fits 24 bits:
 // 24-bit multiplies (full rate; a 32-bit v_mul_lo is quarter rate).
 template <class QR, class QC>
@@ -167,28 +169,8 @@ __device__ __forceinline__ void up_weigh(const QR& ur, const QC& uc, const int (
     }
 }
 
-template <class T, class UNPACK>
-__device__ __forceinline__ void up_quad_lds(const UpQuad& ur, const UpQuad& uc, int r0, int c0, const T* patch,
-                                            UNPACK unpack, Up9& o) {
-    int v[3][3][3];  // [row][col][ch]
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        const int pr = min(max((int)ur.idx[j] - r0, 0), kUpPatchRows - 1);  // zero-weight taps may lie outside
-#pragma unroll
-        for (int k = 0; k < 3; k++) {
-            const int pc = min(max((int)uc.idx[k] - c0, 0), kUpPatchCols - 1);
-            unpack(patch[pr * kUpPatchCols + pc], v[j][k]);
-        }
-    }
-    up_weigh(ur, uc, v, o);
-}
-
-// The 3 x 3 taps of a quad straight from global memory (the table's indices are clamped into the
-// source; neighbouring lanes share the lines, so these are mostly L1 / L2 hits): no LDS staging and
-// no barriers.
-__device__ __forceinline__ UpQuad load_up(const UpQuad* t, int i) {
-    return __builtin_bit_cast(UpQuad, *reinterpret_cast<const uint4*>(t + i));
-}
+// The 3 x 3 taps of a quad straight from global memory (indices clamped into the source; neighbouring
+// lanes share the lines, so these are mostly L1 / L2 hits): no LDS staging and no barriers.
 template <class T>
 struct Taps9 {
     T t[3][3];
@@ -260,74 +242,20 @@ __device__ __forceinline__ void up_g_packed(const UpArith& ur, const UpArith& uc
     }
 }
 
-// Cooperative load of an 8 x 72 patch (rows r0.., cols c0.., clamped to the source) into registers:
-// entries tid, tid + 256, tid + 512 (< 576).
-constexpr int kPatchN = kUpPatchRows * kUpPatchCols;
-template <class T>
-struct PatchRegs {
-    T v[3];
-};
-template <class T>
-__device__ __forceinline__ void patch_issue(const uint8_t* base, int64_t pitch, int rows, int cols, int r0, int c0,
-                                            PatchRegs<T>& o) {
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int i = min((int)threadIdx.x + 256 * k, kPatchN - 1);
-        const int r = min(r0 + i / kUpPatchCols, rows - 1), c = min(c0 + i % kUpPatchCols, cols - 1);
-        o.v[k] = *reinterpret_cast<const T*>(base + (int64_t)r * pitch + (int64_t)c * sizeof(T));
-    }
-}
-template <class T>
-__device__ __forceinline__ void patch_store(const PatchRegs<T>& o, T* lds) {
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const int i = (int)threadIdx.x + 256 * k;
-        if (i < kPatchN) lds[i] = o.v[k];
-    }
-}
-
-#ifndef MB_PAIR_LOADS  // one 8-byte load per quad row for G and the weights
-#define MB_PAIR_LOADS 1
-#endif
-#ifndef MB_DIRECT_TAPS  // pyrUp taps read per lane from global memory instead of LDS-staged patches
-#define MB_DIRECT_TAPS 1
-#endif
-
-#ifndef MB_RUP_EARLY
-#define MB_RUP_EARLY 0
-#endif
-#ifndef MB_LOADS_FIRST  // a camera's loads all issued before their first use (one round trip per camera)
-#define MB_LOADS_FIRST 1
-#endif
-#ifndef MB_COLLAPSE_FIRST
-#define MB_COLLAPSE_FIRST 0
-#endif
-#ifndef MB_PACKED_UP  // the Gaussian pyrUp in packed 16-bit halves (up_g_packed)
-#define MB_PACKED_UP 1
-#endif
-#ifndef MB_ARITH_TAPS  // direct taps: computed in registers (up_arith), not read from the UpQuad tables
-#define MB_ARITH_TAPS 1
-#endif
-#ifndef MB_BLEND_WAVES  // waves per SIMD the blend is compiled for (register budget)
-#define MB_BLEND_WAVES 7
-#endif
+constexpr int kBlendWaves = 7;  // waves per SIMD the blend is compiled for (register budget)
 // 1e-5f + 1.0f (one weight-1 camera: (float)(1. / 255) * 255.0f rounds to exactly 1.0f) and the
 // correctly rounded reciprocals of the two common weight sums (constant-folded)
 constexpr float kWsumOwned = 1e-5f + 1.0f, kRcpOwned = 1.0f / kWsumOwned, kRcpNone = 1.0f / 1e-5f;
 static_assert((float)(1. / 255) * 255.0f == 1.0f, "seam weight 255 / 255");
 
-__global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendArgs a) {
-#if !MB_DIRECT_TAPS
-    __shared__ uint2 s_r[kPatchN];     // collapsed coarser level (s16x4)
-    __shared__ uint32_t s_g[kPatchN];  // the current camera's coarser Gaussian level (u8x4)
-#endif
+__global__ void __launch_bounds__(256, kBlendWaves) mb_blend_kernel(MbBlendArgs a) {
     const int tid = threadIdx.x;
     const int wv = uniform(tid >> 6), lane = tid & 63;
     // Multi-band: wave w of block b blends sub-tile work[4 b + w] (32 x 8: lane = quad, 16 per quad row;
     // a scalar load through the constant address space): tile | quarter << 24 | kind << 27, its cameras.
-    // Waves share nothing (no LDS, no barriers in the direct-taps build), so a workgroup's four sub-tiles
-    // may lie anywhere.  Feather (no list): one tile per workgroup, wave = quad row, lane = quad.
-    static_assert(MB_DIRECT_TAPS, "per-wave sub-tiles need the barrier-free direct-taps blend");
+    // Waves share nothing (no LDS, no barriers: every pyrUp tap is read straight from global memory), so
+    // a workgroup's four sub-tiles may lie anywhere.  Feather (no list): one tile per workgroup, wave =
+    // quad row, lane = quad.
     typedef __attribute__((address_space(4))) const uint64_t kU64;
     const uint64_t wk64 = a.work ? ((const kU64*)a.work)[blockIdx.x * 4 + wv] : 0ull;
     const uint2 wk = make_uint2((uint32_t)wk64, (uint32_t)(wk64 >> 32));
@@ -339,40 +267,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
     bool valid[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) valid[p] = (x + (p & 1)) < a.W && (y + (p >> 1)) < a.H;
-#if !MB_DIRECT_TAPS
-    // the collapse patch first: its loads overlap the camera loop
-    PatchRegs<uint2> rp;
-    int rr0 = 0, rc0 = 0;
-    if (!top) {
-        rr0 = a.rup_r0[ty];
-        rc0 = a.rup_c0[tx];
-        patch_issue<uint2>(reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, a.H_next, a.W_next, rr0,
-                           rc0, rp);
-    }
-#endif
-#if MB_RUP_EARLY  // the collapse's per-column tap table loaded before the camera loop, kept raw
-    uint4 ucR_raw = make_uint4(0u, 0u, 0u, 0u);
-    if (!top) ucR_raw = *reinterpret_cast<const uint4*>(a.rup_cols + (x >> 1));
-#endif
-#if MB_COLLAPSE_FIRST
-    // the collapse's 9 taps issued before the camera loop: their latency overlaps the first camera's
-    // loads instead of following the loop (18 VGPRs held across it)
-    UpArith urR = up_arith(y, 0, a.H, a.H_next, true), ucR = up_arith(x, 0, a.W, a.W_next, false);
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-        urR.w0[j] = ucR.w0[j] = j == 1 ? 6 : 1;
-        urR.w1[j] = ucR.w1[j] = j == 0 ? 0 : 4;
-    }
-    Taps9<uint2> tpR;
-    if (!top) {
-        up_taps_issue<uint2>(urR, ucR, reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, tpR);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 3; j++)
-#pragma unroll
-            for (int k = 0; k < 3; k++) tpR.t[j][k] = make_uint2(0u, 0u);
-    }
-#endif
     int R[4][3];
     uint32_t m = a.work ? (uint32_t)uniform((int)wk.y) : (uint32_t)uniform((int)a.tile_cams[tile]);
     // Tiles owned by one camera (its weight is exactly 1.0f on every tile pixel: seam 255 at level 0,
@@ -436,7 +330,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
         const int xl = x - c.ox, yl = y - c.oy;  // camera-local quad origin (any parity)
         float w[4];
         float g[4][3];  // G - pyrUp(G_next) (G at the top level): small exact integers
-#if MB_LOADS_FIRST
         if (c.w >= 2) {
             // Every load of this camera is issued before any of them is used — the G pairs and weight
             // pairs of both quad rows and the 9 pyrUp taps — so a camera costs one memory round trip.
@@ -455,21 +348,8 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             const uint2 gp0 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy0 * c.g_pitch + x0 * 4);
             const uint2 gp1 = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy1 * c.g_pitch + x0 * 4);
             const uint32_t at0 = dlt + (uint32_t)(cy0 * c.w + x0), at1 = dlt + (uint32_t)(cy1 * c.w + x0);
-#if MB_LF_F32_GLOBAL
-            u32x2 wq0, wq1;
-            if (a.w_u8) {
-                wq0 = __builtin_amdgcn_raw_buffer_load_b64(wr, at0 & ~3u, 0, 0);
-                wq1 = __builtin_amdgcn_raw_buffer_load_b64(wr, at1 & ~3u, 0, 0);
-            } else {
-                const uint2 t0 = *reinterpret_cast<const uint2*>(static_cast<const float*>(c.weight) + at0);
-                const uint2 t1 = *reinterpret_cast<const uint2*>(static_cast<const float*>(c.weight) + at1);
-                wq0 = u32x2{t0.x, t0.y};
-                wq1 = u32x2{t1.x, t1.y};
-            }
-#else
             const u32x2 wq0 = __builtin_amdgcn_raw_buffer_load_b64(wr, a.w_u8 ? at0 & ~3u : at0 * 4u, 0, 0);
             const u32x2 wq1 = __builtin_amdgcn_raw_buffer_load_b64(wr, a.w_u8 ? at1 & ~3u : at1 * 4u, 0, 0);
-#endif
             // unconditionally (the top level reads its own G as a stand-in, unused): a branch here would
             // let the compiler merge it with the one below, after the weight decode's waits
             const MbCamLevel cn = *(top ? a.cams + n : a.cams_next + n);
@@ -521,54 +401,9 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
 #pragma unroll
                     for (int ch = 0; ch < 3; ch++) g[p][ch] = (float)ch_of(gv[p], ch);
             }
-        } else
-#endif
-        {
-            // (cameras 1 pixel wide at this level, or the MB_LOADS_FIRST = 0 build)
+        } else {
+            // (cameras 1 pixel wide at this level): per-pixel loads
             uint32_t gv[4];
-#if MB_PAIR_LOADS
-            if (c.w >= 2) {
-                // per quad row one 8-byte load of G and of the weights at the clamped pair start x0:
-                // pixel px is element px - x0 (0 or 1 whenever it lies inside the camera)
-                const int x0 = min(max(xl, 0), c.w - 2);
-                // u8 level-0 weights: an 8-byte buffer load from the dword at or below the pair (dword loads
-                // ignore the low address bits, so the resource starts at the dword below the weights and
-                // reads past the end return 0)
-                const uint32_t dlt = (uint32_t)(reinterpret_cast<uintptr_t>(c.weight) & 3u);
-                const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-                    const_cast<uint8_t*>(static_cast<const uint8_t*>(c.weight) - dlt), 0,
-                    (int)(c.w * c.h + dlt), 0x00020000);
-#pragma unroll
-                for (int r = 0; r < 2; r++) {
-                    const int py = yl + r, cy = min(max(py, 0), c.h - 1);
-                    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                    const uint2 gp = *reinterpret_cast<const uint2*>(a.g + c.g_off + (int64_t)cy * c.g_pitch + x0 * 4);
-                    float wp[2];
-                    if (a.w_u8) {
-                        const uint32_t at = dlt + (uint32_t)(cy * c.w + x0), a4 = at & ~3u;
-                        const u32x2 t = __builtin_amdgcn_raw_buffer_load_b64(wr, a4, 0, 0);
-                        const uint64_t q = ((uint64_t)t.y << 32) | t.x;
-                        const uint32_t sh = 8u * (at - a4);
-                        // level 0: convertTo(CV_32F, 1/255.) of the seam mask (gpu_mat.cu:458-480): alpha * v + 0
-                        wp[0] = (float)(1. / 255) * (float)(uint32_t)((q >> sh) & 255u);
-                        wp[1] = (float)(1. / 255) * (float)(uint32_t)((q >> (sh + 8u)) & 255u);
-                    } else {  // f32 levels: in-bounds 8-byte load at the pair start
-                        const float2 t = *reinterpret_cast<const float2*>(static_cast<const float*>(c.weight) +
-                                                                          (int64_t)cy * c.w + x0);
-                        wp[0] = t.x;
-                        wp[1] = t.y;
-                    }
-#pragma unroll
-                    for (int pc = 0; pc < 2; pc++) {
-                        const int p = 2 * r + pc, px = xl + pc;
-                        const bool in = valid[p] && px >= 0 && py >= 0 && px < c.w && py < c.h;
-                        const bool hi = ((px - x0) & 1) != 0;
-                        w[p] = in ? (hi ? wp[1] : wp[0]) : 0.f;
-                        gv[p] = hi ? gp.y : gp.x;
-                    }
-                }
-            } else
-#endif
 #pragma unroll
             for (int p = 0; p < 4; p++) {
                 const int px = xl + (p & 1), py = yl + (p >> 1);
@@ -583,7 +418,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             }
             if (!top) {
                 const MbCamLevel cn = a.cams_next[n];
-#if MB_DIRECT_TAPS && MB_ARITH_TAPS && MB_PACKED_UP
                 const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
                 Taps9<uint32_t> tp;
                 up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
@@ -595,36 +429,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
                     g[p][1] = (float)ch_of(gv[p], 1) - (float)ug[p];
                     g[p][2] = (float)ch_of(gv[p], 2) - (float)(urb[p] >> 16);
                 }
-#else
-                Up9 u;
-                auto unpack = [](uint32_t v, int (&o)[3]) {
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++) o[ch] = (int)ch_of(v, ch);
-                };
-#if MB_DIRECT_TAPS
-#if MB_ARITH_TAPS
-                const UpArith ur = up_arith(y, c.oy, c.h, cn.h, true), uc = up_arith(x, c.ox, c.w, cn.w, false);
-#else
-                const UpQuad ur = c.up_rows[y >> 1], uc = load_up(c.up_cols, x >> 1);
-#endif
-                Taps9<uint32_t> tp;
-                up_taps_issue<uint32_t>(ur, uc, a.g_next + cn.g_off, cn.g_pitch, tp);
-                up_quad_taps(ur, uc, tp, unpack, u);
-#else
-                PatchRegs<uint32_t> gp;
-                const int gr0 = c.up_r0[ty], gc0 = c.up_c0[tx];
-                patch_issue<uint32_t>(a.g_next + cn.g_off, cn.g_pitch, cn.h, cn.w, gr0, gc0, gp);
-                __syncthreads();  // the previous camera's patch readers are done
-                patch_store(gp, s_g);
-                __syncthreads();
-                up_quad_lds(c.up_rows[y >> 1], c.up_cols[x >> 1], gr0, gc0, s_g, unpack, u);
-#endif
-#pragma unroll
-                for (int p = 0; p < 4; p++)
-#pragma unroll
-                    for (int ch = 0; ch < 3; ch++)
-                        g[p][ch] = (float)((int)ch_of(gv[p], ch) - min(max(rne_shr<6>(u.s[p][ch]), 0), 255));  // sat u8
-#endif
             } else {
 #pragma unroll
                 for (int p = 0; p < 4; p++)
@@ -666,10 +470,6 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             o[1] = (int)(int16_t)(v.x >> 16);
             o[2] = (int)(int16_t)(v.y & 0xFFFFu);
         };
-#if MB_DIRECT_TAPS && MB_COLLAPSE_FIRST
-        up_quad_taps(urR, ucR, tpR, unpack, u);
-#elif MB_DIRECT_TAPS
-#if MB_ARITH_TAPS
         // x and y are even on the level grid: every quad has the even tap pattern (1 6 1 | 0 4 4) as
         // constants; the zero weights up_arith gives pixels outside the level only matter for pixels
         // that are never stored (W, H even at level 0; level > 0 stores valid pixels only)
@@ -679,20 +479,9 @@ __global__ void __launch_bounds__(256, MB_BLEND_WAVES) mb_blend_kernel(MbBlendAr
             ur.w0[j] = uc.w0[j] = j == 1 ? 6 : 1;
             ur.w1[j] = uc.w1[j] = j == 0 ? 0 : 4;
         }
-#elif MB_RUP_EARLY
-        asm volatile("" : "+v"(ucR_raw.x), "+v"(ucR_raw.y), "+v"(ucR_raw.z), "+v"(ucR_raw.w));
-        const UpQuad ur = a.rup_rows[y >> 1], uc = __builtin_bit_cast(UpQuad, ucR_raw);
-#else
-        const UpQuad ur = a.rup_rows[y >> 1], uc = load_up(a.rup_cols, x >> 1);
-#endif
         Taps9<uint2> tp;
         up_taps_issue<uint2>(ur, uc, reinterpret_cast<const uint8_t*>(a.r_next), (int64_t)a.W_next * 8, tp);
         up_quad_taps(ur, uc, tp, unpack, u);
-#else
-        patch_store(rp, s_r);
-        __syncthreads();
-        up_quad_lds(a.rup_rows[y >> 1], a.rup_cols[x >> 1], rr0, rc0, s_r, unpack, u);
-#endif
 #pragma unroll
         for (int p = 0; p < 4; p++)
 #pragma unroll
