@@ -92,10 +92,14 @@ uint2 make_entry(float m1, float m2, float sx, float sy, uint8_t w) {
 }
 
 // The compact form of a plane's wide entries: per block the smallest in-use tap (entries of weight 0
-// are never used) as the header, per entry the 11-bit offsets from it, the fractions and the weight.
-// Returns false (nothing written) when some block's in-use taps span 2048 pixels or more.
-bool compact_entries(const std::vector<uint2>& e, size_t nblk, std::vector<uint32_t>& off, std::vector<uint8_t>& wgt,
-                     std::vector<uint2>& hdr) {
+// are never used; their offsets stay 0, i.e. that tap) as the header, per entry the 11-bit offsets from
+// it, the fractions and the weight.  Header word y, bit kFastInterior (fastmapper.hip): every in-use entry
+// has its taps at x <= pw - 2, y <= ph - 3 of its camera's plane (blk_cam), so the kernel may take them
+// without clamps or masks.  Returns false when some block's in-use taps span 2048 pixels or more.
+constexpr uint32_t kFastInterior = 1u;
+bool compact_entries(const std::vector<uint2>& e, size_t nblk, const std::vector<uint8_t>& blk_cam,
+                     const std::vector<int>& plane_w, const std::vector<int>& plane_h, std::vector<uint32_t>& off,
+                     std::vector<uint8_t>& wgt, std::vector<uint2>& hdr) {
     off.assign(e.size(), 0u);
     wgt.assign(e.size(), 0u);
     hdr.assign(std::max<size_t>(nblk, 1), make_uint2(0u, 0u));
@@ -112,7 +116,9 @@ bool compact_entries(const std::vector<uint2>& e, size_t nblk, std::vector<uint3
             fits[b] = 0;
             return;
         }
-        hdr[b] = make_uint2((uint32_t)(uint16_t)x0 | (uint32_t)(uint16_t)y0 << 16, 0u);
+        const int cw = plane_w[blk_cam[b]], ch = plane_h[blk_cam[b]];
+        const bool interior = x1 >= x0 && x0 >= 0 && y0 >= 0 && x1 <= cw - 2 && y1 <= ch - 3;
+        hdr[b] = make_uint2((uint32_t)(uint16_t)x0 | (uint32_t)(uint16_t)y0 << 16, interior ? kFastInterior : 0u);
         for (size_t k = b * 256; k < b * 256 + 256; k++) {
             const uint32_t w = e[k].y >> 16;
             wgt[k] = (uint8_t)w;
@@ -244,8 +250,18 @@ static FastPlan fast_plan(const octvr_rig* rig, int n_inputs, const int* in_w, c
                 euv[blk * 256 + (k - r * 256)] = make_entry(h1[k], h2[k], hx, hy, hm_i[k]);
         });
     }
-    P.y.compact = !force_wide && compact_entries(ey, by, P.y.off, P.y.wgt, P.y.hdr);
-    P.uv.compact = !force_wide && compact_entries(euv, buv, P.uv.off, P.uv.wgt, P.uv.hdr);
+    // the camera of every block (run r's cameras in ascending order from its first block)
+    auto block_cams = [](const std::vector<uint32_t>& m, size_t nb) {
+        std::vector<uint8_t> c(std::max<size_t>(nb, 1), 0);
+        size_t b = 0;
+        for (uint32_t mr : m)
+            for (uint32_t x = mr; x; x &= x - 1) c[b++] = (uint8_t)__builtin_ctz(x);
+        return c;
+    };
+    std::vector<int> pw_y(in_w, in_w + n), ph_y(in_h, in_h + n), pw_uv(n), ph_uv(n);
+    for (int i = 0; i < n; i++) pw_uv[i] = in_w[i] / 2, ph_uv[i] = in_h[i] / 2;
+    P.y.compact = !force_wide && compact_entries(ey, by, block_cams(my, by), pw_y, ph_y, P.y.off, P.y.wgt, P.y.hdr);
+    P.uv.compact = !force_wide && compact_entries(euv, buv, block_cams(muv, buv), pw_uv, ph_uv, P.uv.off, P.uv.wgt, P.uv.hdr);
     for (FastPlaneHost* pl : {&P.y, &P.uv})
         if (!pl->compact) pl->off.clear(), pl->wgt.clear(), pl->hdr.clear();
     // per stitch: the entries read (compact: 5 B per entry and 8 B per block header; wide: 8 B per
@@ -302,7 +318,7 @@ static bool force_wide_env() {  // OCTVR_FAST_WIDE=1 keeps the 8-byte entries (t
 // w + pitch_pad: st + 8 <= size), the byte selectors of in-image taps (inside the 8 loaded bytes and
 // equal to the tap's own byte), and the last output byte of each run.  Counts go to `c`.
 struct AuditCounts {
-    uint64_t groups = 0, slot_loads = 0, live_slots = 0, taps_in = 0, violations = 0;
+    uint64_t groups = 0, slot_loads = 0, live_slots = 0, taps_in = 0, violations = 0, interior_slots = 0;
     int64_t max_block = -1;
     std::string first;
 };
@@ -352,11 +368,13 @@ static void audit_plane(const FastPlan& P, const FastPlaneHost& pl, int plane, s
                     for (int k = 0; k < 4; k++) {
                         if (!live[k] || b[k] >= pl.nblk) continue;
                         a.live_slots++;
+                        if (pl.compact && (pl.hdr[b[k]].y & kFastInterior)) a.interior_slots++;
                         const int fw = P.in_w[cam[k]], fh = P.in_h[cam[k]];
                         const uint32_t pitch = (uint32_t)(fw + pitch_pad);
                         const uint32_t size = pitch * (uint32_t)(fh + fh / 2);
                         const int sw = plane ? fw / 2 : fw, sh = plane ? fh / 2 : fh;
                         const uint32_t base = plane ? (uint32_t)fh * pitch : 0u;
+                        const bool interior = pl.compact && (pl.hdr[b[k]].y & kFastInterior) != 0;
                         for (uint32_t lane = 0; lane < 256; lane++) {
                             const size_t e = (size_t)b[k] * 256 + lane;
                             int sx, sy;
@@ -378,16 +396,21 @@ static void audit_plane(const FastPlan& P, const FastPlaneHost& pl, int plane, s
                                 sy = (int)(int16_t)(we.x >> 16);
                                 w = we.y >> 16;
                             }
-                            const int xa = std::min(std::max(sx, 0), sw - 1);
+                            // interior blocks (fast_group<INNER>): no clamps — the claim itself is checked
+                            if (interior && w && !(sx >= 0 && sy >= 0 && sx <= sw - 2 && sy <= sh - 3))
+                                bad("interior block with a tap near or past the plane's edge", r, k, lane);
+                            if (interior && !w && (sx < 0 || sy < 0 || sx > sw - 2 || sy > sh - 3))
+                                bad("interior block with an unused entry off the interior", r, k, lane);
+                            const int xa = interior ? sx : std::min(std::max(sx, 0), sw - 1);
                             const uint32_t bx = (uint32_t)xa * bpp & ~3u;
                             for (int rr = 0; rr < 2; rr++) {
-                                const int y = std::min(std::max(sy + rr, 0), sh - 1);
+                                const int y = interior ? sy + rr : std::min(std::max(sy + rr, 0), sh - 1);
                                 const uint32_t row = base + (uint32_t)y * pitch;
                                 if (size < 8u) { bad("frame under 8 bytes", r, k, lane); continue; }
-                                const uint32_t st = std::min(row + bx, size - 8u);
+                                const uint32_t st = interior ? row + bx : std::min(row + bx, size - 8u);
                                 if ((uint64_t)st + 8 > size) bad("tap-row load past the frame", r, k, lane);
                                 if (!w) continue;
-                                const uint32_t d = row + (uint32_t)sx * bpp - st;
+                                const uint32_t d = interior ? ((uint32_t)sx * bpp & 3u) : row + (uint32_t)sx * bpp - st;
                                 for (int cc = 0; cc < 2; cc++) {  // in-image taps: their bytes in the loaded 8
                                     const int tx = sx + cc, ty = sy + rr;
                                     if (tx < 0 || ty < 0 || tx >= sw || ty >= sh) continue;
@@ -415,6 +438,7 @@ static void audit_plane(const FastPlan& P, const FastPlaneHost& pl, int plane, s
         c.slot_loads += a.slot_loads;
         c.live_slots += a.live_slots;
         c.taps_in += a.taps_in;
+        c.interior_slots += a.interior_slots;
         c.max_block = std::max(c.max_block, a.max_block);
     }
 }
@@ -436,11 +460,11 @@ int octvr_debug_fastmapper_audit(const octvr_rig* rig, int n_inputs, const int* 
             char b[512];
             snprintf(b, sizeof b,
                      "%s\"%s\": {\"compact\": %d, \"runs\": %zu, \"blocks\": %zu, \"groups\": %llu, "
-                     "\"slot_loads\": %llu, \"live_slots\": %llu, \"taps_in_image\": %llu, \"max_block\": %lld, "
+                     "\"slot_loads\": %llu, \"live_slots\": %llu, \"interior_slots\": %llu, \"taps_in_image\": %llu, \"max_block\": %lld, "
                      "\"violations\": %llu, \"first\": \"%s\"}",
                      plane ? ", " : "", plane ? "uv" : "y", pl.compact ? 1 : 0, pl.runs.size(), pl.nblk,
                      (unsigned long long)c.groups, (unsigned long long)c.slot_loads, (unsigned long long)c.live_slots,
-                     (unsigned long long)c.taps_in, (long long)c.max_block, (unsigned long long)c.violations,
+                     (unsigned long long)c.interior_slots, (unsigned long long)c.taps_in, (long long)c.max_block, (unsigned long long)c.violations,
                      c.first.c_str());
             js += b;
         }

@@ -73,12 +73,85 @@ struct FastPlane {
     const uint2* runs;    // per run: camera mask, first block
     uint32_t nblk;        // blocks allocated (>= 1)
 };
+// compact block header bit (y word): every weighted entry of the block is interior (fastmapper.cpp)
+constexpr uint32_t kFastInterior = 1u;
+
+// One group of up to kFastGroup cameras of a run, after the entry loads: per camera and tap row one 8-byte
+// load from the 4-byte aligned start at or below the row's first in-image tap byte (it holds both taps'
+// bytes: Y x, x + 1; chroma the V, U pairs of x, x + 1), then remap_weighted's sum in integers.
+// INNER: every tap of the group's weighted entries lies inside the plane, at least two rows above its
+// last (host-checked per block, kFastInterior), so the address clamps, the end-of-frame clamp and the
+// in-image masks are identities and are left out.
+template <int PLANE, bool INNER>
+__device__ __forceinline__ void fast_group(const FrameSet& frames, const bool (&live)[kFastGroup], const int (&cam)[kFastGroup],
+                                           const int (&sxk)[kFastGroup], const int (&syk)[kFastGroup],
+                                           const uint32_t (&code)[kFastGroup], const uint32_t (&wk)[kFastGroup],
+                                           uint32_t& acc0, uint32_t& acc1) {
+    constexpr uint32_t bpp = PLANE ? 2u : 1u;  // bytes per source pixel of the plane
+    uint2 rw[kFastGroup][2];
+    uint32_t sel[kFastGroup][2];
+#pragma unroll
+    for (int k = 0; k < kFastGroup; k++) {
+        rw[k][0] = rw[k][1] = make_uint2(0u, 0u);
+        sel[k][0] = sel[k][1] = 0u;
+        if (!live[k]) continue;
+        const SourceFrame f = frames.f[cam[k]];
+        const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
+        const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
+        const uint32_t size = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2);  // >= 8 (host check)
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(f.yuv), 0, (int)size, 0x00020000);
+        const int sx = sxk[k], sy = syk[k];
+        const int xa = INNER ? sx : min(max(sx, 0), sw - 1);
+        const uint32_t bx = (uint32_t)xa * bpp & ~3u;  // 4-byte aligned row start
+#pragma unroll
+        for (int r = 0; r < 2; r++) {
+            const int y = INNER ? sy + r : min(max(sy + r, 0), sh - 1);
+            // y < 2^15, pitch < 2^24 (host check): a 24-bit multiply
+            const uint32_t row = base + __umul24((uint32_t)y, (uint32_t)f.pitch);
+            // the buffer range-checks whole dwords: a start within 8 bytes of the frame's end (its last
+            // chroma row, a pitch not a multiple of 4) is clamped to size - 8 and the taps taken from there
+            const uint32_t st = INNER ? row + bx : min(row + bx, size - 8u);
+            // byte index of taps x = sx, sx + 1 in the 8 loaded bytes (exact for taps inside the image,
+            // any byte for the ones outside, which are masked below); an in-image chroma pair starts
+            // at most at byte 6, so its second byte is i + 1 <= 7
+            const uint32_t d = INNER ? (uint32_t)sx * bpp & 3u : row + (uint32_t)sx * bpp - st;
+            const uint32_t i0 = d & 7u, i1 = (d + bpp) & 7u;
+            // u16 pairs {tap x, tap x + 1} (chroma: of U; V is the next byte of each)
+            sel[k][r] = i0 | i1 << 16 | 0x0C000C00u;
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, st, 0, 0);
+            rw[k][r] = make_uint2(v.x, v.y);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kFastGroup; k++) {
+        if (!live[k]) continue;
+        if (wk[k] == 0) continue;
+        const uint32_t fx = code[k] & 31u, fy = code[k] >> 5;
+        uint32_t wx = 32u + fx * 0xFFFFu, wy = 32u + fy * 0xFFFFu;  // {32 - f, f} as u16 pairs
+        if (!INNER) {  // taps outside the image weigh 0: column / row masks
+            const SourceFrame f = frames.f[cam[k]];
+            const uint32_t sw = (uint32_t)(PLANE ? f.w / 2 : f.w), sh = (uint32_t)(PLANE ? f.h / 2 : f.h);
+            const int sx = sxk[k], sy = syk[k];
+            const bool ix0 = (uint32_t)sx < sw, ix1 = (uint32_t)(sx + 1) < sw;
+            const bool iy0 = (uint32_t)sy < sh, iy1 = (uint32_t)(sy + 1) < sh;
+            wx &= (ix0 ? 0xFFFFu : 0u) | (ix1 ? 0xFFFF0000u : 0u);
+            wy &= (iy0 ? 0xFFFFu : 0u) | (iy1 ? 0xFFFF0000u : 0u);
+        }
+        const float wf = (float)wk[k] * (1.f / 1024.f);
+        const uint2 q0 = rw[k][0], q1 = rw[k][1];
+        acc0 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0] + (PLANE ? 0x00010001u : 0u)),
+                                 __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1] + (PLANE ? 0x00010001u : 0u)), wx, wy, wf);
+        if (PLANE)
+            acc1 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0]), __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1]),
+                                     wx, wy, wf);
+    }
+}
 
 template <int PLANE, bool COMPACT>
 __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPlane& fp, int W, int H, uint8_t* out,
                                            int64_t out_pitch) {
     typedef __attribute__((address_space(4))) const uint64_t kU64;
-    constexpr uint32_t bpp = PLANE ? 2u : 1u;  // bytes per source pixel of the plane
     const int pw = PLANE ? W / 2 : W, ph = PLANE ? H / 2 : H;
     const uint32_t npx = (uint32_t)pw * (uint32_t)ph;  // < 2^31 (host check)
     const uint2 rr = fp.runs[blockIdx.x];
@@ -127,64 +200,16 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
         }
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) blk += live[k] ? 1u : 0u;
-        // per camera and tap row one 8-byte load from the 4-byte aligned start at or below the row's
-        // first in-image tap byte: it holds both taps' bytes (Y: x, x + 1; chroma: the V, U pairs of x, x + 1)
-        uint2 rw[kFastGroup][2];
-        uint32_t sel[kFastGroup][2];
+        // Interior groups (compact blocks flagged by the host: every weighted entry's taps at x <= w - 2,
+        // y <= h - 3 of the plane, so no tap is outside the image and no 8-byte row load reaches the frame's
+        // end) take the taps without clamps, end-of-frame clamp or in-image masks; the rest the general path.
+        bool inner = COMPACT;
 #pragma unroll
-        for (int k = 0; k < kFastGroup; k++) {
-            rw[k][0] = rw[k][1] = make_uint2(0u, 0u);
-            sel[k][0] = sel[k][1] = 0u;
-            if (!live[k]) continue;
-            const SourceFrame f = frames.f[cam[k]];
-            const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
-            const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
-            const uint32_t size = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2);  // >= 8 (host check)
-            const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(f.yuv), 0, (int)size, 0x00020000);
-            const int sx = sxk[k], sy = syk[k];
-            const int xa = min(max(sx, 0), sw - 1);
-            const uint32_t bx = (uint32_t)xa * bpp & ~3u;  // 4-byte aligned row start
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const int y = min(max(sy + r, 0), sh - 1);
-                // y < 2^15, pitch < 2^24 (host check): a 24-bit multiply
-                const uint32_t row = base + __umul24((uint32_t)y, (uint32_t)f.pitch);
-                // the buffer range-checks whole dwords: a start within 8 bytes of the frame's end (its last
-                // chroma row, a pitch not a multiple of 4) is clamped to size - 8 and the taps taken from there
-                const uint32_t st = min(row + bx, size - 8u);
-                // byte index of taps x = sx, sx + 1 in the 8 loaded bytes (exact for taps inside the image,
-                // any byte for the ones outside, which are masked below); an in-image chroma pair starts
-                // at most at byte 6, so its second byte is i + 1 <= 7
-                const uint32_t d = row + (uint32_t)sx * bpp - st;
-                const uint32_t i0 = d & 7u, i1 = (d + bpp) & 7u;
-                // u16 pairs {tap x, tap x + 1} (chroma: of U; V is the next byte of each)
-                sel[k][r] = i0 | i1 << 16 | 0x0C000C00u;
-                typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, st, 0, 0);
-                rw[k][r] = make_uint2(v.x, v.y);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kFastGroup; k++) {
-            if (!live[k]) continue;
-            if (wk[k] == 0) continue;
-            const SourceFrame f = frames.f[cam[k]];
-            const uint32_t sw = (uint32_t)(PLANE ? f.w / 2 : f.w), sh = (uint32_t)(PLANE ? f.h / 2 : f.h);
-            const int sx = sxk[k], sy = syk[k];
-            const bool ix0 = (uint32_t)sx < sw, ix1 = (uint32_t)(sx + 1) < sw;
-            const bool iy0 = (uint32_t)sy < sh, iy1 = (uint32_t)(sy + 1) < sh;
-            const uint32_t fx = code[k] & 31u, fy = code[k] >> 5;
-            // {32 - f, f} as u16 pairs: 32 + f * 0xFFFF, masked per column / row
-            const uint32_t wx = (32u + fx * 0xFFFFu) & ((ix0 ? 0xFFFFu : 0u) | (ix1 ? 0xFFFF0000u : 0u));
-            const uint32_t wy = (32u + fy * 0xFFFFu) & ((iy0 ? 0xFFFFu : 0u) | (iy1 ? 0xFFFF0000u : 0u));
-            const float wf = (float)wk[k] * (1.f / 1024.f);
-            const uint2 q0 = rw[k][0], q1 = rw[k][1];
-            acc0 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0] + (PLANE ? 0x00010001u : 0u)),
-                                     __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1] + (PLANE ? 0x00010001u : 0u)), wx, wy, wf);
-            if (PLANE)
-                acc1 += weighted_sum_int(__builtin_amdgcn_perm(q0.y, q0.x, sel[k][0]), __builtin_amdgcn_perm(q1.y, q1.x, sel[k][1]),
-                                         wx, wy, wf);
-        }
+        for (int k = 0; k < kFastGroup; k++) inner = inner && (!live[k] || ((hd[k] >> 32) & kFastInterior) != 0);
+        if (inner)
+            fast_group<PLANE, true>(frames, live, cam, sxk, syk, code, wk, acc0, acc1);
+        else
+            fast_group<PLANE, false>(frames, live, cam, sxk, syk, code, wk, acc0, acc1);
     }
     // pixel index -> (x, y): the run's first row by one scalar division, then at most 256 / pw row steps
     const uint32_t idx0 = blockIdx.x * 256u;
