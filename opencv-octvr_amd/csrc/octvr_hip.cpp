@@ -1837,6 +1837,53 @@ int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, co
     });
 }
 
+int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, char* json,
+                               size_t len) {
+    return guarded([&] {
+        REQUIRE(rig && in_w && in_h && json && len > 0, "bad arguments");
+        const int n = (int)rig->inputs.size();
+        REQUIRE(n_inputs == n && n > 0 && n <= kMaxCams, "in_sizes must cover the inputs");
+        const int W = rig->out_w, H = rig->out_h;
+        // the copy chain's winner per pixel (composite_lut_kernel on the host): the last camera whose ROI
+        // holds the pixel and whose LUT mask is set
+        std::vector<CompositeEntry> lut((size_t)W * H, CompositeEntry{0u, 0u});
+        parallel_for((size_t)H, [&](size_t y) {
+            for (int i = 0; i < n; i++) {
+                const RigInput& in = rig->inputs[i];
+                const int ry = (int)y - in.roi[1];
+                if (ry < 0 || ry >= in.roi[3]) continue;
+                for (int rx = 0; rx < in.roi[2]; rx++) {
+                    const size_t k = (size_t)ry * in.roi[2] + rx;
+                    if (!in.mask[k]) continue;
+                    lut[y * W + (size_t)(rx + in.roi[0])] = make_entry(in.map1[k], in.map2[k], (float)in_w[i], (float)in_h[i], i);
+                }
+            }
+        });
+        const int qpl = composite_qpl();
+        const int tx_n = (W + kTileW - 1) / kTileW, ty_n = (H + kTileH * qpl - 1) / (kTileH * qpl);
+        std::vector<TileJob> jobs;
+        for (int ty = 0; ty < ty_n; ty++)
+            for (int tx = 0; tx < tx_n; tx++) jobs.push_back(TileJob{tx, ty, 0});
+        // build_tiled_lut checks that every tap of every pixel lies in a staged group of its slot
+        const TiledLutBuild b = build_tiled_lut(jobs, [&](int, int x, int y) {
+            return (x < W && y < H) ? lut[(size_t)y * W + x] : CompositeEntry{0u, 0u};
+        }, std::vector<int>(in_w, in_w + n), std::vector<int>(in_h, in_h + n), qpl);
+        double box_px = 0;
+        for (int t = 0; t < b.n_items; t++)
+            for (int j = 0; j < (int)(b.hdr[t].nslots & 0xFFu); j++)
+                box_px += (double)b.slots[(size_t)t * kTileSlots + j].bw * b.slots[(size_t)t * kTileSlots + j].bh;
+        char tmp[512];
+        snprintf(tmp, sizeof tmp,
+                 "{\"items\": %d, \"wide_tiles\": %d, \"staged_px\": %.0f, \"box_px\": %.0f, \"staged_bytes\": %.0f, "
+                 "\"source_bytes\": %.0f, \"grp1_entries\": %zu, ",
+                 b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
+                 b.grp1.size());
+        std::string js = std::string(tmp) + b.stats + "}";
+        REQUIRE(js.size() < len, "buffer too small");
+        memcpy(json, js.c_str(), js.size() + 1);
+    });
+}
+
 int octvr_debug_json_number(const char* json, int flags, double* value) {
     return guarded([&] {
         REQUIRE(json && value, "NULL argument");

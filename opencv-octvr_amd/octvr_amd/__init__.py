@@ -101,6 +101,9 @@ _lib.octvr_fastmapper_destroy.restype = None
 # self-test hooks (absent from older builds that OCTVR_HIP_LIB may select for an A/B)
 if hasattr(_lib, "octvr_debug_json_number"):
     _lib.octvr_debug_json_number.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double)]
+if hasattr(_lib, "octvr_debug_tiled_lut_info"):
+    _lib.octvr_debug_tiled_lut_info.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p,
+                                                C.c_size_t]
 if hasattr(_lib, "octvr_debug_fastmapper_audit"):
     _lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
                                                   C.c_int, C.c_char_p, C.c_size_t]
@@ -128,6 +131,18 @@ def debug_project_f64(rig_json, out_w, out_h, input, device=0, where=0):
                                         int(input), int(device), int(where), x.ctypes.data_as(_VP),
                                         y.ctypes.data_as(_VP), f.ctypes.data_as(_VP)))
     return x, y, (f if where == 0 else None)
+
+
+def debug_tiled_lut_info(mt, in_sizes):
+    """The blend = 0 composite's tiled LUT built on the host (octvr_debug_tiled_lut_info; no GPU), with its
+    staged-group coverage check: a dict of items, wide tiles, staged / box pixels, bytes, histograms."""
+    n = len(in_sizes)
+    w = (C.c_int * n)(*[s[0] for s in in_sizes])
+    h = (C.c_int * n)(*[s[1] for s in in_sizes])
+    buf = C.create_string_buffer(4096)
+    _check(_lib.octvr_debug_tiled_lut_info(mt._h, n, w, h, buf, len(buf)))
+    import json as _json
+    return _json.loads(buf.value.decode())
 
 
 def debug_json_number(text, exact=True):

@@ -1,0 +1,56 @@
+"""The blend = 0 composite's tiled LUT on the CPU (no GPU): octvr_debug_tiled_lut_info picks the copy chain's
+winner per output pixel (the last camera whose ROI holds it and whose mask is set — the reference's
+copy-mode chain, modules/octvr/src/mapper.cpp) and builds the tiled LUT exactly as octvr_mapper_create
+does (opencv-octvr_amd/csrc/tiling.cpp build_tiled_lut).  build_tiled_lut REQUIREs that every tap of every
+pixel lies in a staged row-span group of its camera slot ("staging groups"), so a build
+that passes here is one whose stitch_tiled_kernel reads only staged LDS.  The checks below pin the
+round-5 staging numbers DESIGN.md quotes for C2 (boxes 17.37 M pixels, spans 10.06 M)."""
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+
+@pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
+def test_tiled_lut_golden_rigs(product_lib, name):
+    ox = product_lib
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), [z[f"map1_{i}"] for i in range(n)],
+                                       [z[f"map2_{i}"] for i in range(n)], [z[f"mask_{i}"] for i in range(n)])
+    sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
+    info = ox.debug_tiled_lut_info(mt, sizes)
+    assert info["items"] > 0
+    # spans stage at most the bounding boxes, in u16 pixels (2 bytes each)
+    assert 0 < info["staged_px"] <= info["box_px"]
+    assert info["staged_bytes"] == 2 * info["staged_px"]
+    assert sum(info["items_by_chunks"].values()) == info["items"]
+    assert sum(info["items_by_lds_kib"]) == info["items"]
+
+
+def test_tiled_lut_rejects_short_sizes(product_lib):
+    ox = product_lib
+    rig, z = O.load_rig("rigA")
+    mt = ox.MapperTemplate.from_arrays(512, 256, z["rois"].tolist(), [z["map1_0"], z["map1_1"]],
+                                       [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]])
+    with pytest.raises(ox.OctvrError):
+        ox.debug_tiled_lut_info(mt, [(64, 64)])
+
+
+def test_tiled_lut_c2(product_lib):
+    """The C2 bench workload (6 x 3840x2160 fisheyes -> 7680x3840 with ROIs)."""
+    ox = product_lib
+    from octvr_amd import synthetic
+    rig, W, H, sizes = synthetic.CONFIGS["C2"]()
+    luts = O.lut_build(rig, W, H, use_roi=True, threads=8)
+    mt = ox.MapperTemplate.from_arrays(W, H, [l[0] for l in luts], [l[1] for l in luts], [l[2] for l in luts],
+                                       [l[3] for l in luts])
+    info = ox.debug_tiled_lut_info(mt, sizes)
+    assert info["items"] == (W // 128) * (H // 16)
+    assert info["wide_tiles"] == 0
+    assert info["box_px"] == pytest.approx(17.37e6, rel=0.01)
+    assert info["staged_px"] == pytest.approx(10.06e6, rel=0.01)
+    # every item fits the 16 KiB tile LDS; no item needs more than 4 staging chunks
+    assert info["items_by_lds_kib"][5:] == [0, 0]
+    assert sum(v for k, v in info["items_by_chunks"].items() if int(k) > 4) == 0
