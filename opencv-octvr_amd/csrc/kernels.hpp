@@ -92,6 +92,9 @@ constexpr uint32_t kWtabBytes = 1024u * 8u;
 constexpr int kTileZeroDwords = 4;
 // Staging stores: 2 x 16 bytes per 8-pixel group, so a row stride is a multiple of 4 dwords.
 constexpr int kStageAlignDwords = 4;
+// The tiler pads an item's row stride by up to this many dwords (tiling.cpp: the stride whose tap reads
+// conflict least in the LDS banks)
+constexpr uint32_t kStridePadMax = 28;
 
 struct TileSlot {
     uint16_t cam;
@@ -106,10 +109,11 @@ struct TileHdr {           // one staged item
     uint32_t tile;          // item column | item row << 16 (items of 128 x 8 qpl pixels)
     uint32_t nslots;        // bits 0-7: slots used (0..4); bits 8-15: 64-group staging chunks
     uint32_t stage_groups;  // 4-pixel groups to convert into LDS (host; the device word: TiledLutDev::upload)
-    uint32_t stride;        // bits 0-8: LDS row stride in dwords (max box width of the item); bits 9-31:
+    uint32_t stride;        // bits 0-8: LDS row stride in dwords (max box width of the item + a bank pad); bits 9-31:
                             // the item's first chunk in the group overflow table (TiledLut::grp1)
 };
 constexpr int kStrideBits = 9;
+static_assert(256 + kStridePadMax < (1u << kStrideBits), "a padded stride fits its field");
 // Staging groups: an item stages, per slot and box row, only the 8-pixel groups between the row's leftmost
 // and rightmost tap (the box layout in LDS is kept: the entries' tap offsets do not change).  One u16 per
 // group: bit 15 valid, bits 8-12 the group's column in the box (x = bx0 + 8 col), bits 0-7 its row.  A

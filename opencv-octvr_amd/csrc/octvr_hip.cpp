@@ -1872,11 +1872,82 @@ int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in
         for (int t = 0; t < b.n_items; t++)
             for (int j = 0; j < (int)(b.hdr[t].nslots & 0xFFu); j++)
                 box_px += (double)b.slots[(size_t)t * kTileSlots + j].bw * b.slots[(size_t)t * kTileSlots + j].bh;
-        char tmp[512];
+        // LDS bank model of the composite's reads and staging stores (MI355X_MICROARCH.md §LDS): per
+        // wave-instruction and lane group, the busiest bank's distinct dword addresses; "extra" = the cycles
+        // above one per group, as SQ_LDS_BANK_CONFLICT counts them.  Taps: two ds_read2_b32 per pixel (each
+        // dword as a ds_read_b32: 2 x 32 lanes, bank (a/4) mod 32); weights: ds_read_b64 (2 x 32, mod 64);
+        // staging: two ds_write_b128 per group (8 x 8 lanes, mod 32).
+        double tap_cyc = 0, tap_extra = 0, wt_cyc = 0, wt_extra = 0, st_cyc = 0, st_extra = 0;
+        {
+            const int item_px = kTilePx * qpl;
+            auto group_cost = [](const uint32_t* a, int n, int lanes, int banks, double& cyc, double& extra) {
+                // a: n dword addresses per lane, lanes lanes in the group
+                uint32_t seen[64][16];
+                int cnt[64] = {};
+                int mx = 0;
+                for (int l = 0; l < lanes; l++)
+                    for (int i = 0; i < n; i++) {
+                        const uint32_t d = a[l * n + i], bk = d % (uint32_t)banks;
+                        bool dup = false;
+                        for (int k = 0; k < cnt[bk]; k++) dup |= seen[bk][k] == d;
+                        if (!dup && cnt[bk] < 16) seen[bk][cnt[bk]++] = d;
+                        mx = std::max(mx, cnt[bk]);
+                    }
+                cyc += std::max(mx, 1);
+                extra += std::max(mx, 1) - 1;
+            };
+            uint32_t a[64 * 4];
+            for (int t = 0; t < b.n_items; t++) {
+                const TileHdr& hd = b.hdr[t];
+                const uint32_t S = hd.stride & ((1u << kStrideBits) - 1u);
+                const uint32_t* E = b.entries.data() + (size_t)t * item_px;
+                for (int h = 0; h < qpl; h++)
+                    for (int w = 0; w < 4; w++)
+                        for (int p = 0; p < 4; p++) {
+                            for (int half = 0; half < 2; half++) {
+                                const uint32_t* e = E + (size_t)h * kTilePx + (size_t)(w * 64 + half * 32) * 4 + p;
+                                for (int r = 0; r < 2; r++)
+                                    for (int c = 0; c < 2; c++) {
+                                        for (int l = 0; l < 32; l++) a[l] = ((e[l * 4] >> 13) & 0x3FFFu) / 4u + r * S + c;
+                                        group_cost(a, 1, 32, 32, tap_cyc, tap_extra);
+                                    }
+                                for (int l = 0; l < 32; l++) {
+                                    const uint32_t d = (0x4000u | (e[l * 4] & 0x1FF8u)) / 4u;
+                                    a[2 * l] = d;
+                                    a[2 * l + 1] = d + 1;
+                                }
+                                group_cost(a, 2, 32, 64, wt_cyc, wt_extra);
+                            }
+                        }
+                const int ns = (int)(hd.nslots & 0xFFu), nch = (int)((hd.nslots >> 8) & 0xFFu);
+                const TileSlot* ts = b.slots.data() + (size_t)t * kTileSlots;
+                for (int c = 0; c < nch; c++) {
+                    int j = 0;
+                    for (int k = 1; k < ns; k++)
+                        if (c >= (int)ts[k].chunk0) j = k;
+                    const uint16_t* G = c < kGroupFirst ? b.grp0.data() + ((size_t)t * kGroupFirst + c) * 64
+                                                        : b.grp1.data() + ((size_t)(hd.stride >> kStrideBits) + c - kGroupFirst) * 64;
+                    for (int sgi = 0; sgi < 2; sgi++)  // the two 16-byte stores of a group
+                        for (int grp = 0; grp < 8; grp++) {
+                            int n = 0;
+                            for (int l = grp * 8; l < grp * 8 + 8; l++) {
+                                if (!(G[l] & kGroupValid)) continue;
+                                const uint32_t d = ts[j].lds + (G[l] & 255u) * S + ((G[l] >> 8) & 31u) * 8u + 4u * sgi;
+                                for (int i = 0; i < 4; i++) a[n * 4 + i] = d + i;
+                                n++;
+                            }
+                            if (n) group_cost(a, 4, n, 32, st_cyc, st_extra);
+                        }
+                }
+            }
+        }
+        char tmp[1024];
         snprintf(tmp, sizeof tmp,
-                 "{\"items\": %d, \"wide_tiles\": %d, \"staged_px\": %.0f, \"box_px\": %.0f, \"staged_bytes\": %.0f, "
+                 "{\"lds_model\": {\"tap_cycles\": %.0f, \"tap_extra\": %.0f, \"wtab_cycles\": %.0f, "
+                 "\"wtab_extra\": %.0f, \"stage_cycles\": %.0f, \"stage_extra\": %.0f}, "
+                 "\"items\": %d, \"wide_tiles\": %d, \"staged_px\": %.0f, \"box_px\": %.0f, \"staged_bytes\": %.0f, "
                  "\"source_bytes\": %.0f, \"grp1_entries\": %zu, ",
-                 b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
+                 tap_cyc, tap_extra, wt_cyc, wt_extra, st_cyc, st_extra, b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
                  b.grp1.size());
         std::string js = std::string(tmp) + b.stats + "}";
         REQUIRE(js.size() < len, "buffer too small");

@@ -163,6 +163,62 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                             "tiled LUT: a tap outside the staged groups (internal error)");
                 }
             }
+            // Row stride of the staged boxes: the widest box, padded by 0-28 dwords to the value whose tap
+            // reads conflict least in the LDS banks.  A tap read is a ds_read_b32 per dword (bank (a/4) mod 32,
+            // lanes 0-31 and 32-63 one group each, MI355X_MICROARCH.md §LDS); a group's 32 lanes are 32 quads
+            // of one quad row, whose taps lie on a curved strip across one or two box rows, so rows r and
+            // r + 1 collide when the stride aliases the strip's spread onto the same banks.
+            if (!wide && ns > 0) {
+                uint32_t bh_sum = 0;
+                for (int j = 0; j < ns; j++) bh_sum += (uint32_t)bhs[j];
+                uint32_t lo[kTileSlots];
+                auto cycles = [&](uint32_t S) {
+                    uint32_t base = kTileZeroDwords;
+                    for (int j = 0; j < ns; j++) {
+                        lo[j] = base;
+                        base += S * (uint32_t)bhs[j];
+                    }
+                    uint64_t cyc = 0;
+                    uint32_t a[32];
+                    for (int h = 0; h < qpl; h++)
+                        for (int q0 = 0; q0 < 256; q0 += 32)
+                            for (int p = 0; p < 4; p++) {
+                                for (int l = 0; l < 32; l++) {
+                                    const Px& x = px[(size_t)h * kTilePx + (size_t)(q0 + l) * 4 + p];
+                                    const TileSlot& sl = ts[x.slot];
+                                    a[l] = x.mask ? lo[x.slot] + (uint32_t)(x.y0 - sl.by0) * S + (uint32_t)(x.x0 - sl.bx0) : 0u;
+                                }
+                                for (int r = 0; r < 2; r++)
+                                    for (int c = 0; c < 2; c++) {
+                                        uint8_t cnt[32] = {};
+                                        uint32_t seen[32][4];
+                                        int mx = 1;
+                                        for (int l = 0; l < 32; l++) {
+                                            const uint32_t d = a[l] + (uint32_t)r * S + (uint32_t)c, bk = d & 31u;
+                                            bool dup = false;
+                                            for (int k = 0; k < std::min<int>(cnt[bk], 4); k++) dup |= seen[bk][k] == d;
+                                            if (dup) continue;
+                                            if (cnt[bk] < 4) seen[bk][cnt[bk]] = d;
+                                            mx = std::max(mx, (int)++cnt[bk]);
+                                        }
+                                        cyc += (uint64_t)mx;
+                                    }
+                            }
+                    return cyc;
+                };
+                uint32_t best = stride;
+                uint64_t best_cyc = UINT64_MAX;
+                for (uint32_t pad = 0; pad <= kStridePadMax; pad += kStageAlignDwords) {
+                    const uint32_t S = stride + pad;
+                    if ((kTileZeroDwords + S * bh_sum) * 4 > (uint32_t)kTileLdsBytes && pad > 0) break;
+                    const uint64_t c = cycles(S);
+                    if (c < best_cyc) {
+                        best_cyc = c;
+                        best = S;
+                    }
+                }
+                stride = best;
+            }
             uint32_t lds = kTileZeroDwords;
             for (int j = 0; j < ns && !wide; j++) {
                 ts[j].lds = (uint16_t)std::min<uint32_t>(lds, 65535u);
