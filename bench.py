@@ -175,10 +175,11 @@ def pmc_valu_busy(config):
     return None
 
 
-def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
-    """AsyncMultiMapper end to end (async.cpp:32-193): host YUV420P planes pushed, copied into pinned
-    staging, uploaded, stitched, downloaded and copied out, 3 frames in flight (the reference's
-    BUF_SIZE, async.cpp:261-310).  PCIe-inclusive: reported beside `value`, never as it."""
+def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24, footprint_bytes=None):
+    """AsyncMultiMapper end to end (async.cpp:32-193): host YUV420P planes pushed, the bytes the mapper
+    reads (its source footprint) copied into pinned staging and uploaded, stitched, downloaded and copied
+    out, 3 frames in flight (the reference's BUF_SIZE, async.cpp:261-310).  PCIe-inclusive: reported
+    beside `value`, never as it."""
     import numpy as np
     am = ox.AsyncMultiMapper([mt], sizes, (W, H), [blend], [0], [(0.0, 0.0, 1.0, 1.0)], device=dev)
     ins = [(f[:h], f[h:, :w // 2], f[h:, w // 2:]) for f, (w, h) in zip(frames_np, sizes)]
@@ -200,9 +201,11 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24):
     am.close()
     in_b = sum(w * h * 3 // 2 for w, h in sizes)
     return {"value": round(frames * W * H / 1e6 / dt, 1), "unit": "MP/s", "ms_per_frame": round(dt * 1e3 / frames, 3),
-            "frames": frames, "h2d_bytes_per_frame": in_b, "d2h_bytes_per_frame": W * H * 3 // 2,
-            "note": "AsyncMultiMapper push->pop of host YUV420P planes: copy-in to pinned staging, H2D, stitch, "
-                    "D2H, copy-out, 3 frames in flight; PCIe- and host-copy-inclusive, not the roofline basis"}
+            "frames": frames, "input_bytes_per_frame": in_b,
+            "h2d_bytes_per_frame": int(footprint_bytes) if footprint_bytes else in_b, "d2h_bytes_per_frame": W * H * 3 // 2,
+            "note": "AsyncMultiMapper push->pop of host YUV420P planes: copy-in of the mapper's source footprint to "
+                    "pinned staging, H2D, unpack, stitch, D2H, copy-out, 3 frames in flight; PCIe- and "
+                    "host-copy-inclusive, not the roofline basis"}
 
 
 # frames in flight per config, from interleaved sweeps on one box (scripts/r4_inflight_sweep.sh): C2 2 / 3 / 4 =
@@ -601,7 +604,8 @@ def gpu_rank(args, world, rank, local_rank, dist):
         "mapper": m.info(),
     }
     if rank == 0 and world == 1 and not args.no_async_e2e:
-        result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev)
+        result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev,
+                                        footprint_bytes=result["mapper"].get("footprint_bytes"))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend, gain=use_gain)
     return result

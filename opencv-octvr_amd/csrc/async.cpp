@@ -11,8 +11,11 @@
 //     threads loop forever and its destructor clears joinable std::threads, async.cpp:87-90,337-349);
 //   * a failing frame carries its status to pop() instead of asserting;
 //   * the two host-copy stages split their rows over a few helper threads (RowPool): one thread's
-//     memcpy from pageable memory (~15 GB/s) otherwise bounds the whole pipeline (C2: 75 MB in per
-//     frame, scripts/async_trace.py).
+//     memcpy from pageable memory (~15 GB/s) otherwise bounds the whole pipeline (scripts/async_trace.py);
+//   * only the input bytes some kernel of some mapper reads are copied and uploaded (the union of the
+//     mappers' source footprints, host_common.hpp SourceFootprint), packed, and put in place on the
+//     device by one kernel: with the copy chain each output pixel comes from one camera, so a C2 frame
+//     needs ~10 MB of its 75 MB of YUV.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -94,10 +97,44 @@ struct PinnedBuf {
     }
 };
 
-struct Slot {  // one frame's staging buffers ("Y over [U|V]" YUV420P, packed rows)
-    std::vector<std::unique_ptr<PinnedBuf>> in_host, out_host;
+struct Slot {  // one frame's buffers: the packed footprint runs, the device frames ("Y over [U|V]", pitch = width)
+    std::unique_ptr<PinnedBuf> packed_host;
+    DevBuf<uint8_t> packed_dev;
+    std::vector<std::unique_ptr<PinnedBuf>> out_host;
     std::vector<DevBuf<uint8_t>> in_dev, out_dev;
+    FootFrames frames{};
 };
+
+// Runs of the union of the mappers' footprints: per camera and row pair, consecutive set groups, gaps of
+// up to kRunGap groups bridged (a few more bytes for fewer, longer copies)
+constexpr int kRunGap = 2;
+std::vector<FootRun> footprint_runs(const SourceFootprint& f, size_t& bytes) {
+    std::vector<FootRun> runs;
+    bytes = 0;
+    for (int i = 0; i < (int)f.w.size(); i++)
+        for (int r = 0; r < f.row_pairs(i); r++) {
+            int g = 0;
+            const int G = f.groups(i);
+            while (g < G) {
+                if (!f.test(i, r, g)) {
+                    g++;
+                    continue;
+                }
+                int e = g + 1, last = g;  // last set group of the run
+                while (e < G && e - last <= kRunGap + 1) {
+                    if (f.test(i, r, e)) last = e;
+                    e++;
+                }
+                const int ng = last - g + 1;
+                const int yb = std::min(8 * (g + ng), f.w[i]) - 8 * g;
+                const int cb = std::max(0, std::min(4 * (g + ng), f.w[i] / 2) - 4 * g);
+                runs.push_back(FootRun{(uint32_t)i | (uint32_t)r << 8, (uint32_t)g, (uint32_t)ng, (uint32_t)bytes});
+                bytes += (size_t)(2 * yb + 2 * cb);
+                g = last + 1;
+            }
+        }
+    return runs;
+}
 
 struct Job {
     std::vector<const uint8_t*> in_planes;
@@ -199,6 +236,9 @@ struct octvr_async {
     std::vector<octvr_mapper*> mappers;
     std::vector<int> gain_modes;
     std::vector<Rect> regions, regions_uv;  // per mapper: its rectangle in the Y and in the U / V planes
+    std::vector<FootRun> runs;  // what the mappers read of the inputs (footprint_runs)
+    size_t packed_bytes = 0;
+    DevBuf<FootRun> runs_dev;
     Slot slots[kSlots];
     hipStream_t up = nullptr, comp = nullptr, down = nullptr;
     Channel<std::shared_ptr<Job>> q_in, q_up, q_map, q_down, q_out, q_done;
@@ -219,48 +259,49 @@ struct octvr_async {
         for (auto& sl : slots) {
             sl.in_dev.clear();
             sl.out_dev.clear();
-            sl.in_host.clear();
+            sl.packed_dev.reset();
+            sl.packed_host.reset();
             sl.out_host.clear();
         }
         for (auto* m : mappers) octvr_mapper_destroy(m);
         if (prev >= 0) (void)hipSetDevice(prev);
     }
 
-    // run_copy_inputs_mat_to_hostmem (async.cpp:32-56)
+    // run_copy_inputs_mat_to_hostmem (async.cpp:32-56), restricted to the mappers' source footprint: the
+    // rows and columns no kernel of any mapper reads are neither copied nor uploaded
     void copy_in(Job& j) {
         int s = -1;
         if (!free_slots.pop(s)) throw OctvrError(OCTVR_E_INVALID, "pipeline closed");
         j.slot = s;
         stage(j, [&] {
-            for (int i = 0; i < n_in; i++) {
-                const int w = in_w[i], h = in_h[i];
-                uint8_t* dst = slots[s].in_host[i]->p;
-                const uint8_t *Y = j.in_planes[3 * i], *U = j.in_planes[3 * i + 1], *V = j.in_planes[3 * i + 2];
-                const size_t py = j.in_pitches[3 * i], pu = j.in_pitches[3 * i + 1], pv = j.in_pitches[3 * i + 2];
-                // rows 0..h-1: Y; h..h+h/2-1: U | V side by side
-                copy_in_pool.run((size_t)(h + h / 2), [&](size_t lo, size_t hi) {
-                    for (size_t y = lo; y < hi; y++) {
-                        uint8_t* row = dst + y * (size_t)w;
-                        if (y < (size_t)h) {
-                            memcpy(row, Y + y * py, w);
-                        } else {
-                            const size_t c = y - (size_t)h;
-                            memcpy(row, U + c * pu, w / 2);
-                            memcpy(row + w / 2, V + c * pv, w / 2);
-                        }
-                    }
-                });
-            }
+            uint8_t* const dst = slots[s].packed_host->p;
+            copy_in_pool.run(runs.size(), [&](size_t lo, size_t hi) {
+                for (size_t k = lo; k < hi; k++) {
+                    const FootRun& r = runs[k];
+                    const int i = (int)(r.cam & 31u), rp = (int)(r.cam >> 8), w = in_w[i];
+                    const int x0 = 8 * (int)r.g0, yb = std::min(8 * (int)(r.g0 + r.ng), w) - x0;
+                    const int c0 = 4 * (int)r.g0, cb = std::max(0, std::min(4 * (int)(r.g0 + r.ng), w / 2) - c0);
+                    const size_t py = j.in_pitches[3 * i], pu = j.in_pitches[3 * i + 1], pv = j.in_pitches[3 * i + 2];
+                    uint8_t* d = dst + r.off;
+                    memcpy(d, j.in_planes[3 * i] + (size_t)(2 * rp) * py + x0, yb);
+                    memcpy(d + yb, j.in_planes[3 * i] + (size_t)(2 * rp + 1) * py + x0, yb);
+                    memcpy(d + 2 * yb, j.in_planes[3 * i + 1] + (size_t)rp * pu + c0, cb);
+                    memcpy(d + 2 * yb + cb, j.in_planes[3 * i + 2] + (size_t)rp * pv + c0, cb);
+                }
+            });
         });
     }
 
-    // run_upload_inputs_hostmem_to_gpumat (async.cpp:58-68)
+    // run_upload_inputs_hostmem_to_gpumat (async.cpp:58-68): the packed runs, then one kernel puts them in
+    // place in the device frames (bytes outside the footprint keep whatever they held: nothing reads them)
     void upload(Job& j) {
         stage(j, [&] {
             DeviceGuard dg(device);
             Slot& sl = slots[j.slot];
-            for (int i = 0; i < n_in; i++)
-                HIP_CHECK(hipMemcpyAsync(sl.in_dev[i].p, sl.in_host[i]->p, sl.in_host[i]->n, hipMemcpyHostToDevice, up));
+            if (packed_bytes) {
+                HIP_CHECK(hipMemcpyAsync(sl.packed_dev.p, sl.packed_host->p, packed_bytes, hipMemcpyHostToDevice, up));
+                HIP_CHECK(launch_unpack_runs(sl.packed_dev.p, runs_dev.p, (int)runs.size(), sl.frames, up));
+            }
             HIP_CHECK(hipStreamSynchronize(up));
         });
     }
@@ -371,7 +412,7 @@ int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int
     try {
         REQUIRE(rigs && n_rigs > 0 && in_w && in_h && blend_modes && gain_modes && output_regions && out,
                 "NULL argument");
-        REQUIRE(n_inputs > 0 && out_w > 0 && out_h > 0 && out_w % 2 == 0 && out_h % 2 == 0, "bad sizes");
+        REQUIRE(n_inputs > 0 && n_inputs <= kMaxCams && out_w > 0 && out_h > 0 && out_w % 2 == 0 && out_h % 2 == 0, "bad sizes");
         auto a = std::make_unique<octvr_async>();
         a->device = device;
         a->n_in = n_inputs;
@@ -405,13 +446,26 @@ int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int
         HIP_CHECK(hipStreamCreateWithFlags(&a->up, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&a->comp, hipStreamNonBlocking));
         HIP_CHECK(hipStreamCreateWithFlags(&a->down, hipStreamNonBlocking));
+        // what the mappers read of the inputs: one packed upload of those bytes per frame
+        SourceFootprint foot;
+        foot.init(a->in_w, a->in_h);
+        for (auto* m : a->mappers) foot.merge(mapper_footprint(m));
+        a->runs = footprint_runs(foot, a->packed_bytes);
+        REQUIRE(a->packed_bytes < ((size_t)1 << 32), "input footprint exceeds 4 GiB");
+        if (!a->runs.empty()) a->runs_dev.upload(a->runs.data(), a->runs.size());
         for (auto& sl : a->slots) {
+            sl.packed_host.reset(new PinnedBuf());
+            sl.packed_host->alloc(std::max<size_t>(a->packed_bytes, 1));
+            sl.packed_dev.alloc(std::max<size_t>(a->packed_bytes, 1));
             for (int i = 0; i < n_inputs; i++) {
                 const size_t bytes = (size_t)in_w[i] * (in_h[i] / 2 * 3);
-                sl.in_host.emplace_back(new PinnedBuf());
-                sl.in_host.back()->alloc(bytes);
                 sl.in_dev.emplace_back();
                 sl.in_dev.back().alloc(bytes);
+                // bytes outside the footprint are never read; a fixed pattern rather than stale memory
+                HIP_CHECK(hipMemset(sl.in_dev.back().p, 0x5A, bytes));
+                sl.frames.f[i] = sl.in_dev.back().p;
+                sl.frames.w[i] = in_w[i];
+                sl.frames.h[i] = in_h[i];
             }
             for (int k = 0; k < n_rigs; k++) {
                 const size_t bytes = (size_t)a->regions[k].w * (a->regions[k].h / 2 * 3);

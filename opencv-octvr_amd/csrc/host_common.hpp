@@ -197,6 +197,29 @@ struct TiledLutDev {
     void upload(const TiledLutBuild& b);
 };
 
+// ---- source footprint: the input bytes a mapper's kernels may read (tiling.cpp) ------------------------
+// Per camera one bit per (luma row pair r, 8-pixel group g): luma rows 2r, 2r + 1 x columns [8g, 8g + 8)
+// and chroma row r x columns [4g, 4g + 4) of U and V.  Built with the mapper from what drives its source
+// reads: every staged group of its tiled LUTs (stitch_tiled_kernel's staging loads), the in-image taps of
+// every wide-tile entry (stitch_wide_kernel) and gain sample (the gain feed).  Loads outside it are only
+// the clamped addresses of out-of-image taps and invalid staging groups, whose bytes no result uses.  The
+// AsyncMultiMapper uploads only these bytes (async.cpp).
+struct SourceFootprint {
+    std::vector<int> w, h;
+    std::vector<std::vector<uint64_t>> bits;  // per camera: row_pairs x words
+    void init(const std::vector<int>& in_w, const std::vector<int>& in_h);
+    int groups(int i) const { return (w[i] + 7) / 8; }
+    int words(int i) const { return (groups(i) + 63) / 64; }
+    int row_pairs(int i) const { return (h[i] + 1) / 2; }
+    bool test(int cam, int r, int g) const { return (bits[cam][(size_t)r * words(cam) + g / 64] >> (g % 64)) & 1u; }
+    void mark(int cam, int y, int g) { bits[cam][(size_t)(y >> 1) * words(cam) + g / 64] |= 1ull << (g % 64); }
+    void mark_taps(const CompositeEntry& e);  // the in-image taps of a valid entry
+    void merge(const SourceFootprint& o);
+    double bytes() const;  // YUV420P bytes under the set bits
+};
+void footprint_add_tiles(SourceFootprint& f, const TiledLutBuild& b);
+const SourceFootprint& mapper_footprint(const octvr_mapper* m);
+
 // ---- multi-band blend (multiband_host.cpp) ---------------------------------------------------------
 class MultiBand;
 struct MultiBandDeleter {
@@ -206,8 +229,9 @@ struct MultiBandDeleter {
 // pyramid buffers) on `device`.  in_w / in_h: input frame sizes.
 // feather_border > 0 instead builds FeatherGPUBlender(masks, rois, border) (blenders.cpp:531-586):
 // a single level whose weights are the normalised feather weights.
+// foot: when given, the remap's source reads are added to it.
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
-                            const std::vector<int>& in_h, int feather_border = 0);
+                            const std::vector<int>& in_h, int feather_border = 0, SourceFootprint* foot = nullptr);
 // One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P
 // (or, with `rgba`, the RGB result as RGBA for a scaled output).
 // slot: frame slot (0 = the buffers built with the rig, 1..k-1 after multiband_set_slots(k)).

@@ -663,6 +663,34 @@ hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, 
     return hipGetLastError();
 }
 
+// One workgroup per footprint run: its packed bytes into the camera's frame (byte stores of consecutive
+// lanes: whole-line writes per wave).
+__global__ void __launch_bounds__(256) unpack_runs_kernel(const uint8_t* packed, const FootRun* runs, FootFrames fr) {
+    const FootRun r = runs[blockIdx.x];
+    const int cam = (int)(r.cam & 31u), rp = (int)(r.cam >> 8);
+    const int w = fr.w[cam], h = fr.h[cam];
+    const int x0 = 8 * (int)r.g0, yb = min(8 * (int)(r.g0 + r.ng), w) - x0;
+    const int c0 = 4 * (int)r.g0, cb = max(0, min(4 * (int)(r.g0 + r.ng), w / 2) - c0);
+    const uint8_t* src = packed + r.off;
+    uint8_t* const f = fr.f[cam];
+    uint8_t* const d0 = f + (size_t)(2 * rp) * (size_t)w + x0;
+    uint8_t* const d1 = d0 + w;
+    uint8_t* const du = f + (size_t)(h + rp) * (size_t)w + c0;
+    uint8_t* const dv = du + w / 2;
+    const int tot = 2 * yb + 2 * cb;
+    for (int k = threadIdx.x; k < tot; k += 256) {
+        uint8_t* d = k < yb ? d0 + k : k < 2 * yb ? d1 + (k - yb) : k < 2 * yb + cb ? du + (k - 2 * yb) : dv + (k - 2 * yb - cb);
+        *d = src[k];
+    }
+}
+
+hipError_t launch_unpack_runs(const uint8_t* packed, const FootRun* runs, int n_runs, const FootFrames& frames,
+                              hipStream_t s) {
+    if (n_runs <= 0) return hipSuccess;
+    hipLaunchKernelGGL(unpack_runs_kernel, dim3(n_runs), dim3(256), 0, s, packed, runs, frames);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------------------
 // Per-frame stitch, blend = 0 (mapper.cpp:219-306 with the copy chain resolved into the tiled LUT):
 // for every 2x2 output quad the winning camera of each pixel is sampled (15-bit bilinear on the

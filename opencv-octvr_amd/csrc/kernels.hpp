@@ -195,6 +195,21 @@ hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* sample
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 
+// AsyncMultiMapper footprint upload (async.cpp): a run is `ng` consecutive 8-pixel groups from group g0 of
+// row pair r of camera `cam` (host_common.hpp SourceFootprint), packed at `off` as luma row 2r, luma row
+// 2r + 1, then its chroma row of U and of V; the frames are "Y over [U | V]" with pitch = width.
+struct FootRun {
+    uint32_t cam;  // camera | row pair << 8
+    uint32_t g0, ng;
+    uint32_t off;
+};
+struct FootFrames {
+    uint8_t* f[kMaxCams];
+    int w[kMaxCams], h[kMaxCams];
+};
+hipError_t launch_unpack_runs(const uint8_t* packed, const FootRun* runs, int n_runs, const FootFrames& frames,
+                              hipStream_t s);
+
 struct TiledLut {
     const TileHdr* meta;          // per staged item kMetaWords 16-byte words: the TileHdr, then kTileSlots TileSlots
     const uint32_t* entries;      // kTilePx per staged item, quad-major inside the tile

@@ -218,7 +218,7 @@ struct Bitmap {
 }  // namespace
 
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
-                            const std::vector<int>& in_h, int feather_border) {
+                            const std::vector<int>& in_h, int feather_border, SourceFootprint* foot) {
     auto mb = std::unique_ptr<MultiBand>(new MultiBand);
     MultiBand& M = *mb;
     const int n = (int)rig.inputs.size();
@@ -830,6 +830,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             return e;
         };
         TiledLutBuild tb = build_tiled_lut(jobs, entry, in_w, in_h, qpl);
+        if (foot) footprint_add_tiles(*foot, tb);
         M.remap.upload(tb);
     }
     return mb.release();

@@ -876,6 +876,7 @@ struct octvr_mapper {
     size_t n_entries = 0;
     std::vector<double> last_gains;
     std::vector<DevBuf<float>> vig;  // per camera: vignette map resized to the input size, or empty
+    SourceFootprint foot;            // the input bytes this mapper's kernels read (host_common.hpp)
     // scaled output (scaled_output_size != stitch size, mapper.cpp:69,153-155,290-306): the RGB result
     // as an RGBA frame, resized + converted to YUV420P by a second kernel
     int SW = 0, SH = 0;
@@ -1056,6 +1057,7 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
         pmask.push_back(0);
     }
     n_chunks = (int)(uniq.size() / kGainChunk);
+    for (const CompositeEntry& e : uniq) m.foot.mark_taps(e);
     m.samples.upload(uniq.data(), uniq.size());
     m.partners.upload(pmask.data(), pmask.size());
     // exactness bound of the fixed-point totals (kernels.hip, gain feed): < 2^21 samples per camera
@@ -1196,6 +1198,7 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
 int mapper_num_inputs(const octvr_mapper* m) { return m->n; }
 bool mapper_has_gain(const octvr_mapper* m) { return m->use_gain != 0; }
 const double* mapper_gains_dev(const octvr_mapper* m) { return m->slots[m->cur_slot].gains; }
+const SourceFootprint& mapper_footprint(const octvr_mapper* m) { return m->foot; }
 void mapper_out_size(const octvr_mapper* m, int* w, int* h) {
     *w = m->SW;
     *h = m->SH;
@@ -1556,13 +1559,14 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             const std::vector<float> v = resize_linear_f32(in.vignette.data(), in.vig_w, in.vig_h, m->in_w[i], m->in_h[i]);
             m->vig[i].upload(v.data(), v.size());
         }
+        m->foot.init(m->in_w, m->in_h);
         if (m->blend > 0) {
             // MultiBandGPUBlender(seam_masks, rois, bands), bands = ceil(log2(blend)) - 1 (mapper.cpp:171-176)
             const int bands = (int)(std::ceil(std::log((double)m->blend) / std::log(2.)) - 1.);
-            m->mb.reset(multiband_create(*rig, device, bands, m->in_w, m->in_h));
+            m->mb.reset(multiband_create(*rig, device, bands, m->in_w, m->in_h, 0, &m->foot));
         } else if (m->blend < 0) {
             // FeatherGPUBlender(masks, rois, border = -blend) (mapper.cpp:177-182)
-            m->mb.reset(multiband_create(*rig, device, 0, m->in_w, m->in_h, -m->blend));
+            m->mb.reset(multiband_create(*rig, device, 0, m->in_w, m->in_h, -m->blend, &m->foot));
         } else {
             // per-camera templates -> device, composite LUT, then drop the per-camera maps
             std::vector<DevBuf<float>> m1(m->n), m2(m->n);
@@ -1598,9 +1602,11 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             for (int ty = 0; ty < ty_n; ty++)
                 for (int tx = 0; tx < tx_n; tx++) jobs.push_back(TileJob{tx, ty, 0});
             const int W = m->W, H = m->H;
-            m->tiles.upload(build_tiled_lut(jobs, [&](int, int x, int y) {
+            const TiledLutBuild tb = build_tiled_lut(jobs, [&](int, int x, int y) {
                 return (x < W && y < H) ? lut8[(size_t)y * W + x] : CompositeEntry{0u, 0u};
-            }, m->in_w, m->in_h, qpl));
+            }, m->in_w, m->in_h, qpl);
+            footprint_add_tiles(m->foot, tb);
+            m->tiles.upload(tb);
             m->n_tiles = tx_n * ty_n;
         }
         if (m->scaled) ensure_result(*m);
@@ -1805,9 +1811,10 @@ int octvr_mapper_info(const octvr_mapper* m, char* buf, size_t len) {
         snprintf(tmp, sizeof tmp,
                  "{\"inputs\": %d, \"out\": [%d, %d], \"blend\": %d, \"tiles\": %d, \"wide_tiles\": %d, "
                  "\"staged_bytes\": %.0f, \"source_bytes\": %.0f, \"gain\": %d, \"gain_samples\": %d, \"gain_pairs_px\": %zu, "
-                 "\"gain_chunks\": %d, \"scaled_out\": [%d, %d]",
+                 "\"gain_chunks\": %d, \"scaled_out\": [%d, %d], \"footprint_bytes\": %.0f",
                  m->n, m->W, m->H, m->blend, m->n_tiles, m->tiles.view.n_wide,
-                 m->mb ? 0.0 : m->tiles.staged_bytes, m->mb ? 0.0 : m->tiles.source_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks, m->SW, m->SH);
+                 m->mb ? 0.0 : m->tiles.staged_bytes, m->mb ? 0.0 : m->tiles.source_bytes, m->use_gain, m->n_samples, m->n_entries, m->n_chunks, m->SW, m->SH,
+                 m->foot.bytes());
         std::string js = tmp;
         if (m->mb) js += ", " + multiband_info(*m->mb);
         else if (!m->tiles.stats.empty()) js += ", " + m->tiles.stats;
@@ -1941,13 +1948,20 @@ int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in
                 }
             }
         }
+        // the composite's source footprint (what the AsyncMultiMapper uploads, gain samples aside)
+        SourceFootprint fp;
+        fp.init(std::vector<int>(in_w, in_w + n), std::vector<int>(in_h, in_h + n));
+        footprint_add_tiles(fp, b);
+        const double foot = fp.bytes();
+        double frame_bytes = 0;
+        for (int i = 0; i < n; i++) frame_bytes += 1.5 * in_w[i] * in_h[i];
         char tmp[1024];
         snprintf(tmp, sizeof tmp,
-                 "{\"lds_model\": {\"tap_cycles\": %.0f, \"tap_extra\": %.0f, \"wtab_cycles\": %.0f, "
+                 "{\"footprint_bytes\": %.0f, \"frame_bytes\": %.0f, \"lds_model\": {\"tap_cycles\": %.0f, \"tap_extra\": %.0f, \"wtab_cycles\": %.0f, "
                  "\"wtab_extra\": %.0f, \"stage_cycles\": %.0f, \"stage_extra\": %.0f}, "
                  "\"items\": %d, \"wide_tiles\": %d, \"staged_px\": %.0f, \"box_px\": %.0f, \"staged_bytes\": %.0f, "
                  "\"source_bytes\": %.0f, \"grp1_entries\": %zu, ",
-                 tap_cyc, tap_extra, wt_cyc, wt_extra, st_cyc, st_extra, b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
+                 foot, frame_bytes, tap_cyc, tap_extra, wt_cyc, wt_extra, st_cyc, st_extra, b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
                  b.grp1.size());
         std::string js = std::string(tmp) + b.stats + "}";
         REQUIRE(js.size() < len, "buffer too small");

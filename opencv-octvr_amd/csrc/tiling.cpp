@@ -437,4 +437,62 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
                     b.qpl, grp0.p, grp1.p, (uint32_t)b.grp1.size()};
 }
 
+void SourceFootprint::init(const std::vector<int>& in_w, const std::vector<int>& in_h) {
+    w = in_w;
+    h = in_h;
+    bits.assign(w.size(), {});
+    for (size_t i = 0; i < w.size(); i++) bits[i].assign((size_t)row_pairs((int)i) * words((int)i), 0ull);
+}
+
+void SourceFootprint::mark_taps(const CompositeEntry& e) {
+    if (!(e.code & 0x8000u)) return;
+    const int cam = (int)((e.code >> 10) & 31u);
+    if (cam >= (int)w.size()) return;
+    const TapCell c = tap_cell(e.xy, w[cam], h[cam]);
+    if (c.iy0 && c.ix0) mark(cam, c.y0, c.x0 >> 3);
+    if (c.iy0 && c.ix1) mark(cam, c.y0, c.x1 >> 3);
+    if (c.iy1 && c.ix0) mark(cam, c.y1, c.x0 >> 3);
+    if (c.iy1 && c.ix1) mark(cam, c.y1, c.x1 >> 3);
+}
+
+void SourceFootprint::merge(const SourceFootprint& o) {
+    REQUIRE(o.w == w && o.h == h, "footprints of different input sizes");
+    for (size_t i = 0; i < bits.size(); i++)
+        for (size_t k = 0; k < bits[i].size(); k++) bits[i][k] |= o.bits[i][k];
+}
+
+double SourceFootprint::bytes() const {
+    double n = 0;
+    for (int i = 0; i < (int)w.size(); i++)
+        for (int r = 0; r < row_pairs(i); r++)
+            for (int g = 0; g < groups(i); g++) {
+                if (!test(i, r, g)) continue;
+                const int yb = std::min(8, w[i] - 8 * g), cb = std::max(0, std::min(4, w[i] / 2 - 4 * g));
+                n += yb * (2 * r + 1 < h[i] ? 2 : 1) + 2 * cb;
+            }
+    return n;
+}
+
+void footprint_add_tiles(SourceFootprint& f, const TiledLutBuild& b) {
+    for (int t = 0; t < b.n_items; t++) {
+        const TileHdr& hd = b.hdr[t];
+        const int ns = (int)(hd.nslots & 0xFFu), nch = (int)((hd.nslots >> 8) & 0xFFu);
+        const TileSlot* ts = b.slots.data() + (size_t)t * kTileSlots;
+        for (int c = 0; c < nch; c++) {
+            int j = 0;  // the chunk's slot (slots own consecutive chunk ranges from chunk0)
+            for (int k = 1; k < ns; k++)
+                if (c >= (int)ts[k].chunk0) j = k;
+            const uint16_t* G = c < kGroupFirst ? b.grp0.data() + ((size_t)t * kGroupFirst + c) * 64
+                                                : b.grp1.data() + ((size_t)(hd.stride >> kStrideBits) + c - kGroupFirst) * 64;
+            const int cam = ts[j].cam;
+            for (int l = 0; l < 64; l++) {
+                if (!(G[l] & kGroupValid)) continue;
+                const int y = ts[j].by0 + (G[l] & 255), x = ts[j].bx0 + ((G[l] >> 8) & 31) * 8;
+                if (y < f.h[cam] && x < f.w[cam]) f.mark(cam, y, x >> 3);  // else staged as black, unread
+            }
+        }
+    }
+    for (const CompositeEntry& e : b.wide) f.mark_taps(e);
+}
+
 }  // namespace octvr

@@ -109,3 +109,46 @@ def test_gpu_async_rejects_bad_regions(product_lib):
                                        [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]])
     with pytest.raises(ox.OctvrError):  # odd region height
         ox.AsyncMultiMapper([mt], [(256, 144)] * 2, (512, 258), [0], [0], [(0.0, 0.0, 1.0, 0.5)])
+
+
+@pytest.mark.parametrize("name", ["rigC", "rigD", "rigA"])
+def test_gpu_async_footprint_upload(product_lib, name):
+    """Only the input bytes some kernel reads are uploaded (async.cpp footprint runs; the rest of each
+    device frame holds a fixed pattern): rigs with wide tiles (gathered taps), with taps on the image
+    edges, and a two-mapper set with the gain feed and multi-band, every frame bit-exact."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    sizes = [(rig["inputs"][i]["options"]["width"], rig["inputs"][i]["options"]["height"]) for i in range(n)]
+    maps1 = [z[f"map1_{i}"] for i in range(n)]
+    maps2 = [z[f"map2_{i}"] for i in range(n)]
+    masks = [z[f"mask_{i}"] for i in range(n)]
+    seams = [z[f"seam_{i}"] for i in range(n)]
+    blends = [0, 16] if name == "rigA" else [0]
+    mts = [ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks, seams) for _ in blends]
+    info = ox.Mapper(mts[0], sizes, blend=0, enable_gain=True).info()
+    assert 0 < info["footprint_bytes"] <= sum(w * h * 3 // 2 for w, h in sizes)
+    regions = [(0.0, 0.0, 1.0, 1.0)] if len(blends) == 1 else [(0.0, 0.0, 1.0, 0.5), (0.0, 0.5, 1.0, 0.5)]
+    OW, OH = W, H * len(blends)
+    am = ox.AsyncMultiMapper(mts, sizes, (OW, OH), blends, [0] * len(blends), regions)
+    frames, outs = [], []
+    for f in range(4):
+        fr = [synthetic.smooth_yuv_frame(w, h, 900 + 10 * f + i) for i, (w, h) in enumerate(sizes)]
+        out = (np.zeros((OH, OW), np.uint8), np.zeros((OH // 2, OW // 2), np.uint8), np.zeros((OH // 2, OW // 2), np.uint8))
+        am.push([_planes(x, w, h) for x, (w, h) in zip(fr, sizes)], out)
+        frames.append(fr)
+        outs.append(out)
+    for f in range(4):
+        am.pop()
+        for k, bl in enumerate(blends):
+            want, _ = O.stitch_frame(frames[f], sizes, z["rois"].tolist(), maps1, maps2, masks, W, H,
+                                     enable_gain=True, blend=bl, seams=seams, threads=8)
+            y0 = k * H
+            assert np.array_equal(outs[f][0][y0:y0 + H], want[:H]), (f, k, "Y")
+            assert np.array_equal(outs[f][1][y0 // 2:(y0 + H) // 2], want[H:, :W // 2]), (f, k, "U")
+            assert np.array_equal(outs[f][2][y0 // 2:(y0 + H) // 2], want[H:, W // 2:]), (f, k, "V")
+    am.close()
