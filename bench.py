@@ -46,6 +46,8 @@ def parse():
                     help="skip the AsyncMultiMapper end-to-end (PCIe-inclusive) measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-gain", action="store_true", help=argparse.SUPPRESS)  # diagnostic: composite alone
+    ap.add_argument("--remap", default="remap", choices=["remap", "texture"],
+                    help="sampling: cv::remap's fixed point (default) or the CUDA texture convention (OCTVR_REMAP_TEXTURE)")
     return ap.parse_args()
 
 
@@ -422,6 +424,7 @@ def fast_rank(args, world, rank, local_rank, dist):
         "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
                                "template without ROI), NV12 in/out" % (len(sizes), sizes[0][0], sizes[0][1], W, H),
                    "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
+                   **({"remap": "texture (OCTVR_REMAP_TEXTURE)"} if args.remap == "texture" else {}),
                    "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
@@ -456,7 +459,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
     if blend > 0:
         mt.create_masks(dev)  # MapperTemplate::create_masks (DistanceSeamFinder), as octvr_dump does
     use_gain = synthetic.GAIN[args.config] and not args.no_gain
-    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=use_gain, device=dev)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=use_gain, device=dev, remap=args.remap)
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
     inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 3))
@@ -568,6 +571,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
                                    "multi-band blend=%d (%d bands)" % (blend, int(math.ceil(math.log(blend) / math.log(2.)) - 1))
                                    if blend > 0 else "no-blend composite"),
                    "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
+                   **({"remap": "texture (OCTVR_REMAP_TEXTURE)"} if args.remap == "texture" else {}),
                    "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,

@@ -449,9 +449,11 @@ private:
 // vr::Mapper (modules/octvr/src/mapper.hpp:29-95): one rig's per-frame stitch on the GPU.
 class Mapper {
 public:
-    // blend: 0 = do not blend, > 0 = multi-band blend width, < 0 = feather blend width
+    // blend: 0 = do not blend, > 0 = multi-band blend width, < 0 = feather blend width.
+    // flags (not in the reference): OCTVR_REMAP_TEXTURE samples as the reference's CUDA fastRemap does
+    // (octvr_hip.h octvr_mapper_create_ex); 0 = cv::remap's fixed point.
     Mapper(const MapperTemplate& mt, std::vector<cv::Size> in_sizes, int blend = 128,
-           bool enable_gain_compensator = true, cv::Size scale_output = cv::Size(0, 0)) {
+           bool enable_gain_compensator = true, cv::Size scale_output = cv::Size(0, 0), int flags = 0) {
         rig_ = mt.rig();
         std::vector<int> w, h;
         for (const cv::Size& s : in_sizes) {
@@ -460,8 +462,9 @@ public:
         }
         n_ = (int)in_sizes.size();
         octvr_mapper* m = nullptr;
-        detail::check(octvr_mapper_create(rig_.get(), detail::device(), n_, w.data(), h.data(), blend,
-                                          enable_gain_compensator ? 1 : 0, scale_output.width, scale_output.height, &m));
+        detail::check(octvr_mapper_create_ex(rig_.get(), detail::device(), n_, w.data(), h.data(), blend,
+                                             enable_gain_compensator ? 1 : 0, scale_output.width, scale_output.height,
+                                             flags, &m));
         m_ = std::shared_ptr<octvr_mapper>(m, [](octvr_mapper* p) { octvr_mapper_destroy(p); });
         out_ = scale_output.width > 0 ? scale_output : mt.out_size;
         sizes_ = in_sizes;

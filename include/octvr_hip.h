@@ -143,6 +143,17 @@ int octvr_rig_clone(const octvr_rig* rig, octvr_rig** out);
  * scale_w/scale_h: 0 = output at template size, else the output is resized (mapper.cpp:290-306). */
 int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                         int enable_gain, int scale_w, int scale_h, octvr_mapper** mapper);
+/* The same with creation flags (no reference counterpart; 0 = octvr_mapper_create).
+ * OCTVR_REMAP_TEXTURE: sample the camera frames as the reference's live CUDA path does —
+ * cv::cuda::fastRemap through a linear-filtered, clamp-addressed texture (cudawarping/src/cuda/
+ * fast_remap.cu:21-44): x = u W - 0.5, 8-bit fractions, taps clamped to the image, u < 0 -> 0 — instead
+ * of cv::remap's fixed point (imgwarp.cpp; the default, which the CPU and OpenCL paths share).  The
+ * texture filter is NVIDIA hardware behaviour; this mode follows the oracle's model of it
+ * (oracle/octvr_oracle.c orc_fast_remap_tex_rgba) bit for bit, gain samples included.  Every tile takes
+ * the gather path, so the mode is slower than the default.  Other bits: OCTVR_E_INVALID. */
+#define OCTVR_REMAP_TEXTURE 1
+int octvr_mapper_create_ex(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
+                           int enable_gain, int scale_w, int scale_h, int flags, octvr_mapper** mapper);
 /* Mapper::stitch (mapper.cpp:193-323) on device-resident YUV420P frames in the "Y over [U|V]"
  * layout of mapper.hpp:75-83: rows [0,H) = Y (W bytes), rows [H, 3H/2) = U in bytes [0, W/2) and
  * V in bytes [W/2, W) of each row; `pitch` = bytes per row (>= W).  gains: NULL = estimate

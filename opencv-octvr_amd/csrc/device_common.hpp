@@ -194,12 +194,31 @@ __device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t
         cc = vig_mul(cc, g1[x0]);
         cd = vig_mul(cd, g1[x1]);
     }
-    t.c[0] = (valid && tc.ix0 && tc.iy0) ? ca : 0u;
-    t.c[1] = (valid && tc.ix1 && tc.iy0) ? cb : 0u;
-    t.c[2] = (valid && tc.ix0 && tc.iy1) ? cc : 0u;
-    t.c[3] = (valid && tc.ix1 && tc.iy1) ? cd : 0u;
-    t.fx = code & 31u;
-    t.fy = (code >> 5) & 31u;
+    // texture-convention entries (make_entry_tex): clamp addressing, every (clamped) tap is used
+    const bool all = (code & kCodeTex) != 0;
+    t.c[0] = (valid && (all || (tc.ix0 && tc.iy0))) ? ca : 0u;
+    t.c[1] = (valid && (all || (tc.ix1 && tc.iy0))) ? cb : 0u;
+    t.c[2] = (valid && (all || (tc.ix0 && tc.iy1))) ? cc : 0u;
+    t.c[3] = (valid && (all || (tc.ix1 && tc.iy1))) ? cd : 0u;
+    t.fx = all ? (code & 255u) : (code & 31u);
+    t.fy = all ? ((code >> 17) & 255u) : ((code >> 5) & 31u);
+}
+
+// The texture unit's linear filter as oracle/octvr_oracle.c orc_fast_remap_tex_rgba models it (the
+// texture-convention mode, make_entry_tex): per channel the f32 sum of the four normalized texels with
+// weights from the 8-bit fractions, in the oracle's order, then saturate_cast<uchar>(v * 255) (round half
+// to even).  Exact f32 operations (no contraction, correctly rounded division), so bit-equal to it.
+__device__ __forceinline__ void tex_bilerp(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, uint32_t a8,
+                                           uint32_t b8, uint32_t (&rgb)[3]) {
+    const float a = (float)a8 / 256.f, b = (float)b8 / 256.f;
+    const float w00 = (1.f - a) * (1.f - b), w10 = a * (1.f - b), w01 = (1.f - a) * b, w11 = a * b;
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) {
+        const float t00 = (float)((c00 >> (8 * ch)) & 255u) / 255.f, t10 = (float)((c10 >> (8 * ch)) & 255u) / 255.f;
+        const float t01 = (float)((c01 >> (8 * ch)) & 255u) / 255.f, t11 = (float)((c11 >> (8 * ch)) & 255u) / 255.f;
+        const float v = (w00 * t00 + w10 * t10 + w01 * t01 + w11 * t11) * 255.f;
+        rgb[ch] = !(v > 0.f) ? 0u : v >= 255.f ? 255u : (uint32_t)__builtin_rintf(v);
+    }
 }
 
 __device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, Taps& t) {

@@ -229,9 +229,11 @@ struct MultiBandDeleter {
 // pyramid buffers) on `device`.  in_w / in_h: input frame sizes.
 // feather_border > 0 instead builds FeatherGPUBlender(masks, rois, border) (blenders.cpp:531-586):
 // a single level whose weights are the normalised feather weights.
-// foot: when given, the remap's source reads are added to it.
+// foot: when given, the remap's source reads are added to it.  tex: texture-convention remap entries
+// (make_entry_tex, OCTVR_REMAP_TEXTURE).
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
-                            const std::vector<int>& in_h, int feather_border = 0, SourceFootprint* foot = nullptr);
+                            const std::vector<int>& in_h, int feather_border = 0, SourceFootprint* foot = nullptr,
+                            int tex = 0);
 // One frame: camera level-0 images (remap + gain), Gaussian levels, blend + collapse -> YUV420P
 // (or, with `rgba`, the RGB result as RGBA for a scaled output).
 // slot: frame slot (0 = the buffers built with the rig, 1..k-1 after multiband_set_slots(k)).

@@ -127,7 +127,7 @@ hipError_t launch_project_f64(const CameraParams* cams_dev, int W, int H, double
 // LUT mask is non-zero wins; its map value is quantized exactly as RemapInvoker does.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) composite_lut_kernel(const CamTemplate* cams, int n, int W, int H,
-                                                            CompositeEntry* lut) {
+                                                            CompositeEntry* lut, int tex) {
     const int64_t total = (int64_t)W * H;
     for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
          idx += (int64_t)gridDim.x * blockDim.x) {
@@ -141,18 +141,19 @@ __global__ void __launch_bounds__(256) composite_lut_kernel(const CamTemplate* c
             if (rx < 0 || ry < 0 || rx >= c.roi_w || ry >= c.roi_h) continue;
             const int64_t k = (int64_t)ry * c.roi_w + rx;
             if (c.mask[k] == 0) continue;
-            e = make_entry(c.map1[k], c.map2[k], (float)c.in_w, (float)c.in_h, i);
+            e = tex ? make_entry_tex(c.map1[k], c.map2[k], (float)c.in_w, (float)c.in_h, i)
+                    : make_entry(c.map1[k], c.map2[k], (float)c.in_w, (float)c.in_h, i);
         }
         lut[idx] = e;
     }
 }
 
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
-                                hipStream_t s) {
+                                hipStream_t s, int tex) {
     const int64_t total = (int64_t)W * H;
     int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 16);
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(composite_lut_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, n, W, H, lut);
+    hipLaunchKernelGGL(composite_lut_kernel, dim3(blocks), dim3(256), 0, s, cams_dev, n, W, H, lut, tex);
     return hipGetLastError();
 }
 
@@ -454,9 +455,18 @@ __device__ __forceinline__ void feed_taps_finish(const FeedRaw& r, Taps& t) {
 // fits beside frame k's composite (6 workgroups per CU at 72 VGPRs / 96 SGPRs / 20.7 KiB LDS) and runs
 // under it.  Both sum the same exact values: identical gains.
 constexpr int kLeanBatch = 3;  // lean feed: samples per lane in flight per round
+// The sample's warped pixel (RGB) from its taps: cv::remap's fixed-point bilinear, or the texture filter of
+// the texture-convention mode (tex, uniform)
+__device__ __forceinline__ void sample_rgb(const Taps& t, int tex, uint32_t (&rgb)[3]) {
+    if (tex)
+        tex_bilerp(t.c[0], t.c[1], t.c[2], t.c[3], t.fx, t.fy, rgb);
+    else
+        bilerp_rgba(t.c[0], t.c[1], t.c[2], t.c[3], t.fx, t.fy, rgb);
+}
+
 template <bool LEAN>
 __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const CompositeEntry* samples,
-                                               const uint16_t* partners, int n_chunks, const int32_t* N, int n,
+                                               const uint16_t* partners, int tex, int n_chunks, const int32_t* N, int n,
                                                unsigned long long* totals, uint32_t* tickets, double* gains) {
     __shared__ int s_last;
     __shared__ double s_I[kGainMaxCams * kGainMaxCams];
@@ -491,7 +501,7 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
                 pm[u] = partners[k0 + (u0 + u) * 64];
             }
             Taps t[kLeanBatch];
-            if (fr.vig) {  // vignette: per-tap byte gathers with the vignette multiply
+            if (fr.vig || tex) {  // vignette / clamped texture taps: per-tap byte gathers
 #pragma unroll
                 for (int u = 0; u < kLeanBatch; u++) gather_taps_frame(fr, e[u].xy, e[u].code, t[u]);
             } else {
@@ -506,7 +516,7 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
 #pragma unroll
             for (int u = 0; u < kLeanBatch; u++) {
                 uint32_t rgb[3];
-                bilerp_rgba(t[u].c[0], t[u].c[1], t[u].c[2], t[u].c[3], t[u].fx, t[u].fy, rgb);
+                sample_rgb(t[u], tex, rgb);
                 nv[u] = (double)sqrtf((float)(rgb[0] * rgb[0] + rgb[1] * rgb[1] + rgb[2] * rgb[2]));
                 pm_any |= pm[u];
             }
@@ -537,7 +547,7 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
             es[u] = samples[k0 + u * 64];
             pm[u] = partners[k0 + u * 64];
         }
-        if (fr.vig) {  // vignette: per-tap byte gathers with the vignette multiply
+        if (fr.vig || tex) {  // vignette / clamped texture taps: per-tap byte gathers
 #pragma unroll
             for (int u = 0; u < kPer; u++) gather_taps_frame(fr, es[u].xy, es[u].code, t[u]);
         } else {
@@ -550,7 +560,7 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
 #pragma unroll
         for (int u = 0; u < kPer; u++) {
             uint32_t rgb[3];
-            bilerp_rgba(t[u].c[0], t[u].c[1], t[u].c[2], t[u].c[3], t[u].fx, t[u].fy, rgb);
+            sample_rgb(t[u], tex, rgb);
             const double nv = (double)sqrtf((float)(rgb[0] * rgb[0] + rgb[1] * rgb[1] + rgb[2] * rgb[2]));
 #pragma unroll
             for (int j = 0; j < kGainMaxCams; j++)
@@ -626,25 +636,25 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
 }
 
 __global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
-                                                        const uint16_t* partners, int n_chunks, const int32_t* N, int n,
-                                                        unsigned long long* totals, uint32_t* tickets, double* gains) {
-    gain_feed_body<false>(frames, samples, partners, n_chunks, N, n, totals, tickets, gains);
+                                                        const uint16_t* partners, int tex, int n_chunks, const int32_t* N,
+                                                        int n, unsigned long long* totals, uint32_t* tickets, double* gains) {
+    gain_feed_body<false>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains);
 }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(80)))
-gain_feed_lean_kernel(FrameSet frames, const CompositeEntry* samples, const uint16_t* partners, int n_chunks,
+gain_feed_lean_kernel(FrameSet frames, const CompositeEntry* samples, const uint16_t* partners, int tex, int n_chunks,
                       const int32_t* N, int n, unsigned long long* totals, uint32_t* tickets, double* gains) {
-    gain_feed_body<true>(frames, samples, partners, n_chunks, N, n, totals, tickets, gains);
+    gain_feed_body<true>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains);
 }
 
-hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
+hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners, int tex,
                             int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s, bool lean) {
     if (n_chunks <= 0 || n > kGainMaxCams) return hipErrorInvalidValue;
     if (lean)
-        hipLaunchKernelGGL(gain_feed_lean_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners,
+        hipLaunchKernelGGL(gain_feed_lean_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, tex,
                            n_chunks, N, n, totals, tickets, gains);
     else
-        hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners,
+        hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, tex,
                            n_chunks, N, n, totals, tickets, gains);
     return hipGetLastError();
 }
@@ -1300,7 +1310,10 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
     f32x2_t gain[4];
 #pragma unroll
     for (int p = 0; p < 4; p++) {
-        bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
+        if (cd[p] & kCodeTex)  // texture-convention entries (make_entry_tex)
+            tex_bilerp(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
+        else
+            bilerp_rgba(tp[p].c[0], tp[p].c[1], tp[p].c[2], tp[p].c[3], tp[p].fx, tp[p].fy, rgb[p]);
         float gp = (MODE == 1 && (cd[p] & kCodeNoGain)) ? 1.0f : s_gain[(cd[p] >> 10) & 31u];
         gain[p] = f32x2_t{gp, gp};
     }

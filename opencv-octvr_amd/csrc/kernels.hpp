@@ -42,6 +42,27 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
     return e;
 }
 
+// Texture-convention entry (mapper flag OCTVR_REMAP_TEXTURE): the sampling of the reference's live CUDA
+// path, cv::cuda::fastRemap through a linear-filtered, clamp-addressed texture with normalized coordinates
+// (cudawarping/src/cuda/fast_remap.cu:21-44, texture.hpp:124-160), as oracle/octvr_oracle.c
+// orc_fast_remap_tex_rgba models NVIDIA's filter: X = fl32(u W) - 0.5, i0 = floor(X), alpha =
+// floor(frac(X) 256) / 256 (8 fractional bits), taps (i0, i0 + 1) x (j0, j0 + 1) clamped to the image and
+// all four used.  xy: (i0, j0) kept in [-1, size - 1] (the same taps under the clamp); code: alpha | cam <<
+// 10 | valid << 15 | beta << 17 | kCodeTex.  u < 0 or NaN: invalid (fast_remap's fill_zero).  Tiles holding
+// such entries always take the gather path (tiling.cpp), whose taps and weights test kCodeTex.
+constexpr uint32_t kCodeTex = 1u << 31;
+__host__ __device__ inline CompositeEntry make_entry_tex(float m1, float m2, float w, float h, int cam) {
+    CompositeEntry e{0u, 0u};
+    if (!(m1 >= 0.f) || m2 != m2) return e;
+    const float xb = m1 * w - 0.5f, yb = m2 * h - 0.5f;
+    const float fx = floorf(xb), fy = floorf(yb);
+    const uint32_t a = (uint32_t)floorf((xb - fx) * 256.f), b = (uint32_t)floorf((yb - fy) * 256.f);
+    const int i0 = (int)fminf(fmaxf(fx, -1.f), w - 1.f), j0 = (int)fminf(fmaxf(fy, -1.f), h - 1.f);
+    e.xy = (uint32_t)(uint16_t)(int16_t)i0 | ((uint32_t)(uint16_t)(int16_t)j0 << 16);
+    e.code = (a & 255u) | ((uint32_t)cam << 10) | (1u << 15) | ((b & 255u) << 17) | kCodeTex;
+    return e;
+}
+
 // The 2 x 2 taps of an entry's cell (sx, sy) in a w x h image: clamped addresses and in-image flags.
 struct TapCell {
     int x0, x1, y0, y1;
@@ -180,15 +201,17 @@ hipError_t launch_lut_build(const CameraParams* cams_dev, int W, int H, float* m
 hipError_t launch_project_f64(const CameraParams* cams_dev, int W, int H, double* x, double* y, uint8_t* fragile,
                               hipStream_t s);
 
+// tex: texture-convention entries (make_entry_tex) instead of cv::remap's (make_entry)
 hipError_t launch_composite_lut(const CamTemplate* cams_dev, int n, int W, int H, CompositeEntry* lut,
-                                hipStream_t s);
+                                hipStream_t s, int tex = 0);
 
 // Gain feed in ONE launch (no host sync): each workgroup gathers its chunk's warped samples, takes
 // the f32 RGB norm (elementNorm) and adds it per partner camera into exact u64 fixed-point totals
 // (units of 2^-23, see kernels.hip); the last workgroup (per-XCD then global ticket) reads and
 // resets the totals, assembles I(i,j), A, b and solves.  `totals` (kGainMaxCams^2) and `tickets`
-// (9) must be zero before the first launch; the last workgroup leaves them zero.
-hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners,
+// (9) must be zero before the first launch; the last workgroup leaves them zero.  tex: the samples are
+// texture-convention entries (make_entry_tex).
+hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners, int tex,
                             int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s,
                             bool lean = false);  // lean: <= 80 VGPRs (73 used), runs beside a composite (kernels.hip)

@@ -218,7 +218,7 @@ struct Bitmap {
 }  // namespace
 
 MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const std::vector<int>& in_w,
-                            const std::vector<int>& in_h, int feather_border, SourceFootprint* foot) {
+                            const std::vector<int>& in_h, int feather_border, SourceFootprint* foot, int tex) {
     auto mb = std::unique_ptr<MultiBand>(new MultiBand);
     MultiBand& M = *mb;
     const int n = (int)rig.inputs.size();
@@ -822,10 +822,15 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
             if (rx < 0 || ry < 0 || rx >= in.roi[2] || ry >= in.roi[3]) return CompositeEntry{0u, 0u};
             const size_t k = (size_t)ry * in.roi[2] + rx;
             const float m1 = in.map1[k], m2 = in.map2[k];
-            if (in.mask[k]) return make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
+            auto mk = [&]() {
+                return tex ? make_entry_tex(m1, m2, (float)in_w[i], (float)in_h[i], i)
+                           : make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
+            };
+            if (in.mask[k]) return mk();
             // LUT mask 0: the remap still runs there, without gain (mul_scalar_with_mask); a template's
-            // -1 maps put every tap outside the image (black), other values follow remap's rule
-            CompositeEntry e = make_entry(m1, m2, (float)in_w[i], (float)in_h[i], i);
+            // -1 maps put every tap outside the image (black; fastRemap's fill_zero in the texture
+            // convention), other values follow the remap's rule
+            CompositeEntry e = mk();
             e.code |= kCodeNoGain;
             return e;
         };

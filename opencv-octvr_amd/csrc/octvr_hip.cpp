@@ -877,6 +877,7 @@ struct octvr_mapper {
     std::vector<double> last_gains;
     std::vector<DevBuf<float>> vig;  // per camera: vignette map resized to the input size, or empty
     SourceFootprint foot;            // the input bytes this mapper's kernels read (host_common.hpp)
+    int tex = 0;                     // OCTVR_REMAP_TEXTURE: texture-convention entries (make_entry_tex)
     // scaled output (scaled_output_size != stitch size, mapper.cpp:69,153-155,290-306): the RGB result
     // as an RGBA frame, resized + converted to YUV420P by a second kernel
     int SW = 0, SH = 0;
@@ -993,7 +994,9 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
                 int sx = (int)(x * fx), sy = (int)(y * fy);
                 size_t k = (size_t)sy * in.roi[2] + sx;
                 CompositeEntry e{0, 0};
-                if (in.mask[k]) e = make_entry(in.map1[k], in.map2[k], (float)m.in_w[i], (float)m.in_h[i], i);
+                if (in.mask[k])
+                    e = m.tex ? make_entry_tex(in.map1[k], in.map2[k], (float)m.in_w[i], (float)m.in_h[i], i)
+                              : make_entry(in.map1[k], in.map2[k], (float)m.in_w[i], (float)m.in_h[i], i);
                 samp[i][(size_t)y * ww + x] = e;
             }
         int nz = 0;
@@ -1148,7 +1151,7 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
                 // with frames in flight the feed runs beside the previous frame's composite: the lean
                 // variant fits next to it (the wide-prefetch one waits for its workgroups to drain)
                 const bool lean = m->slots.size() > 1;
-                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->n_chunks, m->N.p, m->n, sl.totals,
+                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->tex, m->n_chunks, m->N.p, m->n, sl.totals,
                                            sl.tickets, sl.gains, s, lean));
             }
         }
@@ -1520,8 +1523,14 @@ int octvr_rig_clone(const octvr_rig* src, octvr_rig** out) {
 
 int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                         int enable_gain, int scale_w, int scale_h, octvr_mapper** out) {
+    return octvr_mapper_create_ex(rig, device, n_inputs, in_w, in_h, blend, enable_gain, scale_w, scale_h, 0, out);
+}
+
+int octvr_mapper_create_ex(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
+                           int enable_gain, int scale_w, int scale_h, int flags, octvr_mapper** out) {
     return guarded([&] {
         REQUIRE(rig && out && in_w && in_h, "NULL argument");
+        REQUIRE((flags & ~OCTVR_REMAP_TEXTURE) == 0, "unknown mapper flags");
         if (!rig->overlays.empty())  // checked first: the real reason, whatever n_inputs says
             throw OctvrError(OCTVR_E_UNSUPPORTED, "overlay inputs are not implemented in this ABI version");
         REQUIRE(n_inputs == (int)rig->inputs.size(), "in_sizes must cover every input");
@@ -1530,6 +1539,7 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         REQUIRE(rig->out_w % 2 == 0 && rig->out_h % 2 == 0, "YUV420 output needs even width/height");
         auto m = std::make_unique<octvr_mapper>();
         m->device = device;
+        m->tex = (flags & OCTVR_REMAP_TEXTURE) ? 1 : 0;
         m->n = (int)rig->inputs.size();
         m->W = rig->out_w;
         m->H = rig->out_h;
@@ -1563,10 +1573,10 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
         if (m->blend > 0) {
             // MultiBandGPUBlender(seam_masks, rois, bands), bands = ceil(log2(blend)) - 1 (mapper.cpp:171-176)
             const int bands = (int)(std::ceil(std::log((double)m->blend) / std::log(2.)) - 1.);
-            m->mb.reset(multiband_create(*rig, device, bands, m->in_w, m->in_h, 0, &m->foot));
+            m->mb.reset(multiband_create(*rig, device, bands, m->in_w, m->in_h, 0, &m->foot, m->tex));
         } else if (m->blend < 0) {
             // FeatherGPUBlender(masks, rois, border = -blend) (mapper.cpp:177-182)
-            m->mb.reset(multiband_create(*rig, device, 0, m->in_w, m->in_h, -m->blend, &m->foot));
+            m->mb.reset(multiband_create(*rig, device, 0, m->in_w, m->in_h, -m->blend, &m->foot, m->tex));
         } else {
             // per-camera templates -> device, composite LUT, then drop the per-camera maps
             std::vector<DevBuf<float>> m1(m->n), m2(m->n);
@@ -1584,7 +1594,7 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
             ctd.upload(ct.data(), ct.size());
             DevBuf<CompositeEntry> lut;
             lut.alloc((size_t)m->W * m->H);
-            HIP_CHECK(launch_composite_lut(ctd.p, m->n, m->W, m->H, lut.p, nullptr));
+            HIP_CHECK(launch_composite_lut(ctd.p, m->n, m->W, m->H, lut.p, nullptr, m->tex));
             HIP_CHECK(hipDeviceSynchronize());
             std::vector<CompositeEntry> lut8((size_t)m->W * m->H);
             HIP_CHECK(hipMemcpy(lut8.data(), lut.p, lut8.size() * sizeof(CompositeEntry), hipMemcpyDeviceToHost));

@@ -51,6 +51,10 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 raw[k] = e;
                 px[k].mask = 0;
                 if (!(e.code & 0x8000u)) continue;
+                if (e.code & kCodeTex) {  // texture-convention entries: the gather path (clamped taps)
+                    wide = true;
+                    continue;
+                }
                 const int cam = (int)((e.code >> 10) & 31u);
                 const int sx = (int)(int16_t)(e.xy & 0xFFFFu), sy = (int)(int16_t)(e.xy >> 16);
                 const int iw = in_w[cam], ih = in_h[cam];
@@ -449,10 +453,11 @@ void SourceFootprint::mark_taps(const CompositeEntry& e) {
     const int cam = (int)((e.code >> 10) & 31u);
     if (cam >= (int)w.size()) return;
     const TapCell c = tap_cell(e.xy, w[cam], h[cam]);
-    if (c.iy0 && c.ix0) mark(cam, c.y0, c.x0 >> 3);
-    if (c.iy0 && c.ix1) mark(cam, c.y0, c.x1 >> 3);
-    if (c.iy1 && c.ix0) mark(cam, c.y1, c.x0 >> 3);
-    if (c.iy1 && c.ix1) mark(cam, c.y1, c.x1 >> 3);
+    const bool all = (e.code & kCodeTex) != 0;  // texture convention: all four clamped taps are used
+    if (all || (c.iy0 && c.ix0)) mark(cam, c.y0, c.x0 >> 3);
+    if (all || (c.iy0 && c.ix1)) mark(cam, c.y0, c.x1 >> 3);
+    if (all || (c.iy1 && c.ix0)) mark(cam, c.y1, c.x0 >> 3);
+    if (all || (c.iy1 && c.ix1)) mark(cam, c.y1, c.x1 >> 3);
 }
 
 void SourceFootprint::merge(const SourceFootprint& o) {

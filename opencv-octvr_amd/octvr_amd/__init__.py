@@ -67,6 +67,10 @@ _lib.octvr_rig_destroy.argtypes = [_VP]
 _lib.octvr_rig_destroy.restype = None
 _lib.octvr_mapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, C.c_int,
                                      C.c_int, C.c_int, C.POINTER(_VP)]
+if hasattr(_lib, "octvr_mapper_create_ex"):
+    _lib.octvr_mapper_create_ex.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
+                                            C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]
+REMAP_TEXTURE = 1  # octvr_hip.h OCTVR_REMAP_TEXTURE
 _lib.octvr_mapper_stitch_yuv420p.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t,
                                              C.POINTER(C.c_double), C.c_int, _VP]
 _lib.octvr_mapper_stitch_preview.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP, C.c_int,
@@ -329,14 +333,22 @@ class FrameRefs:
 class Mapper:
     """vr::Mapper on one device: stitch(inputs YUV420P, output YUV420P) with optional gain."""
 
-    def __init__(self, mt, in_sizes, blend=0, enable_gain=True, device=0, scale_output=(0, 0)):
+    def __init__(self, mt, in_sizes, blend=0, enable_gain=True, device=0, scale_output=(0, 0), remap="remap"):
+        """remap: "remap" (cv::remap's fixed point, the default) or "texture" (the reference's CUDA
+        fastRemap texture sampling, OCTVR_REMAP_TEXTURE)."""
         n = len(in_sizes)
         w = (C.c_int * n)(*[s[0] for s in in_sizes])
         h = (C.c_int * n)(*[s[1] for s in in_sizes])
         scale_output = tuple(scale_output) if scale_output else (0, 0)  # None / () = unscaled
+        if remap not in ("remap", "texture"):
+            raise ValueError("remap must be 'remap' or 'texture'")
         hd = _VP()
-        _check(_lib.octvr_mapper_create(mt._h, device, n, w, h, blend, int(enable_gain), scale_output[0],
-                                        scale_output[1], C.byref(hd)))
+        if remap == "texture":
+            _check(_lib.octvr_mapper_create_ex(mt._h, device, n, w, h, blend, int(enable_gain), scale_output[0],
+                                               scale_output[1], REMAP_TEXTURE, C.byref(hd)))
+        else:
+            _check(_lib.octvr_mapper_create(mt._h, device, n, w, h, blend, int(enable_gain), scale_output[0],
+                                            scale_output[1], C.byref(hd)))
         self._h = hd
         self.n = n
         self.device = device

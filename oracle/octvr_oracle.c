@@ -1310,6 +1310,12 @@ static void remap_rows(void* c, int y0, int y1) {
     const orc_frame* f = s->f;
     int i = s->cam;
     const int* r = f->rois + 4 * i;
+    if (f->remap_tex) { /* the reference's live CUDA path: fastRemap through the texture (A12 model) */
+        orc_fast_remap_tex_rgba(s->rgba, f->in_w[i], f->in_h[i], (size_t)f->in_w[i] * 4, f->map1[i] + (size_t)y0 * r[2],
+                                f->map2[i] + (size_t)y0 * r[2], r[2], y1 - y0, r[2],
+                                s->warped + (size_t)y0 * r[2] * 4, (size_t)r[2] * 4);
+        return;
+    }
     orc_remap_u8(s->rgba, f->in_w[i], f->in_h[i], (size_t)f->in_w[i] * 4, 4, f->map1[i] + (size_t)y0 * r[2],
                  f->map2[i] + (size_t)y0 * r[2], r[2], y1 - y0, r[2], (float)f->in_w[i], (float)f->in_h[i],
                  s->warped + (size_t)y0 * r[2] * 4, (size_t)r[2] * 4);
@@ -1494,11 +1500,13 @@ void orc_fast_remap_tex_rgba(const uint8_t* src, int w, int h, size_t spitch, co
         for (int x = 0; x < mw; x++) {
             float u = map1[(size_t)y * mpitch + x], v = map2[(size_t)y * mpitch + x];
             uint8_t* o = dst + (size_t)y * dpitch + (size_t)x * 4;
-            if (u < 0) { o[0] = o[1] = o[2] = o[3] = 0; continue; }
+            if (!(u >= 0) || v != v) { o[0] = o[1] = o[2] = o[3] = 0; continue; } /* u < 0 (and NaN): fill_zero */
             float xb = u * (float)w - 0.5f, yb = v * (float)h - 0.5f;
             float fx = floorf(xb), fy = floorf(yb);
             float a = floorf((xb - fx) * 256.f) / 256.f, b = floorf((yb - fy) * 256.f) / 256.f;
-            int i0 = (int)fx, j0 = (int)fy, i1 = i0 + 1, j1 = j0 + 1;
+            /* the cell index, limited to [-1, size - 1] first (the same taps after the clamps below) */
+            int i0 = (int)fminf(fmaxf(fx, -1.f), (float)w - 1.f), j0 = (int)fminf(fmaxf(fy, -1.f), (float)h - 1.f);
+            int i1 = i0 + 1, j1 = j0 + 1;
             i0 = i0 < 0 ? 0 : i0 > w - 1 ? w - 1 : i0;
             i1 = i1 < 0 ? 0 : i1 > w - 1 ? w - 1 : i1;
             j0 = j0 < 0 ? 0 : j0 > h - 1 ? h - 1 : j0;

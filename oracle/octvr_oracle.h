@@ -165,6 +165,8 @@ typedef struct {
                                         to preview_w x preview_h, u8x3 rows of preview_pitch bytes; NULL = none */
     int preview_w, preview_h;
     size_t preview_pitch;
+    int remap_tex;                   /* 1: warp with orc_fast_remap_tex_rgba (the CUDA fastRemap texture model,
+                                        OCTVR_REMAP_TEXTURE) instead of orc_remap_u8 */
 } orc_frame;
 int orc_stitch_frame(const orc_frame* f);
 /* A12 CUDA fastRemap texture bilinear on RGBA (for the documented A12-vs-A13 tolerance only). */

@@ -66,6 +66,7 @@ class OrcFrame(C.Structure):
         ("preview", C.c_void_p),
         ("preview_w", C.c_int), ("preview_h", C.c_int),
         ("preview_pitch", C.c_size_t),
+        ("remap_tex", C.c_int),
     ]
 
 
@@ -465,9 +466,10 @@ def gain_feed(rois, warped, masks, out_w, out_h):
 
 
 def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enable_gain=True, gains=None,
-                 threads=1, row_band=None, blend=0, seams=None, vig=None, scale=None, preview=None):
+                 threads=1, row_band=None, blend=0, seams=None, vig=None, scale=None, preview=None, remap_tex=False):
     """One Mapper::stitch -> (YUV420P output, gains); preview=(w, h): also the preview_output image,
-    returned as a third value."""
+    returned as a third value.  remap_tex: warp as the reference's CUDA fastRemap texture path
+    (orc_fast_remap_tex_rgba; the library's OCTVR_REMAP_TEXTURE mode)."""
     n = len(in_yuv)
     keep = []
 
@@ -499,6 +501,7 @@ def stitch_frame(in_yuv, in_sizes, rois, map1s, map2s, masks, out_w, out_h, enab
     f.out_yuv = out.ctypes.data
     f.out_pitch = ow
     f.enable_gain = int(enable_gain)
+    f.remap_tex = int(remap_tex)
     gin = None
     if gains is not None:
         gin = np.ascontiguousarray(gains, np.float64)

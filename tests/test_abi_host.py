@@ -161,3 +161,19 @@ def test_from_arrays_rejects_overflowing_roi(product_lib, roi):
     one_f = np.zeros(1, np.float32)
     with pytest.raises(product_lib.OctvrError):
         product_lib.MapperTemplate.from_arrays(8, 4, [roi], [one_f], [one_f], [np.zeros(1, np.uint8)])
+
+
+def test_mapper_create_ex_rejects_unknown_flags(product_lib):
+    """octvr_mapper_create_ex validates its flags before any device work (OCTVR_REMAP_TEXTURE = 1 is the only
+    one)."""
+    import ctypes as C
+    rig, z = O.load_rig("rigA")
+    mt = product_lib.MapperTemplate.from_arrays(512, 256, z["rois"].tolist(), [z["map1_0"], z["map1_1"]],
+                                               [z["map2_0"], z["map2_1"]], [z["mask_0"], z["mask_1"]])
+    lib = product_lib.lib()
+    w = (C.c_int * 2)(256, 256)
+    h = (C.c_int * 2)(144, 144)
+    out = C.c_void_p()
+    rc = lib.octvr_mapper_create_ex(mt._h, 0, 2, w, h, 0, 1, 0, 0, 2, C.byref(out))
+    assert rc == product_lib.E_INVALID and not out.value
+    assert b"flags" in lib.octvr_last_error()

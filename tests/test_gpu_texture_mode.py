@@ -1,0 +1,119 @@
+"""The texture-convention mapper mode (OCTVR_REMAP_TEXTURE; VERDICT r04 "Missing 3"): the reference's live
+CUDA path warps each camera with cv::cuda::fastRemap through a linear-filtered, clamp-addressed texture
+(modules/cudawarping/src/cuda/fast_remap.cu:21-44, cudev/ptr2d/texture.hpp:124-160): x = u W - 0.5, 8-bit
+fractions, taps clamped to the image, u < 0 -> 0.  The filter itself is NVIDIA hardware behaviour that no
+file of the reference holds, so parity here is against the oracle's model of it
+(oracle/octvr_oracle.c orc_fast_remap_tex_rgba, the A12 restatement of tests/test_a12_tolerance.py): parity
+unpinned by necessity.  Every output byte and the estimated gains (whose samples are texture-sampled
+warped pixels, mapper.cpp:233-237) are checked against Mapper::stitch in the oracle with the texture warp,
+for the copy chain, multi-band and feather blends, vignetting, scaled output and frames in flight."""
+import json
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _case(name):
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    sizes = [(rig["inputs"][i]["options"]["width"], rig["inputs"][i]["options"]["height"]) for i in range(n)]
+    maps1 = [z[f"map1_{i}"] for i in range(n)]
+    maps2 = [z[f"map2_{i}"] for i in range(n)]
+    masks = [z[f"mask_{i}"] for i in range(n)]
+    seams = [z[f"seam_{i}"] for i in range(n)]
+    return W, H, sizes, z["rois"].tolist(), maps1, maps2, masks, seams
+
+
+@pytest.mark.parametrize("blend", [0, 16, -5])
+@pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
+def test_gpu_texture_mode_bit_exact(product_lib, name, blend):
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    W, H, sizes, rois, maps1, maps2, masks, seams = _case(name)
+    mt = ox.MapperTemplate.from_arrays(W, H, rois, maps1, maps2, masks, seams)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, remap="texture")
+    if blend == 0:  # every tile with a texture-convention entry takes the gather path
+        assert m.info()["wide_tiles"] > 0
+    for kind in ("smooth", "noise"):
+        fn = synthetic.smooth_yuv_frame if kind == "smooth" else synthetic.yuv_frame
+        frames = [fn(w, h, 4000 + 7 * i + (kind == "noise")) for i, (w, h) in enumerate(sizes)]
+        out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+        m.stitch([torch.from_numpy(f).cuda() for f in frames], out)
+        torch.cuda.synchronize()
+        want, g_orc = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, blend=blend,
+                                     seams=seams, threads=8, remap_tex=True)
+        np.testing.assert_array_equal(np.array(m.gains()), g_orc)
+        got = out.cpu().numpy()
+        d = got != want
+        assert not d.any(), (kind, int(d.sum()), np.argwhere(d)[:5].tolist())
+    # and the mode is a different sampling: the default mapper's frame differs
+    ref, _ = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, blend=blend,
+                            seams=seams, threads=8)
+    assert (ref != want).any()
+
+
+def test_gpu_texture_mode_scaled_vignette_inflight(product_lib):
+    """Scaled output (the RGBA result path), vignetting (per-tap multiply before the filter), and two frames in
+    flight on two streams (the lean gain feed with texture samples)."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    rig, _ = O.load_rig("rigB")
+    rig = json.loads(json.dumps(rig))
+    for k, c in enumerate(rig["inputs"]):
+        if k % 2 == 0:
+            c["options"]["vignette"] = [1.0 + 0.05 * k, -0.35, 0.12, -0.04]
+    W, H = 768, 384
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H)
+    n = len(mt)
+    sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
+    vig = []
+    for i, c in enumerate(rig["inputs"]):
+        v = O.vignette_map(c["options"])
+        vig.append(None if v is None else O.resize_linear_cuda_f32(v, sizes[i][0], sizes[i][1]))
+    mt.create_masks(0)
+    rois, maps1, maps2, masks, seams = [], [], [], [], []
+    for i in range(n):
+        roi, m1, m2, mk, sm = mt.input(i)
+        rois.append(roi); maps1.append(m1); maps2.append(m2); masks.append(mk); seams.append(sm)
+    frames = [synthetic.smooth_yuv_frame(w, h, 500 + i) for i, (w, h) in enumerate(sizes)]
+    dev = [torch.from_numpy(f).cuda() for f in frames]
+    # scaled output, blend 0 and multi-band
+    for blend in (0, 16):
+        m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, scale_output=(512, 256), remap="texture")
+        out = torch.zeros((256 * 3 // 2, 512), dtype=torch.uint8, device="cuda")
+        m.stitch(dev, out)
+        torch.cuda.synchronize()
+        want, g = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, blend=blend,
+                                 seams=seams, vig=vig, threads=8, scale=(512, 256), remap_tex=True)
+        np.testing.assert_array_equal(np.array(m.gains()), g)
+        assert np.array_equal(out.cpu().numpy(), want), blend
+    # two frames in flight
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True, remap="texture")
+    m.set_frames_in_flight(2)
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    for k in range(2):
+        m.stitch(dev, outs[k], stream=streams[k])
+    torch.cuda.synchronize()
+    want, g = O.stitch_frame(frames, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, seams=seams, vig=vig,
+                             threads=8, remap_tex=True)
+    np.testing.assert_array_equal(np.array(m.gains()), g)
+    for o in outs:
+        assert np.array_equal(o.cpu().numpy(), want)
+
+
+def test_texture_mode_rejects_unknown_flags(product_lib):
+    ox = product_lib
+    W, H, sizes, rois, maps1, maps2, masks, seams = _case("rigA")
+    mt = ox.MapperTemplate.from_arrays(W, H, rois, maps1, maps2, masks, seams)
+    with pytest.raises(ValueError):
+        ox.Mapper(mt, sizes, remap="nearest")
