@@ -424,7 +424,6 @@ def fast_rank(args, world, rank, local_rank, dist):
         "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
                                "template without ROI), NV12 in/out" % (len(sizes), sizes[0][0], sizes[0][1], W, H),
                    "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
-                   **({"remap": "texture (OCTVR_REMAP_TEXTURE)"} if args.remap == "texture" else {}),
                    "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
