@@ -76,15 +76,34 @@ def test_gpu_fullsize_bit_exact(product_lib, cfg):
         m.stitch(dev[f], outs[f], stream=streams[f])
     g_last = np.array(m.gains())
     torch.cuda.synchronize()
+    exps = []
     for f in range(k):
         exp, g_orc = O.stitch_frame(sets[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None,
                                     blend=blend, seams=seams, threads=THREADS)
+        exps.append(exp)
         got = outs[f].cpu().numpy()
         d = got != exp
         assert not d.any(), (cfg, f, int(d.sum()), np.argwhere(d)[:4].tolist())
         assert all(0.5 < x < 2.0 for x in g_orc) and not np.all(np.array(g_orc) == 1.0)
         if f == k - 1:
             np.testing.assert_array_equal(g_last, np.array(g_orc))
+    # the AsyncMultiMapper from host planes (async.cpp): only each mapper's source footprint is uploaded,
+    # the rest of the device frames hold a fixed pattern — every byte still equal to the oracle's frame
+    if cfg in ("C1", "C2", "C3"):
+        del dev
+        am = ox.AsyncMultiMapper([mt], sizes, (W, H), [blend], [0], [(0.0, 0.0, 1.0, 1.0)])
+        aouts = []
+        for f in range(k):
+            o = (np.zeros((H, W), np.uint8), np.zeros((H // 2, W // 2), np.uint8), np.zeros((H // 2, W // 2), np.uint8))
+            am.push([(x[:h], x[h:, :w // 2], x[h:, w // 2:]) for x, (w, h) in zip(sets[f], sizes)], o)
+            aouts.append(o)
+        for f in range(k):
+            am.pop()
+            exp = exps[f]
+            assert np.array_equal(aouts[f][0], exp[:H]), (cfg, f, "Y")
+            assert np.array_equal(aouts[f][1], exp[H:, :W // 2]) and np.array_equal(aouts[f][2], exp[H:, W // 2:]), (cfg, f)
+        am.close()
+        dev = [[torch.from_numpy(f).cuda() for f in fs] for fs in sets]
     # and each frame's gains, stitched one at a time on one stream
     m.set_frames_in_flight(1)
     for f in range(k):
