@@ -204,21 +204,39 @@ __device__ __forceinline__ void gather_taps_frame(const SourceFrame& f, uint32_t
     t.fy = all ? ((code >> 17) & 255u) : ((code >> 5) & 31u);
 }
 
+// fl32(t / 255) for a byte t: the product with the rounded reciprocal, corrected by one residual step
+// (two FMAs) — equal to the correctly rounded quotient for every t in 0..255
+// (tests/test_tex_division.py), at 3 instead of ~10 instructions.
+__device__ __forceinline__ float div255(uint32_t t) {
+    const float x = (float)t, r = 1.f / 255.f;
+    const float q = x * r;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.f, x), r, q);
+}
+
 // The texture unit's linear filter as oracle/octvr_oracle.c orc_fast_remap_tex_rgba models it (the
 // texture-convention mode, make_entry_tex): per channel the f32 sum of the four normalized texels with
 // weights from the 8-bit fractions, in the oracle's order, then saturate_cast<uchar>(v * 255) (round half
-// to even).  Exact f32 operations (no contraction, correctly rounded division), so bit-equal to it.
-__device__ __forceinline__ void tex_bilerp(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, uint32_t a8,
-                                           uint32_t b8, uint32_t (&rgb)[3]) {
-    const float a = (float)a8 / 256.f, b = (float)b8 / 256.f;
+// to even).  Exact f32 operations (no contraction; div255 = the correctly rounded t / 255), so bit-equal to
+// it.  (c00, c10, c01, c11): taps (x0, y0), (x1, y0), (x0, y1), (x1, y1); the result as floats of bytes.
+__device__ __forceinline__ void tex_bilerp_f(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, uint32_t a8,
+                                             uint32_t b8, float (&rgb)[3]) {
+    const float a = (float)a8 / 256.f, b = (float)b8 / 256.f;  // exact: 8-bit fractions
     const float w00 = (1.f - a) * (1.f - b), w10 = a * (1.f - b), w01 = (1.f - a) * b, w11 = a * b;
 #pragma unroll
     for (int ch = 0; ch < 3; ch++) {
-        const float t00 = (float)((c00 >> (8 * ch)) & 255u) / 255.f, t10 = (float)((c10 >> (8 * ch)) & 255u) / 255.f;
-        const float t01 = (float)((c01 >> (8 * ch)) & 255u) / 255.f, t11 = (float)((c11 >> (8 * ch)) & 255u) / 255.f;
+        const uint32_t sh = 8u * ch;
+        const float t00 = div255((c00 >> sh) & 255u), t10 = div255((c10 >> sh) & 255u);
+        const float t01 = div255((c01 >> sh) & 255u), t11 = div255((c11 >> sh) & 255u);
         const float v = (w00 * t00 + w10 * t10 + w01 * t01 + w11 * t11) * 255.f;
-        rgb[ch] = !(v > 0.f) ? 0u : v >= 255.f ? 255u : (uint32_t)__builtin_rintf(v);
+        rgb[ch] = !(v > 0.f) ? 0.f : v >= 255.f ? 255.f : __builtin_rintf(v);
     }
+}
+__device__ __forceinline__ void tex_bilerp(uint32_t c00, uint32_t c10, uint32_t c01, uint32_t c11, uint32_t a8,
+                                           uint32_t b8, uint32_t (&rgb)[3]) {
+    float f[3];
+    tex_bilerp_f(c00, c10, c01, c11, a8, b8, f);
+#pragma unroll
+    for (int ch = 0; ch < 3; ch++) rgb[ch] = (uint32_t)f[ch];
 }
 
 __device__ __forceinline__ void gather_taps(const FrameSet& fs, uint32_t xy, uint32_t code, Taps& t) {

@@ -173,6 +173,7 @@ struct TiledLutBuild {
     std::vector<int32_t> bands;  // kStitchBands + 1 item boundaries, balanced by estimated cost
     int n_items = 0, n_wide = 0;
     int qpl = 1;  // 128x8 halves per item (kernels.hpp TiledLut::qpl)
+    int tex = 0;  // the staged items' entries are texture-convention ones (tiled_entry_tex)
     double staged_bytes = 0;  // YUV bytes staged, summed over items (groups of neighbouring items overlap)
     double source_bytes = 0;  // unique source bytes: the union of the staged groups (+ wide tiles' taps)
     std::string stats;  // JSON fragment: staged items by staging chunks / LDS bytes, per-band chunk sums

@@ -1066,7 +1066,9 @@ __device__ __forceinline__ uint32_t tap_off(uint32_t e) { return (e >> 13) & 0x3
 
 // Staged items.  The staged items are split into 8 contiguous bands, one per XCD under round-robin
 // dispatch (blocks b, b+8, ...), so neighbouring items' source boxes share that XCD's L2.
-template <bool DWORD_STAGE, int MODE, bool VIG>
+// TEX: texture-convention entries (tiled_entry_tex): the taps as usual, the texture filter model instead of
+// the weight table.
+template <bool DWORD_STAGE, int MODE, bool VIG, bool TEX>
 __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
 __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
                                                                    const double* gains, int use_gain, uint8_t* out,
@@ -1240,15 +1242,20 @@ __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet fram
             for (int p = 0; p < 4; p++) {
                 const uint32_t e = ent[p];
                 // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
-                const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) + tap_off(e);
+                const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) + (TEX ? (e >> 15) & 0x3FFCu : tap_off(e));
                 const uint8_t* r1 = r0 + 4u * S;
                 const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
                 const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
                 const uint32_t c10 = reinterpret_cast<const uint32_t*>(r1)[0];
                 const uint32_t c11 = reinterpret_cast<const uint32_t*>(r1)[1];
-                bilerp_rgba_w(c00, c01, c10, c11, wtab_read(e), rgb[p]);
-                // slot << 3 = e >> 27 (bits 27-29 of a tiled entry are zero; kernels.hpp)
-                gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + (e >> 27));
+                if constexpr (TEX) {
+                    tex_bilerp_f(c00, c01, c10, c11, (e >> 1) & 255u, (e >> 9) & 255u, rgb[p]);
+                    gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + ((e >> 30) << 3));
+                } else {
+                    bilerp_rgba_w(c00, c01, c10, c11, wtab_read(e), rgb[p]);
+                    // slot << 3 = e >> 27 (bits 27-29 of a tiled entry are zero; kernels.hpp)
+                    gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + (e >> 27));
+                }
                 if (MODE == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
             }
             prev[h] = finish_any<MODE>(rgb, gain);
@@ -1331,27 +1338,41 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 
 // The weight table's address (wtab_read) assumes the dynamic LDS starts right after StitchLds: checked
 // once per kernel instance against the compiled static LDS size.
-template <bool DW, int MODE, bool V>
+template <bool DW, int MODE, bool V, bool TEX>
 static hipError_t stitch_lds_check() {
     hipFuncAttributes a;
-    const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V>));
+    const hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V, TEX>));
     if (e != hipSuccess) return e;
     return a.sharedSizeBytes == sizeof(StitchLds) ? hipSuccess : hipErrorInvalidKernelFile;
 }
 
-template <bool DW, int MODE, bool V>
+template <bool DW, int MODE, bool V, bool TEX>
 static hipError_t launch_tiled(int blocks, const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                                int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
                                hipEvent_t ev0, hipEvent_t ev1) {
-    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V>();
+    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V, TEX>();
     if (lds_ok != hipSuccess) return lds_ok;
     if (ev0)  // the timing events carried by the dispatch packet itself
-        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, ev0, ev1, 0,
-                              frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);
+        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, TEX>), dim3(blocks), dim3(256), kWtabBytes, s, ev0, ev1,
+                              0, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);
     else
-        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W, H,
-                           gains, use_gain, out, out_pitch, rgba);
+        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, TEX>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut,
+                           W, H, gains, use_gain, out, out_pitch, rgba);
     return hipGetLastError();
+}
+
+// the instance for the frames' staging (dword loads, vignette) and the entries' convention
+template <int MODE, bool TEX>
+static hipError_t launch_tiled_for(bool dw, bool vig, int blocks, const FrameSet& frames, const TiledLut& lut, int W,
+                                   int H, const double* gains, int use_gain, uint8_t* out, int64_t out_pitch,
+                                   const RgbaOut& rgba, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (dw && !vig)
+        return launch_tiled<true, MODE, false, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
+    if (dw)
+        return launch_tiled<true, MODE, true, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
+    if (!vig)
+        return launch_tiled<false, MODE, false, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
+    return launch_tiled<false, MODE, true, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
 }
 
 template <int MODE>
@@ -1379,15 +1400,9 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
             vig |= f.vig != nullptr;
         }
         hipEvent_t e0 = ext_ev ? ev0 : nullptr, e1 = ext_ev ? ev1 : nullptr;
-        hipError_t e;
-        if (dw && !vig)
-            e = launch_tiled<true, MODE, false>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
-        else if (dw)
-            e = launch_tiled<true, MODE, true>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
-        else if (!vig)
-            e = launch_tiled<false, MODE, false>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
-        else
-            e = launch_tiled<false, MODE, true>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
+        const hipError_t e =
+            lut.tex ? launch_tiled_for<MODE, true>(dw, vig, blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1)
+                    : launch_tiled_for<MODE, false>(dw, vig, blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
         if (e != hipSuccess) return e;
     }
     if (lut.n_wide > 0)

@@ -248,6 +248,7 @@ struct TiledLut {
     const uint16_t* grp0;         // staging groups of each item's first kGroupFirst chunks (kGroupFirst * 64 per item)
     const uint16_t* grp1;         // the items' further chunks
     uint32_t n_grp1;              // entries of grp1
+    int tex;                      // staged entries are texture-convention ones (tiled_entry_tex)
 };
 constexpr int kMetaWords = 1 + kTileSlots;
 constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter
@@ -268,6 +269,12 @@ constexpr uint32_t kCodeNoGain = 1u << 16;
 // staging area, fxy = fx | fy << 5.
 __host__ __device__ constexpr uint32_t tiled_entry(uint32_t off, uint32_t fxy, uint32_t slot, bool nogain) {
     return (nogain ? kEntryNoGain : 0u) | (fxy & 1023u) << 3 | off << 13 | slot << kEntrySlotShift;
+}
+
+// A staged texture-convention pixel (make_entry_tex with all four taps inside the image): bit 0 "no gain",
+// bits 1-8 alpha, 9-16 beta (8-bit fractions), 17-28 the tap's LDS dword offset, 30-31 the slot.
+__host__ __device__ constexpr uint32_t tiled_entry_tex(uint32_t off, uint32_t ab, uint32_t slot, bool nogain) {
+    return (nogain ? kEntryNoGain : 0u) | (ab & 0xFFFFu) << 1 | (off >> 2) << 17 | slot << kEntrySlotShift;
 }
 
 // 128 x 8 halves per item of the tiled composite (kItemHalves): the tiler's qpl.

@@ -8,6 +8,7 @@
 // pixel as a 4-byte box-relative LDS byte offset + fractions + slot; jobs that do not
 // fit (> 4 cameras, a box > 256 px, or LDS above kTileLdsBytes) become "wide" with 8-byte entries.
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <cstdlib>
 #include <thread>
@@ -31,6 +32,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     std::vector<std::vector<CompositeEntry>> wide_raw(n_jobs);
     std::vector<std::vector<uint16_t>> grp_job(n_jobs);  // per job its staging groups, chunk-padded
     const int T = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::atomic<int> any_tex{0};  // some staged item holds texture-convention entries (b.tex)
     auto work = [&](int tid) {
         struct Px {
             int slot, x0, y0, fxy, mask, nogain;
@@ -41,7 +43,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             const TileJob& J = jobs[t];
             int cams[8], ns = 0;
             int minx[8], maxx[8], miny[8], maxy[8];
-            bool wide = false;
+            bool wide = false, item_tex = false;
             for (int k = 0; k < item_px; k++) {
                 // half h = k / kTilePx holds rows 8 h .. 8 h + 7; inside it quad-major (lane = quad)
                 const int h = k / kTilePx, q = (k % kTilePx) >> 2, p = k & 3;
@@ -51,22 +53,33 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 raw[k] = e;
                 px[k].mask = 0;
                 if (!(e.code & 0x8000u)) continue;
-                if (e.code & kCodeTex) {  // texture-convention entries: the gather path (clamped taps)
-                    wide = true;
-                    continue;
-                }
                 const int cam = (int)((e.code >> 10) & 31u);
                 const int sx = (int)(int16_t)(e.xy & 0xFFFFu), sy = (int)(int16_t)(e.xy >> 16);
                 const int iw = in_w[cam], ih = in_h[cam];
-                const TapCell tc = tap_cell(e.xy, iw, ih);
-                const int mask = ((tc.ix0 && tc.iy0) ? 1 : 0) | ((tc.ix1 && tc.iy0) ? 2 : 0) |
-                                 ((tc.ix0 && tc.iy1) ? 4 : 0) | ((tc.ix1 && tc.iy1) ? 8 : 0);
-                if (!mask) continue;  // every tap outside: black
-                // a cell straddling the image's left or top edge (only in morphed / external LUTs):
-                // the staged boxes start inside the image, so the tile takes the gather path
-                if (sx < 0 || sy < 0) {
-                    wide = true;
-                    continue;
+                int mask, fxy;
+                if (e.code & kCodeTex) {
+                    // texture-convention entry (make_entry_tex): a cell whose taps the clamp moves (on the
+                    // image's border) takes the gather path; an interior one reads its four taps from the
+                    // staged box like any other, with the 8-bit fractions in a 16-bit code
+                    if (sx < 0 || sy < 0 || sx + 1 >= iw || sy + 1 >= ih) {
+                        wide = true;
+                        continue;
+                    }
+                    mask = 15;
+                    fxy = (int)((e.code & 255u) | ((e.code >> 17) & 255u) << 8);
+                    item_tex = true;
+                } else {
+                    const TapCell tc = tap_cell(e.xy, iw, ih);
+                    mask = ((tc.ix0 && tc.iy0) ? 1 : 0) | ((tc.ix1 && tc.iy0) ? 2 : 0) | ((tc.ix0 && tc.iy1) ? 4 : 0) |
+                           ((tc.ix1 && tc.iy1) ? 8 : 0);
+                    if (!mask) continue;  // every tap outside: black
+                    // a cell straddling the image's left or top edge (only in morphed / external LUTs):
+                    // the staged boxes start inside the image, so the tile takes the gather path
+                    if (sx < 0 || sy < 0) {
+                        wide = true;
+                        continue;
+                    }
+                    fxy = (int)(e.code & 1023u);
                 }
                 // here sx < iw and sy < ih; the +1 taps may sit on the zero column / row just past
                 // the image, which the box then includes
@@ -88,7 +101,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 maxx[sl] = std::max(maxx[sl], x1);
                 miny[sl] = std::min(miny[sl], y0);
                 maxy[sl] = std::max(maxy[sl], y1);
-                px[k] = Px{sl, x0, y0, (int)(e.code & 1023u), mask, (e.code & kCodeNoGain) ? 1 : 0};
+                px[k] = Px{sl, x0, y0, fxy, mask, (e.code & kCodeNoGain) ? 1 : 0};
             }
             if (ns > kTileSlots) wide = true;
             TileSlot ts[kTileSlots] = {};
@@ -237,6 +250,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 G.clear();
                 continue;
             }
+            if (item_tex) any_tex = 1;
             b.hdr[t] = TileHdr{(uint32_t)J.tx | ((uint32_t)J.ty << 16),
                                (uint32_t)ns | (chunks << 8) | ((uint32_t)J.cam << 16),
                                2 * groups, stride};
@@ -246,13 +260,15 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
                 if (!px[k].mask) continue;  // black
                 const TileSlot& sl = ts[px[k].slot];
                 const uint32_t off = sl.lds + (uint32_t)(px[k].y0 - sl.by0) * stride + (uint32_t)(px[k].x0 - sl.bx0);
-                out[k] = tiled_entry(off * 4u, (uint32_t)px[k].fxy, (uint32_t)px[k].slot, px[k].nogain != 0);
+                out[k] = item_tex ? tiled_entry_tex(off * 4u, (uint32_t)px[k].fxy, (uint32_t)px[k].slot, px[k].nogain != 0)
+                                  : tiled_entry(off * 4u, (uint32_t)px[k].fxy, (uint32_t)px[k].slot, px[k].nogain != 0);
             }
         }
     };
     std::vector<std::thread> th;
     for (int i = 0; i < T; i++) th.emplace_back(work, i);
     for (auto& x : th) x.join();
+    b.tex = any_tex.load();
     // staged items: the non-wide jobs in job order, compacted in place; wide jobs in job order
     int n_items = 0;
     for (int t = 0; t < n_jobs; t++) {
@@ -438,7 +454,7 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     if (b.item_flags.empty()) g0_bytes = 4.0 * kTilePx * ((double)b.n_items * b.qpl + b.n_wide);  // no flags: every half
     stats = b.stats;
     view = TiledLut{meta.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
-                    b.qpl, grp0.p, grp1.p, (uint32_t)b.grp1.size()};
+                    b.qpl, grp0.p, grp1.p, (uint32_t)b.grp1.size(), b.tex};
 }
 
 void SourceFootprint::init(const std::vector<int>& in_w, const std::vector<int>& in_h) {
