@@ -210,6 +210,11 @@ typedef struct octvr_async octvr_async;
 int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
                        const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
                        const double* output_regions, octvr_async** async);
+/* The same with mapper creation flags for every mapper (octvr_mapper_create_ex; OCTVR_REMAP_TEXTURE keeps
+ * the reference's CUDA sampling, which its AsyncMultiMapper runs through vr::Mapper). */
+int octvr_async_create_ex(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
+                          const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
+                          const double* output_regions, int flags, octvr_async** async);
 /* push(inputs, output) (async.cpp:174-189): in_planes[3*i+0/1/2] = Y, U, V host planes of input i
  * (W x H, W/2 x H/2, W/2 x H/2) with row pitches in_pitches[3*i+k]; out_planes[0/1/2] / out_pitches: the
  * merged output's Y (out_w x out_h), U and V (out_w/2 x out_h/2) planes.  Returns once the frame is queued;

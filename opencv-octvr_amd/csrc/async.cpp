@@ -409,6 +409,13 @@ extern "C" {
 int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
                        const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
                        const double* output_regions, octvr_async** out) {
+    return octvr_async_create_ex(rigs, n_rigs, device, n_inputs, in_w, in_h, out_w, out_h, blend_modes, gain_modes,
+                                 output_regions, 0, out);
+}
+
+int octvr_async_create_ex(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
+                          const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
+                          const double* output_regions, int flags, octvr_async** out) {
     try {
         REQUIRE(rigs && n_rigs > 0 && in_w && in_h && blend_modes && gain_modes && output_regions && out,
                 "NULL argument");
@@ -436,8 +443,8 @@ int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int
             a->regions_uv.push_back(c);
             octvr_mapper* m = nullptr;
             // Mapper(mts[i], in_sizes, blend_modes[i], gain_modes[i] >= 0, r.size()) (async.cpp:250-255)
-            const int rc = octvr_mapper_create(rigs[k], device, n_inputs, in_w, in_h, blend_modes[k],
-                                               gain_modes[k] >= 0 ? 1 : 0, r.w, r.h, &m);
+            const int rc = octvr_mapper_create_ex(rigs[k], device, n_inputs, in_w, in_h, blend_modes[k],
+                                                  gain_modes[k] >= 0 ? 1 : 0, r.w, r.h, flags, &m);
             if (rc != OCTVR_OK) throw OctvrError(rc, std::string("mapper ") + std::to_string(k) + ": " + octvr_last_error());
             a->mappers.push_back(m);
             REQUIRE(mapper_num_inputs(m) == n_inputs, "every rig must have n_inputs inputs (no overlays)");

@@ -91,6 +91,10 @@ _lib.octvr_mapper_destroy.restype = None
 _lib.octvr_async_create.argtypes = [C.POINTER(_VP), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                     C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_double),
                                     C.POINTER(_VP)]
+if hasattr(_lib, "octvr_async_create_ex"):
+    _lib.octvr_async_create_ex.argtypes = [C.POINTER(_VP), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                           C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
+                                           C.POINTER(C.c_double), C.c_int, C.POINTER(_VP)]
 _lib.octvr_async_push.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), C.POINTER(_VP), C.POINTER(C.c_size_t)]
 _lib.octvr_async_pop.argtypes = [_VP]
 _lib.octvr_async_pending.argtypes = [_VP, C.POINTER(C.c_int)]
@@ -482,7 +486,9 @@ class AsyncMultiMapper:
     templates: list of MapperTemplate (all with the same inputs); output_regions: list of (x, y, w, h)
     fractions of out_size; gain_modes[i]: -1 no gain, i estimate, j < i reuse mapper j's gains."""
 
-    def __init__(self, templates, in_sizes, out_size, blend_modes, gain_modes, output_regions, device=0):
+    def __init__(self, templates, in_sizes, out_size, blend_modes, gain_modes, output_regions, device=0, remap="remap"):
+        if remap not in ("remap", "texture"):
+            raise ValueError("remap must be 'remap' or 'texture'")
         k, n = len(templates), len(in_sizes)
         rigs = (_VP * k)(*[t._h.value for t in templates])
         w = (C.c_int * n)(*[s[0] for s in in_sizes])
@@ -491,7 +497,11 @@ class AsyncMultiMapper:
         gm = (C.c_int * k)(*gain_modes)
         rg = (C.c_double * (4 * k))(*[float(v) for r in output_regions for v in r])
         hd = _VP()
-        _check(_lib.octvr_async_create(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg, C.byref(hd)))
+        if remap == "texture":
+            _check(_lib.octvr_async_create_ex(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg,
+                                              REMAP_TEXTURE, C.byref(hd)))
+        else:
+            _check(_lib.octvr_async_create(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg, C.byref(hd)))
         self._h = hd
         self._templates = list(templates)  # the mappers copy what they need; kept for symmetry with the reference
         self.n = n

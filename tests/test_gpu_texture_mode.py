@@ -111,6 +111,39 @@ def test_gpu_texture_mode_scaled_vignette_inflight(product_lib):
         assert np.array_equal(o.cpu().numpy(), want)
 
 
+def test_gpu_texture_mode_async(product_lib):
+    """AsyncMultiMapper with the texture convention (octvr_async_create_ex): two regions (copy chain and
+    multi-band, the second reusing the first's gains), frames pipelined, each region equal to the oracle's."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    W, H, sizes, rois, maps1, maps2, masks, seams = _case("rigB")
+    mts = [ox.MapperTemplate.from_arrays(W, H, rois, maps1, maps2, masks, seams) for _ in range(2)]
+    blends, gain_modes = [0, 16], [0, 0]
+    am = ox.AsyncMultiMapper(mts, sizes, (W, 2 * H), blends, gain_modes, [(0.0, 0.0, 1.0, 0.5), (0.0, 0.5, 1.0, 0.5)],
+                             remap="texture")
+    frames, outs = [], []
+    for f in range(4):
+        fr = [synthetic.smooth_yuv_frame(w, h, 60 + 10 * f + i) for i, (w, h) in enumerate(sizes)]
+        out = (np.zeros((2 * H, W), np.uint8), np.zeros((H, W // 2), np.uint8), np.zeros((H, W // 2), np.uint8))
+        am.push([(x[:h], x[h:, :w // 2], x[h:, w // 2:]) for x, (w, h) in zip(fr, sizes)], out)
+        frames.append(fr)
+        outs.append(out)
+    for f in range(4):
+        am.pop()
+        g0 = None
+        for k, bl in enumerate(blends):
+            want, g = O.stitch_frame(frames[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=g0,
+                                     blend=bl, seams=seams, threads=8, remap_tex=True)
+            g0 = g
+            y0 = k * H
+            assert np.array_equal(outs[f][0][y0:y0 + H], want[:H]), (f, k)
+            assert np.array_equal(outs[f][1][y0 // 2:(y0 + H) // 2], want[H:, :W // 2]), (f, k)
+            assert np.array_equal(outs[f][2][y0 // 2:(y0 + H) // 2], want[H:, W // 2:]), (f, k)
+    am.close()
+
+
 def test_texture_mode_rejects_unknown_flags(product_lib):
     ox = product_lib
     W, H, sizes, rois, maps1, maps2, masks, seams = _case("rigA")
