@@ -527,7 +527,8 @@ class AsyncMultiMapper {
 public:
     static AsyncMultiMapper* New(const std::vector<MapperTemplate>& mts, std::vector<cv::Size> in_sizes,
                                  cv::Size out_size, std::vector<int> blend_modes, std::vector<int> gain_modes,
-                                 std::vector<cv::Rect_<double>> output_regions, cv::Size preview_size);
+                                 std::vector<cv::Rect_<double>> output_regions, cv::Size preview_size,
+                                 int flags = 0);  // flags (not in the reference): octvr_async_create_ex
     // Push one frame, in YUV420P format: per input (Y, U, V) host planes; the output's (Y, U, V) planes
     virtual void push(std::vector<std::tuple<cv::Mat, cv::Mat, cv::Mat>>& inputs,
                       std::tuple<cv::Mat, cv::Mat, cv::Mat>& output) = 0;
@@ -540,7 +541,7 @@ class AsyncMultiMapperImpl : public AsyncMultiMapper {
 public:
     AsyncMultiMapperImpl(const std::vector<MapperTemplate>& mts, std::vector<cv::Size> in_sizes, cv::Size out_size,
                          std::vector<int> blend_modes, std::vector<int> gain_modes,
-                         std::vector<cv::Rect_<double>> output_regions) {
+                         std::vector<cv::Rect_<double>> output_regions, int flags = 0) {
         const size_t k = mts.size();
         if (blend_modes.size() != k || gain_modes.size() != k || output_regions.size() != k)
             throw cv::Exception(OCTVR_E_INVALID, "one blend mode, gain mode and output region per template");
@@ -559,8 +560,8 @@ public:
         for (const cv::Rect_<double>& r : output_regions) reg.insert(reg.end(), {r.x, r.y, r.width, r.height});
         n_ = (int)in_sizes.size();
         octvr_async* a = nullptr;
-        check(octvr_async_create(rp.data(), (int)k, device(), n_, w.data(), h.data(), out_size.width, out_size.height,
-                                 blend_modes.data(), gain_modes.data(), reg.data(), &a));
+        check(octvr_async_create_ex(rp.data(), (int)k, device(), n_, w.data(), h.data(), out_size.width,
+                                    out_size.height, blend_modes.data(), gain_modes.data(), reg.data(), flags, &a));
         a_ = a;
     }
     ~AsyncMultiMapperImpl() override { octvr_async_destroy(a_); }
@@ -602,9 +603,10 @@ private:
 inline AsyncMultiMapper* AsyncMultiMapper::New(const std::vector<MapperTemplate>& mts, std::vector<cv::Size> in_sizes,
                                                cv::Size out_size, std::vector<int> blend_modes,
                                                std::vector<int> gain_modes,
-                                               std::vector<cv::Rect_<double>> output_regions, cv::Size preview_size) {
+                                               std::vector<cv::Rect_<double>> output_regions, cv::Size preview_size,
+                                               int flags) {
     (void)preview_size;  // Qt shared-memory preview (async.cpp:113-172): not part of the stitching path
-    return new detail::AsyncMultiMapperImpl(mts, in_sizes, out_size, blend_modes, gain_modes, output_regions);
+    return new detail::AsyncMultiMapperImpl(mts, in_sizes, out_size, blend_modes, gain_modes, output_regions, flags);
 }
 
 // FastMapper (octvr.hpp:123-144, mapper_fast.cpp:27-195): the feather-blended NV12 stitch.
