@@ -286,9 +286,10 @@ int octvr_debug_fastmapper_audit(const octvr_rig* rig, int n_inputs, const int* 
 /* The blend = 0 composite's tiling on the host only (no GPU): the copy chain's winner per output pixel,
  * then the tiled LUT exactly as octvr_mapper_create builds it — including its check that every tap of
  * every pixel lies in a staged group of its slot (OCTVR_E_INVALID otherwise) — reported as JSON (items,
- * wide tiles, staged pixels against the boxes' pixels, bytes, chunk histogram). */
-int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, char* json,
-                               size_t len);
+ * wide tiles, staged pixels against the boxes' pixels, bytes, chunk histogram).  flags: the mapper's
+ * creation flags (OCTVR_REMAP_TEXTURE: texture-convention entries, interior ones staged, border tiles wide). */
+int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, int flags,
+                               char* json, size_t len);
 /* The rig-config JSON reader on one document: the first number of `json` (a number, or the first element
  * of an array), parsed with rapidjson's rules (flags 0, as the reference reads its configs) or correctly
  * rounded (OCTVR_JSON_EXACT; out-of-range literals give +-HUGE_VAL / the subnormal / 0 as strtod). */

@@ -1854,10 +1854,12 @@ int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, co
     });
 }
 
-int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, char* json,
-                               size_t len) {
+int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, int flags,
+                               char* json, size_t len) {
     return guarded([&] {
         REQUIRE(rig && in_w && in_h && json && len > 0, "bad arguments");
+        REQUIRE((flags & ~OCTVR_REMAP_TEXTURE) == 0, "unknown mapper flags");
+        const bool tex = (flags & OCTVR_REMAP_TEXTURE) != 0;
         const int n = (int)rig->inputs.size();
         REQUIRE(n_inputs == n && n > 0 && n <= kMaxCams, "in_sizes must cover the inputs");
         const int W = rig->out_w, H = rig->out_h;
@@ -1872,7 +1874,9 @@ int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in
                 for (int rx = 0; rx < in.roi[2]; rx++) {
                     const size_t k = (size_t)ry * in.roi[2] + rx;
                     if (!in.mask[k]) continue;
-                    lut[y * W + (size_t)(rx + in.roi[0])] = make_entry(in.map1[k], in.map2[k], (float)in_w[i], (float)in_h[i], i);
+                    lut[y * W + (size_t)(rx + in.roi[0])] =
+                        tex ? make_entry_tex(in.map1[k], in.map2[k], (float)in_w[i], (float)in_h[i], i)
+                            : make_entry(in.map1[k], in.map2[k], (float)in_w[i], (float)in_h[i], i);
                 }
             }
         });
@@ -1925,9 +1929,11 @@ int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in
                                 const uint32_t* e = E + (size_t)h * kTilePx + (size_t)(w * 64 + half * 32) * 4 + p;
                                 for (int r = 0; r < 2; r++)
                                     for (int c = 0; c < 2; c++) {
-                                        for (int l = 0; l < 32; l++) a[l] = ((e[l * 4] >> 13) & 0x3FFFu) / 4u + r * S + c;
+                                        for (int l = 0; l < 32; l++)
+                                            a[l] = (b.tex ? (e[l * 4] >> 17) & 0xFFFu : ((e[l * 4] >> 13) & 0x3FFFu) / 4u) + r * S + c;
                                         group_cost(a, 1, 32, 32, tap_cyc, tap_extra);
                                     }
+                                if (b.tex) continue;  // the texture filter reads no weight table
                                 for (int l = 0; l < 32; l++) {
                                     const uint32_t d = (0x4000u | (e[l * 4] & 0x1FF8u)) / 4u;
                                     a[2 * l] = d;
@@ -1967,11 +1973,11 @@ int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in
         for (int i = 0; i < n; i++) frame_bytes += 1.5 * in_w[i] * in_h[i];
         char tmp[1024];
         snprintf(tmp, sizeof tmp,
-                 "{\"footprint_bytes\": %.0f, \"frame_bytes\": %.0f, \"lds_model\": {\"tap_cycles\": %.0f, \"tap_extra\": %.0f, \"wtab_cycles\": %.0f, "
+                 "{\"tex\": %d, \"footprint_bytes\": %.0f, \"frame_bytes\": %.0f, \"lds_model\": {\"tap_cycles\": %.0f, \"tap_extra\": %.0f, \"wtab_cycles\": %.0f, "
                  "\"wtab_extra\": %.0f, \"stage_cycles\": %.0f, \"stage_extra\": %.0f}, "
                  "\"items\": %d, \"wide_tiles\": %d, \"staged_px\": %.0f, \"box_px\": %.0f, \"staged_bytes\": %.0f, "
                  "\"source_bytes\": %.0f, \"grp1_entries\": %zu, ",
-                 foot, frame_bytes, tap_cyc, tap_extra, wt_cyc, wt_extra, st_cyc, st_extra, b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
+                 b.tex, foot, frame_bytes, tap_cyc, tap_extra, wt_cyc, wt_extra, st_cyc, st_extra, b.n_items, b.n_wide, b.staged_bytes / 2.0, box_px, b.staged_bytes, b.source_bytes,
                  b.grp1.size());
         std::string js = std::string(tmp) + b.stats + "}";
         REQUIRE(js.size() < len, "buffer too small");

@@ -110,8 +110,8 @@ _lib.octvr_fastmapper_destroy.restype = None
 if hasattr(_lib, "octvr_debug_json_number"):
     _lib.octvr_debug_json_number.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_double)]
 if hasattr(_lib, "octvr_debug_tiled_lut_info"):
-    _lib.octvr_debug_tiled_lut_info.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_char_p,
-                                                C.c_size_t]
+    _lib.octvr_debug_tiled_lut_info.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
+                                                C.c_char_p, C.c_size_t]
 if hasattr(_lib, "octvr_debug_fastmapper_audit"):
     _lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
                                                   C.c_int, C.c_char_p, C.c_size_t]
@@ -141,14 +141,14 @@ def debug_project_f64(rig_json, out_w, out_h, input, device=0, where=0):
     return x, y, (f if where == 0 else None)
 
 
-def debug_tiled_lut_info(mt, in_sizes):
+def debug_tiled_lut_info(mt, in_sizes, remap="remap"):
     """The blend = 0 composite's tiled LUT built on the host (octvr_debug_tiled_lut_info; no GPU), with its
     staged-group coverage check: a dict of items, wide tiles, staged / box pixels, bytes, histograms."""
     n = len(in_sizes)
     w = (C.c_int * n)(*[s[0] for s in in_sizes])
     h = (C.c_int * n)(*[s[1] for s in in_sizes])
     buf = C.create_string_buffer(4096)
-    _check(_lib.octvr_debug_tiled_lut_info(mt._h, n, w, h, buf, len(buf)))
+    _check(_lib.octvr_debug_tiled_lut_info(mt._h, n, w, h, REMAP_TEXTURE if remap == "texture" else 0, buf, len(buf)))
     import json as _json
     return _json.loads(buf.value.decode())
 

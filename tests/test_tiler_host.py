@@ -29,6 +29,28 @@ def test_tiled_lut_golden_rigs(product_lib, name):
     assert sum(info["items_by_lds_kib"]) == info["items"]
 
 
+@pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
+def test_tiled_lut_texture_convention(product_lib, name):
+    """OCTVR_REMAP_TEXTURE entries (make_entry_tex): pixels whose four clamped taps lie inside the image are
+    staged (16-bit fraction codes, tiled_entry_tex) under the same staged-group check; tiles with a border
+    pixel take the gather path."""
+    ox = product_lib
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), [z[f"map1_{i}"] for i in range(n)],
+                                       [z[f"map2_{i}"] for i in range(n)], [z[f"mask_{i}"] for i in range(n)])
+    sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
+    base = ox.debug_tiled_lut_info(mt, sizes)
+    info = ox.debug_tiled_lut_info(mt, sizes, remap="texture")
+    assert base["tex"] == 0
+    assert info["items"] + info["wide_tiles"] // 2 >= 1
+    if info["items"]:
+        assert info["tex"] == 1 and 0 < info["staged_px"] <= info["box_px"]
+    # border taps move tiles to the gather path, never the other way
+    assert info["wide_tiles"] >= base["wide_tiles"]
+
+
 def test_tiled_lut_rejects_short_sizes(product_lib):
     ox = product_lib
     rig, z = O.load_rig("rigA")
@@ -54,3 +76,7 @@ def test_tiled_lut_c2(product_lib):
     # every item fits the 16 KiB tile LDS; no item needs more than 4 staging chunks
     assert info["items_by_lds_kib"][5:] == [0, 0]
     assert sum(v for k, v in info["items_by_chunks"].items() if int(k) > 4) == 0
+    # the texture convention stages the same rig with one more column / row of taps per cell at most
+    tex = ox.debug_tiled_lut_info(mt, sizes, remap="texture")
+    assert tex["tex"] == 1 and tex["items"] + tex["wide_tiles"] // 2 == info["items"]
+    assert tex["wide_tiles"] < 0.05 * info["items"]
