@@ -48,13 +48,15 @@ __host__ __device__ inline CompositeEntry make_entry(float m1, float m2, float w
 // orc_fast_remap_tex_rgba models NVIDIA's filter: X = fl32(u W) - 0.5, i0 = floor(X), alpha =
 // floor(frac(X) 256) / 256 (8 fractional bits), taps (i0, i0 + 1) x (j0, j0 + 1) clamped to the image and
 // all four used.  xy: (i0, j0) kept in [-1, size - 1] (the same taps under the clamp); code: alpha | cam <<
-// 10 | valid << 15 | beta << 17 | kCodeTex.  u < 0 or NaN: invalid (fast_remap's fill_zero).  Tiles holding
+// 10 | valid << 15 | beta << 17 | kCodeTex.  u < 0, NaN or infinite coordinates: invalid (black).  Tiles holding
 // such entries always take the gather path (tiling.cpp), whose taps and weights test kCodeTex.
 constexpr uint32_t kCodeTex = 1u << 31;
 __host__ __device__ inline CompositeEntry make_entry_tex(float m1, float m2, float w, float h, int cam) {
     CompositeEntry e{0u, 0u};
-    if (!(m1 >= 0.f) || m2 != m2) return e;
     const float xb = m1 * w - 0.5f, yb = m2 * h - 0.5f;
+    // u < 0: fill_zero; NaN or an infinite coordinate: the model's weights are NaN and every channel
+    // saturates to 0 — the same black
+    if (!(m1 >= 0.f) || !(fabsf(xb) <= 3.0e38f) || !(fabsf(yb) <= 3.0e38f)) return e;
     const float fx = floorf(xb), fy = floorf(yb);
     const uint32_t a = (uint32_t)floorf((xb - fx) * 256.f), b = (uint32_t)floorf((yb - fy) * 256.f);
     const int i0 = (int)fminf(fmaxf(fx, -1.f), w - 1.f), j0 = (int)fminf(fmaxf(fy, -1.f), h - 1.f);

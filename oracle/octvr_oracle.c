@@ -1500,8 +1500,9 @@ void orc_fast_remap_tex_rgba(const uint8_t* src, int w, int h, size_t spitch, co
         for (int x = 0; x < mw; x++) {
             float u = map1[(size_t)y * mpitch + x], v = map2[(size_t)y * mpitch + x];
             uint8_t* o = dst + (size_t)y * dpitch + (size_t)x * 4;
-            if (!(u >= 0) || v != v) { o[0] = o[1] = o[2] = o[3] = 0; continue; } /* u < 0 (and NaN): fill_zero */
             float xb = u * (float)w - 0.5f, yb = v * (float)h - 0.5f;
+            /* u < 0: fill_zero; NaN / infinite coordinates give NaN weights, i.e. 0 in every channel */
+            if (!(u >= 0) || !(fabsf(xb) <= 3.0e38f) || !(fabsf(yb) <= 3.0e38f)) { o[0] = o[1] = o[2] = o[3] = 0; continue; }
             float fx = floorf(xb), fy = floorf(yb);
             float a = floorf((xb - fx) * 256.f) / 256.f, b = floorf((yb - fy) * 256.f) / 256.f;
             /* the cell index, limited to [-1, size - 1] first (the same taps after the clamps below) */
