@@ -150,3 +150,40 @@ def test_texture_mode_rejects_unknown_flags(product_lib):
     mt = ox.MapperTemplate.from_arrays(W, H, rois, maps1, maps2, masks, seams)
     with pytest.raises(ValueError):
         ox.Mapper(mt, sizes, remap="nearest")
+
+
+def test_gpu_texture_mode_edge_maps(product_lib):
+    """Map values the texture convention must treat like the oracle: u < 0 (fill_zero), NaN and infinite
+    values, values far outside the image (clamped taps), taps on every edge (border tiles through the
+    gather path, interior ones staged), two cameras with fixed gains."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    W, H = 256, 64
+    sizes = [(96, 48), (64, 32)]
+    rng = np.random.default_rng(5)
+    m1 = [rng.uniform(-0.2, 1.2, (H, W)).astype(np.float32) for _ in sizes]
+    m2 = [rng.uniform(-0.2, 1.2, (H, W)).astype(np.float32) for _ in sizes]
+    for m in m1 + m2:  # specials scattered over both cameras
+        flat = m.reshape(-1)
+        idx = rng.choice(flat.size, 400, replace=False)
+        flat[idx[:100]] = np.nan
+        flat[idx[100:200]] = np.inf
+        flat[idx[200:300]] = -np.inf
+        flat[idx[300:]] = rng.choice(np.array([1e6, -1e6, 0.0, 1.0, 3e38], np.float32), 100)
+    m1[0][:, :W // 2] = np.linspace(0.0, 1.0, W // 2, dtype=np.float32)[None, :]  # a smooth interior band
+    m2[0][:, :W // 2] = np.linspace(0.02, 0.98, H, dtype=np.float32)[:, None]
+    mk = [np.full((H, W), 255, np.uint8) for _ in sizes]
+    mk[1][:, : W // 3] = 0
+    mt = ox.MapperTemplate.from_arrays(W, H, [[0, 0, W, H]] * 2, m1, m2, mk)
+    frames = [synthetic.yuv_frame(w, h, 77 + i) for i, (w, h) in enumerate(sizes)]
+    gains = [1.07, 0.93]
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True, remap="texture")
+    out = torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda")
+    m.stitch([torch.from_numpy(f).cuda() for f in frames], out, gains=gains)
+    torch.cuda.synchronize()
+    want, _ = O.stitch_frame(frames, sizes, [[0, 0, W, H]] * 2, m1, m2, mk, W, H, enable_gain=True, gains=gains,
+                             threads=4, remap_tex=True)
+    got = out.cpu().numpy()
+    d = got != want
+    assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
