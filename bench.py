@@ -132,9 +132,10 @@ def lib_sha256():
 
 
 def pmc_traffic(config, blend):
-    """(bytes, source) — per composite launch (blend 0) or per frame over the whole blend sequence
-    (blend > 0) — from the profiles/*_pmc_<config>.json whose so_sha256 is the running library's;
-    (None, reason) when no summary of this binary exists."""
+    """(bytes, source) — per composite launch (blend 0) or per frame over the blend sequence (blend > 0:
+    the remap, pyrDown and blend launches, i.e. what bytes_per_launch models and kernel_us times; the gain
+    feed runs before the sequence and is excluded as for blend 0) — from the profiles/*_pmc_<config>.json
+    whose so_sha256 is the running library's; (None, reason) when no summary of this binary exists."""
     import glob
     sha = lib_sha256()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % config))):
@@ -142,7 +143,10 @@ def pmc_traffic(config, blend):
         if d.get("so_sha256") != sha:
             continue
         if blend > 0:
-            return round(d["traffic_per_frame_bytes"]), os.path.basename(path)
+            seq = [v for k, v in d.get("traffic_bytes", {}).items() if "gain_feed" not in k]
+            if seq:
+                return round(sum(seq)), os.path.basename(path)
+            continue
         hit = [v for k, v in d.get("traffic_bytes", {}).items() if "stitch_tiled_kernel" in k]
         if hit:
             return round(hit[0]), os.path.basename(path)
