@@ -31,7 +31,12 @@ def test_pmc_traffic_keyed_to_library(bench_at):
     _write(d, "r01_pmc_C2.json", "b" * 64, per_launch=1.0)  # another binary: skipped
     _write(d, "r02_pmc_C2.json", "a" * 64, per_launch=1234.4, per_frame=99.6)
     assert bench.pmc_traffic("C2", 0) == (1234, "r02_pmc_C2.json")  # the composite launch
-    assert bench.pmc_traffic("C2", 3) == (100, "r02_pmc_C2.json")  # the whole blend sequence per frame
+    # blend > 0: the blend sequence per frame, every kernel but the gain feed (outside the timed events)
+    (d / "profiles" / "r03_pmc_C3.json").write_text(json.dumps({
+        "so_sha256": "a" * 64, "traffic_per_frame_bytes": 1e9,
+        "traffic_bytes": {"octvr::gain_feed_lean_kernel(...)": 500.0, KERNEL: 1000.4, "octvr::mb_down_kernel@1": 200.2,
+                          "octvr::mb_blend_kernel@2": 30.0}}))
+    assert bench.pmc_traffic("C3", 3) == (1231, "r03_pmc_C3.json")
 
 
 def test_pmc_traffic_absent_for_other_binaries(bench_at):
