@@ -181,7 +181,7 @@ def pmc_valu_busy(config):
     return None
 
 
-def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=24, footprint_bytes=None):
+def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, footprint_bytes=None):
     """AsyncMultiMapper end to end (async.cpp:32-193): host YUV420P planes pushed, the bytes the mapper
     reads (its source footprint) copied into pinned staging and uploaded, stitched, downloaded and copied
     out, 3 frames in flight (the reference's BUF_SIZE, async.cpp:261-310).  PCIe-inclusive: reported
