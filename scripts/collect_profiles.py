@@ -35,7 +35,10 @@ def main():
             continue
         cfg, inf = os.path.basename(d)[len(tag) + 4:].split("_if")
         st = os.path.join(d, "run_kernel_stats.csv")
-        if os.path.exists(st):
+        # --stats averages are per-kernel durations only with one frame in flight: with several, launches
+        # on different streams overlap and a launch's span exceeds the step time (the trace union,
+        # scripts/union_check.py, is that run's evidence instead)
+        if os.path.exists(st) and inf == "1":
             shutil.copy(st, os.path.join(P, "%s_%s_inflight%s_kernel_stats.csv" % (tag, cfg, inf)))
         tr = os.path.join(d, "run_kernel_trace.csv")
         if cfg == "C3" and inf == "1" and os.path.exists(tr):
