@@ -73,6 +73,10 @@ def test_tiled_lut_c2(product_lib):
     assert info["wide_tiles"] == 0
     assert info["box_px"] == pytest.approx(17.37e6, rel=0.01)
     assert info["staged_px"] == pytest.approx(10.06e6, rel=0.01)
+    # the composite's source footprint (what the AsyncMultiMapper uploads, gain samples aside): the union
+    # of the staged groups, 13 % of the frames' YUV
+    assert info["footprint_bytes"] == pytest.approx(info["source_bytes"], rel=0.01)
+    assert info["footprint_bytes"] < 0.15 * info["frame_bytes"]
     # every item fits the 16 KiB tile LDS; no item needs more than 4 staging chunks
     assert info["items_by_lds_kib"][5:] == [0, 0]
     assert sum(v for k, v in info["items_by_chunks"].items() if int(k) > 4) == 0
