@@ -327,9 +327,11 @@ struct OutFrame {
     uint32_t u_off, v_off;  // byte offsets of the U and V planes
 };
 constexpr uint32_t kDropOffset = 0x7FFFFFC0u;  // > any valid output byte (host: frame < 2^31 - 64 B)
-// Cache-policy bits of the output-frame stores (gfx950: 1 sc0, 2 nt, 16 sc1).  sc1 writes the frame
-// through (nothing of it left dirty in the XCD L2s when the kernel ends): C2 stitch -1.5 %.
-constexpr int kOutPolicy = 16;
+// Cache-policy bits of the output-frame stores (gfx950: 1 sc0, 2 nt, 16 sc1).  nt: streaming stores (no
+// launch reads the frame back): C2 composite 46.1-47.6 against 47.4-51.6 us with sc1 (six interleaved
+// pairs, round 5; sc1 had been 1.5 % faster than the default policy), C4 unchanged; nt | sc1 and sc0 | nt
+// were no better.
+constexpr int kOutPolicy = 2;
 
 __device__ __forceinline__ void store_quad(const OutFrame& o, const QuadOut& q, int x, int y, bool in) {
     const uint32_t oy = in ? (uint32_t)y * o.pitch + (uint32_t)x : kDropOffset;
