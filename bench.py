@@ -31,7 +31,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="ranks (one GPU each); without a launcher's WORLD_SIZE, bench.py starts them itself")
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -46,9 +46,27 @@ def parse():
                     help="skip the AsyncMultiMapper end-to-end (PCIe-inclusive) measurement")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--no-gain", action="store_true", help=argparse.SUPPRESS)  # diagnostic: composite alone
+    ap.add_argument("--preroll", type=float, default=0.5,
+                    help="seconds of untimed steps after the warmup steps, so that the timed steps run at the "
+                         "GPU's settled clock (it idles during setup and takes ~0.1 s to ramp, DESIGN.md §4)")
     ap.add_argument("--remap", default="remap", choices=["remap", "texture"],
                     help="sampling: cv::remap's fixed point (default) or the CUDA texture convention (OCTVR_REMAP_TEXTURE)")
     return ap.parse_args()
+
+
+def preroll(step, seconds, sync, chunk=256):
+    """Untimed steps until `seconds` have passed (in chunks, each synchronised, so the host never queues
+    more than a chunk ahead): the GPU's shader clock falls while the host sets up and ramps back over ~0.1 s
+    of load, which a timed region of a few milliseconds would otherwise partly measure.  Returns the
+    steps run."""
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(chunk):
+            step(n)
+            n += 1
+        sync()
+    return n
 
 
 def cpu_model():
@@ -406,6 +424,7 @@ def fast_rank(args, world, rank, local_rank, dist):
     for k in range(max(args.warmup, inflight, nsets)):  # every stream and frame set once outside the timed region
         step(k)
     torch.cuda.synchronize(dev)
+    n_pre = preroll(step, args.preroll, lambda: torch.cuda.synchronize(dev))
     elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
     # kernel time: events around 16 back-to-back stitches (both plane launches) on one stream, after the
     # timed region
@@ -421,7 +440,7 @@ def fast_rank(args, world, rank, local_rank, dist):
     result = {
         "metric": "stitched megapixels/sec (6x4K->8K equirect, FastMapper NV12)",
         "value": round(aggregate_mps(world, args.steps, W * H, elapsed), 1), "unit": "MP/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "steps": args.steps, "warmup": args.warmup, "preroll": {"s": args.preroll, "steps": n_pre}, "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "host_issue_ms_per_step": round(ISSUE_S[0] * 1e3 / args.steps, 4),
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (splitmix64 frames as NV12, further sets derived by a splitmix64 key, SURVEY.md §8d rig)",
@@ -501,6 +520,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
     for k in range(args.warmup):
         step(k)
     torch.cuda.synchronize(dev)
+    n_pre = preroll(step, args.preroll, lambda: torch.cuda.synchronize(dev))
     m.kernel_time()  # drop anything recorded before the timed region
     # HIP events around the composite.  One frame in flight: every 4th step (an event pair costs ~5 us
     # of that stream's timeline).  Several: every step on every stream, so the union of the launches'
@@ -561,6 +581,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "preroll": {"s": args.preroll, "steps": n_pre},
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
         "host_issue_ms_per_step": round(ISSUE_S[0] * 1e3 / args.steps, 4),
         "higher_is_better": True,

@@ -25,7 +25,7 @@ fi
 timeout -k 10 500 python bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.err \
   || { tail -5 gpurun_out/${TAG}_bench_default.err; exit 1; }
 for CFG in C1 C2 C3 C4 F2; do
-  timeout -k 10 300 python bench.py --config $CFG --steps 50 --warmup 5 --no-async-e2e --no-cpu-baseline \
+  timeout -k 10 300 python bench.py --config $CFG --no-async-e2e --no-cpu-baseline \
     > gpurun_out/${TAG}_bench_$CFG.json 2> gpurun_out/${TAG}_bench_$CFG.err || { echo "$CFG rc=$?"; tail -5 gpurun_out/${TAG}_bench_$CFG.err; exit 1; }
   python3 -c "import json; d=json.loads(open('gpurun_out/${TAG}_bench_$CFG.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$CFG', d['value'], d['ms_per_step'], r['kernel_us'], r['frac'], r.get('traffic'))"
 done
@@ -34,7 +34,7 @@ for spec in C2:1 C2:3 C4:1 C4:3 C3:1 C3:4 C1:3 F2:3; do
   CFG=${spec%:*}; IF=${spec#*:}
   d=gpurun_out/kt_${TAG}_${CFG}_if$IF
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- \
-    python3 bench.py --config $CFG --steps 30 --warmup 5 --inflight $IF --no-cpu-baseline --no-async-e2e \
+    python3 bench.py --config $CFG --steps 200 --warmup 5 --inflight $IF --no-cpu-baseline --no-async-e2e \
     > $d.log 2>&1 || { echo "kt $CFG if$IF rc=$?"; tail -5 $d.log; exit 1; }
   echo "kt $CFG if$IF ok"
 done

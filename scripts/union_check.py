@@ -5,7 +5,8 @@ bench line).  The timed region is bench.py's launches [skip, skip + count) of th
 frame: one setup stitch per frame set, then the warmup, then the timed steps); the union of the intervals
 of every kernel matching `pattern` that starts inside that window, per frame, is the trace's counterpart
 of the line's kernel_us (the union of the HIP-event intervals with frames in flight), and
-bytes_per_launch / union is its achieved rate.
+bytes_per_launch / union is its achieved rate.  The line's own preroll steps (bench.py --preroll) are added to
+`skip`, and `count` defaults to the line's timed steps.
 
     python scripts/union_check.py <kt dir> <pattern regex> <anchor regex> [skip [count]] > out.json
 """
@@ -18,8 +19,12 @@ import sys
 
 def main():
     d, pat, anchor = sys.argv[1], re.compile(sys.argv[2]), re.compile(sys.argv[3])
-    skip = int(sys.argv[4]) if len(sys.argv) > 4 else 13
-    count = int(sys.argv[5]) if len(sys.argv) > 5 else 30
+    line = [l for l in open(d + ".log").read().splitlines() if l.startswith("{")][-1]
+    b = json.loads(line)
+    # the untimed preroll's steps (bench.py --preroll) come after the setup and warmup launches
+    pre = b.get("preroll", {}).get("steps", 0)
+    skip = (int(sys.argv[4]) if len(sys.argv) > 4 else 13) + pre
+    count = int(sys.argv[5]) if len(sys.argv) > 5 else b["steps"]
     rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     anchors = [a for a, b, n in iv if anchor.search(n)]
@@ -36,12 +41,10 @@ def main():
             cb = max(cb, b)
     if cb is not None:
         union += cb - ca
-    line = [l for l in open(d + ".log").read().splitlines() if l.startswith("{")][-1]
-    b = json.loads(line)
     r = b["roofline"]
     u_us = union / count / 1e3
     out = {"trace": os.path.basename(d), "pattern": sys.argv[2], "anchor": sys.argv[3], "frames": count,
-           "skip_first": skip, "launches": len(sel), "union_us_per_frame": round(u_us, 2),
+           "skip_first": skip, "preroll_steps": pre, "launches": len(sel), "union_us_per_frame": round(u_us, 2),
            "line_kernel_us": r["kernel_us"], "line_kernel_us_basis": r.get("kernel_us_basis"),
            "bytes_per_launch": r["bytes_per_launch"], "line_frac": r["frac"],
            "frac_from_trace": round(r["bytes_per_launch"] / (u_us * 1e-6) / 1e9 / r["peak"], 4),
