@@ -53,7 +53,10 @@ def main():
                     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
                     w.writerow([r["Kernel_Name"].split("(")[0], r["Grid_Size_X"], round((s - t0) / 1e3, 2),
                                 round((e - s) / 1e3, 2)])
-    t_session = os.path.getmtime(os.path.join(G, "%s_tests.log" % tag))
+    tests_log = os.path.join(G, "%s_tests.log" % tag)
+    if not os.path.exists(tests_log):  # a bench-only session (PART=B): its PMC summaries are an earlier tag's
+        return
+    t_session = os.path.getmtime(tests_log)
     for d in sorted(glob.glob(os.path.join(G, "pmc_*_if*_so.sha"))):
         if os.path.getmtime(d) < t_session:  # an older session's passes
             continue

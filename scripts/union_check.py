@@ -20,11 +20,11 @@ import sys
 def main():
     d, pat, anchor = sys.argv[1], re.compile(sys.argv[2]), re.compile(sys.argv[3])
     line = [l for l in open(d + ".log").read().splitlines() if l.startswith("{")][-1]
-    b = json.loads(line)
+    bl = json.loads(line)
     # the untimed preroll's steps (bench.py --preroll) come after the setup and warmup launches
-    pre = b.get("preroll", {}).get("steps", 0)
+    pre = bl.get("preroll", {}).get("steps", 0)
     skip = (int(sys.argv[4]) if len(sys.argv) > 4 else 13) + pre
-    count = int(sys.argv[5]) if len(sys.argv) > 5 else b["steps"]
+    count = int(sys.argv[5]) if len(sys.argv) > 5 else bl["steps"]
     rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     anchors = [a for a, b, n in iv if anchor.search(n)]
@@ -41,6 +41,7 @@ def main():
             cb = max(cb, b)
     if cb is not None:
         union += cb - ca
+    b = bl
     r = b["roofline"]
     u_us = union / count / 1e3
     out = {"trace": os.path.basename(d), "pattern": sys.argv[2], "anchor": sys.argv[3], "frames": count,
