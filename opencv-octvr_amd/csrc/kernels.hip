@@ -842,8 +842,11 @@ __device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, 
 
 // The lane's group of an item's chunk c < kGroupFirst (c = the wave: each wave's first chunk), addressed
 // by the item index alone (loop-invariant voffset, scalar soffset), so it is loaded one iteration ahead
-// with the item's metadata.
-__device__ __forceinline__ uint32_t group_issue(const __amdgpu_buffer_rsrc_t& gr, int t, int t_end) {
+// with the item's metadata.  Carried across the loop as the u16 the load returns: as a u32 the compiler
+// zero-extended it right after the load, into the loop-carried register, and that copy waited on every
+// load of the iteration (vmcnt(0) before the compute); widened at the use, an iteration later, it waits
+// on nothing (one frame in flight: C2 composite -1 %, C3 +1 %, `u16`).
+__device__ __forceinline__ uint16_t group_issue(const __amdgpu_buffer_rsrc_t& gr, int t, int t_end) {
     const int tt = t < t_end ? t : 0;
     return __builtin_amdgcn_raw_buffer_load_b16(gr, (uint32_t)threadIdx.x * 2u,
                                                 (uint32_t)uniform(tt) * (uint32_t)(kGroupFirst * 64 * 2), 0);
@@ -1136,7 +1139,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
     uint4 mv = meta_issue(mrsrc, t_mv, t_end);
-    uint32_t mg = group_issue(grsrc, t_mv, t_end);  // the lane's first staging group of item t_mv
+    uint16_t mg = group_issue(grsrc, t_mv, t_end);  // the lane's first staging group of item t_mv
     uint32_t claim = 0u;  // lane 0 of wave 0: returned value of the claim in flight
     bool claimed = false; // a claim for the item after t_n2 is in flight (uniform)
     bool first = true;
