@@ -120,3 +120,22 @@ def test_derived_frame_sets_match_on_device_and_host():
         want = synthetic.derived_frame(t.numpy(), 1107 + i)
         assert np.array_equal(got[i].numpy(), want)
         assert (want != t.numpy()).mean() > 0.9
+
+
+def test_preroll_runs_untimed_chunks_until_the_time_passes():
+    """bench.preroll (the clock-settling steps before the timed region): whole
+    synchronised chunks until `seconds` have passed, step indices consecutive from 0; none for 0 s."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import time
+    import bench
+    seen, syncs = [], []
+
+    def step(k):
+        seen.append(k)
+        time.sleep(0.0005)
+
+    n = bench.preroll(step, 0.05, lambda: syncs.append(len(seen)), chunk=16)
+    assert n == len(seen) and n % 16 == 0 and n >= 16
+    assert seen == list(range(n)) and syncs[-1] == n and all(s % 16 == 0 for s in syncs)
+    assert bench.preroll(step, 0.0, lambda: None) == 0
