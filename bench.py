@@ -11,7 +11,10 @@ Prints ONE JSON line on rank 0.  Extra objects: "roofline" (the composite kernel
 live over the timed region) and "cpu_baseline" (the oracle restatement of the reference CPU path,
 timed on this host).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu-baseline]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2] [--no-cpu-baseline] [--preroll S]
+
+K timed steps (default 1,000) follow W warmup steps and S seconds (default 0.5) of untimed preroll steps,
+so that the timed region runs at the GPU's settled clock.
 """
 import argparse
 import json
