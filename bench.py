@@ -202,13 +202,15 @@ def pmc_valu_busy(config):
     return None
 
 
-def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, footprint_bytes=None):
+def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, gain=True, remap="remap"):
     """AsyncMultiMapper end to end (async.cpp:32-193): host YUV420P planes pushed, the bytes the mapper
     reads (its source footprint) copied into pinned staging and uploaded, stitched, downloaded and copied
-    out, 3 frames in flight (the reference's BUF_SIZE, async.cpp:261-310).  PCIe-inclusive: reported
-    beside `value`, never as it."""
+    out, 3 frames in flight (the reference's BUF_SIZE, async.cpp:261-310), with the line's own sampling
+    and gain mode.  PCIe-inclusive: reported beside `value`, never as it."""
     import numpy as np
-    am = ox.AsyncMultiMapper([mt], sizes, (W, H), [blend], [0], [(0.0, 0.0, 1.0, 1.0)], device=dev)
+    am = ox.AsyncMultiMapper([mt], sizes, (W, H), [blend], [0 if gain else -1], [(0.0, 0.0, 1.0, 1.0)], device=dev,
+                             remap=remap)
+    info = am.info()
     ins = [(f[:h], f[h:, :w // 2], f[h:, w // 2:]) for f, (w, h) in zip(frames_np, sizes)]
     outs = [(np.empty((H, W), np.uint8), np.empty((H // 2, W // 2), np.uint8), np.empty((H // 2, W // 2), np.uint8))
             for _ in range(4)]
@@ -229,7 +231,8 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, footprint_b
     in_b = sum(w * h * 3 // 2 for w, h in sizes)
     return {"value": round(frames * W * H / 1e6 / dt, 1), "unit": "MP/s", "ms_per_frame": round(dt * 1e3 / frames, 3),
             "frames": frames, "input_bytes_per_frame": in_b,
-            "h2d_bytes_per_frame": int(footprint_bytes) if footprint_bytes else in_b, "d2h_bytes_per_frame": W * H * 3 // 2,
+            "h2d_bytes_per_frame": int(info["packed_bytes"]), "d2h_bytes_per_frame": info["output_bytes"],
+            "gain": "estimated" if gain else "none", "remap": remap,
             "note": "AsyncMultiMapper push->pop of host YUV420P planes: copy-in of the mapper's source footprint to "
                     "pinned staging, H2D, unpack, stitch, D2H, copy-out, 3 frames in flight; PCIe- and "
                     "host-copy-inclusive, not the roofline basis"}
@@ -635,8 +638,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
         "mapper": m.info(),
     }
     if rank == 0 and world == 1 and not args.no_async_e2e:
-        result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev,
-                                        footprint_bytes=result["mapper"].get("footprint_bytes"))
+        result["async_e2e"] = async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, gain=use_gain, remap=args.remap)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(mt, frames_np, sizes, W, H, blend, gain=use_gain)
     return result

@@ -20,8 +20,11 @@
  *   - MapperTemplate copies are independent deep copies (octvr_rig_clone; the reference double-deletes
  *     its camera pointers); output_cam / input_cams stay null (camera models live behind the C ABI).
  *   - create_masks(imgs) with images needs GraphCutSeamFinder: not on the path, throws.
- *   - AsyncMultiMapper's preview_size (Qt shared-memory preview) is ignored; its worker threads are
- *     joined on destruction instead of running forever (async.cpp:337-349).
+ *   - AsyncMultiMapper's preview_size enables the preview in every build (the reference only under
+ *     HAVE_QT5, async.cpp:218-221); with HAVE_QT5 it is written into the reference's two Qt shared-memory
+ *     zones exactly as async.cpp:149-171 does, and AsyncMultiMapper::preview() reads the latest one in any
+ *     build (an addition).  Its worker threads are joined on destruction instead of running forever
+ *     (async.cpp:337-349).
  *   - Mapper::override_logo_option is a no-op (trial-mode logo, licensing code not reproduced).
  */
 #ifndef OCTVR_HPP
@@ -37,6 +40,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstring>
 #include <deque>
 #include <fstream>
 #include <iostream>
@@ -70,6 +74,10 @@
 #include "rapidjson/stringbuffer.h"
 #include "rapidjson/writer.h"
 #endif
+#endif
+
+#ifdef HAVE_QT5
+#include <QSharedMemory>
 #endif
 
 #define OCTVR_PREVIEW_DATA0_MEMORY_KEY "opencv_octvr_preview_0"
@@ -520,6 +528,7 @@ struct PreviewDataHeader {
     int step;
     double fps;
 };
+static_assert(sizeof(PreviewDataHeader) == sizeof(octvr_preview_header), "PreviewDataHeader = octvr_preview_header");
 
 // AsyncMultiMapper (octvr.hpp:103-121, async.cpp:195-350): several mappers over the same frames, each
 // writing its region of one merged output, behind a 3-deep H2D / stitch / D2H pipeline.
@@ -533,6 +542,9 @@ public:
     virtual void push(std::vector<std::tuple<cv::Mat, cv::Mat, cv::Mat>>& inputs,
                       std::tuple<cv::Mat, cv::Mat, cv::Mat>& output) = 0;
     virtual void pop() = 0;
+    // Not in the reference: the latest published preview (CV_8UC3, preview_size) and its header; false
+    // before the first frame completes.  Throws without a preview.
+    virtual bool preview(cv::Mat& rgb, PreviewDataHeader& hdr) = 0;
     virtual ~AsyncMultiMapper() {}
 };
 
@@ -541,7 +553,8 @@ class AsyncMultiMapperImpl : public AsyncMultiMapper {
 public:
     AsyncMultiMapperImpl(const std::vector<MapperTemplate>& mts, std::vector<cv::Size> in_sizes, cv::Size out_size,
                          std::vector<int> blend_modes, std::vector<int> gain_modes,
-                         std::vector<cv::Rect_<double>> output_regions, int flags = 0) {
+                         std::vector<cv::Rect_<double>> output_regions, cv::Size preview_size, int flags = 0)
+        : preview_size_(preview_size.area() > 0 ? preview_size : cv::Size(0, 0)) {
         const size_t k = mts.size();
         if (blend_modes.size() != k || gain_modes.size() != k || output_regions.size() != k)
             throw cv::Exception(OCTVR_E_INVALID, "one blend mode, gain mode and output region per template");
@@ -560,9 +573,19 @@ public:
         for (const cv::Rect_<double>& r : output_regions) reg.insert(reg.end(), {r.x, r.y, r.width, r.height});
         n_ = (int)in_sizes.size();
         octvr_async* a = nullptr;
-        check(octvr_async_create_ex(rp.data(), (int)k, device(), n_, w.data(), h.data(), out_size.width,
-                                    out_size.height, blend_modes.data(), gain_modes.data(), reg.data(), flags, &a));
+        check(octvr_async_create_preview(rp.data(), (int)k, device(), n_, w.data(), h.data(), out_size.width,
+                                         out_size.height, blend_modes.data(), gain_modes.data(), reg.data(), flags,
+                                         preview_size_.width, preview_size_.height, &a));
         a_ = a;
+#ifdef HAVE_QT5
+        if (preview_size_.area() > 0) {  // async.cpp:307-334: attach the zones the preview widget created
+            qt_.reset(new QtZones());
+            attach(qt_->d0, OCTVR_PREVIEW_DATA0_MEMORY_KEY);
+            attach(qt_->d1, OCTVR_PREVIEW_DATA1_MEMORY_KEY);
+            attach(qt_->meta, OCTVR_PREVIEW_DATA_META_MEMORY_KEY);
+            check(octvr_async_set_preview_sink(a_, &AsyncMultiMapperImpl::qt_sink, qt_.get()));
+        }
+#endif
     }
     ~AsyncMultiMapperImpl() override { octvr_async_destroy(a_); }
     void push(std::vector<std::tuple<cv::Mat, cv::Mat, cv::Mat>>& inputs,
@@ -591,9 +614,49 @@ public:
         if (!held_.empty()) held_.pop_front();
         check(rc);
     }
+    bool preview(cv::Mat& rgb, PreviewDataHeader& hdr) override {
+        if (preview_size_.area() == 0) throw cv::Exception(OCTVR_E_INVALID, "no preview (preview_size 0)");
+        if (rgb.rows != preview_size_.height || rgb.cols != preview_size_.width || rgb.type() != CV_8UC3)
+            rgb.create(preview_size_.height, preview_size_.width, CV_8UC3);
+        octvr_preview_header h{};
+        check(octvr_async_pop_preview(a_, rgb.data, rgb.step, &h));
+        hdr.width = h.width;
+        hdr.height = h.height;
+        hdr.step = h.step;
+        hdr.fps = h.fps;
+        return h.width != 0;
+    }
 
 private:
+#ifdef HAVE_QT5
+    struct QtZones {
+        QSharedMemory d0, d1, meta;
+    };
+    static void attach(QSharedMemory& x, const char* key) {
+        x.setKey(key);
+        if (!x.attach()) throw cv::Exception(OCTVR_E_INVALID, "preview shared memory: " + x.errorString().toStdString());
+    }
+    // run_copy_outputs_hostmem_to_mat's preview write (async.cpp:149-171): the zone the widget is not
+    // reading (meta byte), locked, RGB bytes after the header, then the header
+    static void qt_sink(void* user, const uint8_t* rgb, size_t pitch, const octvr_preview_header* h) {
+        QtZones* z = static_cast<QtZones*>(user);
+        const char zone = *static_cast<const char*>(z->meta.data());
+        QSharedMemory& target = zone == 0 ? z->d0 : z->d1;
+        target.lock();
+        char* base = static_cast<char*>(target.data());
+        for (int y = 0; y < h->height; y++)
+            memcpy(base + sizeof(PreviewDataHeader) + (size_t)y * h->width * 3, rgb + (size_t)y * pitch, (size_t)h->width * 3);
+        PreviewDataHeader* hdr = reinterpret_cast<PreviewDataHeader*>(base);
+        hdr->width = h->width;
+        hdr->height = h->height;
+        hdr->step = 0;
+        hdr->fps = h->fps;
+        target.unlock();
+    }
+    std::unique_ptr<QtZones> qt_;
+#endif
     typedef std::vector<cv::Mat> Held;
+    cv::Size preview_size_;
     octvr_async* a_ = nullptr;
     int n_ = 0;
     std::deque<Held> held_;
@@ -605,8 +668,8 @@ inline AsyncMultiMapper* AsyncMultiMapper::New(const std::vector<MapperTemplate>
                                                std::vector<int> gain_modes,
                                                std::vector<cv::Rect_<double>> output_regions, cv::Size preview_size,
                                                int flags) {
-    (void)preview_size;  // Qt shared-memory preview (async.cpp:113-172): not part of the stitching path
-    return new detail::AsyncMultiMapperImpl(mts, in_sizes, out_size, blend_modes, gain_modes, output_regions, flags);
+    return new detail::AsyncMultiMapperImpl(mts, in_sizes, out_size, blend_modes, gain_modes, output_regions,
+                                            preview_size, flags);
 }
 
 // FastMapper (octvr.hpp:123-144, mapper_fast.cpp:27-195): the feather-blended NV12 stitch.

@@ -149,8 +149,11 @@ int octvr_mapper_create(const octvr_rig* rig, int device, int n_inputs, const in
  * fast_remap.cu:21-44): x = u W - 0.5, 8-bit fractions, taps clamped to the image, u < 0 -> 0 — instead
  * of cv::remap's fixed point (imgwarp.cpp; the default, which the CPU and OpenCL paths share).  The
  * texture filter is NVIDIA hardware behaviour; this mode follows the oracle's model of it
- * (oracle/octvr_oracle.c orc_fast_remap_tex_rgba) bit for bit, gain samples included.  Every tile takes
- * the gather path, so the mode is slower than the default.  Other bits: OCTVR_E_INVALID. */
+ * (oracle/octvr_oracle.c orc_fast_remap_tex_rgba) bit for bit, gain samples included.  Tiles whose taps
+ * all lie inside their camera's image are staged in LDS like the default's (stitch_tiled_tex_kernel, a
+ * 16-bit fraction code per pixel); tiles with a tap the clamp moves take the gather kernel.  The f32
+ * filter model costs about twice the default's VALU per pixel, so the mode is slower.  Other bits:
+ * OCTVR_E_INVALID. */
 #define OCTVR_REMAP_TEXTURE 1
 int octvr_mapper_create_ex(const octvr_rig* rig, int device, int n_inputs, const int* in_w, const int* in_h, int blend,
                            int enable_gain, int scale_w, int scale_h, int flags, octvr_mapper** mapper);
@@ -205,7 +208,7 @@ void octvr_mapper_destroy(octvr_mapper* mapper);
  * of out_w x out_h, async.cpp:20-30) of one merged YUV420P output.  gain_modes[i]: -1 = no gain, i = estimate,
  * j in [0, i) = use mapper j's gains of the same frame (async.cpp:78-86).  A 3-deep pipeline of pinned host
  * and device buffers overlaps the host copies, the H2D upload, the stitch and the D2H download of
- * consecutive frames (async.cpp:32-172); the preview output (Qt shared memory) is not part of the ABI. */
+ * consecutive frames (async.cpp:32-172).  No preview: octvr_async_create_preview adds it. */
 typedef struct octvr_async octvr_async;
 int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
                        const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
@@ -215,6 +218,40 @@ int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int
 int octvr_async_create_ex(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
                           const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
                           const double* output_regions, int flags, octvr_async** async);
+/* The same with AsyncMultiMapper::New's preview_size (async.cpp:73-110, 141-171): every frame, each mapper
+ * also writes Mapper::stitch's preview_output (its RGB result resized, cuda::resize INTER_LINEAR,
+ * mapper.cpp:308-312) into its region _rect_mul_size(output_regions[i], preview) of one preview_w x
+ * preview_h RGB image (CV_8UC3, black where no region writes; a region whose rectangle is empty writes
+ * none), which is downloaded with the outputs and published when the frame's outputs are written:
+ * octvr_async_pop_preview reads the latest, a sink receives every one.  preview_w = preview_h = 0: none
+ * (= octvr_async_create_ex).  Mappers with a preview stitch through their RGB result frame
+ * (mapper.cpp:266-312 order: composite, then RGB -> YUV420P and the preview resize). */
+int octvr_async_create_preview(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
+                               const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
+                               const double* output_regions, int flags, int preview_w, int preview_h,
+                               octvr_async** async);
+/* vr::PreviewDataHeader (octvr.hpp:97-101): what the reference writes in front of the RGB bytes of each
+ * Qt shared-memory zone (async.cpp:163-167): width, height, step = 0, fps = 1 / (mean frame interval over
+ * the last completed block of 10 frames, in s), 0 until 10 frames have completed (async.cpp:141-147). */
+typedef struct octvr_preview_header {
+    int width, height;
+    int step;
+    double fps;
+} octvr_preview_header;
+/* The latest published preview: rgb (host, preview_h rows of preview_w * 3 bytes, row pitch `pitch`) and
+ * its header.  Before the first frame completes, hdr->width = hdr->height = 0 and rgb is untouched (the
+ * reference's zones start with a zeroed header, preview_video.cpp:62-66).  OCTVR_E_INVALID without a
+ * preview.  After pop() of frame k with no later frame pushed, this is frame k's preview. */
+int octvr_async_pop_preview(octvr_async* async, uint8_t* rgb, size_t pitch, octvr_preview_header* hdr);
+/* Called on the pipeline's copy-out thread for every frame's preview, after that frame's outputs are written
+ * and before its pop() returns (the reference's Qt shared-memory write, async.cpp:149-171): rgb = the
+ * downloaded preview (host, valid during the call only), pitch = preview_w * 3.  A Qt caller writes it into
+ * zone *meta of its two QSharedMemory zones.  NULL removes the sink. */
+typedef void (*octvr_preview_sink)(void* user, const uint8_t* rgb, size_t pitch, const octvr_preview_header* hdr);
+int octvr_async_set_preview_sink(octvr_async* async, octvr_preview_sink sink, void* user);
+/* Build-time facts of the pipeline as a JSON object: packed_bytes (the footprint bytes uploaded per frame,
+ * run gaps included), runs, frame bytes, preview size, the mappers' creation flags. */
+int octvr_async_info(const octvr_async* async, char* buf, size_t len);
 /* push(inputs, output) (async.cpp:174-189): in_planes[3*i+0/1/2] = Y, U, V host planes of input i
  * (W x H, W/2 x H/2, W/2 x H/2) with row pitches in_pitches[3*i+k]; out_planes[0/1/2] / out_pitches: the
  * merged output's Y (out_w x out_h), U and V (out_w/2 x out_h/2) planes.  Returns once the frame is queued;
@@ -294,6 +331,10 @@ int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in
  * of an array), parsed with rapidjson's rules (flags 0, as the reference reads its configs) or correctly
  * rounded (OCTVR_JSON_EXACT; out-of-range literals give +-HUGE_VAL / the subnormal / 0 as strtod). */
 int octvr_debug_json_number(const char* json, int flags, double* value);
+/* The host build's worker threads (tiler, seam finder, blender weights, audits) on n_threads threads of
+ * which thread `failing` raises an error (test hook, no GPU): the error reaches the caller as a status
+ * (OCTVR_E_INVALID + octvr_last_error) instead of terminating the process; failing < 0 = none fails. */
+int octvr_debug_worker_failure(int n_threads, int failing);
 /* Saturating float -> u8 conversion as the kernels implement it (method 0: rint + clamp in VALU,
  * method 1: v_cvt_pk_u8_f32), for a known-answer test of round-half-even and clamping on device. */
 int octvr_selftest_sat_u8(const float* in_dev, uint8_t* out_dev, int n, int method, void* stream);

@@ -15,9 +15,14 @@
 //   * only the input bytes some kernel of some mapper reads are copied and uploaded (the union of the
 //     mappers' source footprints, host_common.hpp SourceFootprint), packed, and put in place on the
 //     device by one kernel: with the copy chain each output pixel comes from one camera, so a C2 frame
-//     needs ~10 MB of its 75 MB of YUV.
+//     needs ~18 MB of its 75 MB of YUV (the composite's staged groups plus the gain samples' row pairs,
+//     DESIGN.md §6);
+//   * the preview (async.cpp:73-110, 141-171) is published to a caller-read buffer and an optional sink
+//     (octvr_async_pop_preview / octvr_async_set_preview_sink) instead of Qt shared memory, which stays
+//     the caller's.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstring>
@@ -100,6 +105,8 @@ struct PinnedBuf {
 struct Slot {  // one frame's buffers: the packed footprint runs, the device frames ("Y over [U|V]", pitch = width)
     std::unique_ptr<PinnedBuf> packed_host;
     DevBuf<uint8_t> packed_dev;
+    DevBuf<uint8_t> preview_dev;  // preview_w x preview_h RGB, black outside the regions (async.cpp:314-316)
+    std::unique_ptr<PinnedBuf> preview_host;
     std::vector<std::unique_ptr<PinnedBuf>> out_host;
     std::vector<DevBuf<uint8_t>> in_dev, out_dev;
     FootFrames frames{};
@@ -236,6 +243,20 @@ struct octvr_async {
     std::vector<octvr_mapper*> mappers;
     std::vector<int> gain_modes;
     std::vector<Rect> regions, regions_uv;  // per mapper: its rectangle in the Y and in the U / V planes
+    int flags = 0;
+    // preview (async.cpp:73-76): preview_w x preview_h RGB; per mapper its rectangle (w or h <= 0: none)
+    int preview_w = 0, preview_h = 0;
+    std::vector<Rect> preview_rects;
+    std::mutex pub_mu;  // the published preview, its header and the sink
+    std::vector<uint8_t> pub;
+    octvr_preview_header pub_hdr{0, 0, 0, 0.0};
+    octvr_preview_sink sink = nullptr;
+    void* sink_user = nullptr;
+    // fps over blocks of 10 frames, as the reference's copy-out thread keeps it (async.cpp:141-147): the
+    // frame interval is measured from the previous frame's copy-out (the first from creation, fps_timer)
+    std::chrono::steady_clock::time_point fps_t = std::chrono::steady_clock::now();
+    int64_t frame_count = 0;
+    double frame_total_ms = 0, frame_fps = 0;
     std::vector<FootRun> runs;  // what the mappers read of the inputs (footprint_runs)
     size_t packed_bytes = 0;
     DevBuf<FootRun> runs_dev;
@@ -261,6 +282,8 @@ struct octvr_async {
             sl.out_dev.clear();
             sl.packed_dev.reset();
             sl.packed_host.reset();
+            sl.preview_dev.reset();
+            sl.preview_host.reset();
             sl.out_host.clear();
         }
         for (auto* m : mappers) octvr_mapper_destroy(m);
@@ -321,8 +344,17 @@ struct octvr_async {
                 const int gm = gain_modes[k];
                 const double* chained = nullptr;
                 if (gm >= 0 && gm < (int)k && mapper_has_gain(mappers[gm])) chained = mapper_gains_dev(mappers[gm]);
+                // preview_output(_rect_mul_size(output_regions[i], preview_output.size())) (async.cpp:75-76): the
+                // region's view of the preview image (an empty view is no preview, mapper.cpp:308)
+                PreviewOut pv{};
+                const bool with_pv = preview_w > 0 && preview_rects[k].w > 0 && preview_rects[k].h > 0;
+                if (with_pv) {
+                    const Rect& r = preview_rects[k];
+                    const size_t pp = (size_t)preview_w * 3;
+                    pv = PreviewOut{sl.preview_dev.p + (size_t)r.y * pp + (size_t)r.x * 3, r.w, r.h, pp};
+                }
                 mapper_stitch(mappers[k], in.data(), pitch.data(), sl.out_dev[k].p, (size_t)regions[k].w, nullptr, 0,
-                              chained, comp);
+                              chained, comp, with_pv ? &pv : nullptr);
             }
             HIP_CHECK(hipStreamSynchronize(comp));
         });
@@ -335,6 +367,9 @@ struct octvr_async {
             Slot& sl = slots[j.slot];
             for (size_t k = 0; k < mappers.size(); k++)
                 HIP_CHECK(hipMemcpyAsync(sl.out_host[k]->p, sl.out_dev[k].p, sl.out_host[k]->n, hipMemcpyDeviceToHost,
+                                         down));
+            if (preview_w > 0)  // async.cpp:102-103
+                HIP_CHECK(hipMemcpyAsync(sl.preview_host->p, sl.preview_dev.p, sl.preview_host->n, hipMemcpyDeviceToHost,
                                          down));
             HIP_CHECK(hipStreamSynchronize(down));
         });
@@ -362,6 +397,24 @@ struct octvr_async {
                 });
             }
         });
+        // frame_total_time += fps_timer.tick(); fps over every block of 10 frames (async.cpp:141-147)
+        const auto now = std::chrono::steady_clock::now();
+        frame_total_ms += std::chrono::duration<double, std::milli>(now - fps_t).count();
+        fps_t = now;
+        if (++frame_count == 10) {
+            frame_fps = 1.0 / (frame_total_ms / (double)frame_count / 1000);
+            frame_count = 0;
+            frame_total_ms = 0;
+        }
+        // the preview with its PreviewDataHeader (async.cpp:149-171): published, then handed to the sink
+        if (preview_w > 0 && j.status == OCTVR_OK) {
+            const Slot& sl = slots[j.slot];
+            const octvr_preview_header h{preview_w, preview_h, 0, frame_fps};
+            std::lock_guard<std::mutex> g(pub_mu);
+            memcpy(pub.data(), sl.preview_host->p, pub.size());
+            pub_hdr = h;
+            if (sink) sink(sink_user, sl.preview_host->p, (size_t)preview_w * 3, &h);
+        }
     }
 
     template <class F>
@@ -416,12 +469,29 @@ int octvr_async_create(const octvr_rig* const* rigs, int n_rigs, int device, int
 int octvr_async_create_ex(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
                           const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
                           const double* output_regions, int flags, octvr_async** out) {
+    return octvr_async_create_preview(rigs, n_rigs, device, n_inputs, in_w, in_h, out_w, out_h, blend_modes, gain_modes,
+                                      output_regions, flags, 0, 0, out);
+}
+
+int octvr_async_create_preview(const octvr_rig* const* rigs, int n_rigs, int device, int n_inputs, const int* in_w,
+                               const int* in_h, int out_w, int out_h, const int* blend_modes, const int* gain_modes,
+                               const double* output_regions, int flags, int preview_w, int preview_h,
+                               octvr_async** out) {
     try {
         REQUIRE(rigs && n_rigs > 0 && in_w && in_h && blend_modes && gain_modes && output_regions && out,
                 "NULL argument");
         REQUIRE(n_inputs > 0 && n_inputs <= kMaxCams && out_w > 0 && out_h > 0 && out_w % 2 == 0 && out_h % 2 == 0, "bad sizes");
+        REQUIRE(preview_w >= 0 && preview_h >= 0 && (uint64_t)preview_w * (uint64_t)preview_h * 3 < 0x7FFFFF80ull,
+                "bad preview size");
         auto a = std::make_unique<octvr_async>();
         a->device = device;
+        a->flags = flags;
+        // preview_size.area() > 0 enables the preview (async.cpp:99, 299)
+        if ((int64_t)preview_w * preview_h > 0) {
+            a->preview_w = preview_w;
+            a->preview_h = preview_h;
+            a->pub.assign((size_t)preview_w * preview_h * 3, 0);
+        }
         a->n_in = n_inputs;
         a->out_w = out_w;
         a->out_h = out_h;
@@ -441,6 +511,8 @@ int octvr_async_create_ex(const octvr_rig* const* rigs, int n_rigs, int device, 
             REQUIRE(c.w == r.w / 2 && c.h == r.h / 2, "output region's chroma rectangle is not half its luma rectangle");
             a->regions.push_back(r);
             a->regions_uv.push_back(c);
+            a->preview_rects.push_back(a->preview_w ? rect_mul_size(output_regions + 4 * k, a->preview_w, a->preview_h)
+                                                    : Rect{0, 0, 0, 0});
             octvr_mapper* m = nullptr;
             // Mapper(mts[i], in_sizes, blend_modes[i], gain_modes[i] >= 0, r.size()) (async.cpp:250-255)
             const int rc = octvr_mapper_create_ex(rigs[k], device, n_inputs, in_w, in_h, blend_modes[k],
@@ -473,6 +545,13 @@ int octvr_async_create_ex(const octvr_rig* const* rigs, int n_rigs, int device, 
                 sl.frames.f[i] = sl.in_dev.back().p;
                 sl.frames.w[i] = in_w[i];
                 sl.frames.h[i] = in_h[i];
+            }
+            if (a->preview_w) {  // GpuMat(preview_size, CV_8UC3).setTo(0) + HostMem (async.cpp:299-305)
+                const size_t pb = (size_t)a->preview_w * a->preview_h * 3;
+                sl.preview_dev.alloc(pb);
+                HIP_CHECK(hipMemset(sl.preview_dev.p, 0, pb));
+                sl.preview_host.reset(new PinnedBuf());
+                sl.preview_host->alloc(pb);
             }
             for (int k = 0; k < n_rigs; k++) {
                 const size_t bytes = (size_t)a->regions[k].w * (a->regions[k].h / 2 * 3);
@@ -544,6 +623,56 @@ int octvr_async_pending(const octvr_async* a, int* n) {
         return OCTVR_E_INVALID;
     }
     *n = a->pending;
+    return OCTVR_OK;
+}
+
+int octvr_async_pop_preview(octvr_async* a, uint8_t* rgb, size_t pitch, octvr_preview_header* hdr) {
+    if (!a || !hdr || (a->preview_w > 0 && (!rgb || pitch < (size_t)a->preview_w * 3))) {
+        set_last_error("bad arguments");
+        return OCTVR_E_INVALID;
+    }
+    if (a->preview_w == 0) {
+        set_last_error("the pipeline has no preview (preview size 0)");
+        return OCTVR_E_INVALID;
+    }
+    std::lock_guard<std::mutex> g(a->pub_mu);
+    *hdr = a->pub_hdr;
+    if (a->pub_hdr.width == 0) return OCTVR_OK;  // nothing published yet
+    const size_t rb = (size_t)a->preview_w * 3;
+    for (int y = 0; y < a->preview_h; y++) memcpy(rgb + (size_t)y * pitch, a->pub.data() + (size_t)y * rb, rb);
+    return OCTVR_OK;
+}
+
+int octvr_async_set_preview_sink(octvr_async* a, octvr_preview_sink sink, void* user) {
+    if (!a) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    std::lock_guard<std::mutex> g(a->pub_mu);
+    a->sink = sink;
+    a->sink_user = user;
+    return OCTVR_OK;
+}
+
+int octvr_async_info(const octvr_async* a, char* buf, size_t len) {
+    if (!a || !buf || len == 0) {
+        set_last_error("bad arguments");
+        return OCTVR_E_INVALID;
+    }
+    size_t in_bytes = 0, out_bytes = 0;
+    for (int i = 0; i < a->n_in; i++) in_bytes += (size_t)a->in_w[i] * (a->in_h[i] / 2 * 3);
+    for (const Rect& r : a->regions) out_bytes += (size_t)r.w * (r.h / 2 * 3);
+    char tmp[512];
+    snprintf(tmp, sizeof tmp,
+             "{\"mappers\": %d, \"inputs\": %d, \"packed_bytes\": %zu, \"runs\": %zu, \"input_frame_bytes\": %zu, "
+             "\"output_bytes\": %zu, \"preview\": [%d, %d], \"flags\": %d, \"slots\": %d}",
+             (int)a->mappers.size(), a->n_in, a->packed_bytes, a->runs.size(), in_bytes, out_bytes, a->preview_w,
+             a->preview_h, a->flags, kSlots);
+    if (strlen(tmp) >= len) {
+        set_last_error("buffer too small");
+        return OCTVR_E_INVALID;
+    }
+    memcpy(buf, tmp, strlen(tmp) + 1);
     return OCTVR_OK;
 }
 

@@ -341,98 +341,95 @@ static void audit_plane(const FastPlan& P, const FastPlaneHost& pl, int plane, s
     if (pl.runs.size() != nruns) bad("runs[] does not match the grid", 0, -1, 0);
     std::vector<AuditCounts> part(16);
     const size_t T = part.size();
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < T; t++)
-        th.emplace_back([&, t] {
-            AuditCounts& a = part[t];
-            for (size_t r = nruns * t / T; r < std::min(nruns * (t + 1) / T, pl.runs.size()); r++) {
-                uint32_t m = pl.runs[r].x, blk = pl.runs[r].y;
-                while (m) {
-                    a.groups++;
-                    bool live[4];
-                    int cam[4];
-                    uint32_t b[4];
-                    for (int k = 0; k < 4; k++) {
-                        live[k] = m != 0u;
-                        cam[k] = live[k] ? __builtin_ctz(m) : 0;
-                        m &= m - 1u;
-                        b[k] = live[k] ? blk + (uint32_t)k : blk;
-                        a.slot_loads++;
-                        a.max_block = std::max<int64_t>(a.max_block, b[k]);
-                        if (b[k] >= std::max<size_t>(pl.nblk, 1)) bad("block index past the plane's blocks", r, k, 0);
-                        if (pl.compact && b[k] >= cap_h) bad("header index past the headers", r, k, 0);
-                        if ((uint64_t)b[k] * 256 + 255 >= cap_e) bad("entry index past the entries", r, k, 255);
-                        if (live[k] && cam[k] >= P.n) bad("camera past the frame set", r, k, 0);
-                    }
-                    for (int k = 0; k < 4; k++) blk += live[k] ? 1u : 0u;
-                    for (int k = 0; k < 4; k++) {
-                        if (!live[k] || b[k] >= pl.nblk) continue;
-                        a.live_slots++;
-                        if (pl.compact && (pl.hdr[b[k]].y & kFastInterior)) a.interior_slots++;
-                        const int fw = P.in_w[cam[k]], fh = P.in_h[cam[k]];
-                        const uint32_t pitch = (uint32_t)(fw + pitch_pad);
-                        const uint32_t size = pitch * (uint32_t)(fh + fh / 2);
-                        const int sw = plane ? fw / 2 : fw, sh = plane ? fh / 2 : fh;
-                        const uint32_t base = plane ? (uint32_t)fh * pitch : 0u;
-                        const bool interior = pl.compact && (pl.hdr[b[k]].y & kFastInterior) != 0;
-                        for (uint32_t lane = 0; lane < 256; lane++) {
-                            const size_t e = (size_t)b[k] * 256 + lane;
-                            int sx, sy;
-                            uint32_t w;
-                            if (pl.compact) {
-                                const uint32_t o = pl.off[e], h = pl.hdr[b[k]].x;
-                                sx = (int)(int16_t)(h & 0xFFFFu) + (int)(o & 2047u);
-                                sy = (int)(int16_t)(h >> 16) + (int)((o >> 11) & 2047u);
-                                w = pl.wgt[e];
-                                if (w) {  // the compact form holds the same tap as the wide entry
-                                    const uint2 we = pl.ent[e];
-                                    if (sx != (int)(int16_t)(we.x & 0xFFFFu) || sy != (int)(int16_t)(we.x >> 16) ||
-                                        (o >> 22) != (we.y & 1023u) || w != (we.y >> 16))
-                                        bad("compact entry differs from the wide one", r, k, lane);
-                                }
-                            } else {
+    run_threads(T, [&](size_t t) {
+        AuditCounts& a = part[t];
+        for (size_t r = nruns * t / T; r < std::min(nruns * (t + 1) / T, pl.runs.size()); r++) {
+            uint32_t m = pl.runs[r].x, blk = pl.runs[r].y;
+            while (m) {
+                a.groups++;
+                bool live[4];
+                int cam[4];
+                uint32_t b[4];
+                for (int k = 0; k < 4; k++) {
+                    live[k] = m != 0u;
+                    cam[k] = live[k] ? __builtin_ctz(m) : 0;
+                    m &= m - 1u;
+                    b[k] = live[k] ? blk + (uint32_t)k : blk;
+                    a.slot_loads++;
+                    a.max_block = std::max<int64_t>(a.max_block, b[k]);
+                    if (b[k] >= std::max<size_t>(pl.nblk, 1)) bad("block index past the plane's blocks", r, k, 0);
+                    if (pl.compact && b[k] >= cap_h) bad("header index past the headers", r, k, 0);
+                    if ((uint64_t)b[k] * 256 + 255 >= cap_e) bad("entry index past the entries", r, k, 255);
+                    if (live[k] && cam[k] >= P.n) bad("camera past the frame set", r, k, 0);
+                }
+                for (int k = 0; k < 4; k++) blk += live[k] ? 1u : 0u;
+                for (int k = 0; k < 4; k++) {
+                    if (!live[k] || b[k] >= pl.nblk) continue;
+                    a.live_slots++;
+                    if (pl.compact && (pl.hdr[b[k]].y & kFastInterior)) a.interior_slots++;
+                    const int fw = P.in_w[cam[k]], fh = P.in_h[cam[k]];
+                    const uint32_t pitch = (uint32_t)(fw + pitch_pad);
+                    const uint32_t size = pitch * (uint32_t)(fh + fh / 2);
+                    const int sw = plane ? fw / 2 : fw, sh = plane ? fh / 2 : fh;
+                    const uint32_t base = plane ? (uint32_t)fh * pitch : 0u;
+                    const bool interior = pl.compact && (pl.hdr[b[k]].y & kFastInterior) != 0;
+                    for (uint32_t lane = 0; lane < 256; lane++) {
+                        const size_t e = (size_t)b[k] * 256 + lane;
+                        int sx, sy;
+                        uint32_t w;
+                        if (pl.compact) {
+                            const uint32_t o = pl.off[e], h = pl.hdr[b[k]].x;
+                            sx = (int)(int16_t)(h & 0xFFFFu) + (int)(o & 2047u);
+                            sy = (int)(int16_t)(h >> 16) + (int)((o >> 11) & 2047u);
+                            w = pl.wgt[e];
+                            if (w) {  // the compact form holds the same tap as the wide entry
                                 const uint2 we = pl.ent[e];
-                                sx = (int)(int16_t)(we.x & 0xFFFFu);
-                                sy = (int)(int16_t)(we.x >> 16);
-                                w = we.y >> 16;
+                                if (sx != (int)(int16_t)(we.x & 0xFFFFu) || sy != (int)(int16_t)(we.x >> 16) ||
+                                    (o >> 22) != (we.y & 1023u) || w != (we.y >> 16))
+                                    bad("compact entry differs from the wide one", r, k, lane);
                             }
-                            // interior blocks (fast_group<INNER>): no clamps — the claim itself is checked
-                            if (interior && w && !(sx >= 0 && sy >= 0 && sx <= sw - 2 && sy <= sh - 3))
-                                bad("interior block with a tap near or past the plane's edge", r, k, lane);
-                            if (interior && !w && (sx < 0 || sy < 0 || sx > sw - 2 || sy > sh - 3))
-                                bad("interior block with an unused entry off the interior", r, k, lane);
-                            const int xa = interior ? sx : std::min(std::max(sx, 0), sw - 1);
-                            const uint32_t bx = (uint32_t)xa * bpp & ~3u;
-                            for (int rr = 0; rr < 2; rr++) {
-                                const int y = interior ? sy + rr : std::min(std::max(sy + rr, 0), sh - 1);
-                                const uint32_t row = base + (uint32_t)y * pitch;
-                                if (size < 8u) { bad("frame under 8 bytes", r, k, lane); continue; }
-                                const uint32_t st = interior ? row + bx : std::min(row + bx, size - 8u);
-                                if ((uint64_t)st + 8 > size) bad("tap-row load past the frame", r, k, lane);
-                                if (!w) continue;
-                                const uint32_t d = interior ? ((uint32_t)sx * bpp & 3u) : row + (uint32_t)sx * bpp - st;
-                                for (int cc = 0; cc < 2; cc++) {  // in-image taps: their bytes in the loaded 8
-                                    const int tx = sx + cc, ty = sy + rr;
-                                    if (tx < 0 || ty < 0 || tx >= sw || ty >= sh) continue;
-                                    a.taps_in++;
-                                    const uint32_t i = (d + (uint32_t)cc * bpp) & 7u;
-                                    const uint64_t want = (uint64_t)base + (uint64_t)ty * pitch + (uint64_t)tx * bpp;
-                                    if (i + bpp - 1 > 7u || (uint64_t)st + i != want) bad("tap byte outside the loaded row", r, k, lane);
-                                }
+                        } else {
+                            const uint2 we = pl.ent[e];
+                            sx = (int)(int16_t)(we.x & 0xFFFFu);
+                            sy = (int)(int16_t)(we.x >> 16);
+                            w = we.y >> 16;
+                        }
+                        // interior blocks (fast_group<INNER>): no clamps — the claim itself is checked
+                        if (interior && w && !(sx >= 0 && sy >= 0 && sx <= sw - 2 && sy <= sh - 3))
+                            bad("interior block with a tap near or past the plane's edge", r, k, lane);
+                        if (interior && !w && (sx < 0 || sy < 0 || sx > sw - 2 || sy > sh - 3))
+                            bad("interior block with an unused entry off the interior", r, k, lane);
+                        const int xa = interior ? sx : std::min(std::max(sx, 0), sw - 1);
+                        const uint32_t bx = (uint32_t)xa * bpp & ~3u;
+                        for (int rr = 0; rr < 2; rr++) {
+                            const int y = interior ? sy + rr : std::min(std::max(sy + rr, 0), sh - 1);
+                            const uint32_t row = base + (uint32_t)y * pitch;
+                            if (size < 8u) { bad("frame under 8 bytes", r, k, lane); continue; }
+                            const uint32_t st = interior ? row + bx : std::min(row + bx, size - 8u);
+                            if ((uint64_t)st + 8 > size) bad("tap-row load past the frame", r, k, lane);
+                            if (!w) continue;
+                            const uint32_t d = interior ? ((uint32_t)sx * bpp & 3u) : row + (uint32_t)sx * bpp - st;
+                            for (int cc = 0; cc < 2; cc++) {  // in-image taps: their bytes in the loaded 8
+                                const int tx = sx + cc, ty = sy + rr;
+                                if (tx < 0 || ty < 0 || tx >= sw || ty >= sh) continue;
+                                a.taps_in++;
+                                const uint32_t i = (d + (uint32_t)cc * bpp) & 7u;
+                                const uint64_t want = (uint64_t)base + (uint64_t)ty * pitch + (uint64_t)tx * bpp;
+                                if (i + bpp - 1 > 7u || (uint64_t)st + i != want) bad("tap byte outside the loaded row", r, k, lane);
                             }
                         }
                     }
                 }
-                // the output bytes of the run's lanes (y * pitch + x, chroma (H + y) * pitch + 2x + 1)
-                const uint64_t i0 = (uint64_t)r * 256, i1 = std::min<uint64_t>(i0 + 256, npx);
-                if (i1 > i0) {
-                    const uint64_t yl = (i1 - 1) / pw, xl = (i1 - 1) % pw;
-                    const uint64_t last = plane ? ((uint64_t)P.H + yl) * P.W + 2 * xl + 1 : yl * P.W + xl;
-                    if (last >= (uint64_t)P.W * (P.H + P.H / 2)) bad("output byte past the frame", r, -1, 0);
-                }
             }
-        });
-    for (auto& x : th) x.join();
+            // the output bytes of the run's lanes (y * pitch + x, chroma (H + y) * pitch + 2x + 1)
+            const uint64_t i0 = (uint64_t)r * 256, i1 = std::min<uint64_t>(i0 + 256, npx);
+            if (i1 > i0) {
+                const uint64_t yl = (i1 - 1) / pw, xl = (i1 - 1) % pw;
+                const uint64_t last = plane ? ((uint64_t)P.H + yl) * P.W + 2 * xl + 1 : yl * P.W + xl;
+                if (last >= (uint64_t)P.W * (P.H + P.H / 2)) bad("output byte past the frame", r, -1, 0);
+            }
+        }
+    });
     for (auto& a : part) {
         c.groups += a.groups;
         c.slot_loads += a.slot_loads;

@@ -7,8 +7,10 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <exception>
 #include <functional>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <thread>
@@ -36,6 +38,29 @@ struct OctvrError : std::runtime_error {
         if (!(cond)) throw ::octvr::OctvrError(OCTVR_E_INVALID, (msg));     \
     } while (0)
 
+// f(t) for t in [0, T) on T host threads.  An exception thrown by f (a REQUIRE, a HIP_CHECK, bad_alloc)
+// never leaves its thread — that would std::terminate the host process, Python caller included: the
+// first one is kept and rethrown on the calling thread after every thread has joined, so the C ABI's
+// guard turns it into a status code.
+template <class F>
+void run_threads(size_t T, F f) {
+    std::exception_ptr first;
+    std::mutex mu;
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (size_t t = 0; t < T; t++)
+        th.emplace_back([&, t] {
+            try {
+                f(t);
+            } catch (...) {
+                std::lock_guard<std::mutex> g(mu);
+                if (!first) first = std::current_exception();
+            }
+        });
+    for (auto& x : th) x.join();
+    if (first) std::rethrow_exception(first);
+}
+
 // f(k) for k in [0, n) on up to 16 host threads (contiguous ranges; build-time work only).
 template <class F>
 void parallel_for(size_t n, F f) {
@@ -44,12 +69,9 @@ void parallel_for(size_t n, F f) {
         for (size_t k = 0; k < n; k++) f(k);
         return;
     }
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < T; t++)
-        th.emplace_back([&, t] {
-            for (size_t k = n * t / T; k < n * (t + 1) / T; k++) f(k);
-        });
-    for (auto& x : th) x.join();
+    run_threads(T, [&](size_t t) {
+        for (size_t k = n * t / T; k < n * (t + 1) / T; k++) f(k);
+    });
 }
 
 // octvr_last_error() text of the calling thread (octvr_hip.cpp).

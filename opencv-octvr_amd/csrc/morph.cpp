@@ -456,14 +456,11 @@ int rig_morph_controlpoints(octvr_rig& rig, const JsonValue& cps_json) {
     for (const ControlPoint& cp : cps) need[cp.n0] = need[cp.n1] = 1;
     std::vector<std::vector<float>> dist(n);
     {
-        std::vector<std::thread> th;
-        for (int i = 0; i < n; i++)
-            if (need[i])
-                th.emplace_back([&, i] {
-                    const RigInput& in = rig.inputs[i];
-                    dist[i] = camera_distance(in, in.roi[0] == 0 && in.roi[2] == ux1 - ux0);
-                });
-        for (auto& t : th) t.join();
+        run_threads((size_t)n, [&](size_t i) {
+            if (!need[i]) return;
+            const RigInput& in = rig.inputs[i];
+            dist[i] = camera_distance(in, in.roi[0] == 0 && in.roi[2] == ux1 - ux0);
+        });
     }
     for (size_t k = 0; k < cps.size(); k++) {  // :126-133, all float
         ControlPoint& cp = cps[k];

@@ -298,18 +298,15 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
     if (M.feather) {
         auto& L0 = M.lv[0];
         std::vector<std::vector<float>> w(n);
-        std::vector<std::thread> th;
-        for (int i = 0; i < n; i++)
-            th.emplace_back([&, i] {
-                const RigInput& in = rig.inputs[i];
-                w[i].resize((size_t)in.roi[2] * in.roi[3]);
-                chamfer_l2_3x3(in.mask.data(), in.roi[2], in.roi[3], w[i].data());
-                for (float& v : w[i]) {
-                    const float d = v - (float)feather_border;
-                    v = d > 0.f ? d : 0.f;  // threshold(THRESH_TOZERO, 0)
-                }
-            });
-        for (auto& t : th) t.join();
+        run_threads((size_t)n, [&](size_t i) {
+            const RigInput& in = rig.inputs[i];
+            w[i].resize((size_t)in.roi[2] * in.roi[3]);
+            chamfer_l2_3x3(in.mask.data(), in.roi[2], in.roi[3], w[i].data());
+            for (float& v : w[i]) {
+                const float d = v - (float)feather_border;
+                v = d > 0.f ? d : 0.f;  // threshold(THRESH_TOZERO, 0)
+            }
+        });
         std::vector<float> W((size_t)M.arr.w * M.arr.h, 1e-5f);
         for (int i = 0; i < n; i++) {
             const RigInput& in = rig.inputs[i];

@@ -1994,6 +1994,15 @@ int octvr_debug_json_number(const char* json, int flags, double* value) {
     });
 }
 
+int octvr_debug_worker_failure(int n_threads, int failing) {
+    return guarded([&] {
+        REQUIRE(n_threads > 0 && n_threads <= 64, "bad arguments");
+        run_threads((size_t)n_threads, [&](size_t t) {
+            REQUIRE((int)t != failing, "worker " + std::to_string(t) + " failed (test hook)");
+        });
+    });
+}
+
 int octvr_rig_lut_recomputed(const octvr_rig* rig, int i, uint64_t* n) {
     return guarded([&] {
         REQUIRE(rig && n && i >= 0 && i < (int)rig->inputs.size(), "bad arguments");

@@ -171,50 +171,45 @@ void rig_create_masks(octvr_rig& rig) {
     // distances, one host thread per camera; a camera spanning the whole width (and starting at
     // column 0) is transformed as three side-by-side copies so the seam wraps at +-180 degrees
     // (warpedDistanceTransform, seam_finders.cpp:86-95)
-    std::vector<std::thread> th;
-    for (int i = 0; i < n; i++)
-        th.emplace_back([&, i] {
-            Work& k = wk[i];
-            k.dist.resize((size_t)k.w * k.h);
-            if (k.x == 0 && k.w == rx1 - rx0) {
-                std::vector<uint8_t> tri((size_t)3 * k.w * k.h);
-                for (int y = 0; y < k.h; y++)
-                    for (int c = 0; c < 3; c++)
-                        memcpy(&tri[((size_t)y * 3 + c) * k.w], &k.mask[(size_t)y * k.w], k.w);
-                std::vector<float> d3(tri.size());
-                chamfer_l2_3x3(tri.data(), 3 * k.w, k.h, d3.data());
-                for (int y = 0; y < k.h; y++)
-                    memcpy(&k.dist[(size_t)y * k.w], &d3[((size_t)y * 3 + 1) * k.w], sizeof(float) * k.w);
-            } else {
-                chamfer_l2_3x3(k.mask.data(), k.w, k.h, k.dist.data());
-            }
-        });
-    for (auto& t : th) t.join();
-    th.clear();
+    run_threads((size_t)n, [&](size_t i) {
+        Work& k = wk[i];
+        k.dist.resize((size_t)k.w * k.h);
+        if (k.x == 0 && k.w == rx1 - rx0) {
+            std::vector<uint8_t> tri((size_t)3 * k.w * k.h);
+            for (int y = 0; y < k.h; y++)
+                for (int c = 0; c < 3; c++)
+                    memcpy(&tri[((size_t)y * 3 + c) * k.w], &k.mask[(size_t)y * k.w], k.w);
+            std::vector<float> d3(tri.size());
+            chamfer_l2_3x3(tri.data(), 3 * k.w, k.h, d3.data());
+            for (int y = 0; y < k.h; y++)
+                memcpy(&k.dist[(size_t)y * k.w], &d3[((size_t)y * 3 + 1) * k.w], sizeof(float) * k.w);
+        } else {
+            chamfer_l2_3x3(k.mask.data(), k.w, k.h, k.dist.data());
+        }
+    });
     // arbitration: each working pixel keeps only the camera with the largest distance (first
     // camera on ties); the masks are read-only here except for the zeroing of losers, and the
     // distances were fixed beforehand, so rows are independent
     const int T = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    for (int tid = 0; tid < T; tid++)
-        th.emplace_back([&, tid] {
-            for (int y = ry0 + tid; y < ry1; y += T)
-                for (int x = rx0; x < rx1; x++) {
-                    int best = -1;
-                    float bd = -1.f;
-                    for (int i = 0; i < n; i++) {
-                        const Work& k = wk[i];
-                        if (y < k.y || x < k.x || y - k.y >= k.h || x - k.x >= k.w) continue;
-                        const float d = k.dist[(size_t)(y - k.y) * k.w + (x - k.x)];
-                        if (best < 0 || d > bd) best = i, bd = d;
-                    }
-                    for (int i = 0; i < n; i++) {
-                        Work& k = wk[i];
-                        if (i == best || y < k.y || x < k.x || y - k.y >= k.h || x - k.x >= k.w) continue;
-                        k.mask[(size_t)(y - k.y) * k.w + (x - k.x)] = 0;
-                    }
+    run_threads((size_t)T, [&](size_t t) {
+        const int tid = (int)t;
+        for (int y = ry0 + tid; y < ry1; y += T)
+            for (int x = rx0; x < rx1; x++) {
+                int best = -1;
+                float bd = -1.f;
+                for (int i = 0; i < n; i++) {
+                    const Work& k = wk[i];
+                    if (y < k.y || x < k.x || y - k.y >= k.h || x - k.x >= k.w) continue;
+                    const float d = k.dist[(size_t)(y - k.y) * k.w + (x - k.x)];
+                    if (best < 0 || d > bd) best = i, bd = d;
                 }
-        });
-    for (auto& t : th) t.join();
+                for (int i = 0; i < n; i++) {
+                    Work& k = wk[i];
+                    if (i == best || y < k.y || x < k.x || y - k.y >= k.h || x - k.x >= k.w) continue;
+                    k.mask[(size_t)(y - k.y) * k.w + (x - k.x)] = 0;
+                }
+            }
+    });
     rig.seam_masks.resize(n);
     for (int i = 0; i < n; i++) {
         const RigInput& in = rig.inputs[i];

@@ -265,9 +265,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
             }
         }
     };
-    std::vector<std::thread> th;
-    for (int i = 0; i < T; i++) th.emplace_back(work, i);
-    for (auto& x : th) x.join();
+    run_threads((size_t)T, [&](size_t i) { work((int)i); });
     b.tex = any_tex.load();
     // staged items: the non-wide jobs in job order, compacted in place; wide jobs in job order
     int n_items = 0;

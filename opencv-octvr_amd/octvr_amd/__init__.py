@@ -95,6 +95,21 @@ if hasattr(_lib, "octvr_async_create_ex"):
     _lib.octvr_async_create_ex.argtypes = [C.POINTER(_VP), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
                                            C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                            C.POINTER(C.c_double), C.c_int, C.POINTER(_VP)]
+_lib.octvr_async_create_preview.argtypes = [C.POINTER(_VP), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int),
+                                            C.POINTER(C.c_int), C.c_int, C.c_int, C.POINTER(C.c_int),
+                                            C.POINTER(C.c_int), C.POINTER(C.c_double), C.c_int, C.c_int, C.c_int,
+                                            C.POINTER(_VP)]
+
+
+class PreviewDataHeader(C.Structure):
+    """vr::PreviewDataHeader (octvr.hpp:97-101) = octvr_preview_header."""
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("step", C.c_int), ("fps", C.c_double)]
+
+
+PREVIEW_SINK = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C.POINTER(PreviewDataHeader))
+_lib.octvr_async_pop_preview.argtypes = [_VP, _VP, C.c_size_t, C.POINTER(PreviewDataHeader)]
+_lib.octvr_async_set_preview_sink.argtypes = [_VP, PREVIEW_SINK, _VP]
+_lib.octvr_async_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
 _lib.octvr_async_push.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), C.POINTER(_VP), C.POINTER(C.c_size_t)]
 _lib.octvr_async_pop.argtypes = [_VP]
 _lib.octvr_async_pending.argtypes = [_VP, C.POINTER(C.c_int)]
@@ -115,6 +130,8 @@ if hasattr(_lib, "octvr_debug_tiled_lut_info"):
 if hasattr(_lib, "octvr_debug_fastmapper_audit"):
     _lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
                                                   C.c_int, C.c_char_p, C.c_size_t]
+if hasattr(_lib, "octvr_debug_worker_failure"):
+    _lib.octvr_debug_worker_failure.argtypes = [C.c_int, C.c_int]
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
                                 C.c_float, C.c_float, _VP, C.c_size_t, _VP]
 
@@ -151,6 +168,12 @@ def debug_tiled_lut_info(mt, in_sizes, remap="remap"):
     _check(_lib.octvr_debug_tiled_lut_info(mt._h, n, w, h, REMAP_TEXTURE if remap == "texture" else 0, buf, len(buf)))
     import json as _json
     return _json.loads(buf.value.decode())
+
+
+def debug_worker_failure(n_threads, failing):
+    """Run the host build's worker-thread helper with thread `failing` raising (octvr_debug_worker_failure;
+    no GPU): raises OctvrError with the worker's message, as a failing tiler / seam / audit worker does."""
+    _check(_lib.octvr_debug_worker_failure(int(n_threads), int(failing)))
 
 
 def debug_json_number(text, exact=True):
@@ -484,11 +507,16 @@ class AsyncMultiMapper:
     a 3-deep pinned-buffer pipeline (copy-in, H2D, stitch, D2H, copy-out overlap across frames).
 
     templates: list of MapperTemplate (all with the same inputs); output_regions: list of (x, y, w, h)
-    fractions of out_size; gain_modes[i]: -1 no gain, i estimate, j < i reuse mapper j's gains."""
+    fractions of out_size; gain_modes[i]: -1 no gain, i estimate, j < i reuse mapper j's gains.
+    preview_size (w, h): AsyncMultiMapper::New's preview — each mapper also writes its region of one RGB
+    preview image every frame (async.cpp:73-110); read the latest with preview(), or receive every one
+    through set_preview_sink()."""
 
-    def __init__(self, templates, in_sizes, out_size, blend_modes, gain_modes, output_regions, device=0, remap="remap"):
+    def __init__(self, templates, in_sizes, out_size, blend_modes, gain_modes, output_regions, device=0, remap="remap",
+                 preview_size=(0, 0)):
         if remap not in ("remap", "texture"):
             raise ValueError("remap must be 'remap' or 'texture'")
+        self._h = C.c_void_p(0)
         k, n = len(templates), len(in_sizes)
         rigs = (_VP * k)(*[t._h.value for t in templates])
         w = (C.c_int * n)(*[s[0] for s in in_sizes])
@@ -497,12 +525,18 @@ class AsyncMultiMapper:
         gm = (C.c_int * k)(*gain_modes)
         rg = (C.c_double * (4 * k))(*[float(v) for r in output_regions for v in r])
         hd = _VP()
-        if remap == "texture":
+        pw, ph = (int(v) for v in preview_size)
+        if pw or ph:
+            _check(_lib.octvr_async_create_preview(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg,
+                                                   REMAP_TEXTURE if remap == "texture" else 0, pw, ph, C.byref(hd)))
+        elif remap == "texture":
             _check(_lib.octvr_async_create_ex(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg,
                                               REMAP_TEXTURE, C.byref(hd)))
         else:
             _check(_lib.octvr_async_create(rigs, k, device, n, w, h, out_size[0], out_size[1], bm, gm, rg, C.byref(hd)))
         self._h = hd
+        self.preview_size = (pw, ph) if pw * ph > 0 else (0, 0)
+        self._sink = None
         self._templates = list(templates)  # the mappers copy what they need; kept for symmetry with the reference
         self.n = n
         self.out_size = tuple(out_size)
@@ -532,6 +566,40 @@ class AsyncMultiMapper:
         n = C.c_int()
         _check(_lib.octvr_async_pending(self._h, C.byref(n)))
         return n.value
+
+    def preview(self):
+        """(rgb, header): the latest published preview as an (h, w, 3) uint8 array and its PreviewDataHeader
+        (width 0 and rgb None before the first frame completes)."""
+        pw, ph = self.preview_size
+        rgb = np.zeros((max(ph, 1), max(pw, 1), 3), np.uint8)
+        hdr = PreviewDataHeader()
+        _check(_lib.octvr_async_pop_preview(self._h, rgb.ctypes.data, rgb.strides[0], C.byref(hdr)))
+        return (rgb if hdr.width else None), hdr
+
+    def set_preview_sink(self, fn):
+        """fn(rgb, header) on the pipeline's copy-out thread for every frame's preview (rgb: a copy); None
+        removes it."""
+        if fn is None:
+            _check(_lib.octvr_async_set_preview_sink(self._h, PREVIEW_SINK(), None))
+            self._sink = None
+            return
+        pw, ph = self.preview_size
+
+        def _cb(user, p, pitch, hdr):
+            a = np.ctypeslib.as_array(p, shape=(ph * pitch,)).reshape(ph, pitch)[:, :pw * 3].reshape(ph, pw, 3).copy()
+            h = hdr.contents
+            fn(a, PreviewDataHeader(h.width, h.height, h.step, h.fps))
+
+        cb = PREVIEW_SINK(_cb)
+        _check(_lib.octvr_async_set_preview_sink(self._h, cb, None))
+        self._sink = cb  # keep the ctypes thunk alive
+
+    def info(self):
+        """Build-time facts of the pipeline (octvr_async_info): packed_bytes uploaded per frame, runs, ..."""
+        buf = C.create_string_buffer(1024)
+        _check(_lib.octvr_async_info(self._h, buf, len(buf)))
+        import json as _json
+        return _json.loads(buf.value.decode())
 
     def close(self):
         if self._h and self._h.value:

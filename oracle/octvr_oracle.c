@@ -1484,7 +1484,7 @@ void orc_resize_linear_cuda_f32(const float* src, int sw, int sh, float* dst, in
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* A12: CUDA fastRemap's texture bilinear, for measuring its distance from the adopted A13    */
+/* A12: CUDA fastRemap's texture bilinear (the OCTVR_REMAP_TEXTURE checker; A12 vs A13)      */
 /* ------------------------------------------------------------------------------------------ */
 /* fast_remap<uchar4> (cudawarping/src/cuda/fast_remap.cu:21-44) through a texture object with
  * normalized coordinates, clamp addressing, linear filtering and cudaReadModeNormalizedFloat
@@ -1492,8 +1492,10 @@ void orc_resize_linear_cuda_f32(const float* src, int sw, int sh, float* dst, in
  * repository; modelled after the CUDA Programming Guide's "Texture Fetching" appendix: x = u W - 0.5,
  * i = floor(x), alpha = frac(x) held with 8 fractional bits (truncated here), taps clamped to the
  * image, the weighted sum of the normalized texels in f32, then saturate_cast<uchar>(v * 255) (round
- * half to even).  map1 < 0 -> 0 (fill_zero).  Test infrastructure for the documented A12 tolerance
- * only: no product path follows these semantics (arithmetic contract). */
+ * half to even).  map1 < 0 -> 0 (fill_zero).  Test infrastructure: the checker of the product's
+ * opt-in OCTVR_REMAP_TEXTURE mode (stitch_tiled_tex_kernel / tex_bilerp_f follow these semantics bit for
+ * bit, tests/test_gpu_texture_mode.py, test_gpu_fullsize.py) and the measure of the default A13 path's
+ * documented A12 tolerance (arithmetic contract). */
 void orc_fast_remap_tex_rgba(const uint8_t* src, int w, int h, size_t spitch, const float* map1, const float* map2,
                              int mw, int mh, size_t mpitch, uint8_t* dst, size_t dpitch) {
     for (int y = 0; y < mh; y++)

@@ -115,7 +115,7 @@ int main(int argc, char** argv) {
         // ---- AsyncMultiMapper::New + push / pop (async.cpp:174-193) ---------------------------------
         std::vector<vr::MapperTemplate> mts{mt2};
         std::unique_ptr<vr::AsyncMultiMapper> am(vr::AsyncMultiMapper::New(
-            mts, sizes, mt2.out_size, {blend}, {0}, {cv::Rect_<double>(0, 0, 1, 1)}, cv::Size(0, 0)));
+            mts, sizes, mt2.out_size, {blend}, {0}, {cv::Rect_<double>(0, 0, 1, 1)}, cv::Size(pw, ph)));
         const int frames_n = 3;
         std::vector<std::vector<std::tuple<cv::Mat, cv::Mat, cv::Mat>>> ins(frames_n);
         std::vector<std::tuple<cv::Mat, cv::Mat, cv::Mat>> outs(frames_n);
@@ -140,6 +140,13 @@ int main(int argc, char** argv) {
             spit_mat(d + "out_async" + std::to_string(f) + "_y", std::get<0>(outs[f]));
             spit_mat(d + "out_async" + std::to_string(f) + "_u", std::get<1>(outs[f]));
             spit_mat(d + "out_async" + std::to_string(f) + "_v", std::get<2>(outs[f]));
+        }
+        {  // the preview of the last frame (async.cpp:149-171) and its PreviewDataHeader
+            cv::Mat pv;
+            vr::PreviewDataHeader hdr{};
+            if (!am->preview(pv, hdr)) throw std::runtime_error("no preview published");
+            spit_mat(d + "out_async_preview.rgb", pv);
+            std::ofstream(d + "preview_hdr.txt") << hdr.width << " " << hdr.height << " " << hdr.step << "\n";
         }
         am.reset();
 

@@ -177,3 +177,15 @@ def test_mapper_create_ex_rejects_unknown_flags(product_lib):
     rc = lib.octvr_mapper_create_ex(mt._h, 0, 2, w, h, 0, 1, 0, 0, 2, C.byref(out))
     assert rc == product_lib.E_INVALID and not out.value
     assert b"flags" in lib.octvr_last_error()
+
+
+@pytest.mark.parametrize("failing", [0, 3, 15])
+def test_worker_thread_error_becomes_a_status(product_lib, failing):
+    """A REQUIRE inside a host worker thread (the tiler's staged-group check, the seam finder, the audits)
+    reaches the caller as OCTVR_E_INVALID with the worker's message, and the process keeps running
+    (an exception leaving a std::thread would std::terminate it, Python included)."""
+    with pytest.raises(product_lib.OctvrError, match="worker %d failed" % failing):
+        product_lib.debug_worker_failure(16, failing)
+    product_lib.debug_worker_failure(16, -1)  # none fails: OK
+    with pytest.raises(product_lib.OctvrError):  # the library is still usable after the error
+        product_lib.debug_worker_failure(0, -1)

@@ -136,6 +136,11 @@ def test_gpu_cpp_api_drop_in(product_lib, tmp_path, name, blend):
         v = np.fromfile(os.path.join(d, "out_async%d_v" % f), np.uint8).reshape(H // 2, W // 2)
         assert np.array_equal(y, want[:H]), f
         assert np.array_equal(u, want[H:, :W // 2]) and np.array_equal(v, want[H:, W // 2:]), f
+    # AsyncMultiMapper::New(..., preview_size): the last frame's preview and its header
+    _, _, want_pv = O.stitch_frame(fr, sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, blend=blend,
+                                   seams=seams, threads=8, preview=(pw, ph))
+    assert np.array_equal(np.fromfile(os.path.join(d, "out_async_preview.rgb"), np.uint8).reshape(ph, pw, 3), want_pv)
+    assert open(os.path.join(d, "preview_hdr.txt")).read().split() == [str(pw), str(ph), "0"]
     # FastMapper::stitch_nv12 on the template without ROI
     luts = O.lut_build(O.json_loads_rj(text), W, H, use_roi=False)
     nv12 = []

@@ -34,22 +34,39 @@ def _frames(sizes, seed):
     return out
 
 
+_LUTS = {}
+
+
+def _oracle_lut(cfg):
+    """(rig, W, H, sizes, text, rois, maps1, maps2, masks) of a BASELINE config, the LUT built by the
+    oracle (cached per module: the 8K builds take seconds each)."""
+    from octvr_amd import synthetic
+    rig, W, H, sizes = synthetic.CONFIGS[cfg]()
+    text = json.dumps(rig)
+    key = (text, W, H)  # C3 shares C2's rig
+    if key not in _LUTS:
+        want = O.lut_build(O.json_loads_rj(text), W, H, threads=THREADS)
+        _LUTS[key] = ([list(r[0]) for r in want], [r[1] for r in want], [r[2] for r in want], [r[3] for r in want])
+    return (rig, W, H, sizes, text) + tuple(_LUTS[key])
+
+
+def _bench_frames(sizes, j):
+    """Frame set j as bench.py makes it (splitmix64 frames, the later sets derived from set 0)."""
+    from octvr_amd import synthetic
+    base = [synthetic.yuv_frame(w, h, 1000 + i) for i, (w, h) in enumerate(sizes)]
+    return base if j == 0 else [synthetic.derived_frame(f, 1000 + 100 * j + i) for i, f in enumerate(base)]
+
+
 @pytest.mark.parametrize("cfg", ["C1", "C2", "C3", "C4"])
 def test_gpu_fullsize_bit_exact(product_lib, cfg):
     import torch
     from octvr_amd import synthetic
     ox = product_lib
-    rig, W, H, sizes = synthetic.CONFIGS[cfg]()
+    rig, W, H, sizes, text, rois, maps1, maps2, masks = _oracle_lut(cfg)
     blend = synthetic.BLEND[cfg]
-    text = json.dumps(rig)
     n = len(sizes)
     # the LUT: GPU build (with its host recompute of deferred pixels) == oracle, bit for bit
     mt = ox.MapperTemplate.from_json(text, W, H)
-    want = O.lut_build(O.json_loads_rj(text), W, H, threads=THREADS)
-    rois = [list(r[0]) for r in want]
-    maps1 = [r[1] for r in want]
-    maps2 = [r[2] for r in want]
-    masks = [r[3] for r in want]
     for i in range(n):
         roi, g1, g2, gm, _ = mt.input(i)
         assert roi == tuple(rois[i]), (i, roi, rois[i])
@@ -214,3 +231,94 @@ def test_gpu_fullsize_f2_fastmapper(product_lib, monkeypatch, wide):
         d = got != _F2_ORACLE["want"][j]
         assert not d.any(), (wide, j, int(d.sum()), np.argwhere(d)[:4].tolist())
         assert got[:H].std() > 10
+
+
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_gpu_fullsize_texture_mode(product_lib, cfg):
+    """The texture-convention mode (OCTVR_REMAP_TEXTURE: the reference's live CUDA sampling,
+    fast_remap.cu:21-44) at the size its rate is quoted on: the staged instance (stitch_tiled_tex_kernel,
+    12-bit LDS dword offsets, interior tiles) and the gather kernel for border tiles, the multi-band remap
+    (C3) and the texture gain samples — three frames in flight on three streams, gains estimated, the
+    bench's splitmix frame sets and one smooth set, every byte and the gains against the oracle's
+    Mapper::stitch with the texture warp (orc_fast_remap_tex_rgba)."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    rig, W, H, sizes, text, rois, maps1, maps2, masks = _oracle_lut(cfg)
+    blend = synthetic.BLEND[cfg]
+    mt = ox.MapperTemplate.from_json(text, W, H)
+    seams = None
+    if blend:
+        mt.create_masks(0)
+        seams = O.create_masks(rois, masks, W)
+    m = ox.Mapper(mt, sizes, blend=blend, enable_gain=True, remap="texture")
+    info = m.info()
+    if not blend:  # most tiles are staged (interior), the fisheye circles' borders gather
+        assert info["tiles"] > 0 and info["wide_tiles"] < info["tiles"], info
+    k = 3
+    m.set_frames_in_flight(k)
+    sets = [_bench_frames(sizes, 0), _frames(sizes, 1), _bench_frames(sizes, 2)]
+    dev = [[torch.from_numpy(f).cuda() for f in fs] for fs in sets]
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(k)]
+    streams = [torch.cuda.Stream() for _ in range(k)]
+    torch.cuda.synchronize()
+    for f in range(k):
+        m.stitch(dev[f], outs[f], stream=streams[f])
+    g_last = np.array(m.gains())
+    torch.cuda.synchronize()
+    for f in range(k):
+        exp, g_orc = O.stitch_frame(sets[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None,
+                                    blend=blend, seams=seams, threads=THREADS, remap_tex=True)
+        got = outs[f].cpu().numpy()
+        d = got != exp
+        assert not d.any(), (cfg, f, int(d.sum()), np.argwhere(d)[:4].tolist())
+        if f == k - 1:
+            np.testing.assert_array_equal(g_last, np.array(g_orc))
+    if cfg == "C2":  # the AsyncMultiMapper in texture mode (the reference's AsyncMultiMapper runs vr::Mapper)
+        del dev
+        am = ox.AsyncMultiMapper([mt], sizes, (W, H), [0], [0], [(0.0, 0.0, 1.0, 1.0)], remap="texture")
+        aouts = []
+        for f in range(k):
+            o = (np.zeros((H, W), np.uint8), np.zeros((H // 2, W // 2), np.uint8), np.zeros((H // 2, W // 2), np.uint8))
+            am.push([(x[:h], x[h:, :w // 2], x[h:, w // 2:]) for x, (w, h) in zip(sets[f], sizes)], o)
+            aouts.append(o)
+        for f in range(k):
+            am.pop()
+            exp, _ = O.stitch_frame(sets[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True,
+                                    threads=THREADS, remap_tex=True)
+            assert np.array_equal(aouts[f][0], exp[:H]), (f, "Y")
+            assert np.array_equal(aouts[f][1], exp[H:, :W // 2]) and np.array_equal(aouts[f][2], exp[H:, W // 2:]), f
+        am.close()
+
+
+def test_gpu_fullsize_async_preview_c2(product_lib):
+    """AsyncMultiMapper::New(..., preview_size) on the C2 rig at full size with two regions (top and bottom
+    halves of the 8K output, each a scaled vr::Mapper): every preview byte (each region's Mapper preview
+    resize into its rectangle, async.cpp:73-90) and every output byte against the oracle, frames pipelined."""
+    import test_gpu_async as A
+    ox = product_lib
+    rig, W, H, sizes, text, rois, maps1, maps2, masks = _oracle_lut("C2")
+    mt = ox.MapperTemplate.from_json(text, W, H)
+    regions = [(0.0, 0.0, 1.0, 0.5), (0.0, 0.5, 1.0, 0.5)]
+    pv_size = (1920, 961)
+    am = ox.AsyncMultiMapper([mt, mt], sizes, (W, H), [0, 0], [0, 0], regions, preview_size=pv_size)
+    sunk = []
+    am.set_preview_sink(lambda a, h: sunk.append(a))
+    sets = [_frames(sizes, 0), _bench_frames(sizes, 1)]
+    outs = []
+    for fs in sets:
+        o = (np.zeros((H, W), np.uint8), np.zeros((H // 2, W // 2), np.uint8), np.zeros((H // 2, W // 2), np.uint8))
+        am.push([(x[:h], x[h:, :w // 2], x[h:, w // 2:]) for x, (w, h) in zip(fs, sizes)], o)
+        outs.append(o)
+    for _ in sets:
+        am.pop()
+    assert len(sunk) == len(sets)
+    for f, fs in enumerate(sets):
+        want_out, want_pv = A.preview_oracle(fs, sizes, rois, maps1, maps2, masks, W, H, [0, 0], [0, 0], regions,
+                                             (W, H), pv_size, threads=THREADS)
+        for p in range(3):
+            assert np.array_equal(outs[f][p], want_out[p]), (f, p)
+        d = sunk[f] != want_pv
+        assert not d.any(), (f, int(d.sum()), np.argwhere(d)[:4].tolist())
+        assert sunk[f].std() > 5
+    am.close()

@@ -72,25 +72,29 @@ def test_bench_harness_two_ranks_gloo(tmp_path):
     assert r[0]["value"] == pytest.approx(world * 3 * r[0]["px"] / 1e6 / r[0]["elapsed"])
 
 
-def test_bench_entry_point_gpus2_standin():
-    """bench.py's own `--gpus 2` path (no WORLD_SIZE: bench.launch_ranks starts the ranks itself),
-    with the oracle standing in for the HIP stitch: one JSON line, n_gpus 2, both ranks' frames."""
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_entry_point_standin(n):
+    """bench.py's own `--gpus N` path (no WORLD_SIZE: bench.launch_ranks starts the ranks itself),
+    with the oracle standing in for the HIP stitch: one JSON line, n_gpus N, every rank's frames, one
+    local rank (device) per rank.  N = 8 is the driver's scaling run on a full node (SCALE_rNN), which
+    this pool never lets a builder launch on GPUs: here it runs as 8 CPU ranks over gloo."""
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
-    p = subprocess.run([sys.executable, os.path.join(here, "bench_standin.py"), "--gpus", "2", "--steps", "2",
-                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=300)
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, os.path.join(here, "bench_standin.py"), "--gpus", str(n), "--steps", "2",
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=600)
     assert p.returncode == 0, p.stderr[-2000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2
-    assert sorted(r["rank"] for r in d["ranks"]) == [0, 1]
-    assert sorted(r["local_rank"] for r in d["ranks"]) == [0, 1]
+    assert d["n_gpus"] == n and d["steps"] == 2
+    assert sorted(r["rank"] for r in d["ranks"]) == list(range(n))
+    assert sorted(r["local_rank"] for r in d["ranks"]) == list(range(n))
     assert all(r["frames"] == 2 for r in d["ranks"])
-    assert d["ranks"][0]["digest"] != d["ranks"][1]["digest"]  # independent rigs (rank-seeded frames)
-    assert d["value"] == pytest.approx(2 * 2 * d["frame_px"] / 1e6 / d["elapsed"])
+    assert len({r["digest"] for r in d["ranks"]}) == n  # independent rigs (rank-seeded frames)
+    assert d["value"] == pytest.approx(n * 2 * d["frame_px"] / 1e6 / d["elapsed"])
 
 
 def test_bench_entry_point_rejects_mismatch():
