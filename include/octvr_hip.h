@@ -327,6 +327,12 @@ int octvr_debug_fastmapper_audit(const octvr_rig* rig, int n_inputs, const int* 
  * creation flags (OCTVR_REMAP_TEXTURE: texture-convention entries, interior ones staged, border tiles wide). */
 int octvr_debug_tiled_lut_info(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, int flags,
                                char* json, size_t len);
+/* The gain feed's samples as octvr_mapper_create lays them out (host only, no GPU): per sample its entry
+ * (samples[2k] = xy, samples[2k+1] = code, kernels.hpp CompositeEntry) and partner mask, in the order the
+ * feed's waves take them (padding included).  count receives the number of samples; samples / partners
+ * NULL = count only. */
+int octvr_debug_gain_plan(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, int flags,
+                          uint32_t* samples, uint16_t* partners, size_t cap, size_t* count);
 /* The rig-config JSON reader on one document: the first number of `json` (a number, or the first element
  * of an array), parsed with rapidjson's rules (flags 0, as the reference reads its configs) or correctly
  * rounded (OCTVR_JSON_EXACT; out-of-range literals give +-HUGE_VAL / the subnormal / 0 as strtod). */

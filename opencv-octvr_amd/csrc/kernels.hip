@@ -395,6 +395,11 @@ struct FeedRaw {
     uint32_t meta;  // code bits 0-15 (fx, fy, valid), in-image ix0 ix1 iy0 iy1 at 16-19, V row shifts at 20-22 / 23-25
 };
 
+#ifdef OCTVR_DIAG_FEED_NOLOAD
+#define DIAGF(a_) (((a_) & 0u) + (threadIdx.x & 7u) * 8u)
+#else
+#define DIAGF(x) (x)
+#endif
 __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
                                                 uint32_t code, FeedRaw& r) {
     const TapCell tc = tap_cell(xy, f.w, f.h);
@@ -405,17 +410,21 @@ __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const
     const uint32_t xa = x0 & ~3u, ca = c0 & ~3u;
     const uint32_t ry0 = (uint32_t)tc.y0 * p, ry1 = (uint32_t)tc.y1 * p;
     const uint32_t rc0 = (uint32_t)(tc.y0 >> 1) * p, rc1 = (uint32_t)(tc.y1 >> 1) * p;
+#ifdef OCTVR_DIAG_FEED_NOLOAD
+    const uint32_t sv0 = 0, sv1 = 0;
+#else
     const uint32_t sv0 = vo + rc0 + ca, sv1 = vo + rc1 + ca;
+#endif
     const uint32_t lv0 = min(sv0, lim), lv1 = min(sv1, lim);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 t;
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, ry0 + xa, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry0 + xa), 0, 0);
     r.y0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, ry1 + xa, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry1 + xa), 0, 0);
     r.y1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + rc0 + ca, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc0 + ca), 0, 0);
     r.u0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + rc1 + ca, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc1 + ca), 0, 0);
     r.u1 = make_uint2(t.x, t.y);
     t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv0, 0, 0);
     r.v0 = make_uint2(t.x, t.y);
@@ -950,7 +959,11 @@ __device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, con
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++) {
         typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+#ifdef OCTVR_DIAG_HALFENT
+        const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * kItemHalves + 0) * (uint32_t)(kTilePx * 4);
+#else
         const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
+#endif
         const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
         d.e4[h] = uint4{v.x, v.y, v.z, v.w};
     }

@@ -972,9 +972,17 @@ std::vector<float> resize_linear_f32(const float* src, int sw, int sh, int dw, i
 
 // Working-scale gain setup: Mapper ctor (mapper.cpp:94-114,140-142) + GainCompensatorGPU ctor
 // (exposure_compensate.cpp:174-221).  Produces per-pair sample entries of both cameras for every
-// pixel of the bitwise-AND intersection of the resized masks, N(i,j), and chunking.
-void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
-    const int n = m.n;
+// pixel of the bitwise-AND intersection of the resized masks, N(i,j), and chunking — on the host only
+// (plan_gain), then uploaded (setup_gain).
+struct GainPlan {
+    std::vector<CompositeEntry> samples;
+    std::vector<uint16_t> partners;
+    std::vector<int32_t> N;
+    int n_chunks = 0;
+    size_t pairs_px = 0;
+};
+
+GainPlan plan_gain(const octvr_rig& rig, int n, const std::vector<int>& in_w, const std::vector<int>& in_h, int tex) {
     double ws = std::min(1.0, std::sqrt(0.1 * 1e6 / ((double)rig.out_w * rig.out_h)));
     std::vector<std::array<int, 4>> wr(n);
     std::vector<std::vector<uint8_t>> smask(n);
@@ -995,8 +1003,8 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
                 size_t k = (size_t)sy * in.roi[2] + sx;
                 CompositeEntry e{0, 0};
                 if (in.mask[k])
-                    e = m.tex ? make_entry_tex(in.map1[k], in.map2[k], (float)m.in_w[i], (float)m.in_h[i], i)
-                              : make_entry(in.map1[k], in.map2[k], (float)m.in_w[i], (float)m.in_h[i], i);
+                    e = tex ? make_entry_tex(in.map1[k], in.map2[k], (float)in_w[i], (float)in_h[i], i)
+                            : make_entry(in.map1[k], in.map2[k], (float)in_w[i], (float)in_h[i], i);
                 samp[i][(size_t)y * ww + x] = e;
             }
         int nz = 0;
@@ -1060,21 +1068,30 @@ void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
         pmask.push_back(0);
     }
     n_chunks = (int)(uniq.size() / kGainChunk);
-    for (const CompositeEntry& e : uniq) m.foot.mark_taps(e);
-    m.samples.upload(uniq.data(), uniq.size());
-    m.partners.upload(pmask.data(), pmask.size());
     // exactness bound of the fixed-point totals (kernels.hip, gain feed): < 2^21 samples per camera
     for (int i = 0; i < n; i++) REQUIRE(samp[i].size() < (1u << 21), "working-scale ROI too large for exact gain sums");
+    GainPlan g;
+    g.samples = std::move(uniq);
+    g.partners = std::move(pmask);
+    g.N = std::move(N);
+    g.n_chunks = n_chunks;
+    for (uint16_t pm : g.partners) g.pairs_px += (size_t)__builtin_popcount(pm);
+    return g;
+}
+
+void setup_gain(octvr_mapper& m, const octvr_rig& rig) {
+    const GainPlan g = plan_gain(rig, m.n, m.in_w, m.in_h, m.tex);
+    for (const CompositeEntry& e : g.samples) m.foot.mark_taps(e);
+    m.samples.upload(g.samples.data(), g.samples.size());
+    m.partners.upload(g.partners.data(), g.partners.size());
     m.totals.alloc((size_t)kGainMaxCams * kGainMaxCams * kGainTotalStride);
     HIP_CHECK(hipMemset(m.totals.p, 0, sizeof(unsigned long long) * kGainMaxCams * kGainMaxCams * kGainTotalStride));
-    m.N.upload(N.data(), N.size());
+    m.N.upload(g.N.data(), g.N.size());
     m.tickets.alloc(9);
     HIP_CHECK(hipMemset(m.tickets.p, 0, sizeof(uint32_t) * 9));
-    m.n_chunks = n_chunks;
-    m.n_samples = (int)uniq.size();
-    size_t pairs_px = 0;
-    for (uint16_t pm : pmask) pairs_px += (size_t)__builtin_popcount(pm);
-    m.n_entries = pairs_px;
+    m.n_chunks = g.n_chunks;
+    m.n_samples = (int)g.samples.size();
+    m.n_entries = g.pairs_px;
 }
 
 }  // namespace
@@ -1851,6 +1868,26 @@ int octvr_remap_u8(const uint8_t* src, int sw, int sh, size_t spitch, int cn, co
         if (mw == 0 || mh == 0) return;
         HIP_CHECK(launch_remap_u8(src, sw, sh, (int64_t)spitch, cn, map1, map2, mw, mh, (int64_t)mpitch, scale_x,
                                   scale_y, dst, (int64_t)dpitch, (hipStream_t)stream));
+    });
+}
+
+int octvr_debug_gain_plan(const octvr_rig* rig, int n_inputs, const int* in_w, const int* in_h, int flags,
+                          uint32_t* samples, uint16_t* partners, size_t cap, size_t* count) {
+    return guarded([&] {
+        REQUIRE(rig && in_w && in_h && count, "bad arguments");
+        REQUIRE((flags & ~OCTVR_REMAP_TEXTURE) == 0, "unknown mapper flags");
+        const int n = (int)rig->inputs.size();
+        REQUIRE(n_inputs == n && n > 0 && n <= kGainMaxCams, "in_sizes must cover the inputs");
+        const GainPlan g = plan_gain(*rig, n, std::vector<int>(in_w, in_w + n), std::vector<int>(in_h, in_h + n),
+                                     (flags & OCTVR_REMAP_TEXTURE) ? 1 : 0);
+        *count = g.samples.size();
+        if (!samples || !partners) return;
+        REQUIRE(cap >= g.samples.size(), "buffer too small");
+        for (size_t k = 0; k < g.samples.size(); k++) {
+            samples[2 * k] = g.samples[k].xy;
+            samples[2 * k + 1] = g.samples[k].code;
+            partners[k] = g.partners[k];
+        }
     });
 }
 

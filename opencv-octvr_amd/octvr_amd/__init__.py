@@ -130,6 +130,9 @@ if hasattr(_lib, "octvr_debug_tiled_lut_info"):
 if hasattr(_lib, "octvr_debug_fastmapper_audit"):
     _lib.octvr_debug_fastmapper_audit.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
                                                   C.c_int, C.c_char_p, C.c_size_t]
+if hasattr(_lib, "octvr_debug_gain_plan"):
+    _lib.octvr_debug_gain_plan.argtypes = [_VP, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int, _VP, _VP,
+                                           C.c_size_t, C.POINTER(C.c_size_t)]
 if hasattr(_lib, "octvr_debug_worker_failure"):
     _lib.octvr_debug_worker_failure.argtypes = [C.c_int, C.c_int]
 _lib.octvr_remap_u8.argtypes = [_VP, C.c_int, C.c_int, C.c_size_t, C.c_int, _VP, _VP, C.c_int, C.c_int, C.c_size_t,
@@ -174,6 +177,22 @@ def debug_worker_failure(n_threads, failing):
     """Run the host build's worker-thread helper with thread `failing` raising (octvr_debug_worker_failure;
     no GPU): raises OctvrError with the worker's message, as a failing tiler / seam / audit worker does."""
     _check(_lib.octvr_debug_worker_failure(int(n_threads), int(failing)))
+
+
+def debug_gain_plan(mt, in_sizes, remap="remap"):
+    """(entries, partners): the gain feed's samples as the mapper lays them out (octvr_debug_gain_plan; no
+    GPU) — entries an (n, 2) uint32 array of (xy, code), partners a uint16 array."""
+    import numpy as _np
+    n = len(in_sizes)
+    w = (C.c_int * n)(*[s[0] for s in in_sizes])
+    h = (C.c_int * n)(*[s[1] for s in in_sizes])
+    fl = REMAP_TEXTURE if remap == "texture" else 0
+    cnt = C.c_size_t()
+    _check(_lib.octvr_debug_gain_plan(mt._h, n, w, h, fl, None, None, 0, C.byref(cnt)))
+    e = _np.zeros((cnt.value, 2), _np.uint32)
+    p = _np.zeros(cnt.value, _np.uint16)
+    _check(_lib.octvr_debug_gain_plan(mt._h, n, w, h, fl, e.ctypes.data, p.ctypes.data, cnt.value, C.byref(cnt)))
+    return e, p
 
 
 def debug_json_number(text, exact=True):

@@ -84,3 +84,27 @@ def test_tiled_lut_c2(product_lib):
     tex = ox.debug_tiled_lut_info(mt, sizes, remap="texture")
     assert tex["tex"] == 1 and tex["items"] + tex["wide_tiles"] // 2 == info["items"]
     assert tex["wide_tiles"] < 0.05 * info["items"]
+
+
+@pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
+def test_gain_plan_layout(product_lib, name):
+    """The gain feed's sample layout on the host (octvr_debug_gain_plan, as octvr_mapper_create builds it):
+    whole workgroups of 768 samples, one camera per wave run of 192 (kGainWaveRun: the wave's frame is
+    uniform), no sample partnered with its own camera, padding samples invalid with no partner."""
+    ox = product_lib
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    mt = ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), [z[f"map1_{i}"] for i in range(n)],
+                                       [z[f"map2_{i}"] for i in range(n)], [z[f"mask_{i}"] for i in range(n)])
+    sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
+    e, p = ox.debug_gain_plan(mt, sizes)
+    assert len(e) % 768 == 0 and len(e) == len(p)
+    cam = (e[:, 1] >> 10) & 31
+    valid = (e[:, 1] >> 15) & 1
+    runs = cam.reshape(-1, 192)
+    assert (runs == runs[:, :1]).all()  # one camera per wave run
+    assert not ((p.astype(np.uint32) >> cam) & 1).any()  # never its own partner
+    assert (valid[p != 0] <= 1).all()  # (mask-0 samples keep their partners: they add a zero norm)
+    if name != "rigD":  # rigD's inputs do not overlap at the working scale
+        assert (p != 0).sum() > 0
