@@ -400,6 +400,10 @@ struct FeedRaw {
 #else
 #define DIAGF(x) (x)
 #endif
+#ifndef OCTVR_FEED_AUX
+#define OCTVR_FEED_AUX 0
+#endif
+constexpr int kFeedAux = OCTVR_FEED_AUX;
 __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
                                                 uint32_t code, FeedRaw& r) {
     const TapCell tc = tap_cell(xy, f.w, f.h);
@@ -418,17 +422,17 @@ __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const
     const uint32_t lv0 = min(sv0, lim), lv1 = min(sv1, lim);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 t;
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry0 + xa), 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry0 + xa), 0, kFeedAux);
     r.y0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry1 + xa), 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry1 + xa), 0, kFeedAux);
     r.y1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc0 + ca), 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc0 + ca), 0, kFeedAux);
     r.u0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc1 + ca), 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc1 + ca), 0, kFeedAux);
     r.u1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv0, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv0, 0, kFeedAux);
     r.v0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv1, 0, 0);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv1, 0, kFeedAux);
     r.v1 = make_uint2(t.x, t.y);
     const uint32_t iy = x0 & 3u, ic = c0 & 3u;  // x1 - x0, c1 - c0 in {0, 1}
     r.sel = iy | (iy + (x1 - x0)) << 8 | ic << 16 | (ic + (c1 - c0)) << 24;
@@ -824,11 +828,17 @@ __device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, 
     const gu8* Vb = Ub + (f.w >> 1);
     const uint32_t oy = __umul24(row, p32) + col * 8u, oc = __umul24(row >> 1, p32) + col * 4u;
     if (DWORD_STAGE) {
+#ifdef OCTVR_NT_STAGE
+        const uint64_t yy = __builtin_nontemporal_load((const gu64*)(Yb + oy));
+        sg.uq = __builtin_nontemporal_load((const gu32*)(Ub + oc));
+        sg.vq = __builtin_nontemporal_load((const gu32*)(Vb + oc));
+#else
         const uint64_t yy = *(const gu64*)(Yb + oy);
-        sg.y0 = (uint32_t)yy;
-        sg.y1 = (uint32_t)(yy >> 32);
         sg.uq = *(const gu32*)(Ub + oc);
         sg.vq = *(const gu32*)(Vb + oc);
+#endif
+        sg.y0 = (uint32_t)yy;
+        sg.y1 = (uint32_t)(yy >> 32);
     } else {
         const gu8* Yp = Yb + oy;
         const gu8* Up = Ub + oc;
@@ -855,8 +865,13 @@ __device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, 
 // zero-extended it right after the load, into the loop-carried register, and that copy waited on every
 // load of the iteration (vmcnt(0) before the compute); widened at the use, an iteration later, it waits
 // on nothing (one frame in flight: C2 composite -1 %, C3 +1 %, `u16`).
+#ifdef OCTVR_DIAG_DUP
+#define DUPT(t_) ((t_) >> 1)
+#else
+#define DUPT(t_) (t_)
+#endif
 __device__ __forceinline__ uint16_t group_issue(const __amdgpu_buffer_rsrc_t& gr, int t, int t_end) {
-    const int tt = t < t_end ? t : 0;
+    const int tt = DUPT(t < t_end ? t : 0);
     return __builtin_amdgcn_raw_buffer_load_b16(gr, (uint32_t)threadIdx.x * 2u,
                                                 (uint32_t)uniform(tt) * (uint32_t)(kGroupFirst * 64 * 2), 0);
 }
@@ -917,7 +932,7 @@ constexpr int kStitchTexRegBlocks = 5, kStitchTexVgprs = 96;
 // record offset a scalar, so no per-lane 64-bit address is held across the loop.
 __device__ __forceinline__ uint4 meta_issue(const __amdgpu_buffer_rsrc_t& mr, int t, int t_end) {  // t: staged item
     const int lane = threadIdx.x & 63;
-    const int tt = t < t_end ? t : 0;  // t >= 0: every item index derives from bounded claims
+    const int tt = DUPT(t < t_end ? t : 0);  // t >= 0: every item index derives from bounded claims
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     uint4 v;
     if (lane < kMetaWords) {  // exec-masked: the instruction (and its vmcnt) is the same for every wave
@@ -951,6 +966,10 @@ struct TileData {
 // er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
 // scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
 // that the entries fit 32-bit offsets)
+#ifndef OCTVR_ENT_AUX
+#define OCTVR_ENT_AUX 0
+#endif
+constexpr int kEntAux = OCTVR_ENT_AUX;
 template <bool DWORD_STAGE, bool VIG>
 __device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, const TileMeta& m, int t_end,
                                            const StageSlot& sl, uint32_t g, TileData& d) {
@@ -962,9 +981,9 @@ __device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, con
 #ifdef OCTVR_DIAG_HALFENT
         const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * kItemHalves + 0) * (uint32_t)(kTilePx * 4);
 #else
-        const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
+        const uint32_t so = (uint32_t)uniform(DUPT(live ? m.t : 0) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
 #endif
-        const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
+        const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, kEntAux);
         d.e4[h] = uint4{v.x, v.y, v.z, v.w};
     }
     if (!sl.live) {  // wave-uniform: no loads for a chunk the item lacks
@@ -1107,8 +1126,13 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     const int groups = kStitchBands;
     const int g = blockIdx.x % groups;
     const int step = (gridDim.x - g + groups - 1) / groups;
+#ifdef OCTVR_DIAG_DUP
+    const int t_begin = 2 * lut.bands[g];
+    const int t_end = 2 * lut.bands[g + 1];
+#else
     const int t_begin = lut.bands[g];
     const int t_end = lut.bands[g + 1];
+#endif
     const __amdgpu_buffer_rsrc_t ersrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kItemHalves * kTilePx * 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
