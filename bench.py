@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--preroll", type=float, default=0.5,
                     help="seconds of untimed steps after the warmup steps, so that the timed steps run at the "
                          "GPU's settled clock (it idles during setup and takes ~0.1 s to ramp, DESIGN.md §4)")
+    ap.add_argument("--batch", type=int, default=None, choices=[1, 2, 4],
+                    help="frames per composite launch (octvr_mapper_stitch_batch: each frame its own gain feed, one "
+                         "pass over the tiled LUT for all of them); a step is still one frame (default per config, "
+                         "DEFAULT_BATCH)")
     ap.add_argument("--remap", default="remap", choices=["remap", "texture"],
                     help="sampling: cv::remap's fixed point (default) or the CUDA texture convention (OCTVR_REMAP_TEXTURE)")
     return ap.parse_args()
@@ -214,6 +218,8 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, gain=True, 
     ins = [(f[:h], f[h:, :w // 2], f[h:, w // 2:]) for f, (w, h) in zip(frames_np, sizes)]
     outs = [(np.empty((H, W), np.uint8), np.empty((H // 2, W // 2), np.uint8), np.empty((H // 2, W // 2), np.uint8))
             for _ in range(4)]
+    for o in outs:  # a ring of output frames the caller reuses: downloaded straight into (no copy-out)
+        am.register_output(o)
 
     def run(n):
         for k in range(n):
@@ -234,14 +240,17 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, gain=True, 
             "h2d_bytes_per_frame": int(info["packed_bytes"]), "d2h_bytes_per_frame": info["output_bytes"],
             "gain": "estimated" if gain else "none", "remap": remap,
             "note": "AsyncMultiMapper push->pop of host YUV420P planes: copy-in of the mapper's source footprint to "
-                    "pinned staging, H2D, unpack, stitch, D2H, copy-out, 3 frames in flight; PCIe- and "
-                    "host-copy-inclusive, not the roofline basis"}
+                    "pinned staging, H2D, unpack, stitch, D2H straight into the caller's registered output ring "
+                    "(octvr_async_register_output), 3 frames in flight; PCIe- and host-copy-inclusive, not the "
+                    "roofline basis"}
 
 
 # frames in flight per config, from interleaved sweeps on one box (scripts/r4_inflight_sweep.sh): C2 2 / 3 / 4 =
 # 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k, C1 371k / 483k / 485k (3 kept: the
 # two 4s were 511k and 459k), F2 (stitch_nv12 on 1 / 2 / 3 streams) 85k / 91k / 93k
 DEFAULT_INFLIGHT = {"C3": 4, "F2": 3}
+# frames per composite launch (octvr_mapper_stitch_batch), no-blend configs only
+DEFAULT_BATCH = {}
 CPU_BASELINE_S = float(os.environ.get("OCTVR_CPU_BASELINE_S", "10"))
 DEFAULT_FRAME_SETS = 8
 
@@ -491,25 +500,38 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
     inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 3))
-    m.set_frames_in_flight(inflight)
+    # frames per composite launch: a batch of nb frames per call on each of the `inflight` streams
+    nb = args.batch if args.batch is not None else (DEFAULT_BATCH.get(args.config, 1) if blend == 0 else 1)
+    if blend != 0 and nb != 1:
+        raise SystemExit("bench.py: --batch needs the no-blend composite (multi-band / feather stitch frame by frame)")
+    if args.steps % nb:
+        raise SystemExit("bench.py: --steps must be a multiple of --batch")
+    m.set_frames_in_flight(inflight * nb)
     # each rank stitches an independent rig instance: frames seeded by (rank, frame set, camera); the
     # steps rotate through nsets distinct sets (> 256 MB of sources for C2 / C4 at the default 8, so the
     # Infinity Cache cannot keep them between steps)
-    nsets = frame_sets_of(args, inflight)
+    nsets = frame_sets_of(args, inflight * nb)
     frames_np = [synthetic.yuv_frame(w, h, frame_seed(rank, 0, i)) for i, (w, h) in enumerate(sizes)]
     frame_sets = [[torch.from_numpy(f).to(f"cuda:{dev}") for f in frames_np]]
     for j in range(1, nsets):
         frame_sets.append(derive_set(frame_sets[0], [frame_seed(rank, j, i) for i in range(len(sizes))]))
-    outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
+    outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight * nb)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     # the frame sets' pointers marshalled once, raw stream handles (a capture ring reuses its buffers)
     refs = [ox.Mapper.frame_refs(fs) for fs in frame_sets]
     import ctypes
     raw_streams = [ctypes.c_void_p(st.cuda_stream) for st in streams]
+    # batches: call c takes frame sets c nb .. c nb + nb - 1 (mod nsets) and the outputs of its stream
+    ncalls = nsets * inflight
+    brefs = [ox.Mapper.batch_refs([refs[(c * nb + f) % nsets] for f in range(nb)],
+                                  outs[(c % inflight) * nb:(c % inflight + 1) * nb]) for c in range(ncalls)] if nb > 1 else None
 
-    def step(k):
+    def step(k):  # one call: one frame (nb = 1) or a batch of nb frames
         j = k % inflight
-        m.stitch(refs[k % nsets], outs[j], stream=raw_streams[j])
+        if nb == 1:
+            m.stitch(refs[k % nsets], outs[j], stream=raw_streams[j])
+        else:
+            m.stitch_batch(brefs[k % ncalls], stream=raw_streams[j])
 
     if args.pmc_child:  # a few launches for rocprofv3 --pmc passes
         for k in range(max(args.steps, 1)):
@@ -532,11 +554,12 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # of that stream's timeline).  Several: every step on every stream, so the union of the launches'
     # intervals (the wall time some composite was running) is known; a launch's own start-to-end
     # span then also covers the other streams' kernels beside it.
-    m.set_timing(1 if inflight > 1 else 4)
-    elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
+    m.set_timing(1 if inflight > 1 or nb > 1 else 4)
+    elapsed = timed_region(step, args.steps // nb, lambda: torch.cuda.synchronize(dev), dist)
     m.set_timing(False)
     span_ms, busy_ms, launches = m.kernel_busy()
     kern_ms = busy_ms if inflight > 1 else span_ms
+    launches *= nb  # per frame: a batched launch stitches nb frames
     serial = serial_step = None
     if inflight > 1 and not dist:
         # supplementary, after the timed region: the composite kernel's duration with one frame in
@@ -600,15 +623,17 @@ def gpu_rank(args, world, rank, local_rank, dist):
                                    "gain (estimated per frame)" if use_gain else "no gain",
                                    "multi-band blend=%d (%d bands)" % (blend, int(math.ceil(math.log(blend) / math.log(2.)) - 1))
                                    if blend > 0 else "no-blend composite"),
-                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
+                   "rigs_per_gpu": 1, "frames_in_flight": inflight * nb, "streams": inflight,
+                   "frames_per_launch": nb, "frame_sets": nsets,
                    **({"remap": "texture (OCTVR_REMAP_TEXTURE)"} if args.remap == "texture" else {}),
                    "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "multiband sequence (remap, pyrDown, blend levels)" if blend > 0 else "stitch_kernel",
                      "kernel_us": round(avg_kernel_s * 1e6, 2),
-                     "kernel_us_basis": ("union of the launches' HIP-event intervals over %d in-flight streams, per launch"
-                                         % inflight) if inflight > 1 else "HIP-event start-to-end, every 4th launch",
+                     "kernel_us_basis": ("union of the launches' HIP-event intervals over %d in-flight streams, per frame "
+                                         "(%d frames per launch)" % (inflight, nb)) if inflight > 1 or nb > 1 else
+                                        "HIP-event start-to-end, every 4th launch",
                      "kernel_us_span": round(span_ms / 1e3 / max(launches, 1) * 1e6, 2),
                      "bytes_per_launch": bytes_per_launch,
                      "bytes_basis": "algorithmic: what each launch must move, each byte once (DESIGN.md §4; "

@@ -163,6 +163,16 @@ int octvr_mapper_create_ex(const octvr_rig* rig, int device, int n_inputs, const
  * (GainCompensatorGPU::feed), else set_gains (n_gains == n_inputs).  Stream-ordered, no host sync. */
 int octvr_mapper_stitch_yuv420p(octvr_mapper* mapper, const uint8_t* const* in_dev, const size_t* in_pitch,
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream);
+/* n_frames (1, 2 or 4) consecutive frames of the same rig in one call (no reference counterpart; the
+ * reference stitches a frame per Mapper::stitch): frame f's inputs are in_dev[f * n_inputs + i] /
+ * in_pitch[...], its output out_dev[f] (all outputs of pitch out_pitch); gains NULL = estimate every frame's
+ * own gains, else n_frames * n_inputs values.  Each frame gets its own gain feed into its own frame slot, then
+ * ONE composite launch stitches all of them: its work runs over (item, frame) pairs, so an item's LUT entries,
+ * metadata and staging groups are fetched once for the batch.  Every output equals a separate stitch of its
+ * frame, bit for bit.  Needs n_frames frames in flight (octvr_mapper_set_frames_in_flight) and, for 4, at
+ * most 16 inputs; scaled-output and multi-band / feather mappers stitch the frames one by one. */
+int octvr_mapper_stitch_batch(octvr_mapper* mapper, int n_frames, const uint8_t* const* in_dev, const size_t* in_pitch,
+                              uint8_t* const* out_dev, size_t out_pitch, const double* gains, void* stream);
 /* The same with Mapper::stitch's preview_output (mapper.cpp:308-312): the RGB result resized
  * (cuda::resize INTER_LINEAR) into a preview_w x preview_h CV_8UC3 device image (3 bytes per pixel,
  * row pitch preview_pitch); preview_dev NULL = none.  Needs one frame in flight. */
@@ -178,7 +188,7 @@ int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
  * A stitch waits (through an event) only for its slot's previous stitch.
  * k > 1 needs the output at template size (no scaled output; OCTVR_E_UNSUPPORTED otherwise);
  * multi-band / feather mappers get per-slot pyramids.  Synchronizes. */
-#define OCTVR_MAX_FRAMES_IN_FLIGHT 4
+#define OCTVR_MAX_FRAMES_IN_FLIGHT 8
 int octvr_mapper_set_frames_in_flight(octvr_mapper* mapper, int k);
 /* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 4 B tiled
  * LUT entry (8 B in wide tiles) + 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each
@@ -261,6 +271,15 @@ int octvr_async_push(octvr_async* async, const uint8_t* const* in_planes, const 
 /* pop() (async.cpp:191-193): blocks until the oldest pushed frame has been written to its output planes;
  * returns that frame's status (OCTVR_E_INVALID if nothing is pending). */
 int octvr_async_pop(octvr_async* async);
+/* Register an output plane set (Y, U, V of out_w x out_h, out_w/2 x out_h/2, ...) that the caller reuses
+ * (a ring of output frames, as the reference reuses its output Mats, async.cpp:113-138): the planes are
+ * page-locked (hipHostRegister) and every later push with exactly these pointers and pitches is downloaded
+ * straight into them — no pinned staging, no host copy-out.  The planes must stay allocated until
+ * octvr_async_unregister_output or octvr_async_destroy.  OCTVR_E_HIP if the memory cannot be locked (the
+ * planes then keep the staging path). */
+int octvr_async_register_output(octvr_async* async, uint8_t* const* planes, const size_t* pitches);
+/* Undo octvr_async_register_output (no frame may be pending). */
+int octvr_async_unregister_output(octvr_async* async, uint8_t* const* planes);
 /* Frames pushed and not yet popped. */
 int octvr_async_pending(const octvr_async* async, int* n);
 /* Drains the frames in flight and joins the pipeline's worker threads (the reference leaves its five

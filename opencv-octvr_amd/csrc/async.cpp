@@ -17,6 +17,10 @@
 //     device by one kernel: with the copy chain each output pixel comes from one camera, so a C2 frame
 //     needs ~18 MB of its 75 MB of YUV (the composite's staged groups plus the gain samples' row pairs,
 //     DESIGN.md §6);
+//   * output planes the caller registers once (octvr_async_register_output: a ring it reuses, as the
+//     reference's own output Mats are reused, async.cpp:113-138) are page-locked and written by the D2H
+//     copies directly, region by region (2-D copies at the caller's pitch): no pinned staging and no
+//     copy-out for them; other planes take the staging path;
 //   * the preview (async.cpp:73-110, 141-171) is published to a caller-read buffer and an optional sink
 //     (octvr_async_pop_preview / octvr_async_set_preview_sink) instead of Qt shared memory, which stays
 //     the caller's.
@@ -148,6 +152,7 @@ struct Job {
     std::vector<size_t> in_pitches;
     uint8_t* out_planes[3] = {nullptr, nullptr, nullptr};
     size_t out_pitches[3] = {0, 0, 0};
+    bool direct = false;  // the output planes are registered: the D2H writes them, no copy-out
     int slot = -1;
     int status = OCTVR_OK;
     std::string error;
@@ -261,6 +266,12 @@ struct octvr_async {
     size_t packed_bytes = 0;
     DevBuf<FootRun> runs_dev;
     Slot slots[kSlots];
+    // output plane sets the caller registered (octvr_async_register_output): page-locked, downloaded into
+    struct RegOut {
+        uint8_t* p[3];
+        size_t pitch[3];
+    };
+    std::vector<RegOut> reg_out;  // caller thread only (register / push / destroy)
     hipStream_t up = nullptr, comp = nullptr, down = nullptr;
     Channel<std::shared_ptr<Job>> q_in, q_up, q_map, q_down, q_out, q_done;
     Channel<int> free_slots;
@@ -275,6 +286,8 @@ struct octvr_async {
         int prev = -1;
         (void)hipGetDevice(&prev);
         (void)hipSetDevice(device);
+        for (const RegOut& r : reg_out)
+            for (uint8_t* p : r.p) (void)hipHostUnregister(p);
         for (hipStream_t s : {up, comp, down})
             if (s) (void)hipStreamDestroy(s);
         for (auto& sl : slots) {
@@ -365,9 +378,26 @@ struct octvr_async {
         stage(j, [&] {
             DeviceGuard dg(device);
             Slot& sl = slots[j.slot];
-            for (size_t k = 0; k < mappers.size(); k++)
-                HIP_CHECK(hipMemcpyAsync(sl.out_host[k]->p, sl.out_dev[k].p, sl.out_host[k]->n, hipMemcpyDeviceToHost,
-                                         down));
+            for (size_t k = 0; k < mappers.size(); k++) {
+                if (!j.direct) {
+                    HIP_CHECK(hipMemcpyAsync(sl.out_host[k]->p, sl.out_dev[k].p, sl.out_host[k]->n, hipMemcpyDeviceToHost,
+                                             down));
+                    continue;
+                }
+                // straight into the caller's registered planes: the region's Y rows, then its chroma rows'
+                // U (left) and V (right) halves (the device region is "Y over [U|V]", pitch = region width)
+                const Rect& r = regions[k];
+                const Rect& c = regions_uv[k];
+                const uint8_t* src = sl.out_dev[k].p;
+                HIP_CHECK(hipMemcpy2DAsync(j.out_planes[0] + (size_t)r.y * j.out_pitches[0] + r.x, j.out_pitches[0], src,
+                                           (size_t)r.w, (size_t)r.w, (size_t)r.h, hipMemcpyDeviceToHost, down));
+                HIP_CHECK(hipMemcpy2DAsync(j.out_planes[1] + (size_t)c.y * j.out_pitches[1] + c.x, j.out_pitches[1],
+                                           src + (size_t)r.h * r.w, (size_t)r.w, (size_t)c.w, (size_t)c.h,
+                                           hipMemcpyDeviceToHost, down));
+                HIP_CHECK(hipMemcpy2DAsync(j.out_planes[2] + (size_t)c.y * j.out_pitches[2] + c.x, j.out_pitches[2],
+                                           src + (size_t)r.h * r.w + r.w / 2, (size_t)r.w, (size_t)c.w, (size_t)c.h,
+                                           hipMemcpyDeviceToHost, down));
+            }
             if (preview_w > 0)  // async.cpp:102-103
                 HIP_CHECK(hipMemcpyAsync(sl.preview_host->p, sl.preview_dev.p, sl.preview_host->n, hipMemcpyDeviceToHost,
                                          down));
@@ -378,6 +408,7 @@ struct octvr_async {
     // run_copy_outputs_hostmem_to_mat (async.cpp:113-172)
     void copy_out(Job& j) {
         stage(j, [&] {
+            if (j.direct) return;  // the D2H wrote the caller's planes
             Slot& sl = slots[j.slot];
             for (size_t k = 0; k < mappers.size(); k++) {
                 const Rect& r = regions[k];
@@ -597,6 +628,9 @@ int octvr_async_push(octvr_async* a, const uint8_t* const* in_planes, const size
             return OCTVR_E_INVALID;
         }
     }
+    for (const octvr_async::RegOut& r : a->reg_out)
+        j->direct |= r.p[0] == out_planes[0] && r.p[1] == out_planes[1] && r.p[2] == out_planes[2] &&
+                     r.pitch[0] == out_pitches[0] && r.pitch[1] == out_pitches[1] && r.pitch[2] == out_pitches[2];
     a->q_in.push(std::move(j));
     a->pending++;
     return OCTVR_OK;
@@ -624,6 +658,66 @@ int octvr_async_pending(const octvr_async* a, int* n) {
     }
     *n = a->pending;
     return OCTVR_OK;
+}
+
+int octvr_async_register_output(octvr_async* a, uint8_t* const* planes, const size_t* pitches) {
+    if (!a || !planes || !pitches) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    for (int k = 0; k < 3; k++)
+        if (!planes[k] || pitches[k] < (size_t)(k ? a->out_w / 2 : a->out_w)) {
+            set_last_error("bad output plane");
+            return OCTVR_E_INVALID;
+        }
+    for (const octvr_async::RegOut& r : a->reg_out)
+        if (r.p[0] == planes[0] && r.p[1] == planes[1] && r.p[2] == planes[2] && r.pitch[0] == pitches[0] &&
+            r.pitch[1] == pitches[1] && r.pitch[2] == pitches[2])
+            return OCTVR_OK;  // already registered
+    try {
+        DeviceGuard dg(a->device);
+        octvr_async::RegOut r{};
+        int done = 0;
+        for (; done < 3; done++) {
+            const size_t rows = done ? (size_t)a->out_h / 2 : (size_t)a->out_h;
+            const size_t w = done ? (size_t)a->out_w / 2 : (size_t)a->out_w;
+            const hipError_t e = hipHostRegister(planes[done], pitches[done] * (rows - 1) + w, hipHostRegisterDefault);
+            if (e != hipSuccess) {
+                for (int k = 0; k < done; k++) (void)hipHostUnregister(planes[k]);
+                (void)hipGetLastError();
+                set_last_error(std::string("hipHostRegister: ") + hipGetErrorString(e));
+                return OCTVR_E_HIP;
+            }
+            r.p[done] = planes[done];
+            r.pitch[done] = pitches[done];
+        }
+        a->reg_out.push_back(r);
+        return OCTVR_OK;
+    } catch (const OctvrError& e) {
+        set_last_error(e.what());
+        return e.code;
+    }
+}
+
+int octvr_async_unregister_output(octvr_async* a, uint8_t* const* planes) {
+    if (!a || !planes) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    if (a->pending > 0) {  // a queued frame may still be written into them
+        set_last_error("frames pending: pop them before unregistering their planes");
+        return OCTVR_E_INVALID;
+    }
+    for (size_t i = 0; i < a->reg_out.size(); i++) {
+        const octvr_async::RegOut& r = a->reg_out[i];
+        if (r.p[0] != planes[0] || r.p[1] != planes[1] || r.p[2] != planes[2]) continue;
+        DeviceGuard dg(a->device);
+        for (uint8_t* p : r.p) (void)hipHostUnregister(p);
+        a->reg_out.erase(a->reg_out.begin() + (long)i);
+        return OCTVR_OK;
+    }
+    set_last_error("planes not registered");
+    return OCTVR_E_INVALID;
 }
 
 int octvr_async_pop_preview(octvr_async* a, uint8_t* rgb, size_t pitch, octvr_preview_header* hdr) {

@@ -395,15 +395,6 @@ struct FeedRaw {
     uint32_t meta;  // code bits 0-15 (fx, fy, valid), in-image ix0 ix1 iy0 iy1 at 16-19, V row shifts at 20-22 / 23-25
 };
 
-#ifdef OCTVR_DIAG_FEED_NOLOAD
-#define DIAGF(a_) (((a_) & 0u) + (threadIdx.x & 7u) * 8u)
-#else
-#define DIAGF(x) (x)
-#endif
-#ifndef OCTVR_FEED_AUX
-#define OCTVR_FEED_AUX 0
-#endif
-constexpr int kFeedAux = OCTVR_FEED_AUX;
 __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const SourceFrame& f, uint32_t xy,
                                                 uint32_t code, FeedRaw& r) {
     const TapCell tc = tap_cell(xy, f.w, f.h);
@@ -414,25 +405,21 @@ __device__ __forceinline__ void feed_taps_issue(__amdgpu_buffer_rsrc_t rs, const
     const uint32_t xa = x0 & ~3u, ca = c0 & ~3u;
     const uint32_t ry0 = (uint32_t)tc.y0 * p, ry1 = (uint32_t)tc.y1 * p;
     const uint32_t rc0 = (uint32_t)(tc.y0 >> 1) * p, rc1 = (uint32_t)(tc.y1 >> 1) * p;
-#ifdef OCTVR_DIAG_FEED_NOLOAD
-    const uint32_t sv0 = 0, sv1 = 0;
-#else
     const uint32_t sv0 = vo + rc0 + ca, sv1 = vo + rc1 + ca;
-#endif
     const uint32_t lv0 = min(sv0, lim), lv1 = min(sv1, lim);
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     u32x2 t;
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry0 + xa), 0, kFeedAux);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, ry0 + xa, 0, 0);
     r.y0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(ry1 + xa), 0, kFeedAux);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, ry1 + xa, 0, 0);
     r.y1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc0 + ca), 0, kFeedAux);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + rc0 + ca, 0, 0);
     r.u0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, DIAGF(uo + rc1 + ca), 0, kFeedAux);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, uo + rc1 + ca, 0, 0);
     r.u1 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv0, 0, kFeedAux);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv0, 0, 0);
     r.v0 = make_uint2(t.x, t.y);
-    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv1, 0, kFeedAux);
+    t = __builtin_amdgcn_raw_buffer_load_b64(rs, lv1, 0, 0);
     r.v1 = make_uint2(t.x, t.y);
     const uint32_t iy = x0 & 3u, ic = c0 & 3u;  // x1 - x0, c1 - c0 in {0, 1}
     r.sel = iy | (iy + (x1 - x0)) << 8 | ic << 16 | (ic + (c1 - c0)) << 24;
@@ -477,10 +464,14 @@ __device__ __forceinline__ void sample_rgb(const Taps& t, int tex, uint32_t (&rg
         bilerp_rgba(t.c[0], t.c[1], t.c[2], t.c[3], t.fx, t.fy, rgb);
 }
 
+// The feed's FIRST argument (FeedBatch): camera c of frame f read from the kernarg segment (scalar loads)
+typedef __attribute__((address_space(4))) const SourceFrame kSourceFrame;
+typedef __attribute__((address_space(4))) const FeedBatch kFeedBatch;
+static_assert(offsetof(FeedBatch, src) == 0, "FeedBatch layout");
+
 template <bool LEAN>
-__device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const CompositeEntry* samples,
-                                               const uint16_t* partners, int tex, int n_chunks, const int32_t* N, int n,
-                                               unsigned long long* totals, uint32_t* tickets, double* gains) {
+__device__ __forceinline__ void gain_feed_body(const CompositeEntry* samples, const uint16_t* partners, int tex,
+                                               int n_chunks, const int32_t* N, int n) {
     __shared__ int s_last;
     __shared__ double s_I[kGainMaxCams * kGainMaxCams];
     __shared__ double s_A[kGainMaxCams * kGainMaxCams];
@@ -494,9 +485,23 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
     const int wave = tid >> 6;
     __shared__ double s_wsum[4][kGainMaxCams];
     __shared__ int s_wcam[4];
-    const int k0 = (blockIdx.x * 4 + wave) * kGainWaveRun + lane;
-    const int cam = uniform((int)((samples[(blockIdx.x * 4 + wave) * kGainWaveRun].code >> 10) & 31u));
-    const SourceFrame fr = frames.f[cam];  // one camera per wave: uniform frame
+    // workgroup b: frame b / n_chunks of the batch (FeedBatch), chunk cb of it
+    const kFeedBatch* kb = (const kFeedBatch*)__builtin_amdgcn_kernarg_segment_ptr();
+    const int frame = uniform((int)(blockIdx.x / (uint32_t)n_chunks)), cb = (int)blockIdx.x - frame * n_chunks;
+    unsigned long long* const totals = kb->totals[frame];
+    uint32_t* const tickets = kb->tickets[frame];
+    double* const gains = kb->gains[frame];
+    const int k0 = (cb * 4 + wave) * kGainWaveRun + lane;
+    const int cam = uniform((int)((samples[(cb * 4 + wave) * kGainWaveRun].code >> 10) & 15u));
+    SourceFrame fr;  // one camera per wave: uniform frame
+    {
+        const kSourceFrame& kf = kb->src[frame * kGainMaxCams + cam];
+        fr.yuv = kf.yuv;
+        fr.w = kf.w;
+        fr.h = kf.h;
+        fr.pitch = kf.pitch;
+        fr.vig = kf.vig;
+    }
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(fr.yuv), 0, (int)((uint32_t)fr.pitch * (uint32_t)(fr.h + fr.h / 2)), 0x00020000);
     if constexpr (LEAN) {
@@ -608,7 +613,8 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
-        const int xcd = blockIdx.x & 7;
+        // the frame's tickets sharded by chunk (cb & 7: mostly one shard per XCD under round-robin dispatch)
+        const int xcd = cb & 7;
         const uint32_t in_xcd = (uint32_t)((n_chunks - xcd + 7) >> 3);
         int last = 0;
         if (__hip_atomic_fetch_add(&tickets[xcd], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_xcd - 1) {
@@ -648,28 +654,44 @@ __device__ __forceinline__ void gain_feed_body(const FrameSet& frames, const Com
     if (tid < n) gains[tid] = ok ? s_x[tid] : 1.0;  // cv::solve failure leaves gains_ unspecified; 1 as the oracle
 }
 
-__global__ void __launch_bounds__(256) gain_feed_kernel(FrameSet frames, const CompositeEntry* samples,
+__global__ void __launch_bounds__(256) gain_feed_kernel(FeedBatch batch, const CompositeEntry* samples,
                                                         const uint16_t* partners, int tex, int n_chunks, const int32_t* N,
-                                                        int n, unsigned long long* totals, uint32_t* tickets, double* gains) {
-    gain_feed_body<false>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains);
+                                                        int n) {
+    (void)batch;  // read through the kernarg segment (kFeedBatch)
+    gain_feed_body<false>(samples, partners, tex, n_chunks, N, n);
 }
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(80)))
-gain_feed_lean_kernel(FrameSet frames, const CompositeEntry* samples, const uint16_t* partners, int tex, int n_chunks,
-                      const int32_t* N, int n, unsigned long long* totals, uint32_t* tickets, double* gains) {
-    gain_feed_body<true>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains);
+gain_feed_lean_kernel(FeedBatch batch, const CompositeEntry* samples, const uint16_t* partners, int tex, int n_chunks,
+                      const int32_t* N, int n) {
+    (void)batch;
+    gain_feed_body<true>(samples, partners, tex, n_chunks, N, n);
+}
+
+hipError_t launch_gain_feed_batch(const FrameSet* frames, int nf, const CompositeEntry* samples, const uint16_t* partners,
+                                  int tex, int n_chunks, const int32_t* N, int n, unsigned long long* const* totals,
+                                  uint32_t* const* tickets, double* const* gains, hipStream_t s, bool lean) {
+    if (n_chunks <= 0 || n > kGainMaxCams || nf < 1 || nf > kMaxBatch) return hipErrorInvalidValue;
+    FeedBatch fb;
+    memset(&fb, 0, sizeof fb);
+    for (int f = 0; f < nf; f++) {
+        for (int i = 0; i < kGainMaxCams; i++) fb.src[f * kGainMaxCams + i] = frames[f].f[i];
+        fb.totals[f] = totals[f];
+        fb.tickets[f] = tickets[f];
+        fb.gains[f] = gains[f];
+    }
+    if (lean)
+        hipLaunchKernelGGL(gain_feed_lean_kernel, dim3(n_chunks * nf), dim3(256), 0, s, fb, samples, partners, tex,
+                           n_chunks, N, n);
+    else
+        hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks * nf), dim3(256), 0, s, fb, samples, partners, tex, n_chunks,
+                           N, n);
+    return hipGetLastError();
 }
 
 hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* samples, const uint16_t* partners, int tex,
                             int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s, bool lean) {
-    if (n_chunks <= 0 || n > kGainMaxCams) return hipErrorInvalidValue;
-    if (lean)
-        hipLaunchKernelGGL(gain_feed_lean_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, tex,
-                           n_chunks, N, n, totals, tickets, gains);
-    else
-        hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks), dim3(256), 0, s, frames, samples, partners, tex,
-                           n_chunks, N, n, totals, tickets, gains);
-    return hipGetLastError();
+    return launch_gain_feed_batch(&frames, 1, samples, partners, tex, n_chunks, N, n, &totals, &tickets, &gains, s, lean);
 }
 
 struct GainArgs {
@@ -726,20 +748,27 @@ hipError_t launch_unpack_runs(const uint8_t* packed, const FootRun* runs, int n_
 // ---------------------------------------------------------------------------------------------
 static_assert(sizeof(TileSlot) == 16, "TileSlot layout");
 
-// The per-call FrameSet is the FIRST argument of the stitch kernels: index it in the kernarg
+// The per-call FrameBatch is the FIRST argument of the stitch kernels: index it in the kernarg
 // segment directly (a wave-uniform index gives scalar loads; indexing the by-value parameter would
-// copy it to scratch).
+// copy it to scratch).  idx = (frame << cam_log2) + camera (kernels.hpp FrameBatch).
 typedef __attribute__((address_space(4))) const SourceFrame kSourceFrame;
-static_assert(offsetof(FrameSet, f) == 0, "FrameSet layout");
-__device__ __forceinline__ SourceFrame kernarg_frame(uint32_t cam) {
+typedef __attribute__((address_space(4))) const FrameBatch kFrameBatch;
+static_assert(offsetof(FrameBatch, src) == 0, "FrameBatch layout");
+__device__ __forceinline__ SourceFrame kernarg_frame(uint32_t idx) {
     const kSourceFrame* kf = (const kSourceFrame*)__builtin_amdgcn_kernarg_segment_ptr();
     SourceFrame s;
-    s.yuv = kf[cam].yuv;
-    s.w = kf[cam].w;
-    s.h = kf[cam].h;
-    s.pitch = kf[cam].pitch;
-    s.vig = kf[cam].vig;
+    s.yuv = kf[idx].yuv;
+    s.w = kf[idx].w;
+    s.h = kf[idx].h;
+    s.pitch = kf[idx].pitch;
+    s.vig = kf[idx].vig;
     return s;
+}
+__device__ __forceinline__ uint8_t* kernarg_out(uint32_t f) {
+    return ((const kFrameBatch*)__builtin_amdgcn_kernarg_segment_ptr())->out[f];
+}
+__device__ __forceinline__ const double* kernarg_gains(uint32_t f) {
+    return ((const kFrameBatch*)__builtin_amdgcn_kernarg_segment_ptr())->gains[f];
 }
 
 // One 8-pixel staging group of a tile: the YUV bytes it needs and its LDS destination.
@@ -760,10 +789,11 @@ constexpr uint32_t kStageBlack = 1u, kStageNoVig = 2u;
 // Slot q, component j of lane 1 + q: 0 = cam | bw << 16, 1 = bh | lds << 16, 2 = bx0 | by0 << 16,
 // 3 = chunk0.
 struct TileMeta {
-    int t;
+    int t;         // the work unit: item t >> nf_log2, frame t & (nf - 1) (FrameBatch)
     uint4 v;
     uint32_t tile, nslots, stride;
     uint32_t map;  // slot of staging chunk c < 4 in bits 2c, 2c + 1 (TiledLutDev::upload)
+    uint32_t frame, fbase;  // the unit's frame and its first camera's FrameBatch index (frame << cam_log2)
 };
 
 // dword j (0-3) of slot q (wave-uniform)
@@ -803,7 +833,7 @@ __device__ __forceinline__ StageSlot stage_slot(const TileMeta& m, int t_end, in
     s.bx0 = d2 & 0xFFFFu;
     s.by0 = d2 >> 16;
     s.chunk0 = d3 & 0xFFFFu;
-    s.f = kernarg_frame(s.cam);
+    s.f = kernarg_frame(m.fbase + s.cam);
     return s;
 }
 
@@ -828,17 +858,11 @@ __device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, 
     const gu8* Vb = Ub + (f.w >> 1);
     const uint32_t oy = __umul24(row, p32) + col * 8u, oc = __umul24(row >> 1, p32) + col * 4u;
     if (DWORD_STAGE) {
-#ifdef OCTVR_NT_STAGE
-        const uint64_t yy = __builtin_nontemporal_load((const gu64*)(Yb + oy));
-        sg.uq = __builtin_nontemporal_load((const gu32*)(Ub + oc));
-        sg.vq = __builtin_nontemporal_load((const gu32*)(Vb + oc));
-#else
         const uint64_t yy = *(const gu64*)(Yb + oy);
-        sg.uq = *(const gu32*)(Ub + oc);
-        sg.vq = *(const gu32*)(Vb + oc);
-#endif
         sg.y0 = (uint32_t)yy;
         sg.y1 = (uint32_t)(yy >> 32);
+        sg.uq = *(const gu32*)(Ub + oc);
+        sg.vq = *(const gu32*)(Vb + oc);
     } else {
         const gu8* Yp = Yb + oy;
         const gu8* Up = Ub + oc;
@@ -865,13 +889,8 @@ __device__ __forceinline__ void stage_load(const StageSlot& s, uint32_t stride, 
 // zero-extended it right after the load, into the loop-carried register, and that copy waited on every
 // load of the iteration (vmcnt(0) before the compute); widened at the use, an iteration later, it waits
 // on nothing (one frame in flight: C2 composite -1 %, C3 +1 %, `u16`).
-#ifdef OCTVR_DIAG_DUP
-#define DUPT(t_) ((t_) >> 1)
-#else
-#define DUPT(t_) (t_)
-#endif
-__device__ __forceinline__ uint16_t group_issue(const __amdgpu_buffer_rsrc_t& gr, int t, int t_end) {
-    const int tt = DUPT(t < t_end ? t : 0);
+__device__ __forceinline__ uint16_t group_issue(const __amdgpu_buffer_rsrc_t& gr, int t, int t_end, int lg) {
+    const int tt = (t < t_end ? t : 0) >> lg;
     return __builtin_amdgcn_raw_buffer_load_b16(gr, (uint32_t)threadIdx.x * 2u,
                                                 (uint32_t)uniform(tt) * (uint32_t)(kGroupFirst * 64 * 2), 0);
 }
@@ -930,9 +949,9 @@ constexpr int kStitchTexRegBlocks = 5, kStitchTexVgprs = 96;
 //
 // One buffer load by lanes 0..kMetaWords-1: the voffset (lane * 16) is loop-invariant, the item's
 // record offset a scalar, so no per-lane 64-bit address is held across the loop.
-__device__ __forceinline__ uint4 meta_issue(const __amdgpu_buffer_rsrc_t& mr, int t, int t_end) {  // t: staged item
+__device__ __forceinline__ uint4 meta_issue(const __amdgpu_buffer_rsrc_t& mr, int t, int t_end, int lg) {  // t: unit
     const int lane = threadIdx.x & 63;
-    const int tt = DUPT(t < t_end ? t : 0);  // t >= 0: every item index derives from bounded claims
+    const int tt = (t < t_end ? t : 0) >> lg;  // t >= 0: every item index derives from bounded claims
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     uint4 v;
     if (lane < kMetaWords) {  // exec-masked: the instruction (and its vmcnt) is the same for every wave
@@ -943,9 +962,11 @@ __device__ __forceinline__ uint4 meta_issue(const __amdgpu_buffer_rsrc_t& mr, in
     return v;
 }
 
-__device__ __forceinline__ TileMeta meta_read(const uint4& v, int t) {
+__device__ __forceinline__ TileMeta meta_read(const uint4& v, int t, int lg, int cam_lg) {
     TileMeta m;
     m.t = t;
+    m.frame = (uint32_t)t & ((1u << lg) - 1u);
+    m.fbase = m.frame << cam_lg;
     m.v = v;
     m.tile = (uint32_t)__builtin_amdgcn_readlane((int)v.x, 0);
     m.nslots = (uint32_t)__builtin_amdgcn_readlane((int)v.y, 0);
@@ -966,24 +987,16 @@ struct TileData {
 // er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
 // scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
 // that the entries fit 32-bit offsets)
-#ifndef OCTVR_ENT_AUX
-#define OCTVR_ENT_AUX 0
-#endif
-constexpr int kEntAux = OCTVR_ENT_AUX;
 template <bool DWORD_STAGE, bool VIG>
-__device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, const TileMeta& m, int t_end,
+__device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, const TileMeta& m, int t_end, int lg,
                                            const StageSlot& sl, uint32_t g, TileData& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++) {
         typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
-#ifdef OCTVR_DIAG_HALFENT
-        const uint32_t so = (uint32_t)uniform((live ? m.t : 0) * kItemHalves + 0) * (uint32_t)(kTilePx * 4);
-#else
-        const uint32_t so = (uint32_t)uniform(DUPT(live ? m.t : 0) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
-#endif
-        const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, kEntAux);
+        const uint32_t so = (uint32_t)uniform(((live ? m.t : 0) >> lg) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
+        const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
         d.e4[h] = uint4{v.x, v.y, v.z, v.w};
     }
     if (!sl.live) {  // wave-uniform: no loads for a chunk the item lacks
@@ -1084,7 +1097,7 @@ __device__ __forceinline__ void store_half(const OutFrame& of, const RgbaSink& r
 // then the constant 0x4000 (wtab_read).
 struct alignas(16) StitchLds {
     uint32_t rgb[kTileLdsBytes / 4];  // the item's staged RGBA boxes (LDS address 0)
-    float gain[kMaxCams];
+    uint32_t spare[kMaxCams];         // (the frames' camera gains live after the weight table)
     f32x2_t slot_gain[kTileSlots];
     uint32_t claim[2];
     uint32_t pad[2];
@@ -1107,13 +1120,17 @@ __device__ __forceinline__ uint32_t tap_off(uint32_t e) { return (e >> 13) & 0x3
 // dispatch (blocks b, b+8, ...), so neighbouring items' source boxes share that XCD's L2.
 // TEX: texture-convention entries (tiled_entry_tex): the taps as usual, the texture filter model instead of
 // the weight table.
-template <bool DWORD_STAGE, int MODE, bool VIG, bool TEX>
-__device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut, int W, int H, const double* gains,
-                                                  int use_gain, uint8_t* out, int64_t out_pitch, RgbaOut rgba) {
+// LG: 1 << LG frames per launch (FrameBatch; MODE 0 only)
+template <bool DWORD_STAGE, int MODE, bool VIG, bool TEX, int LG>
+__device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lut, int W, int H, int use_gain,
+                                                  int64_t out_pitch, RgbaOut rgba) {
     __shared__ StitchLds L;
     extern __shared__ __attribute__((aligned(16))) uint2 s_wtab[];  // 1,024 weight pairs at LDS 0x4000
     uint32_t* const s_rgb = L.rgb;
-    float* const s_gain = L.gain;
+    // per frame and camera, (frame << cam_log2) + camera: in the dynamic region after the weight table
+    float* const s_gain = reinterpret_cast<float*>(s_wtab + 1024);
+    constexpr int lg = LG, cam_lg = LG <= 1 ? 5 : 4;  // frames per launch 1 << lg (FrameBatch)
+    static_assert(MODE == 0 || LG == 0, "frame batches: MODE 0 only");
     // {g, g} per slot (finish_quad2f).  Written after an item's first barrier and read after its
     // second; the next write comes after the next item's first barrier, i.e. after every wave's last
     // read, so one table suffices.
@@ -1126,13 +1143,8 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     const int groups = kStitchBands;
     const int g = blockIdx.x % groups;
     const int step = (gridDim.x - g + groups - 1) / groups;
-#ifdef OCTVR_DIAG_DUP
-    const int t_begin = 2 * lut.bands[g];
-    const int t_end = 2 * lut.bands[g + 1];
-#else
-    const int t_begin = lut.bands[g];
-    const int t_end = lut.bands[g + 1];
-#endif
+    const int t_begin = lut.bands[g] << lg;  // work units: (item, frame) pairs
+    const int t_end = lut.bands[g + 1] << lg;
     const __amdgpu_buffer_rsrc_t ersrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kItemHalves * kTilePx * 4)), 0x00020000);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -1144,8 +1156,9 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     OutFrame of{};
     RgbaSink ro{};
     bool res_rgba = false;
+    const int out_bytes = (int)((uint32_t)out_pitch * (uint32_t)(H + H / 2));
     if constexpr (MODE == 0) {
-        of = make_out_frame(out, W, H, out_pitch);
+        of = make_out_frame(kernarg_out(0), W, H, out_pitch);
     } else {
         ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
         of = make_result_frame(rgba);
@@ -1154,7 +1167,10 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     const int tid = threadIdx.x;
     const int qx = tid & 63, qy = tid >> 6;
 
-    if (tid < kMaxCams) s_gain[tid] = use_gain ? (float)gains[tid] : 1.0f;
+    if (tid < (1 << (lg + cam_lg))) {
+        const double* gf = kernarg_gains((uint32_t)tid >> cam_lg);
+        s_gain[tid] = use_gain ? (float)gf[tid & ((1 << cam_lg) - 1)] : 1.0f;
+    }
     if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
 #pragma unroll
     for (int k = 0; k < 4; k++) s_wtab[tid + 256 * k] = bilerp_weights((uint32_t)(tid + 256 * k));
@@ -1168,15 +1184,15 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     const int dyn0 = t_begin + 3 * step;  // item of claim value 0
     uint32_t* const q = lut.queue + g * kQueueStride;
     const int wave = uniform(tid >> 6);
-    TileMeta cur = meta_read(meta_issue(mrsrc, t0, t_end), t0);
-    const uint32_t g0 = group_issue(grsrc, t0, t_end);
+    TileMeta cur = meta_read(meta_issue(mrsrc, t0, t_end, lg), t0, lg, cam_lg);
+    const uint32_t g0 = group_issue(grsrc, t0, t_end, lg);
     __syncthreads();
     TileData d;
-    data_issue<DWORD_STAGE, VIG>(ersrc, cur, t_end, stage_slot<true>(cur, t_end, wave), g0, d);
+    data_issue<DWORD_STAGE, VIG>(ersrc, cur, t_end, lg, stage_slot<true>(cur, t_end, wave), g0, d);
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
-    uint4 mv = meta_issue(mrsrc, t_mv, t_end);
-    uint16_t mg = group_issue(grsrc, t_mv, t_end);  // the lane's first staging group of item t_mv
+    uint4 mv = meta_issue(mrsrc, t_mv, t_end, lg);
+    uint16_t mg = group_issue(grsrc, t_mv, t_end, lg);  // the lane's first staging group of item t_mv
     uint32_t claim = 0u;  // lane 0 of wave 0: returned value of the claim in flight
     bool claimed = false; // a claim for the item after t_n2 is in flight (uniform)
     bool first = true;
@@ -1200,6 +1216,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
     int pox = 0, poy = 0;  // the previous item's origin (uniform)
     bool pfull = false;    // the previous item lies wholly inside W x H (uniform)
     uint32_t pcam = 0, pfl = 0;  // the previous item's RGBA-mode camera and flags (item_result_bit / item_g0_bit)
+    uint32_t pfr = 0;            // the previous unit's frame (MODE 0 output)
     bool pin = false;
     uint32_t par = 0;  // iteration parity
     while (cur.t < t_end) {
@@ -1211,12 +1228,12 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
         // every wave has read the previous item's staging area
         __syncthreads();
         if (tid < kTileZeroDwords) s_rgb[tid] = 0u;  // black pixels read offset 0 of the region
-        const TileMeta nxt = meta_read(mv, t_mv);
+        const TileMeta nxt = meta_read(mv, t_mv, lg, cam_lg);
         {  // slot q's camera word sits in lane 1 + q of the metadata's first component
             const uint32_t cw = (uint32_t)__shfl((int)cur.v.x, 1 + (tid & 3), 64);
             // clamped to [0, FLT_MAX] (NaN -> 0) in MODE 0; no result depends on it (finish_quad2f
             // saturates with v_cvt_pk_u8_f32, which maps negative and NaN products to 0 either way)
-            const float gs = s_gain[cw & 31u];
+            const float gs = s_gain[cur.fbase + (cw & 31u)];
             const float gc = MODE == 0 ? __builtin_fminf(__builtin_fmaxf(gs, 0.f), FLT_MAX) : gs;
             if (tid < kTileSlots) s_slot_gain[tid] = f32x2_t{gc, gc};
         }
@@ -1247,6 +1264,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
             t_n2 = v < t_end ? v : t_end;
         }
         first = false;
+        if (MODE == 0 && lg) of.rsrc = __builtin_amdgcn_make_buffer_rsrc(kernarg_out(pfr), 0, out_bytes, 0x00020000);
         if (MODE == 0 && pfull) {
 #pragma unroll
             for (int h = 0; h < kItemHalves; h++) {
@@ -1263,9 +1281,9 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
                 store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
         // the next item's first staging slot resolved only now (short scalar live ranges), then its loads
-        data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, stage_slot<true>(nxt, t_end, wave), mg, d);
-        mv = meta_issue(mrsrc, t_n2, t_end);
-        mg = group_issue(grsrc, t_n2, t_end);
+        data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, lg, stage_slot<true>(nxt, t_end, wave), mg, d);
+        mv = meta_issue(mrsrc, t_n2, t_end, lg);
+        mg = group_issue(grsrc, t_n2, t_end, lg);
         t_mv = t_n2;
         claimed = t_n2 < t_end;  // claim the item after it (only while the sequence is live)
         if (claimed && tid == 0) {
@@ -1308,6 +1326,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
         poy = (int)(cur.tile >> 16) * kItemH;
         pfull = pox + kTileW <= W && poy + kItemH <= H;
         pcam = (cur.nslots >> 16) & 31u;
+        pfr = cur.frame;
         pfl = MODE == 1 ? (cur.map >> 8) & 0xFFFFu : 0u;
         pin = x < W && y < H;
         par ^= 1u;
@@ -1324,24 +1343,24 @@ __device__ __forceinline__ void stitch_tiled_body(FrameSet frames, TiledLut lut,
                 __hip_atomic_exchange(lut.queue + k * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    if (MODE == 0 && lg) of.rsrc = __builtin_amdgcn_make_buffer_rsrc(kernarg_out(pfr), 0, out_bytes, 0x00020000);
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++)
         store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
 }
 
-template <bool DWORD_STAGE, int MODE, bool VIG>
+template <bool DWORD_STAGE, int MODE, bool VIG, int LG>
 __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
-__attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameSet frames, TiledLut lut, int W, int H,
-                                                                   const double* gains, int use_gain, uint8_t* out,
-                                                                   int64_t out_pitch, RgbaOut rgba) {
-    stitch_tiled_body<DWORD_STAGE, MODE, VIG, false>(frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);
+__attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameBatch frames, TiledLut lut, int W, int H,
+                                                                   int use_gain, int64_t out_pitch, RgbaOut rgba) {
+    stitch_tiled_body<DWORD_STAGE, MODE, VIG, false, LG>(frames, lut, W, H, use_gain, out_pitch, rgba);
 }
-template <bool DWORD_STAGE, int MODE, bool VIG>
+template <bool DWORD_STAGE, int MODE, bool VIG, int LG>
 __global__ void __launch_bounds__(256, kStitchTexRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
-__attribute__((amdgpu_num_vgpr(kStitchTexVgprs))) stitch_tiled_tex_kernel(FrameSet frames, TiledLut lut, int W,
-                                                                          int H, const double* gains, int use_gain,
-                                                                          uint8_t* out, int64_t out_pitch, RgbaOut rgba) {
-    stitch_tiled_body<DWORD_STAGE, MODE, VIG, true>(frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);
+__attribute__((amdgpu_num_vgpr(kStitchTexVgprs))) stitch_tiled_tex_kernel(FrameBatch frames, TiledLut lut, int W,
+                                                                          int H, int use_gain, int64_t out_pitch,
+                                                                          RgbaOut rgba) {
+    stitch_tiled_body<DWORD_STAGE, MODE, VIG, true, LG>(frames, lut, W, H, use_gain, out_pitch, rgba);
 }
 
 // Wide tiles: one workgroup per tile, 8-byte absolute entries, direct global gathers.
@@ -1395,56 +1414,88 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 
 // The weight table's address (wtab_read) assumes the dynamic LDS starts right after StitchLds: checked
 // once per kernel instance against the compiled static LDS size.
-template <bool DW, int MODE, bool V, bool TEX>
+template <bool DW, int MODE, bool V, bool TEX, int LG>
 static hipError_t stitch_lds_check() {
     hipFuncAttributes a;
-    const void* k = TEX ? reinterpret_cast<const void*>(stitch_tiled_tex_kernel<DW, MODE, V>)
-                        : reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V>);
+    const void* k = TEX ? reinterpret_cast<const void*>(stitch_tiled_tex_kernel<DW, MODE, V, LG>)
+                        : reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V, LG>);
     const hipError_t e = hipFuncGetAttributes(&a, k);
     if (e != hipSuccess) return e;
     return a.sharedSizeBytes == sizeof(StitchLds) ? hipSuccess : hipErrorInvalidKernelFile;
 }
 
-template <bool DW, int MODE, bool V, bool TEX>
-static hipError_t launch_tiled(int blocks, const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
-                               int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
-                               hipEvent_t ev0, hipEvent_t ev1) {
-    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V, TEX>();
+// dynamic LDS of the composite: the weight table, then the frames' camera gains (FrameBatch order)
+constexpr uint32_t kStitchDynLds = kWtabBytes + 4u * 2u * kMaxCams;
+
+template <bool DW, int MODE, bool V, bool TEX, int LG>
+static hipError_t launch_tiled(int blocks, const FrameBatch& frames, const TiledLut& lut, int W, int H, int use_gain,
+                               int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V, TEX, LG>();
     if (lds_ok != hipSuccess) return lds_ok;
     if constexpr (TEX) {
         // (no packet-carried timing events: the texture convention is not a bench line's timed kernel)
-        hipLaunchKernelGGL((stitch_tiled_tex_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut,
-                           W, H, gains, use_gain, out, out_pitch, rgba);
+        hipLaunchKernelGGL((stitch_tiled_tex_kernel<DW, MODE, V, LG>), dim3(blocks), dim3(256), kStitchDynLds, s,
+                           frames, lut, W, H, use_gain, out_pitch, rgba);
         if (ev0) (void)hipEventRecord(ev1, s);
     } else if (ev0) {  // the timing events carried by the dispatch packet itself
-        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, ev0, ev1, 0,
-                              frames, lut, W, H, gains, use_gain, out, out_pitch, rgba);
+        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, LG>), dim3(blocks), dim3(256), kStitchDynLds, s, ev0,
+                              ev1, 0, frames, lut, W, H, use_gain, out_pitch, rgba);
     } else {
-        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V>), dim3(blocks), dim3(256), kWtabBytes, s, frames, lut, W,
-                           H, gains, use_gain, out, out_pitch, rgba);
+        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, LG>), dim3(blocks), dim3(256), kStitchDynLds, s, frames,
+                           lut, W, H, use_gain, out_pitch, rgba);
     }
     return hipGetLastError();
 }
 
-// the instance for the frames' staging (dword loads, vignette) and the entries' convention
-template <int MODE, bool TEX>
-static hipError_t launch_tiled_for(bool dw, bool vig, int blocks, const FrameSet& frames, const TiledLut& lut, int W,
-                                   int H, const double* gains, int use_gain, uint8_t* out, int64_t out_pitch,
-                                   const RgbaOut& rgba, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (dw && !vig)
-        return launch_tiled<true, MODE, false, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
-    if (dw)
-        return launch_tiled<true, MODE, true, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
-    if (!vig)
-        return launch_tiled<false, MODE, false, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
-    return launch_tiled<false, MODE, true, TEX>(blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
+template <bool DW, int MODE, bool V, bool TEX>
+static hipError_t launch_tiled_lg(int lg, int blocks, const FrameBatch& frames, const TiledLut& lut, int W, int H,
+                                  int use_gain, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0,
+                                  hipEvent_t ev1) {
+    if constexpr (MODE == 0) {
+        if (lg == 1) return launch_tiled<DW, MODE, V, TEX, 1>(blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+        if (lg == 2) return launch_tiled<DW, MODE, V, TEX, 2>(blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+    }
+    if (lg != 0) return hipErrorInvalidValue;
+    return launch_tiled<DW, MODE, V, TEX, 0>(blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
 }
 
+// the instance for the frames' staging (dword loads, vignette) and the entries' convention
+template <int MODE, bool TEX>
+static hipError_t launch_tiled_for(bool dw, bool vig, int lg, int blocks, const FrameBatch& frames, const TiledLut& lut,
+                                   int W, int H, int use_gain, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
+                                   hipEvent_t e0, hipEvent_t e1) {
+    if (dw && !vig)
+        return launch_tiled_lg<true, MODE, false, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    if (dw)
+        return launch_tiled_lg<true, MODE, true, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    if (!vig)
+        return launch_tiled_lg<false, MODE, false, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    return launch_tiled_lg<false, MODE, true, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+}
+
+// nf frame sets (1, 2 or 4) in one launch of the tiled kernel (FrameBatch); wide tiles one launch per frame
 template <int MODE>
-static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
-                                   int use_gain, uint8_t* out, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
-                                   hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
+static hipError_t launch_composite(const FrameSet* frames, int nf, const TiledLut& lut, int W, int H,
+                                   const double* const* gains, int use_gain, uint8_t* const* out, int64_t out_pitch,
+                                   const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0 = nullptr,
+                                   hipEvent_t ev1 = nullptr) {
     if (lut.n_items > 0 && lut.qpl != kItemHalves) return hipErrorInvalidValue;
+    const int lg = nf == 1 ? 0 : nf == 2 ? 1 : nf == 4 ? 2 : -1;
+    if (lg < 0 || (MODE == 1 && nf != 1)) return hipErrorInvalidValue;
+    const int cam_lg = nf <= 2 ? 5 : 4;
+    FrameBatch fb;
+    memset(&fb, 0, sizeof fb);
+    for (int f = 0; f < nf; f++) {
+        for (int i = 0; i < kMaxCams; i++) {
+            if (i >= (1 << cam_lg)) {
+                if (frames[f].f[i].yuv) return hipErrorInvalidValue;  // more cameras than a 4-frame batch holds
+                continue;
+            }
+            fb.src[(f << cam_lg) + i] = frames[f].f[i];
+        }
+        fb.out[f] = out ? out[f] : nullptr;
+        fb.gains[f] = gains[f];
+    }
     // timing events: carried by the dispatch packet when the tiled kernel is the only launch (no marker
     // packets between the launches of the timed loop), else recorded around the launches
     const bool ext_ev = ev0 && lut.n_items > 0 && lut.n_wide == 0;
@@ -1453,30 +1504,33 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
         if (e != hipSuccess) return e;
     }
     if (lut.n_items > 0) {
-        // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU), each walking its XCD band's items;
-        // a frame with fewer than 3 items per workgroup (C1's 4,096) gets a third as many workgroups as items,
-        // so that every workgroup has its three statically dealt items (the first 2.7 rounds of 1,536 left
-        // the last round a third empty: C1 17.4 -> 15.6 us, interleaved)
-        int blocks = std::min(lut.n_items, 256 * kStitchBlocksPerCU);
-        if (lut.n_items < 3 * 256 * kStitchBlocksPerCU) blocks = (lut.n_items + 2) / 3;
+        // one resident wave of workgroups (256 CUs x kStitchBlocksPerCU), each walking its XCD band's units;
+        // fewer than 3 units per workgroup (C1's 4,096 items) get a third as many workgroups as units, so
+        // that every workgroup has its three statically dealt units (the first 2.7 rounds of 1,536 left the
+        // last round a third empty: C1 17.4 -> 15.6 us, interleaved)
+        const int units = lut.n_items * nf;
+        int blocks = std::min(units, 256 * kStitchBlocksPerCU);
+        if (units < 3 * 256 * kStitchBlocksPerCU) blocks = (units + 2) / 3;
         blocks = std::max(8, (blocks + 7) / 8 * 8);
         // wide staging loads need 8-byte aligned Y rows (then U / V rows are 4-byte aligned)
         bool dw = true, vig = false;
-        for (int i = 0; i < kMaxCams; i++) {
-            const SourceFrame& f = frames.f[i];
-            if (!f.yuv) continue;
-            if ((reinterpret_cast<uintptr_t>(f.yuv) & 7u) || (f.pitch & 7) || (f.w & 7)) dw = false;
-            vig |= f.vig != nullptr;
-        }
+        for (int f = 0; f < nf; f++)
+            for (int i = 0; i < kMaxCams; i++) {
+                const SourceFrame& sf = frames[f].f[i];
+                if (!sf.yuv) continue;
+                if ((reinterpret_cast<uintptr_t>(sf.yuv) & 7u) || (sf.pitch & 7) || (sf.w & 7)) dw = false;
+                vig |= sf.vig != nullptr;
+            }
         hipEvent_t e0 = ext_ev ? ev0 : nullptr, e1 = ext_ev ? ev1 : nullptr;
         const hipError_t e =
-            lut.tex ? launch_tiled_for<MODE, true>(dw, vig, blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1)
-                    : launch_tiled_for<MODE, false>(dw, vig, blocks, frames, lut, W, H, gains, use_gain, out, out_pitch, rgba, s, e0, e1);
+            lut.tex ? launch_tiled_for<MODE, true>(dw, vig, lg, blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1)
+                    : launch_tiled_for<MODE, false>(dw, vig, lg, blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
         if (e != hipSuccess) return e;
     }
     if (lut.n_wide > 0)
-        hipLaunchKernelGGL(stitch_wide_kernel<MODE>, dim3(lut.n_wide), dim3(256), 0, s, frames, lut, W, H, gains,
-                           use_gain, out, out_pitch, rgba);
+        for (int f = 0; f < nf; f++)
+            hipLaunchKernelGGL(stitch_wide_kernel<MODE>, dim3(lut.n_wide), dim3(256), 0, s, frames[f], lut, W, H,
+                               gains[f], use_gain, out ? out[f] : nullptr, out_pitch, rgba);
     if (ev0 && !ext_ev) {
         const hipError_t e = hipEventRecord(ev1, s);
         if (e != hipSuccess) return e;
@@ -1486,15 +1540,22 @@ static hipError_t launch_composite(const FrameSet& frames, const TiledLut& lut, 
 
 int composite_qpl() { return kItemHalves; }
 
+hipError_t launch_stitch_batch(const FrameSet* frames, int nf, const TiledLut& lut, int W, int H,
+                               const double* const* gains, int use_gain, uint8_t* const* out, int64_t out_pitch,
+                               hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    if (nf < 1 || nf > kMaxBatch) return hipErrorInvalidValue;
+    return launch_composite<0>(frames, nf, lut, W, H, gains, use_gain, out, out_pitch, RgbaOut{}, s, ev0, ev1);
+}
+
 hipError_t launch_stitch(const FrameSet& frames, const TiledLut& lut, int W, int H, const double* gains,
                          int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    return launch_composite<0>(frames, lut, W, H, gains, use_gain, out, out_pitch, RgbaOut{}, s, ev0, ev1);
+    return launch_composite<0>(&frames, 1, lut, W, H, &gains, use_gain, &out, out_pitch, RgbaOut{}, s, ev0, ev1);
 }
 
 hipError_t launch_mb_remap(const FrameSet& frames, const TiledLut& lut, const double* gains, int use_gain,
                            const RgbaOut& out, hipStream_t s) {
     // W, H: no level-grid bound of its own (the per-camera ROI check drops what lies outside)
-    return launch_composite<1>(frames, lut, 1 << 16, 1 << 16, gains, use_gain, nullptr, 0, out, s);
+    return launch_composite<1>(&frames, 1, lut, 1 << 16, 1 << 16, &gains, use_gain, nullptr, 0, out, s);
 }
 
 // ---------------------------------------------------------------------------------------------

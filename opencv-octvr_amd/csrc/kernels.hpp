@@ -159,6 +159,21 @@ struct FrameSet {
     SourceFrame f[kMaxCams];
 };
 
+// The frames of one composite launch (launch_stitch, octvr_mapper_stitch_batch): 1 << nf_log2 frame sets
+// (at most kMaxBatch) stitched in one pass over the tiled LUT.  The item sequence runs over (item, frame)
+// pairs — unit v = item << nf_log2 | frame — so the units of one item are dealt to neighbouring workgroups
+// of one XCD band at the same time: the item's entries, metadata and staging groups come from HBM (or the
+// Infinity Cache) once for all the frames and from L2 for the others, while each unit stages and computes
+// its own frame.  Camera c of frame f: src[(f << cam_log2) + c], cam_log2 = 5 (32 cameras) for one or two
+// frames, 4 (16 cameras) for four.  The FIRST argument of the composite kernels (kernarg_frame).
+constexpr int kMaxBatch = 4;
+struct FrameBatch {
+    SourceFrame src[2 * kMaxCams];
+    uint8_t* out[kMaxBatch];        // MODE 0: the frames' YUV420P outputs (one pitch)
+    const double* gains[kMaxBatch]; // the frames' gains (device)
+};
+
+
 // One NV12 plane of a FastMapper (fastmapper.cpp / fastmapper.hip): per run {camera mask, first block},
 // and per (camera, run) block either the compact entries (header + u32 offsets/fractions + u8 weights)
 // or the wide uint2 entries; nblk: the blocks allocated (>= 1).
@@ -217,6 +232,18 @@ hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* sample
                             int n_chunks, const int32_t* N, int n,
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s,
                             bool lean = false);  // lean: <= 80 VGPRs (73 used), runs beside a composite (kernels.hip)
+
+// The feeds of nf frames (1, 2 or 4) of a batch in one launch: workgroup b feeds frame b / n_chunks into its
+// own totals / tickets / gains (FeedBatch, the kernel's first argument).
+struct FeedBatch {
+    SourceFrame src[kMaxBatch * kGainMaxCams];  // camera c of frame f at f * kGainMaxCams + c
+    unsigned long long* totals[kMaxBatch];
+    uint32_t* tickets[kMaxBatch];
+    double* gains[kMaxBatch];
+};
+hipError_t launch_gain_feed_batch(const FrameSet* frames, int nf, const CompositeEntry* samples, const uint16_t* partners,
+                                  int tex, int n_chunks, const int32_t* N, int n, unsigned long long* const* totals,
+                                  uint32_t* const* tickets, double* const* gains, hipStream_t s, bool lean);
 
 hipError_t launch_set_gains(const double* host_gains, int n, double* gains_dev, hipStream_t s);
 
@@ -287,6 +314,11 @@ int composite_qpl();
 hipError_t launch_stitch(const FrameSet& frames_dev, const TiledLut& lut, int W, int H,
                          const double* gains, int use_gain, uint8_t* out, int64_t out_pitch, hipStream_t s,
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// nf frames (1, 2 or 4; frame f = frames[f], gains[f], out[f], all outputs of pitch out_pitch) in one
+// composite launch (FrameBatch); more than 16 cameras need nf <= 2
+hipError_t launch_stitch_batch(const FrameSet* frames, int nf, const TiledLut& lut, int W, int H,
+                               const double* const* gains, int use_gain, uint8_t* const* out, int64_t out_pitch,
+                               hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // ---- multi-band blend (blend > 0): MultiBandGPUBlender (blenders.cpp:589-735) ------------------
 // Level l of the blend lives on the "level grid": align_result_roi >> l.  Each camera keeps its

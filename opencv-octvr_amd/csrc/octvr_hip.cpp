@@ -1117,6 +1117,72 @@ void ensure_result(octvr_mapper& m) {
     m.result_view.upload(&v, 1);
 }
 
+namespace {
+
+void check_out_pitch(const octvr_mapper* m, size_t out_pitch) {
+    REQUIRE(out_pitch >= (size_t)m->SW, "output pitch smaller than width");
+    // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
+    REQUIRE((uint64_t)out_pitch * (m->SH + m->SH / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
+}
+
+// The kernels' view of one frame's inputs, with the limits of their address arithmetic checked.
+FrameSet frame_set(const octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch) {
+    FrameSet fs;
+    memset(&fs, 0, sizeof fs);
+    for (int i = 0; i < m->n; i++) {
+        REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
+        // the staging loads form row offsets with 24-bit multiplies (kernels.hip stage_load)
+        REQUIRE(in_pitch[i] < ((size_t)1 << 24), "input pitch must be below 16 MiB");
+        // the gain feed reads frames through 32-bit buffer resources
+        REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) < 0x7FFFFFFFull,
+                "input frame larger than 2 GiB");
+        // ... in 8-byte segments (kernels.hip feed_rows)
+        REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) >= 8, "input frame below 8 bytes");
+        fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
+    }
+    return fs;
+}
+
+// The frame's gains into its slot: copied from another mapper (gains_dev), set (gains), or estimated by the
+// gain feed (GainCompensatorGPU::feed, exposure_compensate.cpp:223-297).
+void stitch_gains(octvr_mapper* m, octvr_mapper::FrameSlot& sl, const FrameSet& fs, const double* gains, int n_gains,
+                  const double* gains_dev, hipStream_t s) {
+    if (!m->use_gain) return;
+    if (gains_dev) {
+        HIP_CHECK(hipMemcpyAsync(sl.gains, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
+    } else if (gains) {
+        REQUIRE(n_gains == m->n, "gains must have one entry per input");
+        HIP_CHECK(launch_set_gains(gains, m->n, sl.gains, s));
+    } else if (m->n_chunks == 0) {  // no intersections: A = diag(b), every gain is 1
+        const std::vector<double> ones(m->n, 1.0);
+        HIP_CHECK(launch_set_gains(ones.data(), m->n, sl.gains, s));
+    } else {
+        // with frames in flight the feed runs beside the previous frame's composite: the lean
+        // variant fits next to it (the wide-prefetch one waits for its workgroups to drain)
+        const bool lean = m->slots.size() > 1;
+        HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->tex, m->n_chunks, m->N.p, m->n, sl.totals,
+                                   sl.tickets, sl.gains, s, lean));
+    }
+}
+
+// The timing events of this stitch, or none (octvr_mapper_set_timing: every `timing`-th stitch)
+std::pair<hipEvent_t, hipEvent_t> stitch_events(octvr_mapper* m) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = m->timing > 0 && (m->timed_calls++ % (uint64_t)m->timing) == 0;
+    if (!timed) return {e0, e1};
+    if (m->free_events.empty()) {
+        HIP_CHECK(hipEventCreate(&e0));
+        HIP_CHECK(hipEventCreate(&e1));
+    } else {
+        e0 = m->free_events.back().first;
+        e1 = m->free_events.back().second;
+        m->free_events.pop_back();
+    }
+    return {e0, e1};
+}
+
+}  // namespace
+
 // Mapper::stitch (mapper.cpp:193-323).  gains_dev (device, n doubles): gains of another mapper of the
 // same inputs, copied stream-ordered (AsyncMultiMapper's gain_modes chaining, async.cpp:78-86).
 void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* in_pitch, uint8_t* out_dev,
@@ -1131,23 +1197,9 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
             REQUIRE(m->slots.size() == 1, "preview output needs one frame in flight");
             ensure_result(*m);
         }
-        REQUIRE(out_pitch >= (size_t)m->SW, "output pitch smaller than width");
-        // the stitch kernel addresses the output through a buffer resource with 32-bit offsets
-        REQUIRE((uint64_t)out_pitch * (m->SH + m->SH / 2) < 0x7FFFFF80ull, "output frame larger than 2 GiB");
+        check_out_pitch(m, out_pitch);
         DeviceGuard dg(m->device);
-        FrameSet fs;
-        memset(&fs, 0, sizeof fs);
-        for (int i = 0; i < m->n; i++) {
-            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)m->in_w[i], "bad input frame");
-            // the staging loads form row offsets with 24-bit multiplies (kernels.hip stage_load)
-            REQUIRE(in_pitch[i] < ((size_t)1 << 24), "input pitch must be below 16 MiB");
-            // the gain feed reads frames through 32-bit buffer resources
-            REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) < 0x7FFFFFFFull,
-                    "input frame larger than 2 GiB");
-            // ... in 8-byte segments (kernels.hip feed_rows)
-            REQUIRE((uint64_t)in_pitch[i] * (uint64_t)(m->in_h[i] + m->in_h[i] / 2) >= 8, "input frame below 8 bytes");
-            fs.f[i] = SourceFrame{in_dev[i], m->in_w[i], m->in_h[i], (int64_t)in_pitch[i], m->vig[i].p};
-        }
+        const FrameSet fs = frame_set(m, in_dev, in_pitch);
         // stitches sharing a frame slot (gains, feed totals, work counters) are ordered: each waits for
         // the slot's previous stitch (with one slot: for the previous stitch, as vr::Mapper is not
         // re-entrant either).  Always through the event, never by comparing stream handles: a destroyed
@@ -1155,36 +1207,11 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         const int k = (m->cur_slot + 1) % (int)m->slots.size();
         octvr_mapper::FrameSlot& sl = m->slots[k];
         if (sl.done) HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
-        if (m->use_gain) {
-            if (gains_dev) {
-                HIP_CHECK(hipMemcpyAsync(sl.gains, gains_dev, sizeof(double) * m->n, hipMemcpyDeviceToDevice, s));
-            } else if (gains) {
-                REQUIRE(n_gains == m->n, "gains must have one entry per input");
-                HIP_CHECK(launch_set_gains(gains, m->n, sl.gains, s));
-            } else if (m->n_chunks == 0) {  // no intersections: A = diag(b), every gain is 1
-                const std::vector<double> ones(m->n, 1.0);
-                HIP_CHECK(launch_set_gains(ones.data(), m->n, sl.gains, s));
-            } else {
-                // with frames in flight the feed runs beside the previous frame's composite: the lean
-                // variant fits next to it (the wide-prefetch one waits for its workgroups to drain)
-                const bool lean = m->slots.size() > 1;
-                HIP_CHECK(launch_gain_feed(fs, m->samples.p, m->partners.p, m->tex, m->n_chunks, m->N.p, m->n, sl.totals,
-                                           sl.tickets, sl.gains, s, lean));
-            }
-        }
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        const bool timed = m->timing > 0 && (m->timed_calls++ % (uint64_t)m->timing) == 0;
-        if (timed) {
-            if (m->free_events.empty()) {
-                HIP_CHECK(hipEventCreate(&e0));
-                HIP_CHECK(hipEventCreate(&e1));
-            } else {
-                e0 = m->free_events.back().first;
-                e1 = m->free_events.back().second;
-                m->free_events.pop_back();
-            }
-            if (m->scaled || m->mb || preview) HIP_CHECK(hipEventRecord(e0, s));  // else the composite records its own
-        }
+        stitch_gains(m, sl, fs, gains, n_gains, gains_dev, s);
+        const auto ev = stitch_events(m);
+        hipEvent_t e0 = ev.first, e1 = ev.second;
+        const bool timed = e0 != nullptr;
+        if (timed && (m->scaled || m->mb || preview)) HIP_CHECK(hipEventRecord(e0, s));  // else the composite records its own
         if (m->scaled || preview) {
             // stitch at template size into the RGB(A) result, then resize + RGB -> YUV420P (mapper.cpp:290-306)
             // (one frame slot only: the result frame is shared); without scaling the resize is the identity
@@ -1213,6 +1240,62 @@ void mapper_stitch(octvr_mapper* m, const uint8_t* const* in_dev, const size_t* 
         HIP_CHECK(hipEventRecord(sl.done, s));
         m->cur_slot = k;
     }
+}
+
+// nb frames (1, 2 or 4) of the same rig in one composite launch (FrameBatch, kernels.hpp): each frame's
+// gains into its own frame slot (nb consecutive slots, each waited for as mapper_stitch waits for one),
+// then one pass over the tiled LUT for all of them.  Scaled-output and multi-band / feather mappers have no
+// batched kernel: their frames are stitched one by one.
+void mapper_stitch_batch(octvr_mapper* m, int nb, const uint8_t* const* in_dev, const size_t* in_pitch,
+                         uint8_t* const* out_dev, size_t out_pitch, const double* gains, hipStream_t s) {
+    REQUIRE(m && in_dev && in_pitch && out_dev, "NULL argument");
+    REQUIRE(nb == 1 || nb == 2 || nb == 4, "a batch holds 1, 2 or 4 frames");
+    for (int f = 0; f < nb; f++) REQUIRE(out_dev[f], "NULL output");
+    if (nb == 1 || m->scaled || m->mb) {
+        for (int f = 0; f < nb; f++)
+            mapper_stitch(m, in_dev + (size_t)f * m->n, in_pitch + (size_t)f * m->n, out_dev[f], out_pitch,
+                          gains ? gains + (size_t)f * m->n : nullptr, gains ? m->n : 0, nullptr, s);
+        return;
+    }
+    REQUIRE((int)m->slots.size() >= nb, "a batch of n frames needs n frames in flight (octvr_mapper_set_frames_in_flight)");
+    REQUIRE(nb <= 2 || m->n <= 16, "a batch of 4 frames holds 16 cameras per frame");
+    check_out_pitch(m, out_pitch);
+    DeviceGuard dg(m->device);
+    FrameSet fs[kMaxBatch];
+    const double* g[kMaxBatch];
+    int ks[kMaxBatch];
+    int k = m->cur_slot;
+    const bool feed = m->use_gain && !gains && m->n_chunks > 0;  // every frame's gains estimated: one feed launch
+    unsigned long long* tot[kMaxBatch];
+    uint32_t* tick[kMaxBatch];
+    double* gd[kMaxBatch];
+    for (int f = 0; f < nb; f++) {
+        k = (k + 1) % (int)m->slots.size();
+        ks[f] = k;
+        octvr_mapper::FrameSlot& sl = m->slots[k];
+        fs[f] = frame_set(m, in_dev + (size_t)f * m->n, in_pitch + (size_t)f * m->n);
+        if (sl.done) HIP_CHECK(hipStreamWaitEvent(s, sl.done, 0));
+        if (!feed) stitch_gains(m, sl, fs[f], gains ? gains + (size_t)f * m->n : nullptr, gains ? m->n : 0, nullptr, s);
+        g[f] = sl.gains;
+        tot[f] = sl.totals;
+        tick[f] = sl.tickets;
+        gd[f] = sl.gains;
+    }
+    if (feed)  // GainCompensatorGPU::feed of each frame (exposure_compensate.cpp:223-297), all in one launch
+        HIP_CHECK(launch_gain_feed_batch(fs, nb, m->samples.p, m->partners.p, m->tex, m->n_chunks, m->N.p, m->n, tot, tick,
+                                         gd, s, true));
+    const auto ev = stitch_events(m);
+    TiledLut view = m->tiles.view;
+    view.queue = m->slots[ks[0]].queue;  // this launch's work counters (the first frame's slot)
+    HIP_CHECK(launch_stitch_batch(fs, nb, view, m->W, m->H, g, m->use_gain, out_dev, (int64_t)out_pitch, s, ev.first,
+                                  ev.second));
+    if (ev.first) m->events.emplace_back(ev.first, ev.second);
+    for (int f = 0; f < nb; f++) {
+        octvr_mapper::FrameSlot& sl = m->slots[ks[f]];
+        if (!sl.done) HIP_CHECK(hipEventCreateWithFlags(&sl.done, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(sl.done, s));
+    }
+    m->cur_slot = ks[nb - 1];
 }
 
 int mapper_num_inputs(const octvr_mapper* m) { return m->n; }
@@ -1656,6 +1739,13 @@ int octvr_mapper_stitch_yuv420p(octvr_mapper* m, const uint8_t* const* in_dev, c
                                 uint8_t* out_dev, size_t out_pitch, const double* gains, int n_gains, void* stream) {
     return guarded([&] {
         mapper_stitch(m, in_dev, in_pitch, out_dev, out_pitch, gains, n_gains, nullptr, (hipStream_t)stream);
+    });
+}
+
+int octvr_mapper_stitch_batch(octvr_mapper* m, int n_frames, const uint8_t* const* in_dev, const size_t* in_pitch,
+                              uint8_t* const* out_dev, size_t out_pitch, const double* gains, void* stream) {
+    return guarded([&] {
+        mapper_stitch_batch(m, n_frames, in_dev, in_pitch, out_dev, out_pitch, gains, (hipStream_t)stream);
     });
 }
 

@@ -71,6 +71,8 @@ if hasattr(_lib, "octvr_mapper_create_ex"):
     _lib.octvr_mapper_create_ex.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.c_int,
                                             C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(_VP)]
 REMAP_TEXTURE = 1  # octvr_hip.h OCTVR_REMAP_TEXTURE
+_lib.octvr_mapper_stitch_batch.argtypes = [_VP, C.c_int, C.POINTER(_VP), C.POINTER(C.c_size_t), C.POINTER(_VP),
+                                           C.c_size_t, _VP, _VP]
 _lib.octvr_mapper_stitch_yuv420p.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t,
                                              C.POINTER(C.c_double), C.c_int, _VP]
 _lib.octvr_mapper_stitch_preview.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP, C.c_int,
@@ -110,6 +112,8 @@ PREVIEW_SINK = C.CFUNCTYPE(None, C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C
 _lib.octvr_async_pop_preview.argtypes = [_VP, _VP, C.c_size_t, C.POINTER(PreviewDataHeader)]
 _lib.octvr_async_set_preview_sink.argtypes = [_VP, PREVIEW_SINK, _VP]
 _lib.octvr_async_info.argtypes = [_VP, C.c_char_p, C.c_size_t]
+_lib.octvr_async_register_output.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t)]
+_lib.octvr_async_unregister_output.argtypes = [_VP, C.POINTER(_VP)]
 _lib.octvr_async_push.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), C.POINTER(_VP), C.POINTER(C.c_size_t)]
 _lib.octvr_async_pop.argtypes = [_VP]
 _lib.octvr_async_pending.argtypes = [_VP, C.POINTER(C.c_int)]
@@ -376,6 +380,24 @@ class FrameRefs:
         self.pitches = (C.c_size_t * self.n)(*[t.stride(0) for t in self.tensors])
 
 
+class BatchRefs:
+    """Several frame sets' device pointers and their outputs marshalled once (Mapper.batch_refs)."""
+    __slots__ = ("keep", "ptrs", "pitches", "outs", "out_pitch", "nf")
+
+    def __init__(self, frame_sets, outputs):
+        refs = [fs if isinstance(fs, FrameRefs) else FrameRefs(fs) for fs in frame_sets]
+        self.nf = len(refs)
+        assert len(outputs) == self.nf, "one output per frame set"
+        self.keep = (refs, list(outputs))
+        ptrs = [p for r in refs for p in r.ptrs]
+        pitches = [p for r in refs for p in r.pitches]
+        self.ptrs = (_VP * len(ptrs))(*ptrs)
+        self.pitches = (C.c_size_t * len(pitches))(*pitches)
+        self.outs = (_VP * self.nf)(*[o.data_ptr() for o in outputs])
+        self.out_pitch = outputs[0].stride(0)
+        assert all(o.stride(0) == self.out_pitch for o in outputs), "the outputs of a batch share one pitch"
+
+
 class Mapper:
     """vr::Mapper on one device: stitch(inputs YUV420P, output YUV420P) with optional gain."""
 
@@ -430,6 +452,24 @@ class Mapper:
                                                     output.stride(0), C.c_void_p(preview.data_ptr()),
                                                     preview.shape[1], preview.shape[0], preview.stride(0), g, ng,
                                                     _stream_ptr(stream)))
+
+    @staticmethod
+    def batch_refs(frame_sets, outputs):
+        """BatchRefs of several frame sets (lists of input tensors or FrameRefs) and their outputs, accepted
+        by stitch_batch() in place of the lists."""
+        return BatchRefs(frame_sets, outputs)
+
+    def stitch_batch(self, frame_sets, outputs=None, gains=None, stream=None):
+        """len(frame_sets) (1, 2 or 4) frames in one call (octvr_mapper_stitch_batch): each frame's gains
+        estimated (or gains: one list per frame), one composite launch for all; outputs: one tensor per
+        frame (same pitch).  frame_sets may be a BatchRefs (outputs then None)."""
+        b = frame_sets if isinstance(frame_sets, BatchRefs) else BatchRefs(frame_sets, outputs)
+        g = None
+        if gains is not None:
+            flat = [float(v) for gl in gains for v in gl]
+            g = (C.c_double * len(flat))(*flat)
+        _check(_lib.octvr_mapper_stitch_batch(self._h, b.nf, b.ptrs, b.pitches, b.outs, b.out_pitch, g,
+                                              _stream_ptr(stream)))
 
     def gains(self):
         g = (C.c_double * self.n)()
@@ -556,6 +596,7 @@ class AsyncMultiMapper:
         self._h = hd
         self.preview_size = (pw, ph) if pw * ph > 0 else (0, 0)
         self._sink = None
+        self._registered = []
         self._templates = list(templates)  # the mappers copy what they need; kept for symmetry with the reference
         self.n = n
         self.out_size = tuple(out_size)
@@ -585,6 +626,21 @@ class AsyncMultiMapper:
         n = C.c_int()
         _check(_lib.octvr_async_pending(self._h, C.byref(n)))
         return n.value
+
+    def register_output(self, output):
+        """Page-lock an output (Y, U, V) plane set the caller will push again (octvr_async_register_output): its
+        frames are then downloaded straight into it.  The arrays are kept alive until close()."""
+        for p in output:
+            assert p.dtype == np.uint8 and p.ndim == 2 and p.strides[1] == 1
+        op = (_VP * 3)(*[p.ctypes.data for p in output])
+        opt = (C.c_size_t * 3)(*[p.strides[0] for p in output])
+        _check(_lib.octvr_async_register_output(self._h, op, opt))
+        self._registered.append(tuple(output))
+
+    def unregister_output(self, output):
+        op = (_VP * 3)(*[p.ctypes.data for p in output])
+        _check(_lib.octvr_async_unregister_output(self._h, op))
+        self._registered = [r for r in self._registered if not all(a is b for a, b in zip(r, output))]
 
     def preview(self):
         """(rgb, header): the latest published preview as an (h, w, 3) uint8 array and its PreviewDataHeader
@@ -625,6 +681,7 @@ class AsyncMultiMapper:
             _lib.octvr_async_destroy(self._h)
             self._h = C.c_void_p(0)
             self._inflight = []
+            self._registered = []
 
     def __del__(self):
         try:

@@ -274,3 +274,53 @@ def test_gpu_async_preview_rejects_bad_size(product_lib):
     with pytest.raises(ox.OctvrError):  # no preview configured
         am.preview()
     am.close()
+
+
+def test_gpu_async_registered_outputs(product_lib):
+    """Output plane sets the caller registers (octvr_async_register_output) are downloaded straight into
+    (2-D D2H copies at the caller's pitch, no staging, no copy-out); pushes mixing registered and
+    unregistered sets, two regions side by side, padded pitches — every frame bit-exact; unregistering
+    with frames pending is refused."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    assert torch.cuda.is_available(), "gpu tests need a HIP device"
+    rig, z = O.load_rig("rigB")
+    W, H = (int(v) for v in z["out_size"])
+    n = len(z["rois"])
+    sizes = [(rig["inputs"][i]["options"]["width"], rig["inputs"][i]["options"]["height"]) for i in range(n)]
+    maps1 = [z[f"map1_{i}"] for i in range(n)]
+    maps2 = [z[f"map2_{i}"] for i in range(n)]
+    masks = [z[f"mask_{i}"] for i in range(n)]
+    mts = [ox.MapperTemplate.from_arrays(W, H, z["rois"].tolist(), maps1, maps2, masks) for _ in range(2)]
+    OW, OH = 2 * W, H
+    am = ox.AsyncMultiMapper(mts, sizes, (OW, OH), [0, 0], [0, 0], [(0.0, 0.0, 0.5, 1.0), (0.5, 0.0, 0.5, 1.0)])
+
+    def planes(pad):  # views into padded buffers: pitch > width
+        y = np.zeros((OH, OW + pad), np.uint8)[:, :OW]
+        u = np.zeros((OH // 2, OW // 2 + pad), np.uint8)[:, :OW // 2]
+        v = np.zeros((OH // 2, OW // 2 + pad), np.uint8)[:, :OW // 2]
+        return (y, u, v)
+
+    ring = [planes(64 * k) for k in range(3)]
+    for r in ring[:2]:
+        am.register_output(r)
+    am.register_output(ring[0])  # again: a no-op
+    frames, outs = [], []
+    for f in range(6):
+        fr = [synthetic.smooth_yuv_frame(w, h, 1700 + 10 * f + i) for i, (w, h) in enumerate(sizes)]
+        out = ring[f % 3]  # ring[2] is not registered: staging path
+        am.push([_planes(x, w, h) for x, (w, h) in zip(fr, sizes)], out)
+        if f == 1:
+            with pytest.raises(ox.OctvrError):
+                am.unregister_output(ring[0])
+        am.pop()
+        want, _ = O.stitch_frame(fr, sizes, z["rois"].tolist(), maps1, maps2, masks, W, H, enable_gain=True,
+                                 threads=8)
+        for k in range(2):
+            x0 = k * W
+            assert np.array_equal(out[0][:, x0:x0 + W], want[:H]), (f, k, "Y")
+            assert np.array_equal(out[1][:, x0 // 2:(x0 + W) // 2], want[H:, :W // 2]), (f, k, "U")
+            assert np.array_equal(out[2][:, x0 // 2:(x0 + W) // 2], want[H:, W // 2:]), (f, k, "V")
+    am.unregister_output(ring[1])
+    am.close()

@@ -322,3 +322,33 @@ def test_gpu_fullsize_async_preview_c2(product_lib):
         assert not d.any(), (f, int(d.sum()), np.argwhere(d)[:4].tolist())
         assert sunk[f].std() > 5
     am.close()
+
+
+@pytest.mark.parametrize("cfg,nb", [("C2", 2), ("C2", 4), ("C4", 4)])
+def test_gpu_fullsize_batch(product_lib, cfg, nb):
+    """Frame batches at the benched size (octvr_mapper_stitch_batch, one composite launch over (item, frame)
+    units): two batches of nb frames on two streams, the bench's splitmix frame sets and smooth ones, gains
+    estimated per frame — every output byte and the last frame's gains against the oracle."""
+    import torch
+    ox = product_lib
+    rig, W, H, sizes, text, rois, maps1, maps2, masks = _oracle_lut(cfg)
+    mt = ox.MapperTemplate.from_json(text, W, H)
+    m = ox.Mapper(mt, sizes, blend=0, enable_gain=True)
+    m.set_frames_in_flight(2 * nb)
+    sets = [_bench_frames(sizes, j) if j % 2 == 0 else _frames(sizes, j) for j in range(2 * nb)]
+    dev = [[torch.from_numpy(f).cuda() for f in fs] for fs in sets]
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(2 * nb)]
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    torch.cuda.synchronize()
+    for b in range(2):
+        m.stitch_batch(dev[b * nb:(b + 1) * nb], outs[b * nb:(b + 1) * nb], stream=streams[b])
+    g_last = np.array(m.gains())
+    torch.cuda.synchronize()
+    for f in range(2 * nb):
+        exp, g_orc = O.stitch_frame(sets[f], sizes, rois, maps1, maps2, masks, W, H, enable_gain=True, gains=None,
+                                    threads=THREADS)
+        got = outs[f].cpu().numpy()
+        d = got != exp
+        assert not d.any(), (cfg, f, int(d.sum()), np.argwhere(d)[:4].tolist())
+        if f == 2 * nb - 1:
+            np.testing.assert_array_equal(g_last, np.array(g_orc))
