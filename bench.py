@@ -249,8 +249,12 @@ def async_e2e(ox, mt, sizes, W, H, blend, frames_np, dev, frames=64, gain=True, 
 # 496k / 607k / 550k MP/s, C3 172k / 178k / 184k, C4 564k / 585k / 578k, C1 371k / 483k / 485k (3 kept: the
 # two 4s were 511k and 459k), F2 (stitch_nv12 on 1 / 2 / 3 streams) 85k / 91k / 93k
 DEFAULT_INFLIGHT = {"C3": 4, "F2": 3}
-# frames per composite launch (octvr_mapper_stitch_batch), no-blend configs only
-DEFAULT_BATCH = {}
+DEFAULT_INFLIGHT_BATCHED = {"F2": 1}  # streams when frames are batched (default 2)
+# frames per composite launch (octvr_mapper_stitch_batch), no-blend configs only; interleaved on one box at
+# 1,000 steps: C1 1 x 3 streams / 2 x 2 / 4 x 2 = 548k-568k / 573k-614k / 809k-813k MP/s,
+# C4 739k-742k / 792k-794k / 819k-820k, C2 707k / 636k / 654k (C2 stays one frame per launch)
+# F2 (FastMapper, one launch per plane): 1 x 3 streams 112k, 2 x 2 111k, 4 x 1 134k, 4 x 2 126k MP/s
+DEFAULT_BATCH = {"C1": 4, "C4": 4, "F2": 4}
 CPU_BASELINE_S = float(os.environ.get("OCTVR_CPU_BASELINE_S", "10"))
 DEFAULT_FRAME_SETS = 8
 
@@ -412,24 +416,34 @@ def fast_rank(args, world, rank, local_rank, dist):
     fm = ox.FastMapper(mt, sizes, device=dev)
     # stitch_nv12 keeps no per-call device state, so a caller may run several at once on their own
     # streams and outputs (frames in flight, as the Mapper configs do through set_frames_in_flight)
-    inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 1))
-    nsets = frame_sets_of(args, inflight)
+    nb = args.batch if args.batch is not None else DEFAULT_BATCH.get(args.config, 1)
+    if args.steps % nb:
+        raise SystemExit("bench.py: --steps must be a multiple of --batch")
+    inflight = max(1, args.inflight if args.inflight is not None else
+                   (DEFAULT_INFLIGHT_BATCHED.get(args.config, 2) if nb > 1 else DEFAULT_INFLIGHT.get(args.config, 1)))
+    nsets = frame_sets_of(args, inflight * nb)
     # distinct frame sets (seeded by rank, set, camera), rotated through the steps as the Mapper configs do
     frame_sets = [[torch.from_numpy(nv12_of(synthetic.yuv_frame(w, h, frame_seed(rank, 0, i)))).to(f"cuda:{dev}")
                    for i, (w, h) in enumerate(sizes)]]
     for j in range(1, nsets):
         frame_sets.append(derive_set(frame_sets[0], [frame_seed(rank, j, i) for i in range(len(sizes))]))
     frames = frame_sets[0]
-    outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight)]
+    outs = [torch.empty((H * 3 // 2, W), dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(inflight * nb)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(inflight - 1)]
     stream, out = streams[0], outs[0]
 
     refs = [ox.Mapper.frame_refs(fs) for fs in frame_sets]
     import ctypes
     raw_streams = [ctypes.c_void_p(st.cuda_stream) for st in streams]
+    ncalls = nsets * inflight
+    brefs = [ox.Mapper.batch_refs([refs[(c * nb + f) % nsets] for f in range(nb)],
+                                  outs[(c % inflight) * nb:(c % inflight + 1) * nb]) for c in range(ncalls)] if nb > 1 else None
 
-    def step(k):
-        fm.stitch_nv12(refs[k % nsets], outs[k % inflight], stream=raw_streams[k % inflight])
+    def step(k):  # one call: one frame (nb = 1) or a batch of nb frames
+        if nb == 1:
+            fm.stitch_nv12(refs[k % nsets], outs[k % inflight], stream=raw_streams[k % inflight])
+        else:
+            fm.stitch_nv12_batch(brefs[k % ncalls], stream=raw_streams[k % inflight])
 
     if args.pmc_child:
         for k in range(max(args.steps, 1)):
@@ -440,9 +454,9 @@ def fast_rank(args, world, rank, local_rank, dist):
         step(k)
     torch.cuda.synchronize(dev)
     n_pre = preroll(step, args.preroll, lambda: torch.cuda.synchronize(dev))
-    elapsed = timed_region(step, args.steps, lambda: torch.cuda.synchronize(dev), dist)
+    elapsed = timed_region(step, args.steps // nb, lambda: torch.cuda.synchronize(dev), dist)
     # kernel time: events around 16 back-to-back stitches (both plane launches) on one stream, after the
-    # timed region
+    # timed region (one frame per launch)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for k in range(16):
@@ -461,8 +475,8 @@ def fast_rank(args, world, rank, local_rank, dist):
         "data": "synthetic (splitmix64 frames as NV12, further sets derived by a splitmix64 key, SURVEY.md §8d rig)",
         "config": {"workload": "F2: %d x %dx%d fullframe_fisheye -> %dx%d, vr::FastMapper::stitch_nv12 (feather, "
                                "template without ROI), NV12 in/out" % (len(sizes), sizes[0][0], sizes[0][1], W, H),
-                   "rigs_per_gpu": 1, "frames_in_flight": inflight, "frame_sets": nsets,
-                   "parallelism": "independent rig per GPU"},
+                   "rigs_per_gpu": 1, "frames_in_flight": inflight * nb, "streams": inflight, "frames_per_launch": nb,
+                   "frame_sets": nsets, "parallelism": "independent rig per GPU"},
         "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "fast_y_kernel + fast_uv_kernel", "kernel_us": round(kern_s * 1e6, 2),
@@ -499,9 +513,10 @@ def gpu_rank(args, world, rank, local_rank, dist):
     m = ox.Mapper(mt, sizes, blend=blend, enable_gain=use_gain, device=dev, remap=args.remap)
     # frames in flight: like a capture pipeline, frame k+1 (its own buffers, its own stream) is issued
     # while frame k is still stitching, so frame k+1's gain feed overlaps frame k's composite
-    inflight = max(1, args.inflight if args.inflight is not None else DEFAULT_INFLIGHT.get(args.config, 3))
     # frames per composite launch: a batch of nb frames per call on each of the `inflight` streams
     nb = args.batch if args.batch is not None else (DEFAULT_BATCH.get(args.config, 1) if blend == 0 else 1)
+    inflight = max(1, args.inflight if args.inflight is not None else
+                   (DEFAULT_INFLIGHT_BATCHED.get(args.config, 2) if nb > 1 else DEFAULT_INFLIGHT.get(args.config, 3)))
     if blend != 0 and nb != 1:
         raise SystemExit("bench.py: --batch needs the no-blend composite (multi-band / feather stitch frame by frame)")
     if args.steps % nb:

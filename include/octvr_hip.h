@@ -188,7 +188,7 @@ int octvr_mapper_gains(octvr_mapper* mapper, double* gains, int n);
  * A stitch waits (through an event) only for its slot's previous stitch.
  * k > 1 needs the output at template size (no scaled output; OCTVR_E_UNSUPPORTED otherwise);
  * multi-band / feather mappers get per-slot pyramids.  Synchronizes. */
-#define OCTVR_MAX_FRAMES_IN_FLIGHT 8
+#define OCTVR_MAX_FRAMES_IN_FLIGHT 16
 int octvr_mapper_set_frames_in_flight(octvr_mapper* mapper, int k);
 /* Algorithmic device bytes read+written by one launch of the composite (stitch) kernel: 4 B tiled
  * LUT entry (8 B in wide tiles) + 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each
@@ -301,6 +301,12 @@ int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fastmapper, const uint8_t* co
                                  uint8_t* out_dev, size_t out_pitch, void* stream);
 /* Algorithmic bytes one stitch_nv12 moves (entries read, output written, source bytes its weighted taps
  * reach): the roofline basis of bench.py --config F2. */
+/* n_frames (1, 2 or 4) frames in one launch per plane (no reference counterpart): frame f's inputs are
+ * in_dev[f * n_inputs + i], its output out_dev[f] (one pitch); each run's entries and feather weights are
+ * loaded once and applied to every frame.  Every output equals stitch_nv12 of its frame, bit for bit.  4
+ * frames hold at most 16 inputs. */
+int octvr_fastmapper_stitch_nv12_batch(octvr_fastmapper* fastmapper, int n_frames, const uint8_t* const* in_dev,
+                                       const size_t* in_pitch, uint8_t* const* out_dev, size_t out_pitch, void* stream);
 int octvr_fastmapper_traffic(const octvr_fastmapper* fastmapper, double* bytes);
 void octvr_fastmapper_destroy(octvr_fastmapper* fastmapper);
 

@@ -26,6 +26,9 @@ using namespace octvr;
 namespace octvr {
 hipError_t launch_fastmapper_nv12(const FrameSet& frames, const FastMapperPlane& y, const FastMapperPlane& uv, int W,
                                   int H, uint8_t* out, int64_t out_pitch, hipStream_t s);
+hipError_t launch_fastmapper_nv12_batch(const FrameSet* frames, int nf, const FastMapperPlane& y,
+                                        const FastMapperPlane& uv, int W, int H, uint8_t* const* out, int64_t out_pitch,
+                                        hipStream_t s);
 }
 
 // One plane's entries: per (run, camera with weight in the run) a block of 256, on the host (FastPlaneHost,
@@ -518,28 +521,40 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
     }
 }
 
-int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_dev, const size_t* in_pitch,
-                                 uint8_t* out_dev, size_t out_pitch, void* stream) {
+int octvr_fastmapper_stitch_nv12_batch(octvr_fastmapper* fm, int n_frames, const uint8_t* const* in_dev,
+                                       const size_t* in_pitch, uint8_t* const* out_dev, size_t out_pitch, void* stream) {
     try {
         REQUIRE(fm && in_dev && in_pitch && out_dev, "NULL argument");
+        REQUIRE(n_frames == 1 || n_frames == 2 || n_frames == 4, "a batch holds 1, 2 or 4 frames");
+        REQUIRE(n_frames <= 2 || fm->n <= 16, "a batch of 4 frames holds 16 cameras per frame");
         REQUIRE(out_pitch >= (size_t)fm->W, "output pitch smaller than width");
         DeviceGuard dg(fm->device);
-        FrameSet fs;
-        memset(&fs, 0, sizeof fs);
-        for (int i = 0; i < fm->n; i++) {
-            REQUIRE(in_dev[i] && in_pitch[i] >= (size_t)fm->in_w[i] && in_pitch[i] < ((size_t)1 << 24), "bad input frame");
-            REQUIRE(in_pitch[i] * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) >= 8 &&
-                        in_pitch[i] * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) < 0x7FFFFFFFull,
-                    "input frame of fewer than 8 or more than 2^31 bytes");
-            fs.f[i] = SourceFrame{in_dev[i], fm->in_w[i], fm->in_h[i], (int64_t)in_pitch[i], nullptr};
+        FrameSet fs[kMaxBatch];
+        for (int f = 0; f < n_frames; f++) {
+            REQUIRE(out_dev[f], "NULL output");
+            memset(&fs[f], 0, sizeof fs[f]);
+            for (int i = 0; i < fm->n; i++) {
+                const uint8_t* p = in_dev[(size_t)f * fm->n + i];
+                const size_t pitch = in_pitch[(size_t)f * fm->n + i];
+                REQUIRE(p && pitch >= (size_t)fm->in_w[i] && pitch < ((size_t)1 << 24), "bad input frame");
+                REQUIRE(pitch * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) >= 8 &&
+                            pitch * (size_t)(fm->in_h[i] + fm->in_h[i] / 2) < 0x7FFFFFFFull,
+                        "input frame of fewer than 8 or more than 2^31 bytes");
+                fs[f].f[i] = SourceFrame{p, fm->in_w[i], fm->in_h[i], (int64_t)pitch, nullptr};
+            }
         }
-        HIP_CHECK(launch_fastmapper_nv12(fs, fm->y.view(), fm->uv.view(), fm->W, fm->H, out_dev, (int64_t)out_pitch,
-                                         (hipStream_t)stream));
+        HIP_CHECK(launch_fastmapper_nv12_batch(fs, n_frames, fm->y.view(), fm->uv.view(), fm->W, fm->H, out_dev,
+                                               (int64_t)out_pitch, (hipStream_t)stream));
         return OCTVR_OK;
     } catch (const OctvrError& e) {
         set_last_error(e.what());
         return e.code;
     }
+}
+
+int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fm, const uint8_t* const* in_dev, const size_t* in_pitch,
+                                 uint8_t* out_dev, size_t out_pitch, void* stream) {
+    return octvr_fastmapper_stitch_nv12_batch(fm, 1, in_dev, in_pitch, &out_dev, out_pitch, stream);
 }
 
 int octvr_fastmapper_traffic(const octvr_fastmapper* fm, double* bytes) {

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstring>
 
 #include "device_common.hpp"
 #include "kernels.hpp"
@@ -76,6 +77,22 @@ struct FastPlane {
 // compact block header bit (y word): every weighted entry of the block is interior (fastmapper.cpp)
 constexpr uint32_t kFastInterior = 1u;
 
+// The frames of one launch (FastBatch, the FIRST kernel argument): camera c of frame f at src[fbase + c],
+// fbase = f << cam_log2; read through the kernarg segment with the camera uniform (scalar loads).
+typedef __attribute__((address_space(4))) const SourceFrame kFastSource;
+typedef __attribute__((address_space(4))) const FastBatch kFastBatch;
+static_assert(offsetof(FastBatch, src) == 0, "FastBatch layout");
+__device__ __forceinline__ SourceFrame fast_frame(uint32_t idx) {
+    const kFastSource* kf = (const kFastSource*)__builtin_amdgcn_kernarg_segment_ptr();
+    SourceFrame s;
+    s.yuv = kf[idx].yuv;
+    s.w = kf[idx].w;
+    s.h = kf[idx].h;
+    s.pitch = kf[idx].pitch;
+    s.vig = nullptr;
+    return s;
+}
+
 // One group of up to kFastGroup cameras of a run, after the entry loads: per camera and tap row one 8-byte
 // load from the 4-byte aligned start at or below the row's first in-image tap byte (it holds both taps'
 // bytes: Y x, x + 1; chroma the V, U pairs of x, x + 1), then remap_weighted's sum in integers.
@@ -83,7 +100,7 @@ constexpr uint32_t kFastInterior = 1u;
 // last (host-checked per block, kFastInterior), so the address clamps, the end-of-frame clamp and the
 // in-image masks are identities and are left out.
 template <int PLANE, bool INNER>
-__device__ __forceinline__ void fast_group(const FrameSet& frames, const bool (&live)[kFastGroup], const int (&cam)[kFastGroup],
+__device__ __forceinline__ void fast_group(uint32_t fbase, const bool (&live)[kFastGroup], const int (&cam)[kFastGroup],
                                            const int (&sxk)[kFastGroup], const int (&syk)[kFastGroup],
                                            const uint32_t (&code)[kFastGroup], const uint32_t (&wk)[kFastGroup],
                                            uint32_t& acc0, uint32_t& acc1) {
@@ -95,7 +112,7 @@ __device__ __forceinline__ void fast_group(const FrameSet& frames, const bool (&
         rw[k][0] = rw[k][1] = make_uint2(0u, 0u);
         sel[k][0] = sel[k][1] = 0u;
         if (!live[k]) continue;
-        const SourceFrame f = frames.f[cam[k]];
+        const SourceFrame f = fast_frame(fbase + (uint32_t)cam[k]);
         const int sw = PLANE ? f.w / 2 : f.w, sh = PLANE ? f.h / 2 : f.h;
         const uint32_t base = PLANE ? (uint32_t)f.h * (uint32_t)f.pitch : 0u;
         const uint32_t size = (uint32_t)f.pitch * (uint32_t)(f.h + f.h / 2);  // >= 8 (host check)
@@ -130,7 +147,7 @@ __device__ __forceinline__ void fast_group(const FrameSet& frames, const bool (&
         const uint32_t fx = code[k] & 31u, fy = code[k] >> 5;
         uint32_t wx = 32u + fx * 0xFFFFu, wy = 32u + fy * 0xFFFFu;  // {32 - f, f} as u16 pairs
         if (!INNER) {  // taps outside the image weigh 0: column / row masks
-            const SourceFrame f = frames.f[cam[k]];
+            const SourceFrame f = fast_frame(fbase + (uint32_t)cam[k]);
             const uint32_t sw = (uint32_t)(PLANE ? f.w / 2 : f.w), sh = (uint32_t)(PLANE ? f.h / 2 : f.h);
             const int sx = sxk[k], sy = syk[k];
             const bool ix0 = (uint32_t)sx < sw, ix1 = (uint32_t)(sx + 1) < sw;
@@ -148,16 +165,19 @@ __device__ __forceinline__ void fast_group(const FrameSet& frames, const bool (&
     }
 }
 
-template <int PLANE, bool COMPACT>
-__device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPlane& fp, int W, int H, uint8_t* out,
-                                           int64_t out_pitch) {
+// LG: 1 << LG frames per launch — each group's entries are loaded once and applied to every frame (FastBatch)
+template <int PLANE, bool COMPACT, int LG>
+__device__ __forceinline__ void fast_plane(const FastPlane& fp, int W, int H, int64_t out_pitch) {
+    constexpr int NF = 1 << LG, cam_lg = LG <= 1 ? 5 : 4;
     typedef __attribute__((address_space(4))) const uint64_t kU64;
     const int pw = PLANE ? W / 2 : W, ph = PLANE ? H / 2 : H;
     const uint32_t npx = (uint32_t)pw * (uint32_t)ph;  // < 2^31 (host check)
     const uint2 rr = fp.runs[blockIdx.x];
     uint32_t m = (uint32_t)uniform((int)rr.x);
     uint32_t blk = (uint32_t)uniform((int)rr.y);
-    uint32_t acc0 = 0, acc1 = 0;  // Y (or V), U
+    uint32_t acc0[NF], acc1[NF];  // per frame: Y (or V), U
+#pragma unroll
+    for (int f = 0; f < NF; f++) acc0[f] = acc1[f] = 0u;
     while (m) {
         int sxk[kFastGroup], syk[kFastGroup];
         uint32_t code[kFastGroup], wk[kFastGroup];
@@ -206,10 +226,13 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
         bool inner = COMPACT;
 #pragma unroll
         for (int k = 0; k < kFastGroup; k++) inner = inner && (!live[k] || ((hd[k] >> 32) & kFastInterior) != 0);
-        if (inner)
-            fast_group<PLANE, true>(frames, live, cam, sxk, syk, code, wk, acc0, acc1);
-        else
-            fast_group<PLANE, false>(frames, live, cam, sxk, syk, code, wk, acc0, acc1);
+#pragma unroll
+        for (int f = 0; f < NF; f++) {
+            if (inner)
+                fast_group<PLANE, true>((uint32_t)f << cam_lg, live, cam, sxk, syk, code, wk, acc0[f], acc1[f]);
+            else
+                fast_group<PLANE, false>((uint32_t)f << cam_lg, live, cam, sxk, syk, code, wk, acc0[f], acc1[f]);
+        }
     }
     // pixel index -> (x, y): the run's first row by one scalar division, then at most 256 / pw row steps
     const uint32_t idx0 = blockIdx.x * 256u;
@@ -220,56 +243,93 @@ __device__ __forceinline__ void fast_plane(const FrameSet& frames, const FastPla
         x -= (uint32_t)pw;
         y++;
     }
-    if (PLANE) {
-        uint8_t* o = out + (int64_t)(H + (int)y) * out_pitch + 2 * x;  // merge(c1c2): V first, then U
-        o[0] = convert_out(acc0);
-        o[1] = convert_out(acc1);
-    } else {
-        out[(int64_t)y * out_pitch + x] = convert_out(acc0);
+    const kFastBatch* kb = (const kFastBatch*)__builtin_amdgcn_kernarg_segment_ptr();
+#pragma unroll
+    for (int f = 0; f < NF; f++) {
+        uint8_t* out = kb->out[f];
+        if (PLANE) {
+            uint8_t* o = out + (int64_t)(H + (int)y) * out_pitch + 2 * x;  // merge(c1c2): V first, then U
+            o[0] = convert_out(acc0[f]);
+            o[1] = convert_out(acc1[f]);
+        } else {
+            out[(int64_t)y * out_pitch + x] = convert_out(acc0[f]);
+        }
     }
 }
 
 // runs[r] = {camera mask, first block}: run r's cameras (ascending) own blocks first, first + 1, ... of
 // 256 entries (fastmapper.cpp)
-template <bool COMPACT>
-__global__ void __launch_bounds__(256) fast_y_kernel(FrameSet frames, FastPlane fp, int W, int H, uint8_t* out,
-                                                     int64_t out_pitch) {
-    fast_plane<0, COMPACT>(frames, fp, W, H, out, out_pitch);
+template <bool COMPACT, int LG>
+__global__ void __launch_bounds__(256) fast_y_kernel(FastBatch batch, FastPlane fp, int W, int H, int64_t out_pitch) {
+    (void)batch;  // read through the kernarg segment (kFastBatch)
+    fast_plane<0, COMPACT, LG>(fp, W, H, out_pitch);
 }
 
-template <bool COMPACT>
-__global__ void __launch_bounds__(256) fast_uv_kernel(FrameSet frames, FastPlane fp, int W, int H, uint8_t* out,
-                                                      int64_t out_pitch) {
-    fast_plane<1, COMPACT>(frames, fp, W, H, out, out_pitch);
+template <bool COMPACT, int LG>
+__global__ void __launch_bounds__(256) fast_uv_kernel(FastBatch batch, FastPlane fp, int W, int H, int64_t out_pitch) {
+    (void)batch;
+    fast_plane<1, COMPACT, LG>(fp, W, H, out_pitch);
+}
+
+template <int PLANE, bool COMPACT, int LG>
+static void launch_plane_kernel(dim3 grid, const FastBatch& b, const FastPlane& fp, int W, int H, int64_t out_pitch,
+                                hipStream_t s) {
+    if (PLANE)
+        hipLaunchKernelGGL((fast_uv_kernel<COMPACT, LG>), grid, dim3(256), 0, s, b, fp, W, H, out_pitch);
+    else
+        hipLaunchKernelGGL((fast_y_kernel<COMPACT, LG>), grid, dim3(256), 0, s, b, fp, W, H, out_pitch);
 }
 
 template <int PLANE, bool COMPACT>
-static void launch_plane_kernel(dim3 grid, const FrameSet& frames, const FastPlane& fp, int W, int H, uint8_t* out,
-                                int64_t out_pitch, hipStream_t s) {
-    if (PLANE)
-        hipLaunchKernelGGL((fast_uv_kernel<COMPACT>), grid, dim3(256), 0, s, frames, fp, W, H, out, out_pitch);
+static void launch_plane_lg(int lg, dim3 grid, const FastBatch& b, const FastPlane& fp, int W, int H, int64_t out_pitch,
+                            hipStream_t s) {
+    if (lg == 2)
+        launch_plane_kernel<PLANE, COMPACT, 2>(grid, b, fp, W, H, out_pitch, s);
+    else if (lg == 1)
+        launch_plane_kernel<PLANE, COMPACT, 1>(grid, b, fp, W, H, out_pitch, s);
     else
-        hipLaunchKernelGGL((fast_y_kernel<COMPACT>), grid, dim3(256), 0, s, frames, fp, W, H, out, out_pitch);
+        launch_plane_kernel<PLANE, COMPACT, 0>(grid, b, fp, W, H, out_pitch, s);
 }
 
 template <int PLANE>
-static hipError_t launch_plane(const FrameSet& frames, const FastMapperPlane& p, int W, int H, uint8_t* out,
-                               int64_t out_pitch, hipStream_t s) {
+static hipError_t launch_plane(int lg, const FastBatch& b, const FastMapperPlane& p, int W, int H, int64_t out_pitch,
+                               hipStream_t s) {
     const int64_t n = PLANE ? (int64_t)(W / 2) * (H / 2) : (int64_t)W * H;
     const dim3 grid((unsigned)((n + 255) / 256));
     const FastPlane fp{p.ent, p.off, p.wgt, p.hdr, p.runs, p.nblk};
     if (p.compact)
-        launch_plane_kernel<PLANE, true>(grid, frames, fp, W, H, out, out_pitch, s);
+        launch_plane_lg<PLANE, true>(lg, grid, b, fp, W, H, out_pitch, s);
     else
-        launch_plane_kernel<PLANE, false>(grid, frames, fp, W, H, out, out_pitch, s);
+        launch_plane_lg<PLANE, false>(lg, grid, b, fp, W, H, out_pitch, s);
     return hipGetLastError();
+}
+
+hipError_t launch_fastmapper_nv12_batch(const FrameSet* frames, int nf, const FastMapperPlane& y,
+                                        const FastMapperPlane& uv, int W, int H, uint8_t* const* out, int64_t out_pitch,
+                                        hipStream_t s) {
+    const int lg = nf == 1 ? 0 : nf == 2 ? 1 : nf == 4 ? 2 : -1;
+    if (lg < 0) return hipErrorInvalidValue;
+    const int cam_lg = lg <= 1 ? 5 : 4;
+    FastBatch b;
+    memset(&b, 0, sizeof b);
+    for (int f = 0; f < nf; f++) {
+        for (int i = 0; i < kMaxCams; i++) {
+            if (i >= (1 << cam_lg)) {
+                if (frames[f].f[i].yuv) return hipErrorInvalidValue;  // more cameras than a 4-frame batch holds
+                continue;
+            }
+            b.src[(f << cam_lg) + i] = frames[f].f[i];
+        }
+        b.out[f] = out[f];
+    }
+    const hipError_t e = launch_plane<0>(lg, b, y, W, H, out_pitch, s);
+    if (e != hipSuccess) return e;
+    return launch_plane<1>(lg, b, uv, W, H, out_pitch, s);
 }
 
 hipError_t launch_fastmapper_nv12(const FrameSet& frames, const FastMapperPlane& y, const FastMapperPlane& uv, int W,
                                   int H, uint8_t* out, int64_t out_pitch, hipStream_t s) {
-    const hipError_t e = launch_plane<0>(frames, y, W, H, out, out_pitch, s);
-    if (e != hipSuccess) return e;
-    return launch_plane<1>(frames, uv, W, H, out, out_pitch, s);
+    return launch_fastmapper_nv12_batch(&frames, 1, y, uv, W, H, &out, out_pitch, s);
 }
 
 }  // namespace octvr

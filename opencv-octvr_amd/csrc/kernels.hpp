@@ -233,6 +233,13 @@ hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* sample
                             unsigned long long* totals, uint32_t* tickets, double* gains, hipStream_t s,
                             bool lean = false);  // lean: <= 80 VGPRs (73 used), runs beside a composite (kernels.hip)
 
+// FastMapper frames of one launch (octvr_fastmapper_stitch_nv12_batch): camera c of frame f at
+// src[(f << cam_log2) + c] (cam_log2 5 for up to 2 frames, 4 for 4), the frames' NV12 outputs.
+struct FastBatch {
+    SourceFrame src[2 * kMaxCams];
+    uint8_t* out[kMaxBatch];
+};
+
 // The feeds of nf frames (1, 2 or 4) of a batch in one launch: workgroup b feeds frame b / n_chunks into its
 // own totals / tickets / gains (FeedBatch, the kernel's first argument).
 struct FeedBatch {

@@ -123,6 +123,8 @@ _lib.octvr_fill_poly_u8.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C
 _lib.octvr_png_decode_rgb.argtypes = [C.c_char_p, C.c_size_t, _VP, C.c_size_t, C.POINTER(C.c_int), C.POINTER(C.c_int)]
 _lib.octvr_fastmapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(_VP)]
 _lib.octvr_fastmapper_stitch_nv12.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP]
+_lib.octvr_fastmapper_stitch_nv12_batch.argtypes = [_VP, C.c_int, C.POINTER(_VP), C.POINTER(C.c_size_t),
+                                                    C.POINTER(_VP), C.c_size_t, _VP]
 _lib.octvr_fastmapper_destroy.argtypes = [_VP]
 _lib.octvr_fastmapper_destroy.restype = None
 # self-test hooks (absent from older builds that OCTVR_HIP_LIB may select for an A/B)
@@ -548,6 +550,13 @@ class FastMapper:
             pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
         _check(_lib.octvr_fastmapper_stitch_nv12(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()), output.stride(0),
                                                  _stream_ptr(stream)))
+
+    def stitch_nv12_batch(self, frame_sets, outputs=None, stream=None):
+        """len(frame_sets) (1, 2 or 4) frames in one launch per plane (octvr_fastmapper_stitch_nv12_batch); outputs:
+        one tensor per frame (same pitch).  frame_sets may be a BatchRefs (outputs then None)."""
+        b = frame_sets if isinstance(frame_sets, BatchRefs) else BatchRefs(frame_sets, outputs)
+        _check(_lib.octvr_fastmapper_stitch_nv12_batch(self._h, b.nf, b.ptrs, b.pitches, b.outs, b.out_pitch,
+                                                       _stream_ptr(stream)))
 
     def close(self):
         if self._h and self._h.value:

@@ -111,3 +111,33 @@ def test_gpu_fastmapper_wide_blocks(product_lib):
     d = got != want
     assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
     assert want.any()
+
+
+@pytest.mark.parametrize("wide", [False, True], ids=["compact", "wide"])
+@pytest.mark.parametrize("name", ["rigA", "rigB", "rigC", "rigD"])
+@pytest.mark.parametrize("nb", [2, 4])
+def test_gpu_fastmapper_batch_bit_exact(product_lib, name, wide, nb, monkeypatch):
+    """octvr_fastmapper_stitch_nv12_batch: nb frames per launch (each run's entries loaded once), both entry
+    formats, the general and the interior paths — every frame equal to the oracle's stitch of that frame."""
+    import torch
+    ox = product_lib
+    monkeypatch.setenv("OCTVR_FAST_WIDE", "1" if wide else "0")
+    rig, z = O.load_rig(name)
+    W, H = (int(v) for v in z["out_size"])
+    mt = ox.MapperTemplate.from_json(json.dumps(rig), W, H, use_roi=False)
+    n = len(mt)
+    sizes = [(c["options"]["width"], c["options"]["height"]) for c in rig["inputs"]]
+    maps1, maps2, masks = [], [], []
+    for i in range(n):
+        _, m1, m2, mk, _ = mt.input(i)
+        maps1.append(m1); maps2.append(m2); masks.append(mk)
+    fm = ox.FastMapper(mt, sizes)
+    frames = [[O.rand_img(w, h * 3 // 2, 1, 700 + 37 * f + i) for i, (w, h) in enumerate(sizes)] for f in range(nb)]
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    fm.stitch_nv12_batch([[torch.from_numpy(x).cuda() for x in fr] for fr in frames], outs)
+    torch.cuda.synchronize()
+    for f in range(nb):
+        want = O.fastmapper_nv12(frames[f], sizes, maps1, maps2, masks, W, H)
+        got = outs[f].cpu().numpy()
+        d = got != want
+        assert not d.any(), (f, int(d.sum()), np.argwhere(d)[:5].tolist())

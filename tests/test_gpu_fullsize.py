@@ -352,3 +352,36 @@ def test_gpu_fullsize_batch(product_lib, cfg, nb):
         assert not d.any(), (cfg, f, int(d.sum()), np.argwhere(d)[:4].tolist())
         if f == 2 * nb - 1:
             np.testing.assert_array_equal(g_last, np.array(g_orc))
+
+
+@pytest.mark.parametrize("nb", [2, 4])
+def test_gpu_fullsize_f2_batch(product_lib, nb):
+    """FastMapper frame batches at the F2 size (octvr_fastmapper_stitch_nv12_batch: each run's entries loaded
+    once for nb frames): the bench's frame sets, every byte against the oracle's FastMapper."""
+    import torch
+    from octvr_amd import synthetic
+    ox = product_lib
+    rig, W, H, sizes = synthetic.CONFIGS["F2"]()
+    text = json.dumps(rig)
+    mt = ox.MapperTemplate.from_json(text, W, H, use_roi=False)
+    k = 3
+    if "sets" not in _F2_ORACLE:  # (shared with test_gpu_fullsize_f2_fastmapper)
+        want = O.lut_build(O.json_loads_rj(text), W, H, use_roi=False, threads=THREADS)
+        _F2_ORACLE["luts"] = [(r[1], r[2], r[3]) for r in want]
+        base = [_nv12(synthetic.yuv_frame(w, h, 1000 + i)) for i, (w, h) in enumerate(sizes)]
+        _F2_ORACLE["sets"] = [base] + [[synthetic.derived_frame(f, 1000 + 100 * j + i) for i, f in enumerate(base)]
+                                       for j in range(1, k)]
+        _F2_ORACLE["want"] = [O.fastmapper_nv12(s, sizes, [l[0] for l in _F2_ORACLE["luts"]],
+                                                [l[1] for l in _F2_ORACLE["luts"]], [l[2] for l in _F2_ORACLE["luts"]],
+                                                W, H) for s in _F2_ORACLE["sets"]]
+    fm = ox.FastMapper(mt, sizes)
+    idx = [f % k for f in range(nb)]
+    dev = [[torch.from_numpy(f).cuda() for f in _F2_ORACLE["sets"][j]] for j in idx]
+    outs = [torch.zeros((H * 3 // 2, W), dtype=torch.uint8, device="cuda") for _ in range(nb)]
+    torch.cuda.synchronize()
+    fm.stitch_nv12_batch(dev, outs)
+    torch.cuda.synchronize()
+    for f, j in enumerate(idx):
+        got = outs[f].cpu().numpy()
+        d = got != _F2_ORACLE["want"][j]
+        assert not d.any(), (nb, f, int(d.sum()), np.argwhere(d)[:4].tolist())

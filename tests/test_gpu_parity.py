@@ -241,7 +241,7 @@ def test_gpu_frames_in_flight_rejected_for_scaled_output(ox):
         assert e.value.code == -4
         m.set_frames_in_flight(1)
     m0 = ox.Mapper(mt, [(256, 144)] * 2, blend=0)
-    for bad in (0, 9):
+    for bad in (0, 17):
         with pytest.raises(ox.OctvrError):
             m0.set_frames_in_flight(bad)
 
