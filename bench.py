@@ -156,16 +156,17 @@ def lib_sha256():
         return hashlib.sha256(f.read()).hexdigest()
 
 
-def pmc_traffic(config, blend):
+def pmc_traffic(config, blend, nb=1):
     """(bytes, source) — per composite launch (blend 0) or per frame over the blend sequence (blend > 0:
     the remap, pyrDown and blend launches, i.e. what bytes_per_launch models and kernel_us times; the gain
     feed runs before the sequence and is excluded as for blend 0) — from the profiles/*_pmc_<config>.json
-    whose so_sha256 is the running library's; (None, reason) when no summary of this binary exists."""
+    whose so_sha256 is the running library's and whose launches stitched nb frames each (per frame: / nb);
+    (None, reason) when no summary of this binary exists."""
     import glob
     sha = lib_sha256()
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_%s.json" % config))):
         d = json.load(open(path))
-        if d.get("so_sha256") != sha:
+        if d.get("so_sha256") != sha or d.get("frames_per_launch", 1) != nb:
             continue
         if blend > 0:
             seq = [v for k, v in d.get("traffic_bytes", {}).items() if "gain_feed" not in k]
@@ -174,7 +175,11 @@ def pmc_traffic(config, blend):
             continue
         hit = [v for k, v in d.get("traffic_bytes", {}).items() if "stitch_tiled_kernel" in k]
         if hit:
-            return round(hit[0]), os.path.basename(path)
+            return round(hit[0] / nb), os.path.basename(path)
+        if config == "F2":
+            fast = [v for k, v in d.get("traffic_bytes", {}).items() if "fast_" in k]
+            if fast:
+                return round(sum(fast) / nb), os.path.basename(path)
     return None, "no PMC summary of this liboctvr_hip.so (sha256 %s...)" % sha[:12]
 
 
@@ -459,13 +464,17 @@ def fast_rank(args, world, rank, local_rank, dist):
     # timed region (one frame per launch)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
-    for k in range(16):
-        fm.stitch_nv12(frames, out, stream=stream)
+    for k in range(16 // nb):  # 16 frames, nb per launch
+        if nb == 1:
+            fm.stitch_nv12(frames, out, stream=stream)
+        else:
+            fm.stitch_nv12_batch(brefs[(k * inflight) % ncalls], stream=stream)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     kern_s = e0.elapsed_time(e1) / 1e3 / 16
-    b = fm.traffic_bytes()
-    traffic, traffic_src = pmc_traffic(args.config, 1)
+    lut_b, frame_b = fm.traffic_parts()
+    b = lut_b / nb + frame_b  # per frame: the entries are read once per launch of nb frames
+    traffic, traffic_src = pmc_traffic(args.config, 1, nb)
     result = {
         "metric": "stitched megapixels/sec (6x4K->8K equirect, FastMapper NV12)",
         "value": round(aggregate_mps(world, args.steps, W * H, elapsed), 1), "unit": "MP/s", "n_gpus": world,
@@ -480,11 +489,11 @@ def fast_rank(args, world, rank, local_rank, dist):
         "roofline": {"bound": "hbm", "achieved": round(b / kern_s / 1e9, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(b / kern_s / 1e9 / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": traffic_src,
                      "kernel": "fast_y_kernel + fast_uv_kernel", "kernel_us": round(kern_s * 1e6, 2),
-                     "kernel_us_basis": "torch events around 16 back-to-back stitch_nv12 on one stream",
+                     "kernel_us_basis": "torch events around 16 back-to-back frames (%d per launch) on one stream, per frame" % nb,
                      "bytes_per_launch": b,
                      "bytes_basis": "per (camera, 256-px run) entry block pixel 5 B (compact entry + weight; 8 B per "
-                                    "block header) or 8 B (wide planes), 1.5 B out per px, source bytes the weighted "
-                                    "taps reach (octvr_fastmapper_traffic)",
+                                    "block header) or 8 B (wide planes), read once per launch of %d frames; 1.5 B out "
+                                    "per px, source bytes the weighted taps reach (octvr_fastmapper_traffic_parts)" % nb,
                      "frac_at_step_time": round(b / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
                      "frac_traffic": round(traffic / kern_s / 1e9 / HBM_PEAK_GBPS, 4) if traffic else None},
     }
@@ -601,7 +610,8 @@ def gpu_rank(args, world, rank, local_rank, dist):
     gains = m.gains()
     frame_px = W * H
     value = aggregate_mps(world, args.steps, frame_px, elapsed)
-    bytes_per_launch = m.traffic_bytes()
+    lut_b, frame_b = m.traffic_parts()
+    bytes_per_launch = lut_b / nb + frame_b  # per frame: the tiled LUT is read once per launch of nb frames
     avg_kernel_s = kern_ms / 1e3 / max(launches, 1)
     achieved = bytes_per_launch / avg_kernel_s / 1e9
     n_valid = 0
@@ -615,7 +625,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # HBM traffic of the dominant kernel(s) from the committed PMC summary of THIS binary and config
     # (scripts/pmc.sh + scripts/pmc_summary.py record the sha256 of the profiled liboctvr_hip.so;
     # rocprofv3 cannot wrap the process that reads the counters)
-    traffic, traffic_src = pmc_traffic(args.config, blend)
+    traffic, traffic_src = pmc_traffic(args.config, blend, nb)
     ncam = len(sizes)
     result = {
         "metric": "stitched megapixels/sec (6x4K->8K equirect)" if args.config in ("C2", "C3") else
@@ -651,8 +661,10 @@ def gpu_rank(args, world, rank, local_rank, dist):
                                         "HIP-event start-to-end, every 4th launch",
                      "kernel_us_span": round(span_ms / 1e3 / max(launches, 1) * 1e6, 2),
                      "bytes_per_launch": bytes_per_launch,
-                     "bytes_basis": "algorithmic: what each launch must move, each byte once (DESIGN.md §4; "
-                                    "octvr_mapper_traffic)" + ("; per launch of the sequence in bytes_parts" if blend > 0 else ""),
+                     "bytes_basis": ("algorithmic: what each launch must move, each byte once (DESIGN.md §4; "
+                                     "octvr_mapper_traffic_parts), per frame") + (
+                                        "; the tiled LUT (%.1f MB) once per launch of %d frames" % (lut_b / 1e6, nb)
+                                        if nb > 1 else "") + ("; per launch of the sequence in bytes_parts" if blend > 0 else ""),
                      **({"bytes_parts": m.info().get("traffic_parts")} if blend > 0 else {}),
                      "frac_at_step_time": round(bytes_per_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS, 4),
                      # the counter-based fraction: PMC HBM bytes of the same binary over the same kernel time

@@ -194,6 +194,10 @@ int octvr_mapper_set_frames_in_flight(octvr_mapper* mapper, int k);
  * LUT entry (8 B in wide tiles) + 1.5 B YUV420 out per output pixel + 1.5 B per input pixel (each
  * source frame read once) + the per-item headers (multi-band / feather: the whole blend sequence). */
 int octvr_mapper_traffic(const octvr_mapper* mapper, double* bytes_per_frame);
+/* The same split into the rig constants the composite reads once per launch (tiled-LUT entries, item headers,
+ * wide-tile entries: read once for a whole frame batch, octvr_mapper_stitch_batch) and the per-frame bytes
+ * (output, source); lut + frame = octvr_mapper_traffic.  Multi-band / feather: lut 0. */
+int octvr_mapper_traffic_parts(const octvr_mapper* mapper, double* lut_bytes, double* frame_bytes);
 /* Live per-kernel timing for roofline accounting: with enable = k > 0, every k-th stitch brackets
  * its main (composite) kernel with HIP events on the caller's stream (0 = off).  kernel_time
  * synchronizes on the recorded events, returns the summed device time and launch count, and resets
@@ -308,6 +312,8 @@ int octvr_fastmapper_stitch_nv12(octvr_fastmapper* fastmapper, const uint8_t* co
 int octvr_fastmapper_stitch_nv12_batch(octvr_fastmapper* fastmapper, int n_frames, const uint8_t* const* in_dev,
                                        const size_t* in_pitch, uint8_t* const* out_dev, size_t out_pitch, void* stream);
 int octvr_fastmapper_traffic(const octvr_fastmapper* fastmapper, double* bytes);
+/* The same split into entries / weights / block headers (once per launch) and per-frame bytes (taps, output). */
+int octvr_fastmapper_traffic_parts(const octvr_fastmapper* fastmapper, double* lut_bytes, double* frame_bytes);
 void octvr_fastmapper_destroy(octvr_fastmapper* fastmapper);
 
 /* ---- standalone kernels --------------------------------------------------------------------- */

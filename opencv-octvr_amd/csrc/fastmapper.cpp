@@ -62,13 +62,14 @@ struct FastPlan {
     std::vector<int> in_w, in_h;
     FastPlaneHost y, uv;
     double bytes = 0;  // algorithmic bytes per stitch (octvr_fastmapper_traffic)
+    double lut_bytes = 0;  // of which the entries, weights and block headers (read once per launch)
 };
 
 struct octvr_fastmapper {
     int device = 0, n = 0, W = 0, H = 0;
     std::vector<int> in_w, in_h;
     FastPlaneDev y, uv;
-    double bytes = 0;
+    double bytes = 0, lut_bytes = 0;
     size_t blocks = 0;  // 256-entry (camera, run) blocks, Y + UV
 };
 
@@ -271,7 +272,8 @@ static FastPlan fast_plan(const octvr_rig* rig, int n_inputs, const int* in_w, c
     // entry), 1.5 B per output pixel written, and the source bytes the weighted taps reach (each once:
     // luma pixels 1 B, interleaved chroma pairs 2 B)
     auto ent_bytes = [](bool compact, size_t blocks) { return compact ? (5.0 * 256 + 8.0) * blocks : 8.0 * 256 * blocks; };
-    P.bytes = ent_bytes(P.y.compact, by) + ent_bytes(P.uv.compact, buv) + 1.5 * (double)npx;
+    P.lut_bytes = ent_bytes(P.y.compact, by) + ent_bytes(P.uv.compact, buv);
+    P.bytes = P.lut_bytes + 1.5 * (double)npx;
     for (int i = 0; i < n; i++) {
         const int w = in_w[i], h = in_h[i];
         std::vector<uint8_t> ty((size_t)w * h, 0), tuv((size_t)(w / 2) * (h / 2), 0);
@@ -494,6 +496,7 @@ int octvr_fastmapper_create(const octvr_rig* rig, int device, int n_inputs, cons
         fm->in_w = P.in_w;
         fm->in_h = P.in_h;
         fm->bytes = P.bytes;
+        fm->lut_bytes = P.lut_bytes;
         fm->blocks = P.y.nblk + P.uv.nblk;
         DeviceGuard dg(device);
         auto upload = [](FastPlaneDev& d, const FastPlaneHost& h) {
@@ -563,6 +566,16 @@ int octvr_fastmapper_traffic(const octvr_fastmapper* fm, double* bytes) {
         return OCTVR_E_INVALID;
     }
     *bytes = fm->bytes;
+    return OCTVR_OK;
+}
+
+int octvr_fastmapper_traffic_parts(const octvr_fastmapper* fm, double* lut_bytes, double* frame_bytes) {
+    if (!fm || !lut_bytes || !frame_bytes) {
+        set_last_error("NULL argument");
+        return OCTVR_E_INVALID;
+    }
+    *lut_bytes = fm->lut_bytes;
+    *frame_bytes = fm->bytes - fm->lut_bytes;
     return OCTVR_OK;
 }
 

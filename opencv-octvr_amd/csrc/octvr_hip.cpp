@@ -1837,6 +1837,23 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
     });
 }
 
+int octvr_mapper_traffic_parts(const octvr_mapper* m, double* lut_bytes, double* frame_bytes) {
+    return guarded([&] {
+        REQUIRE(m && lut_bytes && frame_bytes, "NULL argument");
+        double total = 0;
+        REQUIRE(octvr_mapper_traffic(m, &total) == OCTVR_OK, "traffic");
+        if (m->mb) {  // no batched kernels: everything is per frame
+            *lut_bytes = 0;
+            *frame_bytes = total;
+            return;
+        }
+        const TiledLut& t = m->tiles.view;
+        *lut_bytes = 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx +
+                     (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide;
+        *frame_bytes = total - *lut_bytes;
+    });
+}
+
 int octvr_mapper_set_timing(octvr_mapper* m, int enable) {
     return guarded([&] {
         REQUIRE(m && enable >= 0, "bad arguments");

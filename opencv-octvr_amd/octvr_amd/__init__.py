@@ -125,6 +125,8 @@ _lib.octvr_fastmapper_create.argtypes = [_VP, C.c_int, C.c_int, C.POINTER(C.c_in
 _lib.octvr_fastmapper_stitch_nv12.argtypes = [_VP, C.POINTER(_VP), C.POINTER(C.c_size_t), _VP, C.c_size_t, _VP]
 _lib.octvr_fastmapper_stitch_nv12_batch.argtypes = [_VP, C.c_int, C.POINTER(_VP), C.POINTER(C.c_size_t),
                                                     C.POINTER(_VP), C.c_size_t, _VP]
+_lib.octvr_fastmapper_traffic_parts.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+_lib.octvr_mapper_traffic_parts.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double)]
 _lib.octvr_fastmapper_destroy.argtypes = [_VP]
 _lib.octvr_fastmapper_destroy.restype = None
 # self-test hooks (absent from older builds that OCTVR_HIP_LIB may select for an A/B)
@@ -489,6 +491,12 @@ class Mapper:
         _check(_lib.octvr_mapper_traffic(self._h, C.byref(b)))
         return b.value
 
+    def traffic_parts(self):
+        """(lut bytes read once per launch, bytes per frame) of the composite (octvr_mapper_traffic_parts)."""
+        a, b = C.c_double(), C.c_double()
+        _check(_lib.octvr_mapper_traffic_parts(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def info(self):
         buf = C.create_string_buffer(8192)
         _check(_lib.octvr_mapper_info(self._h, buf, 8192))
@@ -550,6 +558,12 @@ class FastMapper:
             pitches = (C.c_size_t * n)(*[t.stride(0) for t in inputs])
         _check(_lib.octvr_fastmapper_stitch_nv12(self._h, ptrs, pitches, C.c_void_p(output.data_ptr()), output.stride(0),
                                                  _stream_ptr(stream)))
+
+    def traffic_parts(self):
+        """(entry bytes read once per launch, bytes per frame) of one stitch (octvr_fastmapper_traffic_parts)."""
+        a, b = C.c_double(), C.c_double()
+        _check(_lib.octvr_fastmapper_traffic_parts(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
 
     def stitch_nv12_batch(self, frame_sets, outputs=None, stream=None):
         """len(frame_sets) (1, 2 or 4) frames in one launch per plane (octvr_fastmapper_stitch_nv12_batch); outputs:

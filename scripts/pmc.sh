@@ -24,6 +24,7 @@ BATCH=${BATCH:-1}
 D=pmc_${CFG}_if${INFLIGHT}${BATCH_TAG}
 sha256sum opencv-octvr_amd/lib/liboctvr_hip.so | cut -d' ' -f1 > gpurun_out/${D}_so.sha
 echo "$STEPS" > gpurun_out/${D}_frames
+echo "$BATCH" > gpurun_out/${D}_batch
 for p in $PASSES; do
   timeout -s KILL 120 rocprofv3 --pmc ${P[$p]} --kernel-include-regex "$RE" -d gpurun_out/${D}_$p -o run --output-format csv -- \
     python3 bench.py --config $CFG --pmc-child --steps $((STEPS * BATCH)) --inflight $INFLIGHT --batch $BATCH > gpurun_out/${D}_$p.log 2>&1 \

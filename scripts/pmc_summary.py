@@ -37,7 +37,9 @@ def main():
     d = "pmc_%s_if%s" % (cfg, inflight)
     sha = open(os.path.join(g, d + "_so.sha")).read().strip()
     frames = int(open(os.path.join(g, d + "_frames")).read().strip())
-    out = {"config": cfg, "frames_in_flight": int(inflight), "so_sha256": sha, "frames": frames,
+    bpath = os.path.join(g, d + "_batch")
+    batch = int(open(bpath).read().strip()) if os.path.exists(bpath) else 1
+    out = {"config": cfg, "frames_in_flight": int(inflight), "frames_per_launch": batch, "so_sha256": sha, "frames": frames,
            "method": "rocprofv3 --pmc, one pass per counter set (scripts/pmc.sh), bench.py --pmc-child --steps %d "
                      "--inflight %s; traffic = 2 x FETCH_SIZE (gfx950 half count of 16 B/lane reads) + WRITE_SIZE, "
                      "KiB -> bytes; keys: kernel@grid size" % (frames, inflight)}
