@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Copy one evidence session's results (scripts/r4_final.sh, TAG=<tag>) from gpurun_out/ into profiles/:
+"""Copy one evidence session's results (scripts/evidence.sh, TAG=<tag>) from gpurun_out/ into profiles/:
 bench lines, rocprofv3 kernel stats per config / frames in flight, the last frames of the C3 one-in-flight
 kernel trace, and the PMC summaries (scripts/pmc_summary.py).
     python scripts/collect_profiles.py r04d
@@ -33,15 +33,15 @@ def main():
     for d in sorted(glob.glob(os.path.join(G, "kt_%s_*_if*" % tag))):
         if not os.path.isdir(d):
             continue
-        cfg, inf = os.path.basename(d)[len(tag) + 4:].split("_if")
+        cfg, inf = os.path.basename(d)[len(tag) + 4:].split("_if")  # inf: "<streams>b<frames per launch>"
         st = os.path.join(d, "run_kernel_stats.csv")
         # --stats averages are per-kernel durations only with one frame in flight: with several, launches
         # on different streams overlap and a launch's span exceeds the step time (the trace union,
         # scripts/union_check.py, is that run's evidence instead)
-        if os.path.exists(st) and inf == "1":
+        if os.path.exists(st) and inf.startswith("1b"):
             shutil.copy(st, os.path.join(P, "%s_%s_inflight%s_kernel_stats.csv" % (tag, cfg, inf)))
         tr = os.path.join(d, "run_kernel_trace.csv")
-        if cfg == "C3" and inf == "1" and os.path.exists(tr):
+        if cfg == "C3" and inf == "1b1" and os.path.exists(tr):
             rows = [r for r in csv.DictReader(open(tr)) if "octvr" in r["Kernel_Name"]]
             rows.sort(key=lambda r: int(r["Start_Timestamp"]))
             rows = rows[-90:]

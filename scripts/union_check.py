@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Recompute a bench line's roofline from the rocprofv3 kernel trace of the same run (scripts/r5_final.sh
+"""Recompute a bench line's roofline from the rocprofv3 kernel trace of the same run (scripts/evidence.sh
 kt_<tag>_<cfg>_if<k>: `rocprofv3 --kernel-trace --stats -- python3 bench.py ...`, whose log ends with the
 bench line).  The timed region is bench.py's launches [skip, skip + count) of the anchor kernel (one per
 frame: one setup stitch per frame set, then the warmup, then the timed steps); the union of the intervals
@@ -24,7 +24,10 @@ def main():
     # the untimed preroll's steps (bench.py --preroll) come after the setup and warmup launches
     pre = bl.get("preroll", {}).get("steps", 0)
     skip = (int(sys.argv[4]) if len(sys.argv) > 4 else 13) + pre
-    count = int(sys.argv[5]) if len(sys.argv) > 5 else bl["steps"]
+    # frames per launch (octvr_mapper_stitch_batch): the anchor launches and the preroll's steps are calls,
+    # each of nb frames
+    nb = bl["config"].get("frames_per_launch", 1)
+    count = int(sys.argv[5]) if len(sys.argv) > 5 else bl["steps"] // nb
     rows = list(csv.DictReader(open(os.path.join(d, "run_kernel_trace.csv"))))
     iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
     anchors = [a for a, b, n in iv if anchor.search(n)]
@@ -43,8 +46,9 @@ def main():
         union += cb - ca
     b = bl
     r = b["roofline"]
-    u_us = union / count / 1e3
-    out = {"trace": os.path.basename(d), "pattern": sys.argv[2], "anchor": sys.argv[3], "frames": count,
+    u_us = union / (count * nb) / 1e3
+    out = {"trace": os.path.basename(d), "pattern": sys.argv[2], "anchor": sys.argv[3], "frames": count * nb,
+           "frames_per_launch": nb,
            "skip_first": skip, "preroll_steps": pre, "launches": len(sel), "union_us_per_frame": round(u_us, 2),
            "line_kernel_us": r["kernel_us"], "line_kernel_us_basis": r.get("kernel_us_basis"),
            "bytes_per_launch": r["bytes_per_launch"], "line_frac": r["frac"],
