@@ -1219,9 +1219,6 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
     uint32_t pfr = 0;            // the previous unit's frame (MODE 0 output)
     bool pin = false;
     uint32_t par = 0;  // iteration parity
-#ifdef OCTVR_PF_ENT
-    uint32_t pf_sink = 0;
-#endif
     while (cur.t < t_end) {
         const int x = (int)(cur.tile & 0xFFFFu) * kTileW + qx * 2, y = (int)(cur.tile >> 16) * kItemH + qy * 2;
         const uint32_t S = cur.stride & ((1u << kStrideBits) - 1u);
@@ -1287,15 +1284,6 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
         data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, lg, stage_slot<true>(nxt, t_end, wave), mg, d);
         mv = meta_issue(mrsrc, t_n2, t_end, lg);
         mg = group_issue(grsrc, t_n2, t_end, lg);
-#ifdef OCTVR_PF_ENT
-        {  // L2 prefetch of the item after next's entries: one dword per 128-B line (16 lanes per wave)
-            const int tp = (t_n2 < t_end ? t_n2 : 0) >> lg;
-            const uint32_t l = (uint32_t)tid & 63u;
-            const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(
-                ersrc, ((uint32_t)wave * 16u + (l & 15u)) * 128u, (uint32_t)uniform(tp) * (uint32_t)(kItemHalves * kTilePx * 4), 0);
-            pf_sink ^= v;
-        }
-#endif
         t_mv = t_n2;
         claimed = t_n2 < t_end;  // claim the item after it (only while the sequence is live)
         if (claimed && tid == 0) {
@@ -1344,9 +1332,6 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
         par ^= 1u;
         cur = nxt;
     }
-#ifdef OCTVR_PF_ENT
-    if (pf_sink == 0x9E3779B9u && tid == 1023) s_rgb[0] = pf_sink;  // never true (keeps the prefetches)
-#endif
     // the last workgroup to finish resets the work counters for the next launch (stream order makes
     // the reset visible to it); every claim of this workgroup has returned before its ticket
     if (tid == 0) {
