@@ -451,7 +451,7 @@ def fast_rank(args, world, rank, local_rank, dist):
             fm.stitch_nv12_batch(brefs[k % ncalls], stream=raw_streams[k % inflight])
 
     if args.pmc_child:
-        for k in range(max(args.steps, 1)):
+        for k in range(max(args.steps // nb, 1)):  # calls of nb frames
             step(k)
         torch.cuda.synchronize(dev)
         sys.exit(0)
@@ -558,7 +558,7 @@ def gpu_rank(args, world, rank, local_rank, dist):
             m.stitch_batch(brefs[k % ncalls], stream=raw_streams[j])
 
     if args.pmc_child:  # a few launches for rocprofv3 --pmc passes
-        for k in range(max(args.steps, 1)):
+        for k in range(max(args.steps // nb, 1)):  # calls of nb frames
             step(k)
         torch.cuda.synchronize(dev)
         sys.exit(0)

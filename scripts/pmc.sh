@@ -23,7 +23,7 @@ P[TCC]="TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE"
 BATCH=${BATCH:-1}
 D=pmc_${CFG}_if${INFLIGHT}${BATCH_TAG}
 sha256sum opencv-octvr_amd/lib/liboctvr_hip.so | cut -d' ' -f1 > gpurun_out/${D}_so.sha
-echo "$STEPS" > gpurun_out/${D}_frames
+echo "$STEPS" > gpurun_out/${D}_frames  # calls of $BATCH frames
 echo "$BATCH" > gpurun_out/${D}_batch
 for p in $PASSES; do
   timeout -s KILL 120 rocprofv3 --pmc ${P[$p]} --kernel-include-regex "$RE" -d gpurun_out/${D}_$p -o run --output-format csv -- \

@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 --pmc passes of scripts/pmc.sh into profiles/<tag>_pmc_<cfg>[_if<k>].json.
+"""Summarise the rocprofv3 --pmc passes of scripts/pmc.sh into profiles/<tag>_pmc_<cfg>.json (the streams and
+frames per launch of the run inside: rocprofv3 --pmc serialises the dispatches, so one summary per config).
 
 Per kernel and grid size (the multi-band sequence launches mb_down / mb_blend once per level, with a
 different grid each) and per counter: launches, median and total.  HBM traffic per the MI355X guide's
@@ -60,7 +61,7 @@ def main():
                 per_frame += (2.0 * sum(cs["FETCH_SIZE"]) + sum(cs.get("WRITE_SIZE", [0.0]))) * 1024.0
     if traffic:
         out["traffic_bytes"] = traffic  # per launch, per kernel@grid
-        out["traffic_per_frame_bytes"] = per_frame / frames
+        out["traffic_per_frame_bytes"] = per_frame / (frames * batch)
     sq = {}
     for k, cs in counters.items():
         if "SQ_INSTS_VALU" in cs or "SQ_WAVES" in cs:
@@ -76,7 +77,7 @@ def main():
             sq[k] = s
     if sq:
         out["sq_summary"] = sq
-    suffix = "" if inflight == "3" else "_if%s" % inflight
+    suffix = ""
     dst = os.path.join(ROOT, "profiles", "%s_pmc_%s%s.json" % (tag, cfg, suffix))
     json.dump(out, open(dst, "w"), indent=1)
     print(dst, json.dumps({"traffic": traffic, "per_frame": out.get("traffic_per_frame_bytes")}))
