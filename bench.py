@@ -171,7 +171,7 @@ def pmc_traffic(config, blend, nb=1):
         if blend > 0:
             seq = [v for k, v in d.get("traffic_bytes", {}).items() if "gain_feed" not in k]
             if seq:
-                return round(sum(seq)), os.path.basename(path)
+                return round(sum(seq) / nb), os.path.basename(path)
             continue
         hit = [v for k, v in d.get("traffic_bytes", {}).items() if "stitch_tiled_kernel" in k]
         if hit:
