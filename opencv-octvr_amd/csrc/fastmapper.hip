@@ -80,8 +80,7 @@ constexpr uint32_t kFastInterior = 1u;
 // The frames of one launch (FastBatch, the FIRST kernel argument): camera c of frame f at src[fbase + c],
 // fbase = f << cam_log2; read through the kernarg segment with the camera uniform (scalar loads).
 typedef __attribute__((address_space(4))) const SourceFrame kFastSource;
-typedef __attribute__((address_space(4))) const FastBatch kFastBatch;
-static_assert(offsetof(FastBatch, src) == 0, "FastBatch layout");
+static_assert(offsetof(FastBatch<1>, src) == 0 && offsetof(FastBatch<4>, src) == 0, "FastBatch layout");
 __device__ __forceinline__ SourceFrame fast_frame(uint32_t idx) {
     const kFastSource* kf = (const kFastSource*)__builtin_amdgcn_kernarg_segment_ptr();
     SourceFrame s;
@@ -243,6 +242,7 @@ __device__ __forceinline__ void fast_plane(const FastPlane& fp, int W, int H, in
         x -= (uint32_t)pw;
         y++;
     }
+    typedef __attribute__((address_space(4))) const FastBatch<NF> kFastBatch;
     const kFastBatch* kb = (const kFastBatch*)__builtin_amdgcn_kernarg_segment_ptr();
 #pragma unroll
     for (int f = 0; f < NF; f++) {
@@ -260,19 +260,19 @@ __device__ __forceinline__ void fast_plane(const FastPlane& fp, int W, int H, in
 // runs[r] = {camera mask, first block}: run r's cameras (ascending) own blocks first, first + 1, ... of
 // 256 entries (fastmapper.cpp)
 template <bool COMPACT, int LG>
-__global__ void __launch_bounds__(256) fast_y_kernel(FastBatch batch, FastPlane fp, int W, int H, int64_t out_pitch) {
+__global__ void __launch_bounds__(256) fast_y_kernel(FastBatch<1 << LG> batch, FastPlane fp, int W, int H, int64_t out_pitch) {
     (void)batch;  // read through the kernarg segment (kFastBatch)
     fast_plane<0, COMPACT, LG>(fp, W, H, out_pitch);
 }
 
 template <bool COMPACT, int LG>
-__global__ void __launch_bounds__(256) fast_uv_kernel(FastBatch batch, FastPlane fp, int W, int H, int64_t out_pitch) {
+__global__ void __launch_bounds__(256) fast_uv_kernel(FastBatch<1 << LG> batch, FastPlane fp, int W, int H, int64_t out_pitch) {
     (void)batch;
     fast_plane<1, COMPACT, LG>(fp, W, H, out_pitch);
 }
 
 template <int PLANE, bool COMPACT, int LG>
-static void launch_plane_kernel(dim3 grid, const FastBatch& b, const FastPlane& fp, int W, int H, int64_t out_pitch,
+static void launch_plane_kernel(dim3 grid, const FastBatch<1 << LG>& b, const FastPlane& fp, int W, int H, int64_t out_pitch,
                                 hipStream_t s) {
     if (PLANE)
         hipLaunchKernelGGL((fast_uv_kernel<COMPACT, LG>), grid, dim3(256), 0, s, b, fp, W, H, out_pitch);
@@ -280,28 +280,33 @@ static void launch_plane_kernel(dim3 grid, const FastBatch& b, const FastPlane& 
         hipLaunchKernelGGL((fast_y_kernel<COMPACT, LG>), grid, dim3(256), 0, s, b, fp, W, H, out_pitch);
 }
 
-template <int PLANE, bool COMPACT>
-static void launch_plane_lg(int lg, dim3 grid, const FastBatch& b, const FastPlane& fp, int W, int H, int64_t out_pitch,
-                            hipStream_t s) {
-    if (lg == 2)
-        launch_plane_kernel<PLANE, COMPACT, 2>(grid, b, fp, W, H, out_pitch, s);
-    else if (lg == 1)
-        launch_plane_kernel<PLANE, COMPACT, 1>(grid, b, fp, W, H, out_pitch, s);
-    else
-        launch_plane_kernel<PLANE, COMPACT, 0>(grid, b, fp, W, H, out_pitch, s);
-}
-
-template <int PLANE>
-static hipError_t launch_plane(int lg, const FastBatch& b, const FastMapperPlane& p, int W, int H, int64_t out_pitch,
+template <int PLANE, int LG>
+static hipError_t launch_plane(const FastBatch<1 << LG>& b, const FastMapperPlane& p, int W, int H, int64_t out_pitch,
                                hipStream_t s) {
     const int64_t n = PLANE ? (int64_t)(W / 2) * (H / 2) : (int64_t)W * H;
     const dim3 grid((unsigned)((n + 255) / 256));
     const FastPlane fp{p.ent, p.off, p.wgt, p.hdr, p.runs, p.nblk};
     if (p.compact)
-        launch_plane_lg<PLANE, true>(lg, grid, b, fp, W, H, out_pitch, s);
+        launch_plane_kernel<PLANE, true, LG>(grid, b, fp, W, H, out_pitch, s);
     else
-        launch_plane_lg<PLANE, false>(lg, grid, b, fp, W, H, out_pitch, s);
+        launch_plane_kernel<PLANE, false, LG>(grid, b, fp, W, H, out_pitch, s);
     return hipGetLastError();
+}
+
+// both planes of 1 << LG frames, the frames as the kernels' kernarg table (FastBatch<1 << LG>)
+template <int LG>
+static hipError_t launch_nv12(const FrameSet* frames, const FastMapperPlane& y, const FastMapperPlane& uv, int W, int H,
+                              uint8_t* const* out, int64_t out_pitch, hipStream_t s) {
+    constexpr int cam_lg = LG <= 1 ? 5 : 4;
+    FastBatch<1 << LG> b;
+    memset(&b, 0, sizeof b);
+    for (int f = 0; f < (1 << LG); f++) {
+        for (int i = 0; i < (1 << cam_lg); i++) b.src[(f << cam_lg) + i] = frames[f].f[i];
+        b.out[f] = out[f];
+    }
+    const hipError_t e = launch_plane<0, LG>(b, y, W, H, out_pitch, s);
+    if (e != hipSuccess) return e;
+    return launch_plane<1, LG>(b, uv, W, H, out_pitch, s);
 }
 
 hipError_t launch_fastmapper_nv12_batch(const FrameSet* frames, int nf, const FastMapperPlane& y,
@@ -310,21 +315,12 @@ hipError_t launch_fastmapper_nv12_batch(const FrameSet* frames, int nf, const Fa
     const int lg = nf == 1 ? 0 : nf == 2 ? 1 : nf == 4 ? 2 : -1;
     if (lg < 0) return hipErrorInvalidValue;
     const int cam_lg = lg <= 1 ? 5 : 4;
-    FastBatch b;
-    memset(&b, 0, sizeof b);
-    for (int f = 0; f < nf; f++) {
-        for (int i = 0; i < kMaxCams; i++) {
-            if (i >= (1 << cam_lg)) {
-                if (frames[f].f[i].yuv) return hipErrorInvalidValue;  // more cameras than a 4-frame batch holds
-                continue;
-            }
-            b.src[(f << cam_lg) + i] = frames[f].f[i];
-        }
-        b.out[f] = out[f];
-    }
-    const hipError_t e = launch_plane<0>(lg, b, y, W, H, out_pitch, s);
-    if (e != hipSuccess) return e;
-    return launch_plane<1>(lg, b, uv, W, H, out_pitch, s);
+    for (int f = 0; f < nf; f++)
+        for (int i = 1 << cam_lg; i < kMaxCams; i++)
+            if (frames[f].f[i].yuv) return hipErrorInvalidValue;  // more cameras than a 4-frame batch holds
+    if (lg == 2) return launch_nv12<2>(frames, y, uv, W, H, out, out_pitch, s);
+    if (lg == 1) return launch_nv12<1>(frames, y, uv, W, H, out, out_pitch, s);
+    return launch_nv12<0>(frames, y, uv, W, H, out, out_pitch, s);
 }
 
 hipError_t launch_fastmapper_nv12(const FrameSet& frames, const FastMapperPlane& y, const FastMapperPlane& uv, int W,

@@ -466,12 +466,12 @@ __device__ __forceinline__ void sample_rgb(const Taps& t, int tex, uint32_t (&rg
 
 // The feed's FIRST argument (FeedBatch): camera c of frame f read from the kernarg segment (scalar loads)
 typedef __attribute__((address_space(4))) const SourceFrame kSourceFrame;
-typedef __attribute__((address_space(4))) const FeedBatch kFeedBatch;
-static_assert(offsetof(FeedBatch, src) == 0, "FeedBatch layout");
+static_assert(offsetof(FeedBatch<1>, src) == 0 && offsetof(FeedBatch<4>, src) == 0, "FeedBatch layout");
 
-template <bool LEAN>
+template <bool LEAN, int NF>
 __device__ __forceinline__ void gain_feed_body(const CompositeEntry* samples, const uint16_t* partners, int tex,
                                                int n_chunks, const int32_t* N, int n) {
+    typedef __attribute__((address_space(4))) const FeedBatch<NF> kFeedBatch;
     __shared__ int s_last;
     __shared__ double s_I[kGainMaxCams * kGainMaxCams];
     __shared__ double s_A[kGainMaxCams * kGainMaxCams];
@@ -654,37 +654,53 @@ __device__ __forceinline__ void gain_feed_body(const CompositeEntry* samples, co
     if (tid < n) gains[tid] = ok ? s_x[tid] : 1.0;  // cv::solve failure leaves gains_ unspecified; 1 as the oracle
 }
 
-__global__ void __launch_bounds__(256) gain_feed_kernel(FeedBatch batch, const CompositeEntry* samples,
+template <int NF>
+__global__ void __launch_bounds__(256) gain_feed_kernel(FeedBatch<NF> batch, const CompositeEntry* samples,
                                                         const uint16_t* partners, int tex, int n_chunks, const int32_t* N,
                                                         int n) {
     (void)batch;  // read through the kernarg segment (kFeedBatch)
-    gain_feed_body<false>(samples, partners, tex, n_chunks, N, n);
+    gain_feed_body<false, NF>(samples, partners, tex, n_chunks, N, n);
 }
+template <int NF>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_num_vgpr(80)))
-gain_feed_lean_kernel(FeedBatch batch, const CompositeEntry* samples, const uint16_t* partners, int tex, int n_chunks,
+gain_feed_lean_kernel(FeedBatch<NF> batch, const CompositeEntry* samples, const uint16_t* partners, int tex, int n_chunks,
                       const int32_t* N, int n) {
     (void)batch;
-    gain_feed_body<true>(samples, partners, tex, n_chunks, N, n);
+    gain_feed_body<true, NF>(samples, partners, tex, n_chunks, N, n);
 }
 
-hipError_t launch_gain_feed_batch(const FrameSet* frames, int nf, const CompositeEntry* samples, const uint16_t* partners,
-                                  int tex, int n_chunks, const int32_t* N, int n, unsigned long long* const* totals,
-                                  uint32_t* const* tickets, double* const* gains, hipStream_t s, bool lean) {
-    if (n_chunks <= 0 || n > kGainMaxCams || nf < 1 || nf > kMaxBatch) return hipErrorInvalidValue;
-    FeedBatch fb;
+template <int NF>
+static void launch_feed_nf(const FrameSet* frames, const CompositeEntry* samples, const uint16_t* partners, int tex,
+                           int n_chunks, const int32_t* N, int n, unsigned long long* const* totals,
+                           uint32_t* const* tickets, double* const* gains, hipStream_t s, bool lean) {
+    FeedBatch<NF> fb;
     memset(&fb, 0, sizeof fb);
-    for (int f = 0; f < nf; f++) {
+    for (int f = 0; f < NF; f++) {
         for (int i = 0; i < kGainMaxCams; i++) fb.src[f * kGainMaxCams + i] = frames[f].f[i];
         fb.totals[f] = totals[f];
         fb.tickets[f] = tickets[f];
         fb.gains[f] = gains[f];
     }
     if (lean)
-        hipLaunchKernelGGL(gain_feed_lean_kernel, dim3(n_chunks * nf), dim3(256), 0, s, fb, samples, partners, tex,
+        hipLaunchKernelGGL(gain_feed_lean_kernel<NF>, dim3(n_chunks * NF), dim3(256), 0, s, fb, samples, partners, tex,
                            n_chunks, N, n);
     else
-        hipLaunchKernelGGL(gain_feed_kernel, dim3(n_chunks * nf), dim3(256), 0, s, fb, samples, partners, tex, n_chunks,
-                           N, n);
+        hipLaunchKernelGGL(gain_feed_kernel<NF>, dim3(n_chunks * NF), dim3(256), 0, s, fb, samples, partners, tex,
+                           n_chunks, N, n);
+}
+
+hipError_t launch_gain_feed_batch(const FrameSet* frames, int nf, const CompositeEntry* samples, const uint16_t* partners,
+                                  int tex, int n_chunks, const int32_t* N, int n, unsigned long long* const* totals,
+                                  uint32_t* const* tickets, double* const* gains, hipStream_t s, bool lean) {
+    if (n_chunks <= 0 || n > kGainMaxCams) return hipErrorInvalidValue;
+    if (nf == 1)
+        launch_feed_nf<1>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains, s, lean);
+    else if (nf == 2)
+        launch_feed_nf<2>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains, s, lean);
+    else if (nf == 4)
+        launch_feed_nf<4>(frames, samples, partners, tex, n_chunks, N, n, totals, tickets, gains, s, lean);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
@@ -752,8 +768,7 @@ static_assert(sizeof(TileSlot) == 16, "TileSlot layout");
 // segment directly (a wave-uniform index gives scalar loads; indexing the by-value parameter would
 // copy it to scratch).  idx = (frame << cam_log2) + camera (kernels.hpp FrameBatch).
 typedef __attribute__((address_space(4))) const SourceFrame kSourceFrame;
-typedef __attribute__((address_space(4))) const FrameBatch kFrameBatch;
-static_assert(offsetof(FrameBatch, src) == 0, "FrameBatch layout");
+static_assert(offsetof(FrameBatch<1>, src) == 0 && offsetof(FrameBatch<4>, src) == 0, "FrameBatch layout");
 __device__ __forceinline__ SourceFrame kernarg_frame(uint32_t idx) {
     const kSourceFrame* kf = (const kSourceFrame*)__builtin_amdgcn_kernarg_segment_ptr();
     SourceFrame s;
@@ -764,10 +779,14 @@ __device__ __forceinline__ SourceFrame kernarg_frame(uint32_t idx) {
     s.vig = kf[idx].vig;
     return s;
 }
+template <int NF>
 __device__ __forceinline__ uint8_t* kernarg_out(uint32_t f) {
+    typedef __attribute__((address_space(4))) const FrameBatch<NF> kFrameBatch;
     return ((const kFrameBatch*)__builtin_amdgcn_kernarg_segment_ptr())->out[f];
 }
+template <int NF>
 __device__ __forceinline__ const double* kernarg_gains(uint32_t f) {
+    typedef __attribute__((address_space(4))) const FrameBatch<NF> kFrameBatch;
     return ((const kFrameBatch*)__builtin_amdgcn_kernarg_segment_ptr())->gains[f];
 }
 
@@ -1122,7 +1141,7 @@ __device__ __forceinline__ uint32_t tap_off(uint32_t e) { return (e >> 13) & 0x3
 // the weight table.
 // LG: 1 << LG frames per launch (FrameBatch; MODE 0 only)
 template <bool DWORD_STAGE, int MODE, bool VIG, bool TEX, int LG>
-__device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lut, int W, int H, int use_gain,
+__device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& frames, TiledLut lut, int W, int H, int use_gain,
                                                   int64_t out_pitch, RgbaOut rgba) {
     __shared__ StitchLds L;
     extern __shared__ __attribute__((aligned(16))) uint2 s_wtab[];  // 1,024 weight pairs at LDS 0x4000
@@ -1158,7 +1177,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
     bool res_rgba = false;
     const int out_bytes = (int)((uint32_t)out_pitch * (uint32_t)(H + H / 2));
     if constexpr (MODE == 0) {
-        of = make_out_frame(kernarg_out(0), W, H, out_pitch);
+        of = make_out_frame(kernarg_out<1 << LG>(0), W, H, out_pitch);
     } else {
         ro = RgbaSink{__builtin_amdgcn_make_buffer_rsrc(rgba.base, 0, (int)rgba.bytes, 0x00020000), rgba.cams};
         of = make_result_frame(rgba);
@@ -1168,7 +1187,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
     const int qx = tid & 63, qy = tid >> 6;
 
     if (tid < (1 << (lg + cam_lg))) {
-        const double* gf = kernarg_gains((uint32_t)tid >> cam_lg);
+        const double* gf = kernarg_gains<1 << LG>((uint32_t)tid >> cam_lg);
         s_gain[tid] = use_gain ? (float)gf[tid & ((1 << cam_lg) - 1)] : 1.0f;
     }
     if (tid < kTileZeroDwords) s_rgb[tid] = 0u;
@@ -1264,7 +1283,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
             t_n2 = v < t_end ? v : t_end;
         }
         first = false;
-        if (MODE == 0 && lg) of.rsrc = __builtin_amdgcn_make_buffer_rsrc(kernarg_out(pfr), 0, out_bytes, 0x00020000);
+        if (MODE == 0 && lg) of.rsrc = __builtin_amdgcn_make_buffer_rsrc(kernarg_out<1 << LG>(pfr), 0, out_bytes, 0x00020000);
         if (MODE == 0 && pfull) {
 #pragma unroll
             for (int h = 0; h < kItemHalves; h++) {
@@ -1343,7 +1362,7 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
                 __hip_atomic_exchange(lut.queue + k * kQueueStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    if (MODE == 0 && lg) of.rsrc = __builtin_amdgcn_make_buffer_rsrc(kernarg_out(pfr), 0, out_bytes, 0x00020000);
+    if (MODE == 0 && lg) of.rsrc = __builtin_amdgcn_make_buffer_rsrc(kernarg_out<1 << LG>(pfr), 0, out_bytes, 0x00020000);
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++)
         store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
@@ -1351,13 +1370,13 @@ __device__ __forceinline__ void stitch_tiled_body(FrameBatch frames, TiledLut lu
 
 template <bool DWORD_STAGE, int MODE, bool VIG, int LG>
 __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
-__attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameBatch frames, TiledLut lut, int W, int H,
+__attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameBatch<1 << LG> frames, TiledLut lut, int W, int H,
                                                                    int use_gain, int64_t out_pitch, RgbaOut rgba) {
     stitch_tiled_body<DWORD_STAGE, MODE, VIG, false, LG>(frames, lut, W, H, use_gain, out_pitch, rgba);
 }
 template <bool DWORD_STAGE, int MODE, bool VIG, int LG>
 __global__ void __launch_bounds__(256, kStitchTexRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
-__attribute__((amdgpu_num_vgpr(kStitchTexVgprs))) stitch_tiled_tex_kernel(FrameBatch frames, TiledLut lut, int W,
+__attribute__((amdgpu_num_vgpr(kStitchTexVgprs))) stitch_tiled_tex_kernel(FrameBatch<1 << LG> frames, TiledLut lut, int W,
                                                                           int H, int use_gain, int64_t out_pitch,
                                                                           RgbaOut rgba) {
     stitch_tiled_body<DWORD_STAGE, MODE, VIG, true, LG>(frames, lut, W, H, use_gain, out_pitch, rgba);
@@ -1428,7 +1447,7 @@ static hipError_t stitch_lds_check() {
 constexpr uint32_t kStitchDynLds = kWtabBytes + 4u * 2u * kMaxCams;
 
 template <bool DW, int MODE, bool V, bool TEX, int LG>
-static hipError_t launch_tiled(int blocks, const FrameBatch& frames, const TiledLut& lut, int W, int H, int use_gain,
+static hipError_t launch_tiled(int blocks, const FrameBatch<1 << LG>& frames, const TiledLut& lut, int W, int H, int use_gain,
                                int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V, TEX, LG>();
     if (lds_ok != hipSuccess) return lds_ok;
@@ -1447,30 +1466,54 @@ static hipError_t launch_tiled(int blocks, const FrameBatch& frames, const Tiled
     return hipGetLastError();
 }
 
+// the frame sets as the kernel's kernarg table for 1 << LG frames
+template <int LG>
+static void frame_batch(const FrameSet* frames, const double* const* gains, uint8_t* const* out,
+                        FrameBatch<1 << LG>& fb) {
+    constexpr int cam_lg = FrameBatch<1 << LG>::kCamLog2;
+    memset(&fb, 0, sizeof fb);
+    for (int f = 0; f < (1 << LG); f++) {
+        for (int i = 0; i < (1 << cam_lg); i++) fb.src[(f << cam_lg) + i] = frames[f].f[i];
+        fb.out[f] = out ? out[f] : nullptr;
+        fb.gains[f] = gains[f];
+    }
+}
+
 template <bool DW, int MODE, bool V, bool TEX>
-static hipError_t launch_tiled_lg(int lg, int blocks, const FrameBatch& frames, const TiledLut& lut, int W, int H,
-                                  int use_gain, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0,
+static hipError_t launch_tiled_lg(int lg, int blocks, const FrameSet* frames, const double* const* gains,
+                                  uint8_t* const* out, const TiledLut& lut, int W, int H, int use_gain,
+                                  int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0,
                                   hipEvent_t ev1) {
     if constexpr (MODE == 0) {
-        if (lg == 1) return launch_tiled<DW, MODE, V, TEX, 1>(blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
-        if (lg == 2) return launch_tiled<DW, MODE, V, TEX, 2>(blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+        if (lg == 1) {
+            FrameBatch<2> fb;
+            frame_batch<1>(frames, gains, out, fb);
+            return launch_tiled<DW, MODE, V, TEX, 1>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+        }
+        if (lg == 2) {
+            FrameBatch<4> fb;
+            frame_batch<2>(frames, gains, out, fb);
+            return launch_tiled<DW, MODE, V, TEX, 2>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+        }
     }
     if (lg != 0) return hipErrorInvalidValue;
-    return launch_tiled<DW, MODE, V, TEX, 0>(blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+    FrameBatch<1> fb;
+    frame_batch<0>(frames, gains, out, fb);
+    return launch_tiled<DW, MODE, V, TEX, 0>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
 }
 
 // the instance for the frames' staging (dword loads, vignette) and the entries' convention
 template <int MODE, bool TEX>
-static hipError_t launch_tiled_for(bool dw, bool vig, int lg, int blocks, const FrameBatch& frames, const TiledLut& lut,
-                                   int W, int H, int use_gain, int64_t out_pitch, const RgbaOut& rgba, hipStream_t s,
-                                   hipEvent_t e0, hipEvent_t e1) {
+static hipError_t launch_tiled_for(bool dw, bool vig, int lg, int blocks, const FrameSet* fr, const double* const* g,
+                                   uint8_t* const* o, const TiledLut& lut, int W, int H, int use_gain, int64_t out_pitch,
+                                   const RgbaOut& rgba, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     if (dw && !vig)
-        return launch_tiled_lg<true, MODE, false, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+        return launch_tiled_lg<true, MODE, false, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
     if (dw)
-        return launch_tiled_lg<true, MODE, true, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+        return launch_tiled_lg<true, MODE, true, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
     if (!vig)
-        return launch_tiled_lg<false, MODE, false, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
-    return launch_tiled_lg<false, MODE, true, TEX>(lg, blocks, frames, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+        return launch_tiled_lg<false, MODE, false, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    return launch_tiled_lg<false, MODE, true, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
 }
 
 // nf frame sets (1, 2 or 4) in one launch of the tiled kernel (FrameBatch); wide tiles one launch per frame
@@ -1483,19 +1526,9 @@ static hipError_t launch_composite(const FrameSet* frames, int nf, const TiledLu
     const int lg = nf == 1 ? 0 : nf == 2 ? 1 : nf == 4 ? 2 : -1;
     if (lg < 0 || (MODE == 1 && nf != 1)) return hipErrorInvalidValue;
     const int cam_lg = nf <= 2 ? 5 : 4;
-    FrameBatch fb;
-    memset(&fb, 0, sizeof fb);
-    for (int f = 0; f < nf; f++) {
-        for (int i = 0; i < kMaxCams; i++) {
-            if (i >= (1 << cam_lg)) {
-                if (frames[f].f[i].yuv) return hipErrorInvalidValue;  // more cameras than a 4-frame batch holds
-                continue;
-            }
-            fb.src[(f << cam_lg) + i] = frames[f].f[i];
-        }
-        fb.out[f] = out ? out[f] : nullptr;
-        fb.gains[f] = gains[f];
-    }
+    for (int f = 0; f < nf; f++)
+        for (int i = 1 << cam_lg; i < kMaxCams; i++)
+            if (frames[f].f[i].yuv) return hipErrorInvalidValue;  // more cameras than a 4-frame batch holds
     // timing events: carried by the dispatch packet when the tiled kernel is the only launch (no marker
     // packets between the launches of the timed loop), else recorded around the launches
     const bool ext_ev = ev0 && lut.n_items > 0 && lut.n_wide == 0;
@@ -1523,8 +1556,10 @@ static hipError_t launch_composite(const FrameSet* frames, int nf, const TiledLu
             }
         hipEvent_t e0 = ext_ev ? ev0 : nullptr, e1 = ext_ev ? ev1 : nullptr;
         const hipError_t e =
-            lut.tex ? launch_tiled_for<MODE, true>(dw, vig, lg, blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1)
-                    : launch_tiled_for<MODE, false>(dw, vig, lg, blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+            lut.tex ? launch_tiled_for<MODE, true>(dw, vig, lg, blocks, frames, gains, out, lut, W, H, use_gain, out_pitch,
+                                                   rgba, s, e0, e1)
+                    : launch_tiled_for<MODE, false>(dw, vig, lg, blocks, frames, gains, out, lut, W, H, use_gain, out_pitch,
+                                                    rgba, s, e0, e1);
         if (e != hipSuccess) return e;
     }
     if (lut.n_wide > 0)

@@ -165,12 +165,15 @@ struct FrameSet {
 // of one XCD band at the same time: the item's entries, metadata and staging groups come from HBM (or the
 // Infinity Cache) once for all the frames and from L2 for the others, while each unit stages and computes
 // its own frame.  Camera c of frame f: src[(f << cam_log2) + c], cam_log2 = 5 (32 cameras) for one or two
-// frames, 4 (16 cameras) for four.  The FIRST argument of the composite kernels (kernarg_frame).
+// frames, 4 (16 cameras) for four.  The FIRST argument of the composite kernels (kernarg_frame), sized for
+// its frame count (one frame: 1,040 B of kernarg, as the round-5 FrameSet + pointers).
 constexpr int kMaxBatch = 4;
+template <int NF>
 struct FrameBatch {
-    SourceFrame src[2 * kMaxCams];
-    uint8_t* out[kMaxBatch];        // MODE 0: the frames' YUV420P outputs (one pitch)
-    const double* gains[kMaxBatch]; // the frames' gains (device)
+    static constexpr int kCamLog2 = NF <= 2 ? 5 : 4;
+    SourceFrame src[NF << kCamLog2];
+    uint8_t* out[NF];        // MODE 0: the frames' YUV420P outputs (one pitch)
+    const double* gains[NF]; // the frames' gains (device)
 };
 
 
@@ -235,18 +238,20 @@ hipError_t launch_gain_feed(const FrameSet& frames, const CompositeEntry* sample
 
 // FastMapper frames of one launch (octvr_fastmapper_stitch_nv12_batch): camera c of frame f at
 // src[(f << cam_log2) + c] (cam_log2 5 for up to 2 frames, 4 for 4), the frames' NV12 outputs.
+template <int NF>
 struct FastBatch {
-    SourceFrame src[2 * kMaxCams];
-    uint8_t* out[kMaxBatch];
+    SourceFrame src[NF << (NF <= 2 ? 5 : 4)];
+    uint8_t* out[NF];
 };
 
 // The feeds of nf frames (1, 2 or 4) of a batch in one launch: workgroup b feeds frame b / n_chunks into its
-// own totals / tickets / gains (FeedBatch, the kernel's first argument).
+// own totals / tickets / gains (FeedBatch, the kernel's first argument; one frame: 536 B of kernarg).
+template <int NF>
 struct FeedBatch {
-    SourceFrame src[kMaxBatch * kGainMaxCams];  // camera c of frame f at f * kGainMaxCams + c
-    unsigned long long* totals[kMaxBatch];
-    uint32_t* tickets[kMaxBatch];
-    double* gains[kMaxBatch];
+    SourceFrame src[NF * kGainMaxCams];  // camera c of frame f at f * kGainMaxCams + c
+    unsigned long long* totals[NF];
+    uint32_t* tickets[NF];
+    double* gains[NF];
 };
 hipError_t launch_gain_feed_batch(const FrameSet* frames, int nf, const CompositeEntry* samples, const uint16_t* partners,
                                   int tex, int n_chunks, const int32_t* N, int n, unsigned long long* const* totals,
