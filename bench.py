@@ -128,14 +128,26 @@ def timed_region(step, steps, sync, dist=None):
     if dist:
         dist.barrier()
     sync()
-    t0 = time.perf_counter()
-    for k in range(steps):
-        step(k)
+    marks = os.environ.get("OCTVR_BENCH_STEP_MARKS")  # diagnostic: the host time at which each step returned
+    if marks:
+        tk = [0.0] * steps
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(k)
+            tk[k] = time.perf_counter()
+    else:
+        t0 = time.perf_counter()
+        for k in range(steps):
+            step(k)
     ISSUE_S[0] = time.perf_counter() - t0
     sync()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if marks:
+        with open(marks, "a") as f:
+            f.write(json.dumps({"steps": steps, "elapsed_us": elapsed * 1e6,
+                                "step_end_us": [round((t - t0) * 1e6, 1) for t in tk]}) + "\n")
     if dist:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -578,11 +590,22 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # of that stream's timeline).  Several: every step on every stream, so the union of the launches'
     # intervals (the wall time some composite was running) is known; a launch's own start-to-end
     # span then also covers the other streams' kernels beside it.
-    m.set_timing(1 if inflight > 1 or nb > 1 else 4)
+    if not os.environ.get("OCTVR_BENCH_NO_TIMING"):  # diagnostic: the timed region without the event pairs
+        m.set_timing(1 if inflight > 1 or nb > 1 else 4)
     elapsed = timed_region(step, args.steps // nb, lambda: torch.cuda.synchronize(dev), dist)
     m.set_timing(False)
-    span_ms, busy_ms, launches = m.kernel_busy()
+    marks = os.environ.get("OCTVR_BENCH_STEP_MARKS")
+    if marks:  # diagnostic: every timed launch's GPU interval beside the host marks
+        iv = m.kernel_intervals()
+        with open(marks, "a") as f:
+            f.write(json.dumps({"kernel_ms": [[round(a, 4), round(b, 4)] for a, b in iv]}) + "\n")
+        span_ms, busy_ms = ox.interval_union([a for a, _ in iv], [b for _, b in iv])
+        launches = len(iv)
+    else:
+        span_ms, busy_ms, launches = m.kernel_busy()
     kern_ms = busy_ms if inflight > 1 else span_ms
+    if launches == 0:  # (OCTVR_BENCH_NO_TIMING) no events: the wall time stands in
+        kern_ms, launches = elapsed * 1e3, args.steps // nb
     launches *= nb  # per frame: a batched launch stitches nb frames
     serial = serial_step = None
     if inflight > 1 and not dist:

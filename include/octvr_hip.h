@@ -208,6 +208,9 @@ int octvr_mapper_kernel_time(octvr_mapper* mapper, double* total_ms, int* launch
  * start-to-end times, busy_ms = length of the union of the launches' intervals (the wall time some
  * composite was running).  Synchronizes and resets the log. */
 int octvr_mapper_kernel_busy(octvr_mapper* mapper, double* span_ms, double* busy_ms, int* launches);
+/* The logged launches themselves: [start_ms[k], end_ms[k]] relative to the first launch's start, in issue
+ * order, at most `cap` of them (*n: how many were logged); the log is then cleared as by kernel_busy. */
+int octvr_mapper_kernel_intervals(octvr_mapper* mapper, double* start_ms, double* end_ms, int cap, int* n);
 /* The arithmetic behind kernel_busy, on host arrays: span = sum of (end - start), busy = length of the
  * union of the n intervals [start[k], end[k]] (overlapping, nested, touching or disjoint, any order). */
 int octvr_interval_union(const double* start, const double* end, int n, double* span, double* busy);

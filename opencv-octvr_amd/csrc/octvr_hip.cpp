@@ -1859,6 +1859,20 @@ int octvr_mapper_set_timing(octvr_mapper* m, int enable) {
         REQUIRE(m && enable >= 0, "bad arguments");
         m->timing = enable;
         m->timed_calls = 0;
+        if (enable) {
+            // the event pairs of the next timed stitches created now, not inside the caller's timed region
+            // (hipEventCreate there cost the 20-step bench region ~20 us of host time per step)
+            DeviceGuard dg(m->device);
+            constexpr size_t kEventReserve = 1024;
+            while (m->free_events.size() + m->events.size() < kEventReserve) {
+                hipEvent_t e0 = nullptr, e1 = nullptr;
+                HIP_CHECK(hipEventCreate(&e0));
+                const hipError_t e = hipEventCreate(&e1);
+                if (e != hipSuccess) (void)hipEventDestroy(e0);
+                HIP_CHECK(e);
+                m->free_events.emplace_back(e0, e1);
+            }
+        }
     });
 }
 
@@ -1934,6 +1948,28 @@ int octvr_mapper_kernel_busy(octvr_mapper* m, double* span_ms, double* busy_ms, 
         *launches = (int)m->events.size();
         *span_ms = span;
         *busy_ms = busy;
+        m->events.clear();
+    });
+}
+
+int octvr_mapper_kernel_intervals(octvr_mapper* m, double* start_ms, double* end_ms, int cap, int* n) {
+    return guarded([&] {
+        REQUIRE(m && n && cap >= 0 && (cap == 0 || (start_ms && end_ms)), "bad arguments");
+        DeviceGuard dg(m->device);
+        int k = 0;
+        for (auto& e : m->events) {
+            HIP_CHECK(hipEventSynchronize(e.second));
+            if (k < cap) {
+                float a = 0, b = 0;
+                HIP_CHECK(hipEventElapsedTime(&a, m->events[0].first, e.first));
+                HIP_CHECK(hipEventElapsedTime(&b, m->events[0].first, e.second));
+                start_ms[k] = a;
+                end_ms[k] = b;
+            }
+            k++;
+        }
+        for (auto& e : m->events) m->free_events.push_back(e);
+        *n = k;
         m->events.clear();
     });
 }

@@ -83,6 +83,8 @@ _lib.octvr_mapper_traffic.argtypes = [_VP, C.POINTER(C.c_double)]
 _lib.octvr_mapper_set_timing.argtypes = [_VP, C.c_int]
 _lib.octvr_mapper_kernel_time.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_int)]
 _lib.octvr_mapper_kernel_busy.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int)]
+_lib.octvr_mapper_kernel_intervals.argtypes = [_VP, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int,
+                                               C.POINTER(C.c_int)]
 _lib.octvr_rig_lut_recomputed.argtypes = [_VP, C.c_int, C.POINTER(C.c_uint64)]
 _lib.octvr_debug_project_f64.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _VP, _VP, _VP]
 _lib.octvr_interval_union.argtypes = [_VP, _VP, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
@@ -516,6 +518,13 @@ class Mapper:
         sp, bu, k = C.c_double(), C.c_double(), C.c_int()
         _check(_lib.octvr_mapper_kernel_busy(self._h, C.byref(sp), C.byref(bu), C.byref(k)))
         return sp.value, bu.value, k.value
+
+    def kernel_intervals(self, cap=4096):
+        """[(start ms, end ms)] of the logged launches relative to the first one's start, in issue order
+        (synchronizes; clears the log as kernel_busy does)."""
+        st, en, k = (C.c_double * cap)(), (C.c_double * cap)(), C.c_int()
+        _check(_lib.octvr_mapper_kernel_intervals(self._h, st, en, cap, C.byref(k)))
+        return [(st[i], en[i]) for i in range(min(k.value, cap))]
 
     def close(self):
         if self._h and self._h.value:
