@@ -592,9 +592,29 @@ def gpu_rank(args, world, rank, local_rank, dist):
     # span then also covers the other streams' kernels beside it.
     if not os.environ.get("OCTVR_BENCH_NO_TIMING"):  # diagnostic: the timed region without the event pairs
         m.set_timing(1 if inflight > 1 or nb > 1 else 4)
-    elapsed = timed_region(step, args.steps // nb, lambda: torch.cuda.synchronize(dev), dist)
-    m.set_timing(False)
     marks = os.environ.get("OCTVR_BENCH_STEP_MARKS")
+    if marks:  # diagnostic: GPU markers at the region's first step (stream 0) and after its last (every stream)
+        ev_a = torch.cuda.Event(enable_timing=True)
+        ev_z = [torch.cuda.Event(enable_timing=True) for _ in streams]
+        syncs = [0]
+
+        def step_m(k):
+            if k == 0:
+                ev_a.record(streams[0])
+            step(k)
+
+        def sync_m():
+            if syncs[0] == 1:
+                for e, st in zip(ev_z, streams):
+                    e.record(st)
+            syncs[0] += 1
+            torch.cuda.synchronize(dev)
+        elapsed = timed_region(step_m, args.steps // nb, sync_m, dist)
+        with open(marks, "a") as f:
+            f.write(json.dumps({"gpu_region_us": max(ev_a.elapsed_time(e) for e in ev_z) * 1e3}) + "\n")
+    else:
+        elapsed = timed_region(step, args.steps // nb, lambda: torch.cuda.synchronize(dev), dist)
+    m.set_timing(False)
     if marks:  # diagnostic: every timed launch's GPU interval beside the host marks
         iv = m.kernel_intervals()
         with open(marks, "a") as f:

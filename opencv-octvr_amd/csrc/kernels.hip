@@ -304,7 +304,9 @@ __device__ bool lu_solve_block(double* A, double* b, int n, double* x) {
     return true;
 }
 
-__device__ bool solve_dispatch(double* A, double* b, int n, double* x) {
+// inlined into its one call site per feed instance (as a called function — the three frame-count instances
+// made the inliner stop — the one-in-flight C2 feed's serial tail grew from 16.4 to 20.0 us)
+__device__ __forceinline__ bool solve_dispatch(double* A, double* b, int n, double* x) {
     switch (n) {
 #define CASE(K) \
     case K:     \

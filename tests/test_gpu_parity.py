@@ -498,4 +498,17 @@ def test_gpu_kernel_busy_log(ox):
     for f in range(6):
         m.stitch(frames, outs[f % 2], stream=streams[f % 2])
     assert m.kernel_busy()[2] == 3
+    # the launches themselves (octvr_mapper_kernel_intervals), relative to the first one's start, in issue
+    # order; the event pairs come from the pool set_timing fills (1,024), reused across logs
+    m.set_timing(1)
+    for f in range(4):
+        m.stitch(frames, outs[f % 2], stream=streams[f % 2])
+    iv = m.kernel_intervals()
+    assert len(iv) == 4 and iv[0][0] == 0.0 and all(0 <= a <= b for a, b in iv)
+    sp, bu = ox.interval_union([a for a, _ in iv], [b for _, b in iv])
+    assert 0 < bu <= sp + 1e-9
+    assert m.kernel_intervals() == []
+    for f in range(1100):  # more timed stitches than the pool holds: further pairs are created as needed
+        m.stitch(frames, outs[f % 2], stream=streams[f % 2])
+    assert m.kernel_busy()[2] == 1100
     m.set_timing(0)
