@@ -15,6 +15,11 @@ timed on this host).
 
 K timed steps (default 1,000) follow W warmup steps and S seconds (default 0.5) of untimed preroll steps,
 so that the timed region runs at the GPU's settled clock.
+
+Diagnostics (Mapper configs; DESIGN.md §4 Round 6, "The 20-step region"): OCTVR_BENCH_STEP_MARKS=<file> appends
+the host time at which each timed step returned, the GPU span between markers at the region's ends and every
+composite's event interval; OCTVR_BENCH_NO_TIMING=1 times the region without the composites' event pairs (its
+kernel_us is then the wall time, not a roofline figure).
 """
 import argparse
 import json
