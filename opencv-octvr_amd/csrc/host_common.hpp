@@ -217,7 +217,8 @@ struct TiledLutDev {
     double result_bytes = 0;  // RGBA mode: result pixels the items write (kItemResult halves)
     std::string stats;
     TiledLut view{};
-    void upload(const TiledLutBuild& b);
+    // e24: pack the entries to 24 bits when no entry carries "no gain" (tiled_entry24)
+    void upload(const TiledLutBuild& b, bool e24 = false);
 };
 
 // ---- source footprint: the input bytes a mapper's kernels may read (tiling.cpp) ------------------------

@@ -1008,17 +1008,25 @@ struct TileData {
 // er: the entries as a buffer resource — voffset = lane * 16 (loop-invariant), soffset = the item's
 // scalar byte offset, so no per-lane 64-bit address is formed per item (TiledLutDev::upload checks
 // that the entries fit 32-bit offsets)
-template <bool DWORD_STAGE, bool VIG>
+// E24: the lane's four 24-bit entries of each half (tiled_entry24) as three dwords (d.e4[h].w unused)
+template <bool DWORD_STAGE, bool VIG, bool E24>
 __device__ __forceinline__ void data_issue(const __amdgpu_buffer_rsrc_t& er, const TileMeta& m, int t_end, int lg,
                                            const StageSlot& sl, uint32_t g, TileData& d) {
     const bool live = m.t < t_end;
     const int tid = threadIdx.x;
 #pragma unroll
     for (int h = 0; h < kItemHalves; h++) {
-        typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
-        const uint32_t so = (uint32_t)uniform(((live ? m.t : 0) >> lg) * kItemHalves + h) * (uint32_t)(kTilePx * 4);
-        const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
-        d.e4[h] = uint4{v.x, v.y, v.z, v.w};
+        const uint32_t so =
+            (uint32_t)uniform(((live ? m.t : 0) >> lg) * kItemHalves + h) * (uint32_t)(kTilePx * (E24 ? 3 : 4));
+        if constexpr (E24) {
+            typedef unsigned int u32x3e __attribute__((ext_vector_type(3)));
+            const u32x3e v = __builtin_amdgcn_raw_buffer_load_b96(er, (uint32_t)tid * 12u, so, 0);
+            d.e4[h] = uint4{v.x, v.y, v.z, 0u};
+        } else {
+            typedef unsigned int u32x4e __attribute__((ext_vector_type(4)));
+            const u32x4e v = __builtin_amdgcn_raw_buffer_load_b128(er, (uint32_t)tid * 16u, so, 0);
+            d.e4[h] = uint4{v.x, v.y, v.z, v.w};
+        }
     }
     if (!sl.live) {  // wave-uniform: no loads for a chunk the item lacks
         d.sg.dst = -1;
@@ -1142,7 +1150,7 @@ __device__ __forceinline__ uint32_t tap_off(uint32_t e) { return (e >> 13) & 0x3
 // TEX: texture-convention entries (tiled_entry_tex): the taps as usual, the texture filter model instead of
 // the weight table.
 // LG: 1 << LG frames per launch (FrameBatch; MODE 0 only)
-template <bool DWORD_STAGE, int MODE, bool VIG, bool TEX, int LG>
+template <bool DWORD_STAGE, int MODE, bool VIG, bool TEX, int LG, bool E24>
 __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& frames, TiledLut lut, int W, int H, int use_gain,
                                                   int64_t out_pitch, RgbaOut rgba) {
     __shared__ StitchLds L;
@@ -1167,7 +1175,8 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
     const int t_begin = lut.bands[g] << lg;  // work units: (item, frame) pairs
     const int t_end = lut.bands[g + 1] << lg;
     const __amdgpu_buffer_rsrc_t ersrc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t*>(lut.entries), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kItemHalves * kTilePx * 4)), 0x00020000);
+        const_cast<uint32_t*>(lut.entries), 0,
+        (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kItemHalves * kTilePx * (E24 ? 3 : 4))), 0x00020000);
     const __amdgpu_buffer_rsrc_t mrsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<TileHdr*>(lut.meta), 0, (int)((uint32_t)max(lut.n_items, 1) * (uint32_t)(kMetaWords * 16)), 0x00020000);
     const __amdgpu_buffer_rsrc_t grsrc = __builtin_amdgcn_make_buffer_rsrc(
@@ -1209,7 +1218,7 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
     const uint32_t g0 = group_issue(grsrc, t0, t_end, lg);
     __syncthreads();
     TileData d;
-    data_issue<DWORD_STAGE, VIG>(ersrc, cur, t_end, lg, stage_slot<true>(cur, t_end, wave), g0, d);
+    data_issue<DWORD_STAGE, VIG, E24>(ersrc, cur, t_end, lg, stage_slot<true>(cur, t_end, wave), g0, d);
     int t_mv = t0 + step < t_end ? t0 + step : t_end;  // item of the metadata in flight (mv)
     int t_n2 = t_mv < t_end && t0 + 2 * step < t_end ? t0 + 2 * step : t_end;  // item after it
     uint4 mv = meta_issue(mrsrc, t_mv, t_end, lg);
@@ -1221,7 +1230,10 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
     // so the compiler cannot fold them into one load at the header (waited on right there)
     asm volatile("" : "+v"(mv.x), "+v"(mv.y), "+v"(mv.z), "+v"(mv.w), "+v"(mg));
 #pragma unroll
-    for (int h = 0; h < kItemHalves; h++) asm volatile("" : "+v"(d.e4[h].x), "+v"(d.e4[h].y), "+v"(d.e4[h].z), "+v"(d.e4[h].w));
+    for (int h = 0; h < kItemHalves; h++) {
+        asm volatile("" : "+v"(d.e4[h].x), "+v"(d.e4[h].y), "+v"(d.e4[h].z));
+        if constexpr (!E24) asm volatile("" : "+v"(d.e4[h].w));
+    }
     asm volatile("" : "+v"(d.sg.y0), "+v"(d.sg.y1), "+v"(d.sg.uq), "+v"(d.sg.vq));
 
     // the previous item's output, stored in the next iteration: every store is then older than the
@@ -1302,7 +1314,7 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
                 store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
         }
         // the next item's first staging slot resolved only now (short scalar live ranges), then its loads
-        data_issue<DWORD_STAGE, VIG>(ersrc, nxt, t_end, lg, stage_slot<true>(nxt, t_end, wave), mg, d);
+        data_issue<DWORD_STAGE, VIG, E24>(ersrc, nxt, t_end, lg, stage_slot<true>(nxt, t_end, wave), mg, d);
         mv = meta_issue(mrsrc, t_n2, t_end, lg);
         mg = group_issue(grsrc, t_n2, t_end, lg);
         t_mv = t_n2;
@@ -1316,14 +1328,18 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
         }
 #pragma unroll
         for (int h = 0; h < kItemHalves; h++) {
-            const uint32_t ent[4] = {e4[h].x, e4[h].y, e4[h].z, e4[h].w};
+            // E24: the four 24-bit entries from the three dwords (two v_alignbit_b32, one shift)
+            const uint32_t ent[4] = {e4[h].x, E24 ? __builtin_amdgcn_alignbit(e4[h].y, e4[h].x, 24u) : e4[h].y,
+                                     E24 ? __builtin_amdgcn_alignbit(e4[h].z, e4[h].y, 16u) : e4[h].z,
+                                     E24 ? e4[h].z >> 8 : e4[h].w};
             float rgb[4][3];
             f32x2_t gain[4];
 #pragma unroll
             for (int p = 0; p < 4; p++) {
                 const uint32_t e = ent[p];
                 // taps (x, y), (x+1, y) and (x, y+1), (x+1, y+1): two ds_read2_b32, no per-tap masking
-                const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) + (TEX ? (e >> 15) & 0x3FFCu : tap_off(e));
+                const uint8_t* r0 = reinterpret_cast<const uint8_t*>(s_rgb) +
+                                    (TEX ? (e >> 15) & 0x3FFCu : E24 ? (e >> 10) & 0x3FFCu : tap_off(e));
                 const uint8_t* r1 = r0 + 4u * S;
                 const uint32_t c00 = reinterpret_cast<const uint32_t*>(r0)[0];
                 const uint32_t c01 = reinterpret_cast<const uint32_t*>(r0)[1];
@@ -1333,11 +1349,13 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
                     tex_bilerp_f(c00, c01, c10, c11, (e >> 1) & 255u, (e >> 9) & 255u, rgb[p]);
                     gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + ((e >> 30) << 3));
                 } else {
-                    bilerp_rgba_w(c00, c01, c10, c11, wtab_read(e), rgb[p]);
-                    // slot << 3 = e >> 27 (bits 27-29 of a tiled entry are zero; kernels.hpp)
-                    gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + (e >> 27));
+                    // E24: fxy at bits 2-11, so e << 1 holds it where wtab_read masks (bits 3-12)
+                    bilerp_rgba_w(c00, c01, c10, c11, wtab_read(E24 ? e << 1 : e), rgb[p]);
+                    // slot << 3 = e >> 27 (bits 27-29 of a tiled entry are zero; kernels.hpp); E24: bits 0-1
+                    const uint32_t go = E24 ? (e << 3) & 0x18u : e >> 27;
+                    gain[p] = *reinterpret_cast<const f32x2_t*>(reinterpret_cast<const uint8_t*>(s_slot_gain) + go);
                 }
-                if (MODE == 1 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
+                if (MODE == 1 && !E24 && (e & kEntryNoGain)) gain[p] = f32x2_t{1.0f, 1.0f};
             }
             prev[h] = finish_any<MODE>(rgb, gain);
         }
@@ -1370,18 +1388,18 @@ __device__ __forceinline__ void stitch_tiled_body(const FrameBatch<1 << LG>& fra
         store_half<MODE>(of, ro, res_rgba, prev[h], pcam, pfl, h, px, py + h * kTileH, pin && py + h * kTileH < H);
 }
 
-template <bool DWORD_STAGE, int MODE, bool VIG, int LG>
+template <bool DWORD_STAGE, int MODE, bool VIG, int LG, bool E24>
 __global__ void __launch_bounds__(256, kStitchRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
 __attribute__((amdgpu_num_vgpr(kStitchVgprs))) stitch_tiled_kernel(FrameBatch<1 << LG> frames, TiledLut lut, int W, int H,
                                                                    int use_gain, int64_t out_pitch, RgbaOut rgba) {
-    stitch_tiled_body<DWORD_STAGE, MODE, VIG, false, LG>(frames, lut, W, H, use_gain, out_pitch, rgba);
+    stitch_tiled_body<DWORD_STAGE, MODE, VIG, false, LG, E24>(frames, lut, W, H, use_gain, out_pitch, rgba);
 }
 template <bool DWORD_STAGE, int MODE, bool VIG, int LG>
 __global__ void __launch_bounds__(256, kStitchTexRegBlocks) __attribute__((amdgpu_num_sgpr(kStitchSgprs)))
 __attribute__((amdgpu_num_vgpr(kStitchTexVgprs))) stitch_tiled_tex_kernel(FrameBatch<1 << LG> frames, TiledLut lut, int W,
                                                                           int H, int use_gain, int64_t out_pitch,
                                                                           RgbaOut rgba) {
-    stitch_tiled_body<DWORD_STAGE, MODE, VIG, true, LG>(frames, lut, W, H, use_gain, out_pitch, rgba);
+    stitch_tiled_body<DWORD_STAGE, MODE, VIG, true, LG, false>(frames, lut, W, H, use_gain, out_pitch, rgba);
 }
 
 // Wide tiles: one workgroup per tile, 8-byte absolute entries, direct global gathers.
@@ -1435,11 +1453,11 @@ __global__ void __launch_bounds__(256) stitch_wide_kernel(FrameSet frames, Tiled
 
 // The weight table's address (wtab_read) assumes the dynamic LDS starts right after StitchLds: checked
 // once per kernel instance against the compiled static LDS size.
-template <bool DW, int MODE, bool V, bool TEX, int LG>
+template <bool DW, int MODE, bool V, bool TEX, int LG, bool E24>
 static hipError_t stitch_lds_check() {
     hipFuncAttributes a;
     const void* k = TEX ? reinterpret_cast<const void*>(stitch_tiled_tex_kernel<DW, MODE, V, LG>)
-                        : reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V, LG>);
+                        : reinterpret_cast<const void*>(stitch_tiled_kernel<DW, MODE, V, LG, E24>);
     const hipError_t e = hipFuncGetAttributes(&a, k);
     if (e != hipSuccess) return e;
     return a.sharedSizeBytes == sizeof(StitchLds) ? hipSuccess : hipErrorInvalidKernelFile;
@@ -1448,10 +1466,10 @@ static hipError_t stitch_lds_check() {
 // dynamic LDS of the composite: the weight table, then the frames' camera gains (FrameBatch order)
 constexpr uint32_t kStitchDynLds = kWtabBytes + 4u * 2u * kMaxCams;
 
-template <bool DW, int MODE, bool V, bool TEX, int LG>
+template <bool DW, int MODE, bool V, bool TEX, int LG, bool E24>
 static hipError_t launch_tiled(int blocks, const FrameBatch<1 << LG>& frames, const TiledLut& lut, int W, int H, int use_gain,
                                int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
-    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V, TEX, LG>();
+    static const hipError_t lds_ok = stitch_lds_check<DW, MODE, V, TEX, LG, E24>();
     if (lds_ok != hipSuccess) return lds_ok;
     if constexpr (TEX) {
         // (no packet-carried timing events: the texture convention is not a bench line's timed kernel)
@@ -1459,10 +1477,10 @@ static hipError_t launch_tiled(int blocks, const FrameBatch<1 << LG>& frames, co
                            frames, lut, W, H, use_gain, out_pitch, rgba);
         if (ev0) (void)hipEventRecord(ev1, s);
     } else if (ev0) {  // the timing events carried by the dispatch packet itself
-        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, LG>), dim3(blocks), dim3(256), kStitchDynLds, s, ev0,
+        hipExtLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, LG, E24>), dim3(blocks), dim3(256), kStitchDynLds, s, ev0,
                               ev1, 0, frames, lut, W, H, use_gain, out_pitch, rgba);
     } else {
-        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, LG>), dim3(blocks), dim3(256), kStitchDynLds, s, frames,
+        hipLaunchKernelGGL((stitch_tiled_kernel<DW, MODE, V, LG, E24>), dim3(blocks), dim3(256), kStitchDynLds, s, frames,
                            lut, W, H, use_gain, out_pitch, rgba);
     }
     return hipGetLastError();
@@ -1481,7 +1499,7 @@ static void frame_batch(const FrameSet* frames, const double* const* gains, uint
     }
 }
 
-template <bool DW, int MODE, bool V, bool TEX>
+template <bool DW, int MODE, bool V, bool TEX, bool E24>
 static hipError_t launch_tiled_lg(int lg, int blocks, const FrameSet* frames, const double* const* gains,
                                   uint8_t* const* out, const TiledLut& lut, int W, int H, int use_gain,
                                   int64_t out_pitch, const RgbaOut& rgba, hipStream_t s, hipEvent_t ev0,
@@ -1490,32 +1508,46 @@ static hipError_t launch_tiled_lg(int lg, int blocks, const FrameSet* frames, co
         if (lg == 1) {
             FrameBatch<2> fb;
             frame_batch<1>(frames, gains, out, fb);
-            return launch_tiled<DW, MODE, V, TEX, 1>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+            return launch_tiled<DW, MODE, V, TEX, 1, E24>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
         }
         if (lg == 2) {
             FrameBatch<4> fb;
             frame_batch<2>(frames, gains, out, fb);
-            return launch_tiled<DW, MODE, V, TEX, 2>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+            return launch_tiled<DW, MODE, V, TEX, 2, E24>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
         }
     }
     if (lg != 0) return hipErrorInvalidValue;
     FrameBatch<1> fb;
     frame_batch<0>(frames, gains, out, fb);
-    return launch_tiled<DW, MODE, V, TEX, 0>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
+    return launch_tiled<DW, MODE, V, TEX, 0, E24>(blocks, fb, lut, W, H, use_gain, out_pitch, rgba, s, ev0, ev1);
 }
 
 // the instance for the frames' staging (dword loads, vignette) and the entries' convention
+template <int MODE, bool TEX, bool E24>
+static hipError_t launch_tiled_vd(bool dw, bool vig, int lg, int blocks, const FrameSet* fr, const double* const* g,
+                                  uint8_t* const* o, const TiledLut& lut, int W, int H, int use_gain, int64_t out_pitch,
+                                  const RgbaOut& rgba, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (dw && !vig)
+        return launch_tiled_lg<true, MODE, false, TEX, E24>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    if (dw)
+        return launch_tiled_lg<true, MODE, true, TEX, E24>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    if (!vig)
+        return launch_tiled_lg<false, MODE, false, TEX, E24>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    return launch_tiled_lg<false, MODE, true, TEX, E24>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+}
+
+// the entries' width: 24-bit (TiledLut::e24, default sampling only) or 32-bit
 template <int MODE, bool TEX>
 static hipError_t launch_tiled_for(bool dw, bool vig, int lg, int blocks, const FrameSet* fr, const double* const* g,
                                    uint8_t* const* o, const TiledLut& lut, int W, int H, int use_gain, int64_t out_pitch,
                                    const RgbaOut& rgba, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-    if (dw && !vig)
-        return launch_tiled_lg<true, MODE, false, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
-    if (dw)
-        return launch_tiled_lg<true, MODE, true, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
-    if (!vig)
-        return launch_tiled_lg<false, MODE, false, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
-    return launch_tiled_lg<false, MODE, true, TEX>(lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    if constexpr (!TEX) {
+        if (lut.e24)
+            return launch_tiled_vd<MODE, TEX, true>(dw, vig, lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
+    } else {
+        if (lut.e24) return hipErrorInvalidValue;  // texture-convention entries are never packed
+    }
+    return launch_tiled_vd<MODE, TEX, false>(dw, vig, lg, blocks, fr, g, o, lut, W, H, use_gain, out_pitch, rgba, s, e0, e1);
 }
 
 // nf frame sets (1, 2 or 4) in one launch of the tiled kernel (FrameBatch); wide tiles one launch per frame

@@ -290,6 +290,7 @@ struct TiledLut {
     const uint16_t* grp1;         // the items' further chunks
     uint32_t n_grp1;              // entries of grp1
     int tex;                      // staged entries are texture-convention ones (tiled_entry_tex)
+    int e24;                      // entries packed to 24 bits (tiled_entry24): 12 bytes per lane and half
 };
 constexpr int kMetaWords = 1 + kTileSlots;
 constexpr int kQueueStride = 32;  // u32 words: one 128-B line per counter
@@ -310,6 +311,13 @@ constexpr uint32_t kCodeNoGain = 1u << 16;
 // staging area, fxy = fx | fy << 5.
 __host__ __device__ constexpr uint32_t tiled_entry(uint32_t off, uint32_t fxy, uint32_t slot, bool nogain) {
     return (nogain ? kEntryNoGain : 0u) | (fxy & 1023u) << 3 | off << 13 | slot << kEntrySlotShift;
+}
+
+// The same entry in 24 bits, for LUTs without "no gain" pixels (TiledLutDev::upload packs them): bits 0-1
+// the slot, 2-11 fxy, 12-23 the tap's LDS dword offset.  A lane's four entries of a half are packed into
+// three dwords (c0 | c1 << 24, c1 >> 8 | c2 << 16, c2 >> 16 | c3 << 8): 3 instead of 4 bytes per pixel.
+__host__ __device__ constexpr uint32_t tiled_entry24(uint32_t e) {
+    return (e >> 30) | ((e >> 3) & 1023u) << 2 | ((e >> 15) & 4095u) << 12;
 }
 
 // A staged texture-convention pixel (make_entry_tex with all four taps inside the image): bit 0 "no gain",

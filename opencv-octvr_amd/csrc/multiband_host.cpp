@@ -833,7 +833,7 @@ MultiBand* multiband_create(const octvr_rig& rig, int device, int bands, const s
         };
         TiledLutBuild tb = build_tiled_lut(jobs, entry, in_w, in_h, qpl);
         if (foot) footprint_add_tiles(*foot, tb);
-        M.remap.upload(tb);
+        M.remap.upload(tb, true);
     }
     return mb.release();
 }
@@ -964,7 +964,7 @@ std::vector<std::pair<std::string, double>> multiband_traffic_parts(const MultiB
     std::vector<std::pair<std::string, double>> parts;
     const TiledLut& t = M.remap.view;
     const TiledLutDev& r = M.remap;
-    parts.emplace_back("remap", 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + r.g0_bytes +
+    parts.emplace_back("remap", (t.e24 ? 3.0 : 4.0) * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + r.g0_bytes +
                                     1.5 * r.result_bytes + r.source_bytes +
                                     (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)));
     // down l: per item its (2 kTileH + 4) x (2 kTileW + 4) source window (the 5 x 5 support's halo) and the
@@ -1017,6 +1017,7 @@ std::string multiband_info(const MultiBand& M) {
                     std::to_string(M.arr.y) + ", " + std::to_string(M.arr.w) + ", " + std::to_string(M.arr.h) +
                     "], \"remap_items\": " + std::to_string(M.remap.view.n_items) +
                     ", \"remap_wide\": " + std::to_string(M.remap.view.n_wide) +
+                    ", \"remap_entry_bits\": " + std::to_string(M.remap.view.e24 ? 24 : 32) +
                     ", \"remap_result_subtiles\": " + std::to_string(M.n_result) + ", \"traffic_parts\": {";
     {
         bool first = true;

@@ -1831,7 +1831,7 @@ int octvr_mapper_traffic(const octvr_mapper* m, double* bytes) {
             return;
         }
         const TiledLut& t = m->tiles.view;
-        *bytes = 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
+        *bytes = (t.e24 ? 3.0 : 4.0) * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx + 1.5 * m->W * m->H +
                  (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide +
                  m->tiles.source_bytes;
     });
@@ -1848,7 +1848,7 @@ int octvr_mapper_traffic_parts(const octvr_mapper* m, double* lut_bytes, double*
             return;
         }
         const TiledLut& t = m->tiles.view;
-        *lut_bytes = 4.0 * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx +
+        *lut_bytes = (t.e24 ? 3.0 : 4.0) * t.n_items * kTilePx * t.qpl + 8.0 * t.n_wide * kTilePx +
                      (double)t.n_items * (sizeof(TileHdr) + kTileSlots * sizeof(TileSlot)) + 4.0 * t.n_wide;
         *frame_bytes = total - *lut_bytes;
     });

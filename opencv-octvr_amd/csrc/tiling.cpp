@@ -401,7 +401,7 @@ TiledLutBuild build_tiled_lut(const std::vector<TileJob>& jobs, const EntryFn& e
     return b;
 }
 
-void TiledLutDev::upload(const TiledLutBuild& b) {
+void TiledLutDev::upload(const TiledLutBuild& b, bool want_e24) {
     // per staged item one 80-byte record: its TileHdr, then its kTileSlots TileSlots (lane q of the
     // metadata load reads 16-byte word q)
     static_assert(sizeof(TileHdr) == 16 && sizeof(TileSlot) == 16, "16-byte metadata words");
@@ -427,7 +427,26 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     grp1.upload(b.grp1.data(), b.grp1.size());
     // the composite addresses the entries through a buffer resource with 32-bit offsets
     REQUIRE(b.entries.size() * sizeof(uint32_t) < (size_t)1 << 32, "tiled LUT entries exceed 4 GiB");
-    entries.upload(b.entries.data(), b.entries.size());
+    // 24-bit entries (tiled_entry24) when asked for and no entry carries "no gain" (the default sampling
+    // only; OCTVR_ENTRY32=1 keeps the 32-bit layout: measurement knob).  Asked for by the multi-band remap
+    // (C3 +3.4 %); the no-blend composite keeps 32-bit entries (C2 -1.5 % with 24: the two more VALU per
+    // pixel cost more than the quarter of the entry fetches saves there; round 6, `e24ab`)
+    bool e24 = want_e24 && !b.tex && std::getenv("OCTVR_ENTRY32") == nullptr;
+    for (size_t k = 0; e24 && k < b.entries.size(); k++) e24 = (b.entries[k] & kEntryNoGain) == 0u;
+    if (e24) {
+        REQUIRE(b.entries.size() % 4 == 0, "tiled entries: whole quads");
+        std::vector<uint32_t> p(b.entries.size() / 4 * 3);
+        for (size_t q = 0; q < b.entries.size() / 4; q++) {
+            const uint32_t c0 = tiled_entry24(b.entries[4 * q]), c1 = tiled_entry24(b.entries[4 * q + 1]);
+            const uint32_t c2 = tiled_entry24(b.entries[4 * q + 2]), c3 = tiled_entry24(b.entries[4 * q + 3]);
+            p[3 * q] = c0 | c1 << 24;
+            p[3 * q + 1] = c1 >> 8 | c2 << 16;
+            p[3 * q + 2] = c2 >> 16 | c3 << 8;
+        }
+        entries.upload(p.data(), p.size());
+    } else {
+        entries.upload(b.entries.data(), b.entries.size());
+    }
     wide.upload(b.wide.data(), b.wide.size());
     wide_tiles.upload(b.wide_tiles.data(), b.wide_tiles.size());
     wide_cams.upload(b.wide_cams.data(), b.wide_cams.size());
@@ -452,7 +471,7 @@ void TiledLutDev::upload(const TiledLutBuild& b) {
     if (b.item_flags.empty()) g0_bytes = 4.0 * kTilePx * ((double)b.n_items * b.qpl + b.n_wide);  // no flags: every half
     stats = b.stats;
     view = TiledLut{meta.p, entries.p, b.n_items, wide_tiles.p, wide.p, b.n_wide, wide_cams.p, bands.p, queue.p,
-                    b.qpl, grp0.p, grp1.p, (uint32_t)b.grp1.size(), b.tex};
+                    b.qpl, grp0.p, grp1.p, (uint32_t)b.grp1.size(), b.tex, e24 ? 1 : 0};
 }
 
 void SourceFootprint::init(const std::vector<int>& in_w, const std::vector<int>& in_h) {

@@ -408,6 +408,25 @@ def test_gpu_multiband_bit_exact(ox, name, blend):
         assert not d.any(), (int(d.sum()), np.argwhere(d)[:5].tolist())
 
 
+def test_gpu_multiband_entry_widths(ox, monkeypatch):
+    """The multi-band remap's 24-bit entries (tiled_entry24, LUTs without "no gain" pixels) and the 32-bit
+    layout (OCTVR_ENTRY32=1, and every LUT with such pixels) give the same bit-exact outputs; both occur."""
+    from octvr_amd import synthetic
+    seen = set()
+    for e32 in (False, True):
+        if e32:
+            monkeypatch.setenv("OCTVR_ENTRY32", "1")
+        for name in RIGS:
+            info = []
+            got, want, _, _ = _stitch_case(ox, name, synthetic.smooth_yuv_frame, None, blend=4, info=info)
+            bits = info[0]["remap_entry_bits"]
+            assert bits == 32 or not e32
+            seen.add(bits)
+            d = got != want
+            assert not d.any(), (name, bits, int(d.sum()), np.argwhere(d)[:5].tolist())
+    assert seen == {24, 32}, seen
+
+
 def test_gpu_multiband_deep_tiles(ox):
     """Deep tiles (R = G at their level, no pyrUp taps; multiband_host.cpp) occur on the golden rigs and
     the output stays bit-exact with them."""
