@@ -10,7 +10,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp PYTHONUNBUFFERED=1
 mkdir -p gpurun_out
-TAG=${TAG:-r06g}
+TAG=${TAG:-r06h}
 # config: streams frames-per-launch (bench.py DEFAULT_INFLIGHT / DEFAULT_BATCH)
 declare -A BENCHED=([C1]="2 4" [C2]="3 1" [C3]="4 1" [C4]="2 4" [F2]="1 4")
 if [ "${PART:-A}" = A ]; then
